@@ -1,0 +1,295 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident bulk decode of Flat16 spec messages on MI355X.
+
+Metric (BASELINE.json): "Mmsg/s + GB/s decode (device-resident), 1M x 256B batch, 1/2/4/8
+MI355X".  One step = one spec_decode_flat launch over a rank's whole batch (1M records of
+~256 B by default) already resident in HBM.  N GPUs = N processes (torchrun), each decoding
+its own shard (records are independent: no data-path collective, weak scaling); value =
+records decoded by all ranks / max-over-ranks time.
+
+Also reported (extra keys): encode throughput, the PCIe-inclusive end-to-end decode rate from
+pinned host memory, the roofline of the decode kernel (HIP events on its stream), and the
+CPU oracle timed on the host (rank 0, N=1 only).
+
+Input generation uses numpy + this engine's GPU encoder (the oracle is used only for the
+cpu_baseline leg and the optional --verify check).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import spec_amd  # noqa: E402
+from spec_amd import FLAT16, workload  # noqa: E402
+
+METRIC = "Mmsg/s + GB/s decode (device-resident), 1M×256B batch, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+# decode algorithmic bytes per record besides the encoded bytes: ends (8) + columns + status (1)
+COLUMN_BYTES = FLAT16.column_bytes  # 122
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--records", type=int, default=1 << 20, help="records per GPU")
+    p.add_argument("--seed", type=int, default=workload.SEED)
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    p.add_argument("--no-extras", action="store_true", help="skip encode / end-to-end legs")
+    p.add_argument("--verify", action="store_true", help="check a sample against the oracle")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_decode_flat.json"),
+                   help="PMC traffic summary (tools/pmc_summary.py) used for roofline.traffic")
+    return p.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return dist, rank, world, torch.device("cuda", local)
+    torch.cuda.set_device(0)
+    return None, 0, 1, torch.device("cuda", 0)
+
+
+def barrier(dist):
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(dist, x: float) -> float:
+    if dist is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(dist, x: float) -> float:
+    if dist is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def make_batch(n, seed, dev):
+    cols, heaps = workload.flat16(n, seed)
+    d_cols = [torch.from_numpy(c).to(dev) for c in cols]
+    d_heaps = {f: torch.from_numpy(h).to(dev) for f, h in heaps.items()}
+    stream, ends = spec_amd.encode_flat(FLAT16, d_cols, d_heaps, n)
+    torch.cuda.synchronize()
+    return cols, heaps, d_cols, d_heaps, stream, ends
+
+
+def time_decode(dec, steps, warmup, dist):
+    for _ in range(warmup):
+        dec()
+    barrier(dist)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        dec()
+    barrier(dist)
+    return time.perf_counter() - t0
+
+
+def kernel_time_events(fn, reps):
+    """Average per-launch duration from HIP events recorded on the launch stream.  The stream
+    is first parked behind a spin kernel so every launch and event is queued before the GPU
+    reaches them: the intervals measure the kernel, not host submission latency."""
+    s = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    if hasattr(torch.cuda, "_sleep"):
+        torch.cuda._sleep(int(2e8))  # ~0.1 s of GPU spin while the host enqueues
+    for a, b in evs:
+        a.record(s)
+        fn()
+        b.record(s)
+    torch.cuda.synchronize()
+    ms = sorted(a.elapsed_time(b) for a, b in evs)
+    return sum(ms) / len(ms), ms[len(ms) // 2]
+
+
+def cpu_baseline(stream_np, ends_np, seconds):
+    """The oracle's per-record OpenMessageErr + 16 getters loop on host cores (test infra)."""
+    import ctypes as C
+
+    from oracle import oracle as O
+
+    L = O.lib()
+    n = len(ends_np)
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    outc = [np.ones((n, w), np.uint8) for w in FLAT16.widths]
+    st = np.ones(n, np.uint8)
+    ptrs = (C.c_void_p * 16)(*[c.ctypes.data for c in outc])
+    tags = np.array(FLAT16.tags, np.uint16)
+    kinds = np.array(FLAT16.kinds, np.uint8)
+
+    def run(th):
+        L.so_decode_flat_batch(16, O._ptr(tags), O._ptr(kinds), O._ptr(stream_np), O._ptr(ends_np), n,
+                               ptrs, O._ptr(st), th)
+
+    res = {}
+    for th in sorted({1, threads}):
+        run(th)  # warm
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            run(th)
+            reps += 1
+            dt = time.perf_counter() - t0
+            if dt >= seconds / 2:
+                break
+        res[th] = n * reps / dt / 1e6
+    return res, threads, n
+
+
+def e2e_decode(stream_host, ends_host, dev, reps=5):
+    """Pinned host -> H2D -> decode -> D2H of all columns; whole-pipeline rate (Mmsg/s)."""
+    n = ends_host.numel()
+    cols = spec_amd.alloc_columns(FLAT16, n, dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    host_cols = [torch.empty(c.shape, dtype=torch.uint8, pin_memory=True) for c in cols]
+    host_status = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    d_stream = torch.empty(stream_host.numel(), dtype=torch.uint8, device=dev)
+    d_ends = torch.empty(n, dtype=torch.int64, device=dev)
+
+    def once():
+        d_stream.copy_(stream_host, non_blocking=True)
+        d_ends.copy_(ends_host, non_blocking=True)
+        spec_amd.decode_flat(FLAT16, d_stream, d_ends, cols=cols, status=status)
+        for h, c in zip(host_cols, cols):
+            h.copy_(c, non_blocking=True)
+        host_status.copy_(status, non_blocking=True)
+
+    once()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        once()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    return n / dt / 1e6, dt
+
+
+def main():
+    args = parse()
+    dist, rank, world, dev = dist_setup(args)
+    n = args.records
+    cols, heaps, d_cols, d_heaps, stream, ends = make_batch(n, args.seed + rank, dev)
+    stream_bytes = stream.numel()
+    mean_rec = stream_bytes / n
+
+    dec = spec_amd.Decoder(FLAT16, stream, ends)
+    out_cols, status = dec.cols, dec.status
+    elapsed = time_decode(dec, args.steps, args.warmup, dist)
+    elapsed = max_over_ranks(dist, elapsed)
+    total_records = sum_over_ranks(dist, float(n)) * args.steps
+    value = total_records / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # per-launch kernel time on the launch stream (HIP events)
+    avg_ms, med_ms = kernel_time_events(dec, max(10, args.steps))
+    alg_bytes = stream_bytes + n * (8 + COLUMN_BYTES + 1)
+    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
+    read_only = (stream_bytes + 8 * n) / (avg_ms * 1e-3) / 1e9
+
+    traffic = None
+    if os.path.exists(args.traffic):
+        try:
+            t = json.load(open(args.traffic))
+            if t.get("records") == n:
+                traffic = t.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    ok = int((status != 0).sum().item()) == 0
+    extras = {}
+    if not args.no_extras:
+        enc = spec_amd.Encoder(FLAT16, n, dev)
+        out = torch.empty(stream_bytes, dtype=torch.uint8, device=dev)
+        e2 = torch.empty(n, dtype=torch.int64, device=dev)
+        enc_ms, _ = kernel_time_events(lambda: enc.encode_into(d_cols, d_heaps, out, e2), 10)
+        torch.cuda.synchronize()
+        ok = ok and torch.equal(out, stream) and torch.equal(e2, ends)
+        heap_bytes = sum(h.numel() for h in d_heaps.values())
+        enc_alg = n * (COLUMN_BYTES + 8) + heap_bytes + stream_bytes
+        extras["encode"] = {"mmsg_s": round(n / (enc_ms * 1e-3) / 1e6, 1),
+                            "gb_s": round(enc_alg / (enc_ms * 1e-3) / 1e9, 1),
+                            "ms": round(enc_ms, 4), "bit_exact_vs_decode_input": bool(ok)}
+        if rank == 0:
+            sh = stream.cpu().pin_memory()
+            eh = ends.cpu().pin_memory()
+            rate, dt = e2e_decode(sh, eh, dev)
+            extras["e2e_pinned_decode"] = {"mmsg_s": round(rate, 1), "ms": round(dt * 1e3, 3),
+                                           "note": "H2D stream+ends, decode, D2H columns+status, one stream"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        s_np = stream.cpu().numpy()
+        e_np = ends.cpu().numpy().view(np.uint64)
+        res, threads, sample = cpu_baseline(s_np, e_np, args.cpu_seconds)
+        cpu = {"value": round(res[threads], 2), "unit": "Mmsg/s", "cores": threads, "kind": "port",
+               "sample": f"{sample} Flat16 records (the full batch) decoded repeatedly for ~{args.cpu_seconds/2:.0f} s "
+                         f"per thread count; C restatement of OpenMessageErr + 16 getters",
+               "single_core_value": round(res[1], 2)}
+        if args.verify:
+            from oracle import oracle as O
+
+            m = min(n, 200_000)
+            want, wst = O.decode_flat_batch(FLAT16.tags, FLAT16.kinds, s_np, e_np[:m], FLAT16.widths, 8)
+            for f in range(16):
+                ok = ok and np.array_equal(out_cols[f][:m].cpu().numpy(), want[f])
+            extras["verified_records"] = m
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Mmsg/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": "flat16-decode", "records_per_gpu": n,
+                       "mean_record_bytes": round(mean_rec, 1), "stream_bytes_per_gpu": stream_bytes,
+                       "parallelism": f"record-sharded x{world}, no collective"},
+            "gb_s": round(total_records * (mean_rec + 8 + COLUMN_BYTES + 1) / elapsed / 1e9, 1),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "decode_flat_kernel", "kernel_ms_avg": round(avg_ms, 5),
+                         "kernel_ms_median": round(med_ms, 5), "alg_bytes_per_launch": alg_bytes,
+                         "read_only_gb_s": round(read_only, 1)},
+            "cpu_baseline": cpu,
+            "correct": bool(ok),
+        }
+        line.update(extras)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,140 @@
+/*
+ * spec_amd.h — C ABI of the MI355X bulk encode/decode engine for the spec binary format.
+ *
+ * This is the drop-in boundary for the reference's hot path (basecomplextech/spec,
+ * encode.go / decode.go / writer*.go over internal/{encode,decode,format,writer,types}).
+ * The reference has no batch API: callers loop over records calling
+ * spec.OpenMessageErr + generated getters (decode) or NewMessageWriterBuffer + FieldWriter
+ * calls + Build (encode).  Each entry point below replaces exactly such a loop over a
+ * batch of records resident in HBM, with results identical to the per-record Go calls.
+ * The Go binding a maintainer would add (cgo) is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Plain C types only; all buffers are caller-owned DEVICE pointers unless a name ends
+ *    in _host.  `stream` is a hipStream_t passed as void* (NULL = default stream).
+ *  - Return value: SPEC_OK (0) or a negative SPEC_E_* code; launches are asynchronous.
+ *  - A batch is `stream_bytes[stream_len]` = records concatenated, and
+ *    `ends[n]` = exclusive end offset of each record (record i = [ends[i-1], ends[i]),
+ *    ends[-1] = 0): the layout an mpx receiver produces after framing
+ *    (mpx/conn_reader.go:179-194).  One call handles stream_len < 4 GiB; larger batches
+ *    are split by the caller (string/bytes offsets are 32-bit, see below).
+ *  - Columns are structure-of-arrays, one array per schema field, record-major, with the
+ *    element width of spec_kind_width(kind).  string/bytes columns hold spec_span
+ *    {uint32 off, uint32 len}: off is relative to the batch stream (decode output) or to
+ *    the field's heap (encode input); an absent or empty value is {0, 0}.
+ */
+#ifndef SPEC_AMD_H
+#define SPEC_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPEC_AMD_ABI_VERSION 1
+#define SPEC_MAX_FIELDS 64
+
+/* Column kinds: one per typed getter / FieldWriter method
+ * (internal/types/msg.go:219-421, internal/writer/msg.go:99-211). */
+typedef enum spec_kind {
+    SPEC_KIND_BOOL = 1,    /* uint8 0/1        Message.Bool     / FieldWriter.Bool    */
+    SPEC_KIND_BYTE = 2,    /* uint8            Message.Byte     / FieldWriter.Byte    */
+    SPEC_KIND_INT16 = 3,   /* int16            Message.Int16    / FieldWriter.Int16   */
+    SPEC_KIND_INT32 = 4,   /* int32            Message.Int32    / FieldWriter.Int32   */
+    SPEC_KIND_INT64 = 5,   /* int64            Message.Int64    / FieldWriter.Int64   */
+    SPEC_KIND_UINT16 = 6,  /* uint16           Message.Uint16   / FieldWriter.Uint16  */
+    SPEC_KIND_UINT32 = 7,  /* uint32           Message.Uint32   / FieldWriter.Uint32  */
+    SPEC_KIND_UINT64 = 8,  /* uint64           Message.Uint64   / FieldWriter.Uint64  */
+    SPEC_KIND_FLOAT32 = 9, /* float32 bits     Message.Float32  / FieldWriter.Float32 */
+    SPEC_KIND_FLOAT64 = 10,/* float64 bits     Message.Float64  / FieldWriter.Float64 */
+    SPEC_KIND_BIN64 = 11,  /* 8 opaque bytes   Message.Bin64    / FieldWriter.Bin64   */
+    SPEC_KIND_BIN128 = 12, /* 16 opaque bytes  Message.Bin128   / FieldWriter.Bin128  */
+    SPEC_KIND_BIN256 = 13, /* 32 opaque bytes  Message.Bin256   / FieldWriter.Bin256  */
+    SPEC_KIND_STRING = 14, /* spec_span        Message.String   / FieldWriter.String  */
+    SPEC_KIND_BYTES = 15,  /* spec_span        Message.Bytes    / FieldWriter.Bytes   */
+} spec_kind;
+
+/* Per-record status: the error class OpenMessageErr returns for the record
+ * (internal/decode/msg.go:14-99).  Field-level errors are swallowed by the getters,
+ * which return zero values, exactly as in the reference. */
+typedef enum spec_status {
+    SPEC_STATUS_OK = 0,
+    SPEC_STATUS_INVALID_TYPE = 1,       /* "decode message: invalid type"       */
+    SPEC_STATUS_INVALID_TABLE_SIZE = 2, /* "decode message: invalid table size" */
+    SPEC_STATUS_INVALID_DATA_SIZE = 3,  /* "decode message: invalid data size"  */
+    SPEC_STATUS_INVALID_TABLE = 4,      /* "decode message: invalid table"      */
+    SPEC_STATUS_INVALID_DATA = 5,       /* "decode message: invalid data"       */
+    SPEC_STATUS_PANIC = 6,              /* the reference would panic (malformed list table) */
+} spec_status;
+
+typedef enum spec_rc {
+    SPEC_OK = 0,
+    SPEC_E_INVALID_ARGUMENT = -1,
+    SPEC_E_HIP = -2,       /* a HIP runtime call failed (see spec_last_hip_error) */
+    SPEC_E_TOO_LARGE = -3, /* stream_len >= 4 GiB or a record > format.MaxSize */
+    SPEC_E_CAPACITY = -4,  /* output buffer smaller than the encoded batch */
+    SPEC_E_WORKSPACE = -5, /* workspace smaller than *_workspace_size() */
+} spec_rc;
+
+typedef struct spec_span {
+    uint32_t off;
+    uint32_t len;
+} spec_span;
+
+typedef struct spec_field {
+    uint16_t tag;  /* message field tag (1..65535) */
+    uint8_t kind;  /* spec_kind */
+    uint8_t reserved;
+} spec_field;
+
+/* A flat message schema: the fields a generated Write() emits, in write order
+ * (internal/lang/generator/message.go:319-439 emits one FieldWriter call per field). */
+typedef struct spec_schema {
+    uint32_t nfields;
+    spec_field fields[SPEC_MAX_FIELDS];
+} spec_schema;
+
+/* ---- introspection ---- */
+int spec_abi_version(void);
+int spec_kind_width(int kind);
+const char *spec_strerror(int rc);
+int spec_last_hip_error(void);
+
+/* ---- decode ----
+ * spec_decode_flat: for every record i, exactly
+ *     m, err := spec.OpenMessageErr(record_i)          (msg.go:25-27, internal/types/msg.go:43-55)
+ *     status[i] = class(err); column_f[i] = m.<Kind_f>(tag_f)   (internal/types/msg.go:219-475)
+ * replacing the BenchmarkReadMessage loop (internal/bench/parse_test.go:48-111) and the
+ * decoders it reaches (decode.go:9-40 -> internal/decode/...).
+ * columns[f] points at n * spec_kind_width(kind_f) bytes; status may be NULL. */
+int spec_decode_flat(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
+                     const uint64_t *ends, uint64_t n, void *const *columns, uint8_t *status,
+                     void *stream);
+
+/* ---- encode ----
+ * spec_encode_flat: for every record i, exactly
+ *     w := spec.NewMessageWriterBuffer(buf)             (writer_msg.go:26-31)
+ *     w.Field(tag_f).<Kind_f>(column_f[i])  for f in schema order   (internal/writer/msg.go:99-211)
+ *     w.Build()                                          (internal/writer/msg.go:56-60)
+ * appending into one output buffer (encode.go:11-38 -> internal/encode/...), so out[] holds
+ * the records back to back and ends[i] is each record's end offset.  heaps[f] (with
+ * heap_lens[f] bytes) backs string/bytes column f; NULL for other kinds.
+ * Needs a workspace of spec_encode_flat_workspace_size(n) bytes; writes the total encoded
+ * size to *total (device uint64).  If the total exceeds out_cap, nothing is written to
+ * out/ends and *total still reports the required size (check it, then retry).
+ * spec_encode_flat_size runs only the sizing passes (writes *total). */
+size_t spec_encode_flat_workspace_size(uint64_t n);
+int spec_encode_flat_size(const spec_schema *schema, const void *const *columns, uint64_t n,
+                          void *workspace, size_t workspace_size, uint64_t *total, void *stream);
+int spec_encode_flat(const spec_schema *schema, const void *const *columns,
+                     const uint8_t *const *heaps, const uint64_t *heap_lens, uint64_t n,
+                     uint8_t *out, uint64_t out_cap, uint64_t *ends, void *workspace,
+                     size_t workspace_size, uint64_t *total, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

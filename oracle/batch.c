@@ -1,0 +1,286 @@
+/*
+ * batch.c — the reference's per-record loops over a batch of records, used as the
+ * parity oracle for the bulk GPU kernels and as the CPU baseline in bench.py.
+ * TEST INFRASTRUCTURE (oracle).
+ *
+ *   decode: BenchmarkReadMessage pattern, internal/bench/parse_test.go:48-111
+ *           (OpenMessageErr + one typed getter per field)
+ *   encode: BenchmarkWrite_* pattern, internal/bench/write_test.go:16-78
+ *           (NewMessageWriterBuffer + one FieldWriter call per field + Build)
+ */
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "spec_oracle.h"
+
+/* Record status codes, shared with include/spec_amd.h SPEC_STATUS_*. */
+enum {
+    ST_OK = 0,
+    ST_INVALID_TYPE = 1,
+    ST_INVALID_TABLE_SIZE = 2,
+    ST_INVALID_DATA_SIZE = 3,
+    ST_INVALID_TABLE = 4,
+    ST_INVALID_DATA = 5,
+    ST_PANIC = 6, /* the reference would panic (malformed list table) */
+};
+
+/* Map a DecodeMessageTable / DecodeListTable error to its class (msg.go:22-66). */
+static uint8_t classify(so_err e) {
+    if (!e) return ST_OK;
+    const char *s = strstr(e, ": ");
+    s = s ? s + 2 : e;
+    if (!strncmp(s, "invalid type", 12)) return ST_INVALID_TYPE;
+    if (!strncmp(s, "invalid table size", 18)) return ST_INVALID_TABLE_SIZE;
+    if (!strncmp(s, "invalid data size", 17)) return ST_INVALID_DATA_SIZE;
+    if (!strncmp(s, "invalid table", 13)) return ST_INVALID_TABLE;
+    if (!strncmp(s, "invalid data", 12)) return ST_INVALID_DATA;
+    return ST_INVALID_DATA;
+}
+
+int so_kind_width(int kind) {
+    switch (kind) {
+    case SO_KIND_BOOL: case SO_KIND_BYTE: return 1;
+    case SO_KIND_INT16: case SO_KIND_UINT16: return 2;
+    case SO_KIND_INT32: case SO_KIND_UINT32: case SO_KIND_FLOAT32: return 4;
+    case SO_KIND_INT64: case SO_KIND_UINT64: case SO_KIND_FLOAT64: case SO_KIND_BIN64: return 8;
+    case SO_KIND_BIN128: return 16;
+    case SO_KIND_BIN256: return 32;
+    case SO_KIND_STRING: case SO_KIND_BYTES: return 8;
+    }
+    return 0;
+}
+
+static inline uint64_t rec_start(const uint64_t *ends, uint64_t r) { return r ? ends[r - 1] : 0; }
+
+/* Decode one field of one record into its column slot via the typed getter. */
+static void getter(const so_message *m, const uint8_t *stream, uint16_t tag, int kind, uint8_t *dst) {
+    switch (kind) {
+    case SO_KIND_BOOL: dst[0] = (uint8_t)so_message_bool(m, tag); break;
+    case SO_KIND_BYTE: dst[0] = so_message_byte(m, tag); break;
+    case SO_KIND_INT16: { int16_t v = so_message_int16(m, tag); memcpy(dst, &v, 2); } break;
+    case SO_KIND_INT32: { int32_t v = so_message_int32(m, tag); memcpy(dst, &v, 4); } break;
+    case SO_KIND_INT64: { int64_t v = so_message_int64(m, tag); memcpy(dst, &v, 8); } break;
+    case SO_KIND_UINT16: { uint16_t v = so_message_uint16(m, tag); memcpy(dst, &v, 2); } break;
+    case SO_KIND_UINT32: { uint32_t v = so_message_uint32(m, tag); memcpy(dst, &v, 4); } break;
+    case SO_KIND_UINT64: { uint64_t v = so_message_uint64(m, tag); memcpy(dst, &v, 8); } break;
+    case SO_KIND_FLOAT32: { float v = so_message_float32(m, tag); memcpy(dst, &v, 4); } break;
+    case SO_KIND_FLOAT64: { double v = so_message_float64(m, tag); memcpy(dst, &v, 8); } break;
+    case SO_KIND_BIN64: so_message_bin64(m, tag, dst); break;
+    case SO_KIND_BIN128: so_message_bin128(m, tag, dst); break;
+    case SO_KIND_BIN256: so_message_bin256(m, tag, dst); break;
+    case SO_KIND_STRING:
+    case SO_KIND_BYTES: {
+        size_t len;
+        const uint8_t *p = kind == SO_KIND_STRING ? so_message_string(m, tag, &len) : so_message_bytes(m, tag, &len);
+        /* empty or absent => {0, 0}: a zero-length view carries no offset */
+        uint32_t span[2] = {p && len ? (uint32_t)(p - stream) : 0u, p ? (uint32_t)len : 0u};
+        memcpy(dst, span, 8);
+    } break;
+    }
+}
+
+typedef struct {
+    int nfields;
+    const uint16_t *tags;
+    const uint8_t *kinds;
+    const uint8_t *stream;
+    const uint64_t *ends;
+    uint64_t lo, hi;
+    void *const *columns;
+    uint8_t *status;
+} decode_job;
+
+static void *decode_range(void *arg) {
+    decode_job *j = (decode_job *)arg;
+    int widths[256];
+    for (int f = 0; f < j->nfields; f++) widths[f] = so_kind_width(j->kinds[f]);
+    for (uint64_t r = j->lo; r < j->hi; r++) {
+        uint64_t s = rec_start(j->ends, r);
+        so_message m;
+        so_err e = so_open_message_err(j->stream + s, (size_t)(j->ends[r] - s), &m);
+        j->status[r] = classify(e);
+        for (int f = 0; f < j->nfields; f++) {
+            uint8_t *dst = (uint8_t *)j->columns[f] + r * (uint64_t)widths[f];
+            getter(&m, j->stream, j->tags[f], j->kinds[f], dst);
+        }
+    }
+    return NULL;
+}
+
+int so_decode_flat_batch(int nfields, const uint16_t *tags, const uint8_t *kinds,
+                         const uint8_t *stream, const uint64_t *ends, uint64_t n,
+                         void *const *columns, uint8_t *status, int nthreads) {
+    if (nfields > 256) return -1;
+    if (nthreads < 1) nthreads = 1;
+    if ((uint64_t)nthreads > n) nthreads = n ? (int)n : 1;
+    decode_job jobs[256];
+    pthread_t th[256];
+    if (nthreads > 256) nthreads = 256;
+    for (int t = 0; t < nthreads; t++) {
+        decode_job j = {nfields, tags, kinds, stream, ends, n * (uint64_t)t / (uint64_t)nthreads,
+                        n * (uint64_t)(t + 1) / (uint64_t)nthreads, columns, status};
+        jobs[t] = j;
+    }
+    if (nthreads == 1) {
+        decode_range(&jobs[0]);
+        return 0;
+    }
+    for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, decode_range, &jobs[t]);
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    return 0;
+}
+
+/* Write one field through the FieldWriter method for its kind. */
+static so_err write_field(so_writer *w, uint16_t tag, int kind, const uint8_t *src, const uint8_t *heap) {
+    switch (kind) {
+    case SO_KIND_BOOL: return so_field_bool(w, tag, src[0] != 0);
+    case SO_KIND_BYTE: return so_field_byte(w, tag, src[0]);
+    case SO_KIND_INT16: { int16_t v; memcpy(&v, src, 2); return so_field_int16(w, tag, v); }
+    case SO_KIND_INT32: { int32_t v; memcpy(&v, src, 4); return so_field_int32(w, tag, v); }
+    case SO_KIND_INT64: { int64_t v; memcpy(&v, src, 8); return so_field_int64(w, tag, v); }
+    case SO_KIND_UINT16: { uint16_t v; memcpy(&v, src, 2); return so_field_uint16(w, tag, v); }
+    case SO_KIND_UINT32: { uint32_t v; memcpy(&v, src, 4); return so_field_uint32(w, tag, v); }
+    case SO_KIND_UINT64: { uint64_t v; memcpy(&v, src, 8); return so_field_uint64(w, tag, v); }
+    case SO_KIND_FLOAT32: { float v; memcpy(&v, src, 4); return so_field_float32(w, tag, v); }
+    case SO_KIND_FLOAT64: { double v; memcpy(&v, src, 8); return so_field_float64(w, tag, v); }
+    case SO_KIND_BIN64: return so_field_bin64(w, tag, src);
+    case SO_KIND_BIN128: return so_field_bin128(w, tag, src);
+    case SO_KIND_BIN256: return so_field_bin256(w, tag, src);
+    case SO_KIND_STRING:
+    case SO_KIND_BYTES: {
+        uint32_t span[2];
+        memcpy(span, src, 8);
+        const uint8_t *p = heap + span[0];
+        return kind == SO_KIND_STRING ? so_field_string(w, tag, (const char *)p, span[1])
+                                      : so_field_bytes(w, tag, p, span[1]);
+    }
+    }
+    return "unknown kind";
+}
+
+int so_encode_flat_batch(int nfields, const uint16_t *tags, const uint8_t *kinds,
+                         const void *const *columns, const uint8_t *const *heaps, uint64_t n,
+                         uint8_t *out, uint64_t out_cap, uint64_t *ends) {
+    so_buf buf;
+    so_buf_init_fixed(&buf, out, (size_t)out_cap);
+    so_writer *w = so_writer_new(&buf);
+    int widths[256];
+    if (nfields > 256) return -1;
+    for (int f = 0; f < nfields; f++) widths[f] = so_kind_width(kinds[f]);
+    int rc = 0;
+    for (uint64_t r = 0; r < n; r++) {
+        so_writer_reset(w, &buf);
+        so_writer_begin_message(w);
+        for (int f = 0; f < nfields; f++) {
+            const uint8_t *src = (const uint8_t *)columns[f] + r * (uint64_t)widths[f];
+            write_field(w, tags[f], kinds[f], src, heaps ? heaps[f] : NULL);
+        }
+        so_err e = so_writer_end(w, NULL, NULL);
+        if (e) {
+            rc = -1;
+            break;
+        }
+        if (buf.overflow) {
+            rc = -2;
+            break;
+        }
+        ends[r] = buf.len;
+    }
+    so_writer_free(w);
+    return rc;
+}
+
+/* ---- Nested (config 4) ---- */
+
+int so_encode_nested_batch(const uint8_t *id, const int64_t *seq, const uint32_t *name,
+                           const uint8_t *name_heap, const uint32_t *item_begin,
+                           const int32_t *key, const double *value, const uint32_t *label,
+                           const uint8_t *label_heap, uint64_t n, uint8_t *out,
+                           uint64_t out_cap, uint64_t *ends) {
+    so_buf buf;
+    so_buf_init_fixed(&buf, out, (size_t)out_cap);
+    so_writer *w = so_writer_new(&buf);
+    int rc = 0;
+    for (uint64_t r = 0; r < n; r++) {
+        so_writer_reset(w, &buf);
+        so_writer_begin_message(w);
+        so_field_bin128(w, 1, id + 16 * r);
+        so_field_int64(w, 2, seq[r]);
+        so_field_string(w, 3, (const char *)name_heap + name[2 * r], name[2 * r + 1]);
+        so_field_begin_list(w, 4); /* FieldWriter.List() */
+        for (uint32_t i = item_begin[r]; i < item_begin[r + 1]; i++) {
+            so_elem_begin_message(w); /* MessageListWriter.Add() */
+            so_field_int32(w, 1, key[i]);
+            so_field_float64(w, 2, value[i]);
+            so_field_string(w, 3, (const char *)label_heap + label[2 * i], label[2 * i + 1]);
+            so_writer_end(w, NULL, NULL); /* item End() */
+        }
+        so_writer_end(w, NULL, NULL); /* list End() */
+        so_err e = so_writer_end(w, NULL, NULL); /* Build() */
+        if (e) {
+            rc = -1;
+            break;
+        }
+        if (buf.overflow) {
+            rc = -2;
+            break;
+        }
+        ends[r] = buf.len;
+    }
+    so_writer_free(w);
+    return rc;
+}
+
+int so_decode_nested_counts(const uint8_t *stream, const uint64_t *ends, uint64_t n,
+                            uint32_t *counts, uint8_t *status) {
+    for (uint64_t r = 0; r < n; r++) {
+        uint64_t s = rec_start(ends, r);
+        so_message m;
+        so_err e = so_open_message_err(stream + s, (size_t)(ends[r] - s), &m);
+        status[r] = classify(e);
+        so_list l;
+        so_message_list(&m, 4, &l);
+        counts[r] = (uint32_t)so_list_len(&l);
+    }
+    return 0;
+}
+
+int so_decode_nested_batch(const uint8_t *stream, const uint64_t *ends, uint64_t n,
+                           const uint32_t *item_begin, uint8_t *id, int64_t *seq,
+                           uint32_t *name, int32_t *key, double *value, uint32_t *label,
+                           uint8_t *item_status, uint8_t *status) {
+    for (uint64_t r = 0; r < n; r++) {
+        uint64_t s = rec_start(ends, r);
+        so_message m;
+        so_err e = so_open_message_err(stream + s, (size_t)(ends[r] - s), &m);
+        status[r] = classify(e);
+        so_message_bin128(&m, 1, id + 16 * r);
+        seq[r] = so_message_int64(&m, 2);
+        size_t len;
+        const uint8_t *p = so_message_string(&m, 3, &len);
+        name[2 * r] = p && len ? (uint32_t)(p - stream) : 0;
+        name[2 * r + 1] = p ? (uint32_t)len : 0;
+        so_list l;
+        so_message_list(&m, 4, &l);
+        uint32_t cnt = (uint32_t)so_list_len(&l);
+        for (uint32_t i = 0; i < cnt; i++) {
+            uint32_t o = item_begin[r] + i;
+            const uint8_t *ib;
+            size_t ilen;
+            so_message it;
+            if (so_list_get_bytes(&l, (int)i, &ib, &ilen) < 0) {
+                memset(&it, 0, sizeof(it));
+                item_status[o] = ST_PANIC;
+            } else {
+                item_status[o] = classify(so_open_message_err(ib, ilen, &it));
+            }
+            key[o] = so_message_int32(&it, 1);
+            value[o] = so_message_float64(&it, 2);
+            const uint8_t *q = so_message_string(&it, 3, &len);
+            label[2 * o] = q && len ? (uint32_t)(q - stream) : 0;
+            label[2 * o + 1] = q ? (uint32_t)len : 0;
+        }
+    }
+    return 0;
+}

@@ -1,0 +1,15 @@
+"""spec_amd — MI355X-native bulk encode/decode engine for the spec binary format.
+
+Drop-in for the hot path of basecomplextech/spec (encode.go, decode.go, writer*.go over
+internal/{encode,decode,format,writer,types}): batches of records resident in HBM are
+decoded into SoA columns / encoded from them by hand-written gfx950 kernels
+(spec_amd/csrc, C ABI in include/spec_amd.h).  See DESIGN.md.
+"""
+from ._lib import LIB_PATH, SpecError, header_symbols, lib
+from .batch import Columns, Decoder, Encoder, alloc_columns, decode_flat, encode_flat
+from .schema import FLAT16, Field, Kind, Schema
+
+__all__ = [
+    "LIB_PATH", "SpecError", "header_symbols", "lib", "Columns", "Decoder", "Encoder", "alloc_columns",
+    "decode_flat", "encode_flat", "FLAT16", "Field", "Kind", "Schema",
+]

@@ -1,0 +1,83 @@
+"""Loader for libspec_amd.so — the HIP engine behind include/spec_amd.h.
+
+The product path has no fallback: if the library is missing or fails to load, every
+entry point raises.  Build it with `python -c "import __graft_entry__ as g; g.build()"`
+or `make -C spec_amd/csrc`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libspec_amd.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "spec_amd.h")
+
+SPEC_MAX_FIELDS = 64
+
+
+class SpecField(C.Structure):
+    _fields_ = [("tag", C.c_uint16), ("kind", C.c_uint8), ("reserved", C.c_uint8)]
+
+
+class SpecSchema(C.Structure):
+    _fields_ = [("nfields", C.c_uint32), ("fields", SpecField * SPEC_MAX_FIELDS)]
+
+
+class SpecError(RuntimeError):
+    def __init__(self, rc: int, what: str):
+        self.rc = rc
+        super().__init__(f"{what}: {strerror(rc)} (rc={rc}, hip={last_hip_error()})")
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"spec_amd: {LIB_PATH} not built (run make -C spec_amd/csrc)")
+        L = C.CDLL(LIB_PATH)
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+def _declare(L):
+    vp = C.c_void_p
+    L.spec_abi_version.restype = C.c_int
+    L.spec_kind_width.argtypes = [C.c_int]
+    L.spec_strerror.restype = C.c_char_p
+    L.spec_strerror.argtypes = [C.c_int]
+    L.spec_last_hip_error.restype = C.c_int
+    L.spec_decode_flat.argtypes = [C.POINTER(SpecSchema), vp, C.c_uint64, vp, C.c_uint64,
+                                   C.POINTER(vp), vp, vp]
+    L.spec_encode_flat_workspace_size.restype = C.c_size_t
+    L.spec_encode_flat_workspace_size.argtypes = [C.c_uint64]
+    L.spec_encode_flat_size.argtypes = [C.POINTER(SpecSchema), C.POINTER(vp), C.c_uint64, vp,
+                                        C.c_size_t, vp, vp]
+    L.spec_encode_flat.argtypes = [C.POINTER(SpecSchema), C.POINTER(vp), C.POINTER(vp),
+                                   C.POINTER(C.c_uint64), C.c_uint64, vp, C.c_uint64, vp, vp,
+                                   C.c_size_t, vp, vp]
+
+
+def strerror(rc: int) -> str:
+    return lib().spec_strerror(rc).decode()
+
+
+def last_hip_error() -> int:
+    return lib().spec_last_hip_error()
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise SpecError(rc, what)
+
+
+def header_symbols() -> list[str]:
+    """Function names declared in include/spec_amd.h."""
+    src = open(HEADER_PATH).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(spec_[a-z0-9_]+)\s*\(", src)))

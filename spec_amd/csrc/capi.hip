@@ -1,0 +1,175 @@
+// capi.hip — the C ABI of libspec_amd.so (include/spec_amd.h): argument validation, schema
+// preprocessing (table order) and kernel launches.  No host sync on any path.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include "../../include/spec_amd.h"
+#include "spec_internal.hpp"
+
+namespace {
+
+thread_local int g_last_hip_error = 0;
+
+int kind_width(int kind) {
+    switch (kind) {
+    case SPEC_KIND_BOOL: case SPEC_KIND_BYTE: return 1;
+    case SPEC_KIND_INT16: case SPEC_KIND_UINT16: return 2;
+    case SPEC_KIND_INT32: case SPEC_KIND_UINT32: case SPEC_KIND_FLOAT32: return 4;
+    case SPEC_KIND_INT64: case SPEC_KIND_UINT64: case SPEC_KIND_FLOAT64: case SPEC_KIND_BIN64: return 8;
+    case SPEC_KIND_BIN128: return 16;
+    case SPEC_KIND_BIN256: return 32;
+    case SPEC_KIND_STRING: case SPEC_KIND_BYTES: return 8;
+    }
+    return 0;
+}
+
+// Table order a Writer produces for this schema: messageStack.insert over the tags in write
+// order, insertion sort where an equal tag written later moves before the earlier one
+// (internal/writer/stack_msg.go:37-61).  order[j] = schema index of the j-th table entry.
+void table_order(const spec_schema *s, uint8_t *order) {
+    uint16_t tags[SPEC_MAX_FIELDS];
+    uint8_t idx[SPEC_MAX_FIELDS];
+    for (uint32_t f = 0; f < s->nfields; f++) {
+        tags[f] = s->fields[f].tag;
+        idx[f] = (uint8_t)f;
+        for (int i = (int)f; i > 0; i--) {
+            if (tags[i - 1] < tags[i]) break;
+            uint16_t t = tags[i - 1];
+            tags[i - 1] = tags[i];
+            tags[i] = t;
+            uint8_t x = idx[i - 1];
+            idx[i - 1] = idx[i];
+            idx[i] = x;
+        }
+    }
+    memcpy(order, idx, s->nfields);
+}
+
+int check_schema(const spec_schema *s) {
+    if (!s || s->nfields > SPEC_MAX_FIELDS) return SPEC_E_INVALID_ARGUMENT;
+    for (uint32_t f = 0; f < s->nfields; f++)
+        if (kind_width(s->fields[f].kind) == 0) return SPEC_E_INVALID_ARGUMENT;
+    return SPEC_OK;
+}
+
+int hip_rc(hipError_t e) {
+    if (e == hipSuccess) return SPEC_OK;
+    g_last_hip_error = (int)e;
+    return SPEC_E_HIP;
+}
+
+void fill_encode_args(spec::EncodeArgs &a, const spec_schema *schema, const void *const *columns, uint64_t n) {
+    memset(&a, 0, sizeof(a));
+    a.n = n;
+    a.nfields = schema->nfields;
+    for (uint32_t f = 0; f < schema->nfields; f++) {
+        a.tags[f] = schema->fields[f].tag;
+        a.kinds[f] = schema->fields[f].kind;
+        a.cols[f] = columns[f];
+        if (schema->fields[f].tag > 255) a.table_big_forced = 1;
+    }
+    table_order(schema, a.order);
+    a.nblocks = (n + spec::ENC_BLOCK - 1) / spec::ENC_BLOCK;
+}
+
+} // namespace
+
+extern "C" {
+
+int spec_abi_version(void) { return SPEC_AMD_ABI_VERSION; }
+
+int spec_kind_width(int kind) { return kind_width(kind); }
+
+int spec_last_hip_error(void) { return g_last_hip_error; }
+
+const char *spec_strerror(int rc) {
+    switch (rc) {
+    case SPEC_OK: return "ok";
+    case SPEC_E_INVALID_ARGUMENT: return "invalid argument";
+    case SPEC_E_HIP: return "HIP runtime error";
+    case SPEC_E_TOO_LARGE: return "batch too large (stream >= 4 GiB or record > format.MaxSize)";
+    case SPEC_E_CAPACITY: return "output capacity too small";
+    case SPEC_E_WORKSPACE: return "workspace too small";
+    }
+    return "unknown error";
+}
+
+int spec_decode_flat(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
+                     const uint64_t *ends, uint64_t n, void *const *columns, uint8_t *status,
+                     void *stream) {
+    int rc = check_schema(schema);
+    if (rc) return rc;
+    if (n == 0) return SPEC_OK;
+    if (!ends || !columns || (!stream_bytes && stream_len)) return SPEC_E_INVALID_ARGUMENT;
+    if (stream_len >= (1ull << 32)) return SPEC_E_TOO_LARGE;
+    for (uint32_t f = 0; f < schema->nfields; f++)
+        if (!columns[f]) return SPEC_E_INVALID_ARGUMENT;
+    spec::DecodeArgs a;
+    memset(&a, 0, sizeof(a));
+    a.stream = stream_bytes;
+    a.stream_len = stream_len;
+    a.ends = ends;
+    a.n = n;
+    a.status = status;
+    a.nfields = schema->nfields;
+    uint8_t order[SPEC_MAX_FIELDS];
+    table_order(schema, order);
+    for (uint32_t j = 0; j < schema->nfields; j++) a.rank[order[j]] = (uint8_t)j;
+    for (uint32_t f = 0; f < schema->nfields; f++) {
+        a.tags[f] = schema->fields[f].tag;
+        a.kinds[f] = schema->fields[f].kind;
+        a.cols[f] = columns[f];
+    }
+    double avg = (double)stream_len / (double)n;
+    if (spec::launch_decode_flat(a, avg, (hipStream_t)stream)) return hip_rc(hipGetLastError());
+    return SPEC_OK;
+}
+
+size_t spec_encode_flat_workspace_size(uint64_t n) {
+    uint64_t nblocks = (n + spec::ENC_BLOCK - 1) / spec::ENC_BLOCK;
+    return (size_t)((nblocks + 1) * sizeof(uint64_t));
+}
+
+int spec_encode_flat_size(const spec_schema *schema, const void *const *columns, uint64_t n,
+                          void *workspace, size_t workspace_size, uint64_t *total, void *stream) {
+    int rc = check_schema(schema);
+    if (rc) return rc;
+    if (!columns || !workspace) return SPEC_E_INVALID_ARGUMENT;
+    if (workspace_size < spec_encode_flat_workspace_size(n)) return SPEC_E_WORKSPACE;
+    spec::EncodeArgs a;
+    fill_encode_args(a, schema, columns, n);
+    a.block_sums = (uint64_t *)workspace;
+    a.total = total;
+    if (spec::launch_encode_size(a, (hipStream_t)stream)) return hip_rc(hipGetLastError());
+    return SPEC_OK;
+}
+
+int spec_encode_flat(const spec_schema *schema, const void *const *columns,
+                     const uint8_t *const *heaps, const uint64_t *heap_lens, uint64_t n,
+                     uint8_t *out, uint64_t out_cap, uint64_t *ends, void *workspace,
+                     size_t workspace_size, uint64_t *total, void *stream) {
+    int rc = check_schema(schema);
+    if (rc) return rc;
+    if (!columns || !workspace || (n && (!ends || !out))) return SPEC_E_INVALID_ARGUMENT;
+    if (workspace_size < spec_encode_flat_workspace_size(n)) return SPEC_E_WORKSPACE;
+    spec::EncodeArgs a;
+    fill_encode_args(a, schema, columns, n);
+    for (uint32_t f = 0; f < schema->nfields; f++) {
+        int k = schema->fields[f].kind;
+        if (k == SPEC_KIND_STRING || k == SPEC_KIND_BYTES) {
+            if (!heaps || !heap_lens || (!heaps[f] && heap_lens[f])) return SPEC_E_INVALID_ARGUMENT;
+            a.heaps[f] = heaps[f];
+            a.heap_lens[f] = heap_lens[f];
+        }
+    }
+    a.out = out;
+    a.out_cap = out_cap;
+    a.ends = ends;
+    a.block_sums = (uint64_t *)workspace;
+    a.total = total;
+    if (spec::launch_encode_size(a, (hipStream_t)stream)) return hip_rc(hipGetLastError());
+    if (spec::launch_encode_write(a, (hipStream_t)stream)) return hip_rc(hipGetLastError());
+    return SPEC_OK;
+}
+
+} // extern "C"

@@ -1,0 +1,51 @@
+// spec_internal.hpp — kernel argument blocks and launcher declarations shared by the HIP
+// translation units of libspec_amd.so (not part of the public C ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/spec_amd.h"
+
+namespace spec {
+
+// Passed by value as the kernel argument (lives in the kernarg segment => scalar loads,
+// the per-field loop branches are wave-uniform).
+struct DecodeArgs {
+    const uint8_t *stream;
+    uint64_t stream_len;
+    const uint64_t *ends;
+    uint64_t n;
+    uint8_t *status;
+    uint32_t nfields;
+    uint16_t tags[SPEC_MAX_FIELDS];
+    uint8_t kinds[SPEC_MAX_FIELDS];
+    uint8_t rank[SPEC_MAX_FIELDS]; // index of the field's tag in the sorted table a writer emits
+    void *cols[SPEC_MAX_FIELDS];
+};
+
+struct EncodeArgs {
+    uint64_t n;
+    uint32_t nfields;
+    uint16_t tags[SPEC_MAX_FIELDS];
+    uint8_t kinds[SPEC_MAX_FIELDS];
+    uint8_t order[SPEC_MAX_FIELDS]; // table order: order[j] = schema index of j-th table entry
+    const void *cols[SPEC_MAX_FIELDS];
+    const uint8_t *heaps[SPEC_MAX_FIELDS];
+    uint64_t heap_lens[SPEC_MAX_FIELDS];
+    uint32_t table_big_forced; // 1 if any tag > 255 (IsBigMessage holds for every record)
+    uint8_t *out;
+    uint64_t out_cap;
+    uint64_t *ends;
+    uint64_t *block_sums;  // workspace: per-block encoded bytes, then exclusive offsets
+    uint64_t nblocks;
+    uint64_t *total;
+};
+
+int launch_decode_flat(const DecodeArgs &a, double avg_record, hipStream_t stream);
+int launch_encode_size(const EncodeArgs &a, hipStream_t stream);
+int launch_encode_write(const EncodeArgs &a, hipStream_t stream);
+
+constexpr int ENC_BLOCK = 256; // records per encode block (4 waves, one record per lane)
+
+} // namespace spec

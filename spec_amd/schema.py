@@ -1,0 +1,116 @@
+"""Schema descriptors: which typed field each column holds.
+
+A flat schema is the list of (tag, kind) a generated Write() emits in order — one
+FieldWriter call per field (internal/lang/generator/message.go:319-439) — and that the
+generated getters read back (message.go:97-186).  Kinds map one-to-one onto the typed
+getters of types.Message (internal/types/msg.go:219-421).
+"""
+from __future__ import annotations
+
+import enum
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import SPEC_MAX_FIELDS, SpecSchema
+
+
+class Kind(enum.IntEnum):
+    BOOL = 1
+    BYTE = 2
+    INT16 = 3
+    INT32 = 4
+    INT64 = 5
+    UINT16 = 6
+    UINT32 = 7
+    UINT64 = 8
+    FLOAT32 = 9
+    FLOAT64 = 10
+    BIN64 = 11
+    BIN128 = 12
+    BIN256 = 13
+    STRING = 14
+    BYTES = 15
+
+
+WIDTH = {
+    Kind.BOOL: 1, Kind.BYTE: 1, Kind.INT16: 2, Kind.INT32: 4, Kind.INT64: 8,
+    Kind.UINT16: 2, Kind.UINT32: 4, Kind.UINT64: 8, Kind.FLOAT32: 4, Kind.FLOAT64: 8,
+    Kind.BIN64: 8, Kind.BIN128: 16, Kind.BIN256: 32, Kind.STRING: 8, Kind.BYTES: 8,
+}
+
+# numpy view of one column element (bins stay raw bytes)
+NP_DTYPE = {
+    Kind.BOOL: np.uint8, Kind.BYTE: np.uint8, Kind.INT16: np.int16, Kind.INT32: np.int32,
+    Kind.INT64: np.int64, Kind.UINT16: np.uint16, Kind.UINT32: np.uint32,
+    Kind.UINT64: np.uint64, Kind.FLOAT32: np.uint32, Kind.FLOAT64: np.uint64,
+    Kind.BIN64: np.uint8, Kind.BIN128: np.uint8, Kind.BIN256: np.uint8,
+    Kind.STRING: np.uint32, Kind.BYTES: np.uint32,
+}
+
+VARLEN = (Kind.STRING, Kind.BYTES)
+
+
+@dataclass(frozen=True)
+class Field:
+    tag: int
+    kind: Kind
+    name: str = ""
+
+    @property
+    def width(self) -> int:
+        return WIDTH[self.kind]
+
+
+class Schema:
+    def __init__(self, fields):
+        fields = [f if isinstance(f, Field) else Field(*f) for f in fields]
+        if len(fields) > SPEC_MAX_FIELDS:
+            raise ValueError(f"at most {SPEC_MAX_FIELDS} fields")
+        self.fields = tuple(Field(f.tag, Kind(f.kind), f.name) for f in fields)
+        c = SpecSchema()
+        c.nfields = len(self.fields)
+        for i, f in enumerate(self.fields):
+            c.fields[i].tag = f.tag
+            c.fields[i].kind = int(f.kind)
+        self.c = c
+
+    def __len__(self):
+        return len(self.fields)
+
+    @property
+    def tags(self):
+        return [f.tag for f in self.fields]
+
+    @property
+    def kinds(self):
+        return [int(f.kind) for f in self.fields]
+
+    @property
+    def widths(self):
+        return [f.width for f in self.fields]
+
+    @property
+    def column_bytes(self) -> int:
+        return sum(self.widths)
+
+
+# The benchmark schema (SURVEY.md §8(d) "Flat16"): tags 1..16 written in tag order.
+FLAT16 = Schema([
+    Field(1, Kind.BOOL, "bool"),
+    Field(2, Kind.BYTE, "byte"),
+    Field(3, Kind.INT16, "int16"),
+    Field(4, Kind.INT32, "int32"),
+    Field(5, Kind.INT64, "int64"),
+    Field(6, Kind.UINT16, "uint16"),
+    Field(7, Kind.UINT32, "uint32"),
+    Field(8, Kind.UINT64, "uint64"),
+    Field(9, Kind.FLOAT32, "float32"),
+    Field(10, Kind.FLOAT64, "float64"),
+    Field(11, Kind.BIN64, "bin64"),
+    Field(12, Kind.BIN128, "bin128"),
+    Field(13, Kind.BIN256, "bin256"),
+    Field(14, Kind.STRING, "string"),
+    Field(15, Kind.BYTES, "bytes"),
+    Field(16, Kind.INT64, "int64b"),
+])

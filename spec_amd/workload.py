@@ -1,0 +1,110 @@
+"""Synthetic batches for the benchmark and the parity tests.
+
+Flat16 values, seeded numpy PCG64 (seed 0x5EC0DE unless given):
+  signed ints   bit length k ~ U[0, width-1], magnitude ~ U[0, 2^k), random sign
+  unsigned ints bit length k ~ U[0, width],   value ~ U[0, 2^k)
+  floats        finite random bit patterns
+  bins          random bytes
+  string        ASCII, length ~ U[30, 62];  bytes: random, length ~ U[30, 62]
+Mean encoded record ~= 256 B (measured by tests/test_workload.py).
+
+Columns are numpy arrays laid out exactly like the device columns (one uint8 [n, width]
+array per field); string/bytes columns are {uint32 off, uint32 len} into per-field heaps.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .schema import FLAT16, Kind, Schema
+
+SEED = 0x5EC0DE
+
+
+def _signed(rng, n, width):
+    k = rng.integers(0, width, size=n)  # bit length in [0, width-1]
+    mag = (rng.integers(0, 2**62, size=n, dtype=np.uint64) << np.uint64(2)) | rng.integers(0, 4, size=n, dtype=np.uint64)
+    mask = np.where(k >= 64, np.uint64(~np.uint64(0)), (np.uint64(1) << k.astype(np.uint64)) - np.uint64(1))
+    mag &= mask
+    v = mag.astype(np.int64)
+    neg = rng.integers(0, 2, size=n).astype(bool)
+    v = np.where(neg, -v, v)
+    return v
+
+
+def _unsigned(rng, n, width):
+    k = rng.integers(0, width + 1, size=n)
+    v = (rng.integers(0, 2**62, size=n, dtype=np.uint64) << np.uint64(2)) | rng.integers(0, 4, size=n, dtype=np.uint64)
+    shift = np.clip(k, 0, 63).astype(np.uint64)
+    mask = np.where(k >= 64, np.uint64(~np.uint64(0)), (np.uint64(1) << shift) - np.uint64(1))
+    return v & mask
+
+
+def _finite_bits(rng, n, bits):
+    if bits == 32:
+        v = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+        exp = (v >> np.uint32(23)) & np.uint32(0xFF)
+        v = np.where(exp == 0xFF, v & np.uint32(0xBFFFFFFF), v)  # clear an exponent bit
+        return v
+    v = (rng.integers(0, 2**62, size=n, dtype=np.uint64) << np.uint64(2)) | rng.integers(0, 4, size=n, dtype=np.uint64)
+    exp = (v >> np.uint64(52)) & np.uint64(0x7FF)
+    return np.where(exp == 0x7FF, v & np.uint64(0xBFFFFFFFFFFFFFFF), v)
+
+
+def _heap(rng, n, lo, hi, ascii_only):
+    lens = rng.integers(lo, hi + 1, size=n).astype(np.uint32)
+    offs = np.zeros(n, dtype=np.uint64)
+    if n:
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    total = int(lens.sum(dtype=np.uint64))
+    if ascii_only:
+        heap = rng.integers(32, 127, size=total, dtype=np.uint8)
+    else:
+        heap = rng.integers(0, 256, size=total, dtype=np.uint8)
+    span = np.empty((n, 2), dtype=np.uint32)
+    span[:, 0] = offs.astype(np.uint32)
+    span[:, 1] = lens
+    return span, heap
+
+
+def as_bytes(a: np.ndarray, n: int) -> np.ndarray:
+    return np.ascontiguousarray(a).view(np.uint8).reshape(n, -1)
+
+
+def gen_columns(schema: Schema, n: int, seed: int = SEED, str_len=(30, 62)):
+    """Random values for any flat schema -> (columns [uint8 (n, w)], heaps {field: uint8[]})."""
+    rng = np.random.default_rng(seed)
+    cols, heaps = [], {}
+    for f, fld in enumerate(schema.fields):
+        k = fld.kind
+        if k == Kind.BOOL:
+            a = rng.integers(0, 2, size=n, dtype=np.uint8)
+        elif k == Kind.BYTE:
+            a = rng.integers(0, 256, size=n, dtype=np.uint8)
+        elif k == Kind.INT16:
+            a = _signed(rng, n, 16).astype(np.int16)
+        elif k == Kind.INT32:
+            a = _signed(rng, n, 32).astype(np.int32)
+        elif k == Kind.INT64:
+            a = _signed(rng, n, 64)
+        elif k == Kind.UINT16:
+            a = _unsigned(rng, n, 16).astype(np.uint16)
+        elif k == Kind.UINT32:
+            a = _unsigned(rng, n, 32).astype(np.uint32)
+        elif k == Kind.UINT64:
+            a = _unsigned(rng, n, 64)
+        elif k == Kind.FLOAT32:
+            a = _finite_bits(rng, n, 32)
+        elif k == Kind.FLOAT64:
+            a = _finite_bits(rng, n, 64)
+        elif k in (Kind.BIN64, Kind.BIN128, Kind.BIN256):
+            a = rng.integers(0, 256, size=(n, fld.width), dtype=np.uint8)
+        elif k in (Kind.STRING, Kind.BYTES):
+            a, heaps[f] = _heap(rng, n, str_len[0], str_len[1], k == Kind.STRING)
+        else:
+            raise ValueError(k)
+        cols.append(as_bytes(a, n))
+    return cols, heaps
+
+
+def flat16(n: int, seed: int = SEED):
+    return gen_columns(FLAT16, n, seed)
