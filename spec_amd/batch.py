@@ -176,4 +176,6 @@ def encode_flat(schema: Schema, cols, heaps: dict, n: int | None = None, cuda_st
     out = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
     ends = torch.empty(n, dtype=torch.int64, device=dev)
     enc.encode_into(cols, heaps, out, ends, cuda_stream)
+    if int(enc.total.item()) != total:  # heap-range check failed in the full pass
+        raise _lib.SpecError(-1, "spec_encode_flat: encoder error (span outside its heap)")
     return out[:total], ends

@@ -162,6 +162,7 @@ int spec_encode_flat(const spec_schema *schema, const void *const *columns,
             a.heap_lens[f] = heap_lens[f];
         }
     }
+    a.check_heaps = 1;
     a.out = out;
     a.out_cap = out_cap;
     a.ends = ends;

@@ -346,6 +346,17 @@ __global__ __launch_bounds__(256) void decode_flat_kernel(DecodeArgs a) {
                     (uint32_t)aligned_lo + c * 1024 + lane * 16, 0, 0, 0);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // the 16-byte chunk holding the stream's last bytes came back zeroed if it
+            // straddles the end (whole-access range check): refill it bytewise
+            const uint64_t tail = a.stream_len & ~15ull;
+            if (tail < a.stream_len && tail >= aligned_lo && tail < span_hi) {
+                if (lane < 16 && tail + lane < a.stream_len)
+                    slab[SLAB_GUARD + (tail - aligned_lo) + lane] =
+                        (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)(tail + lane), 0, 0);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
             if (valid) {
                 LdsSrc s{(lds_u8 *)slab};
                 int rs = SLAB_GUARD + (int)(rec_lo - aligned_lo);
@@ -357,7 +368,7 @@ __global__ __launch_bounds__(256) void decode_flat_kernel(DecodeArgs a) {
         }
     }
     if (valid) {
-        GlobalSrc s{rsrc};
+        GlobalSrc s{rsrc, a.stream_len};
         long long rs = (long long)rec_lo, re = (long long)rec_hi;
         if (re < rs) re = rs;
         decode_record(s, rs, re, r, a, 0);

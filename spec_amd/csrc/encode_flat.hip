@@ -71,7 +71,7 @@ __device__ __forceinline__ uint64_t field_size(const EncodeArgs &a, uint32_t f, 
     case K_STRING:
     case K_BYTES: {
         uint2 sp = ((const uint2 *)col)[r];
-        if ((uint64_t)sp.y > MAX_SIZE || (uint64_t)sp.x + sp.y > a.heap_lens[f]) err = true;
+        if ((uint64_t)sp.y > MAX_SIZE || (a.check_heaps && (uint64_t)sp.x + sp.y > a.heap_lens[f])) err = true;
         return (uint64_t)sp.y + vlen32(sp.y) + 1 + (a.kinds[f] == K_STRING ? 1 : 0);
     }
     }
@@ -249,17 +249,18 @@ struct Emit {
 
 // Copy len bytes of heap[off..] into the emitter (range-checked buffer loads, 4 at a time).
 template <class E>
-__device__ __forceinline__ void emit_heap(E &em, __amdgpu_buffer_rsrc_t hr, uint32_t off, uint32_t len) {
+__device__ __forceinline__ void emit_heap(E &em, __amdgpu_buffer_rsrc_t hr, uint64_t hlen, uint32_t off,
+                                          uint32_t len) {
     uint32_t a = off & ~3u, sh = off & 3;
-    uint32_t cur = __builtin_amdgcn_raw_buffer_load_b32(hr, a, 0, 0);
+    uint32_t cur = buf_ld32(hr, a, hlen);
     uint32_t i = 0;
     for (; i + 4 <= len; i += 4) {
-        uint32_t nxt = __builtin_amdgcn_raw_buffer_load_b32(hr, a + 4 + i, 0, 0);
+        uint32_t nxt = buf_ld32(hr, a + 4 + i, hlen);
         em.put4(__builtin_amdgcn_alignbyte(nxt, cur, sh));
         cur = nxt;
     }
     if (i < len) {
-        uint32_t nxt = __builtin_amdgcn_raw_buffer_load_b32(hr, a + 4 + i, 0, 0);
+        uint32_t nxt = buf_ld32(hr, a + 4 + i, hlen);
         uint32_t w = __builtin_amdgcn_alignbyte(nxt, cur, sh);
         for (; i < len; i++) {
             em.put1(w & 0xff);
@@ -319,7 +320,7 @@ __device__ __forceinline__ void emit_record(const EncodeArgs &a, const Sink &k, 
             __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(
                 (void *)a.heaps[f], (short)0,
                 (int)(uint32_t)(a.heap_lens[f] > 0xffffffffull ? 0xffffffffull : a.heap_lens[f]), 0x00020000);
-            emit_heap(em, hr, sp.x, sp.y);
+            emit_heap(em, hr, a.heap_lens[f], sp.x, sp.y);
             if (kind == K_STRING) em.put1(0);
             em.rvarint(sp.y);
             em.put1(kind == K_STRING ? T_STRING : T_BYTES);

@@ -68,19 +68,35 @@ struct LdsSrc {
     __device__ __forceinline__ uint32_t d32(int p) const { return *(lds_u32 *)(lds + p); }
 };
 
+// A buffer load that straddles num_records returns 0 for the WHOLE access (not just the
+// bytes past the end), so the last partial word of a buffer is read bytewise.
+__device__ __forceinline__ uint32_t buf_ld32(__amdgpu_buffer_rsrc_t r, uint32_t off, uint64_t len) {
+    if ((uint64_t)off + 4 <= len) return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+    uint32_t w = 0;
+    for (int i = 0; i < 4; i++) w |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, off + i, 0, 0) << (8 * i);
+    return w;
+}
+
 struct GlobalSrc {
     using pos_t = long long;
-    __amdgpu_buffer_rsrc_t rsrc; // range-checked: reads outside [0, stream_len) return 0
+    __amdgpu_buffer_rsrc_t rsrc; // range-checked: reads outside [0, len) return 0
+    uint64_t len;
     __device__ __forceinline__ uint32_t u8(long long p) const {
         return __builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)p, 0, 0);
     }
     __device__ __forceinline__ uint64_t d64(long long p) const {
         // p may be negative near the stream start: wrap to a huge offset => range check => 0
+        if (p >= 0 && (uint64_t)p + 8 > len) {
+            uint64_t v = 0;
+            for (int i = 0; i < 8; i++) v |= (uint64_t)u8(p + i) << (8 * i);
+            return v;
+        }
         auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (uint32_t)p, 0, 0);
         return (uint64_t)v[0] | ((uint64_t)v[1] << 32);
     }
     __device__ __forceinline__ uint32_t d32(long long p) const {
-        return __builtin_amdgcn_raw_buffer_load_b32(rsrc, (uint32_t)p, 0, 0);
+        if (p >= 0) return buf_ld32(rsrc, (uint32_t)p, len);
+        return 0;
     }
 };
 

@@ -34,6 +34,7 @@ struct EncodeArgs {
     const uint8_t *heaps[SPEC_MAX_FIELDS];
     uint64_t heap_lens[SPEC_MAX_FIELDS];
     uint32_t table_big_forced; // 1 if any tag > 255 (IsBigMessage holds for every record)
+    uint32_t check_heaps;      // 1 when heaps/heap_lens are known (full encode, not size-only)
     uint8_t *out;
     uint64_t out_cap;
     uint64_t *ends;
