@@ -108,3 +108,30 @@ def gen_columns(schema: Schema, n: int, seed: int = SEED, str_len=(30, 62)):
 
 def flat16(n: int, seed: int = SEED):
     return gen_columns(FLAT16, n, seed)
+
+
+def nested(n: int, seed: int = SEED, count=(0, 8), name_len=(8, 24), label_len=(4, 12)):
+    """SURVEY.md §8(d) "Nested" (config 4): outer {1 bin128 id, 2 int64 seq, 3 string name,
+    4 list<Item>}, Item {1 int32 key, 2 float64 value, 3 string label}.
+
+    Returns a dict of numpy arrays: id [n,16] u8, seq [n] i64, name [n,2] u32 spans into
+    name_heap, item_begin [n+1] u32 (CSR), key [m] i32, value [m] f64 (finite bits),
+    label [m,2] u32 spans into label_heap."""
+    rng = np.random.default_rng(seed)
+    counts = rng.integers(count[0], count[1] + 1, size=n).astype(np.uint32)
+    item_begin = np.zeros(n + 1, dtype=np.uint32)
+    np.cumsum(counts, out=item_begin[1:])
+    m = int(item_begin[-1])
+    name, name_heap = _heap(rng, n, name_len[0], name_len[1], True)
+    label, label_heap = _heap(rng, m, label_len[0], label_len[1], True)
+    return {
+        "id": rng.integers(0, 256, size=(n, 16), dtype=np.uint8),
+        "seq": _signed(rng, n, 64),
+        "name": name,
+        "name_heap": name_heap,
+        "item_begin": item_begin,
+        "key": _signed(rng, m, 32).astype(np.int32),
+        "value": _finite_bits(rng, m, 64).view(np.float64),
+        "label": label,
+        "label_heap": label_heap,
+    }

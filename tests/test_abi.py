@@ -1,0 +1,64 @@
+"""The C-ABI library (libspec_amd.so) on the CPU: it loads, exports every function
+include/spec_amd.h declares, and validates arguments before touching the GPU.  No compute
+call is made here (no GPU in this container); the parity tests are the -m gpu suite."""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+
+import spec_amd
+from spec_amd import _lib
+
+
+def test_library_loads_and_exports_header():
+    L = spec_amd.lib()
+    syms = _lib.header_symbols()
+    assert len(syms) >= 8
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    assert set(syms) <= exported
+
+
+def test_library_has_gfx950_code_object():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_introspection():
+    L = spec_amd.lib()
+    assert L.spec_abi_version() == 1
+    widths = {1: 1, 2: 1, 3: 2, 4: 4, 5: 8, 6: 2, 7: 4, 8: 8, 9: 4, 10: 8, 11: 8, 12: 16, 13: 32, 14: 8, 15: 8}
+    for k, w in widths.items():
+        assert L.spec_kind_width(k) == w
+    assert L.spec_kind_width(0) == 0 and L.spec_kind_width(99) == 0
+    assert L.spec_strerror(0) == b"ok"
+    assert b"workspace" in L.spec_strerror(-5)
+
+
+def test_argument_validation_without_gpu():
+    L = spec_amd.lib()
+    # NULL schema / bad kind / oversize stream are rejected before any HIP call
+    assert L.spec_decode_flat(None, None, 0, None, 1, None, None, None) == -1
+    bad = _lib.SpecSchema()
+    bad.nfields = 1
+    bad.fields[0].tag = 1
+    bad.fields[0].kind = 42
+    assert L.spec_decode_flat(C.byref(bad), None, 0, None, 1, None, None, None) == -1
+    s = spec_amd.FLAT16.c
+    cols = (C.c_void_p * 16)(*([1] * 16))
+    assert L.spec_decode_flat(C.byref(s), C.c_void_p(1), 1 << 32, C.c_void_p(1), 1, cols, None, None) == -3
+    # n == 0 is a no-op
+    assert L.spec_decode_flat(C.byref(s), None, 0, None, 0, None, None, None) == 0
+    ws = L.spec_encode_flat_workspace_size(1000)
+    assert ws >= 8
+    assert L.spec_encode_flat_size(C.byref(s), cols, 1000, C.c_void_p(1), ws - 1, None, None) == -5
+
+
+def test_schema_limits():
+    import pytest
+
+    with pytest.raises(ValueError):
+        spec_amd.Schema([(i + 1, spec_amd.Kind.INT64) for i in range(65)])
