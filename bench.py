@@ -47,6 +47,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-extras", action="store_true", help="skip encode / end-to-end legs")
     p.add_argument("--verify", action="store_true", help="check a sample against the oracle")
+    p.add_argument("--no-jit", action="store_true", help="generic decode kernel (no schema specialisation)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_decode_flat.json"),
                    help="PMC traffic summary (tools/pmc_summary.py) used for roofline.traffic")
@@ -196,6 +197,9 @@ def main():
     stream_bytes = stream.numel()
     mean_rec = stream_bytes / n
 
+    if args.no_jit:
+        spec_amd.set_jit(False)
+    jit = spec_amd.lib().spec_decode_flat_prepare(FLAT16.c, stream_bytes, n) == 1
     dec = spec_amd.Decoder(FLAT16, stream, ends)
     out_cols, status = dec.cols, dec.status
     elapsed = time_decode(dec, args.steps, args.warmup, dist)
@@ -278,7 +282,7 @@ def main():
             "gb_s": round(total_records * (mean_rec + 8 + COLUMN_BYTES + 1) / elapsed / 1e9, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "decode_flat_kernel", "kernel_ms_avg": round(avg_ms, 5),
+                         "kernel": "spec_decode_flat_jit" if jit else "decode_flat_kernel", "kernel_ms_avg": round(avg_ms, 5),
                          "kernel_ms_median": round(med_ms, 5), "alg_bytes_per_launch": alg_bytes,
                          "read_only_gb_s": round(read_only, 1)},
             "cpu_baseline": cpu,

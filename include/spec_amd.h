@@ -113,6 +113,19 @@ int spec_decode_flat(const spec_schema *schema, const uint8_t *stream_bytes, uin
                      const uint64_t *ends, uint64_t n, void *const *columns, uint8_t *status,
                      void *stream);
 
+/* spec_decode_flat_prepare: compile (once per device, schema and record-size class) the
+ * schema-specialised decode kernel that spec_decode_flat uses when one exists — the
+ * analogue of the reference's generated readers (internal/lang/generator/message.go:97-186).
+ * Optional: spec_decode_flat compiles it on first use.  Returns 1 if a specialised kernel
+ * is ready, 0 if the generic kernel will be used (schema without a fast path, JIT disabled
+ * or unavailable), <0 on an invalid schema.  Results never differ between the two. */
+int spec_decode_flat_prepare(const spec_schema *schema, uint64_t stream_len, uint64_t n);
+/* spec_decode_flat_jit_compile: diagnostic — run only the hiprtc compile of that kernel
+ * (no device needed); returns the code-object size, 0 if the schema has no fast path. */
+long long spec_decode_flat_jit_compile(const spec_schema *schema, uint64_t stream_len, uint64_t n);
+/* spec_set_jit: 0 forces the generic kernel (also: environment SPEC_AMD_JIT=0). */
+void spec_set_jit(int enabled);
+
 /* ---- encode ----
  * spec_encode_flat: for every record i, exactly
  *     w := spec.NewMessageWriterBuffer(buf)             (writer_msg.go:26-31)

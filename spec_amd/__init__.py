@@ -5,11 +5,11 @@ internal/{encode,decode,format,writer,types}): batches of records resident in HB
 decoded into SoA columns / encoded from them by hand-written gfx950 kernels
 (spec_amd/csrc, C ABI in include/spec_amd.h).  See DESIGN.md.
 """
-from ._lib import LIB_PATH, SpecError, header_symbols, lib
+from ._lib import LIB_PATH, SpecError, header_symbols, lib, set_jit
 from .batch import Columns, Decoder, Encoder, alloc_columns, decode_flat, encode_flat
 from .schema import FLAT16, Field, Kind, Schema
 
 __all__ = [
-    "LIB_PATH", "SpecError", "header_symbols", "lib", "Columns", "Decoder", "Encoder", "alloc_columns",
+    "LIB_PATH", "SpecError", "header_symbols", "lib", "set_jit", "Columns", "Decoder", "Encoder", "alloc_columns",
     "decode_flat", "encode_flat", "FLAT16", "Field", "Kind", "Schema",
 ]

@@ -54,6 +54,11 @@ def _declare(L):
     L.spec_last_hip_error.restype = C.c_int
     L.spec_decode_flat.argtypes = [C.POINTER(SpecSchema), vp, C.c_uint64, vp, C.c_uint64,
                                    C.POINTER(vp), vp, vp]
+    L.spec_decode_flat_prepare.argtypes = [C.POINTER(SpecSchema), C.c_uint64, C.c_uint64]
+    L.spec_set_jit.argtypes = [C.c_int]
+    L.spec_set_jit.restype = None
+    L.spec_decode_flat_jit_compile.argtypes = [C.POINTER(SpecSchema), C.c_uint64, C.c_uint64]
+    L.spec_decode_flat_jit_compile.restype = C.c_longlong
     L.spec_encode_flat_workspace_size.restype = C.c_size_t
     L.spec_encode_flat_workspace_size.argtypes = [C.c_uint64]
     L.spec_encode_flat_size.argtypes = [C.POINTER(SpecSchema), C.POINTER(vp), C.c_uint64, vp,
@@ -81,3 +86,8 @@ def header_symbols() -> list[str]:
     src = open(HEADER_PATH).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(spec_[a-z0-9_]+)\s*\(", src)))
+
+
+def set_jit(enabled: bool):
+    """Schema-specialised (hiprtc) decode kernels on/off (off = the precompiled generic kernel)."""
+    lib().spec_set_jit(1 if enabled else 0)

@@ -121,8 +121,26 @@ int spec_decode_flat(const spec_schema *schema, const uint8_t *stream_bytes, uin
         a.cols[f] = columns[f];
     }
     double avg = (double)stream_len / (double)n;
-    if (spec::launch_decode_flat(a, avg, (hipStream_t)stream)) return hip_rc(hipGetLastError());
+    int j = spec::jit_launch_decode_flat(schema, a, avg, (hipStream_t)stream);
+    if (j < 0) return hip_rc(hipGetLastError());
+    if (j == 0 && spec::launch_decode_flat(a, avg, (hipStream_t)stream)) return hip_rc(hipGetLastError());
     return SPEC_OK;
+}
+
+int spec_decode_flat_prepare(const spec_schema *schema, uint64_t stream_len, uint64_t n) {
+    int rc = check_schema(schema);
+    if (rc) return rc;
+    if (n == 0) return 0;
+    return spec::jit_prepare_decode_flat(schema, (double)stream_len / (double)n);
+}
+
+void spec_set_jit(int enabled) { spec::jit_set_enabled(enabled); }
+
+long long spec_decode_flat_jit_compile(const spec_schema *schema, uint64_t stream_len, uint64_t n) {
+    int rc = check_schema(schema);
+    if (rc) return rc;
+    if (n == 0) return 0;
+    return spec::jit_compile_only(schema, (double)stream_len / (double)n);
 }
 
 size_t spec_encode_flat_workspace_size(uint64_t n) {

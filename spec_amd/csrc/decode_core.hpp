@@ -1,0 +1,536 @@
+// decode_core.hpp — device code of the flat-message decoder (gfx950), shared by the
+// precompiled generic kernel (decode_flat.hip) and the schema-specialised kernels that
+// jit.cpp compiles at run time with hiprtc.
+//
+// Replaces, per record, spec.OpenMessageErr (internal/types/msg.go:43-55 ->
+// internal/decode/msg.go:14-99) followed by one typed getter per schema field
+// (internal/types/msg.go:219-475: m.field(tag) = table.Offset(tag) binary search
+// (internal/format/msg.go:227-265) + decode.Decode<Kind>(bytes[:end])).
+//
+// Mapping (MI355X, wave64):
+//   * one wave = 64 consecutive records, one record per lane;
+//   * the wave's contiguous byte span [ends[base-1], ends[base+63]) is staged into the wave's
+//     private LDS slab with LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB per instruction,
+//     range-checked by the buffer descriptor) — one fully coalesced HBM read of the stream;
+//   * each lane parses its record from LDS.  Two code paths:
+//       - the FAST path (schema known at compile time: `Spec` = a generated struct) reads the
+//         whole field table with a few wide LDS reads, checks that it holds exactly the
+//         schema's tags in the order a Writer emits them (then the reference's binary search
+//         provably lands on the same entries), and decodes every field with straight-line,
+//         kind-specialised code the compiler can interleave (ILP across fields);
+//       - the GENERIC path (any table, any record) restates the reference step by step:
+//         trailer, sortedness check, probe at the expected index or exact binary search,
+//         per-kind decode selected at run time.  Records the fast path rejects go here,
+//         so results never depend on which path ran;
+//   * column writes are lane-strided => coalesced per field;
+//   * a wave whose span exceeds its slab parses straight from HBM via range-checked buffer
+//     loads (GlobalSrc, generic path) — correctness never depends on record sizes.
+#pragma once
+
+#include "spec_device.hpp"
+
+namespace spec {
+
+#ifndef SPEC_MAX_FIELDS
+#define SPEC_MAX_FIELDS 64
+#endif
+
+// Passed by value as the kernel argument (lives in the kernarg segment => scalar loads,
+// the per-field loop branches are wave-uniform).
+struct DecodeArgs {
+    const uint8_t *stream;
+    uint64_t stream_len;
+    const uint64_t *ends;
+    uint64_t n;
+    uint8_t *status;
+    uint32_t nfields;
+    uint16_t tags[SPEC_MAX_FIELDS];
+    uint8_t kinds[SPEC_MAX_FIELDS];
+    uint8_t rank[SPEC_MAX_FIELDS]; // index of the field's tag in the sorted table a writer emits
+    void *cols[SPEC_MAX_FIELDS];
+};
+
+constexpr int DEC_WAVES = 4; // waves per 256-thread block
+constexpr int SLAB_GUARD = 16;
+
+// slab bytes per wave for each instantiation (guard + DMA chunks + pad)
+constexpr int SLAB_S = SLAB_GUARD + 11 * 1024 + 16 + 16; // spans <= 11 KiB  (avg rec <~ 150 B)
+constexpr int SLAB_M = SLAB_GUARD + 19 * 1024 + 16 + 16; // spans <= 19 KiB  (avg rec <~ 270 B)
+constexpr int SLAB_L = SLAB_GUARD + 35 * 1024 + 16 + 16; // spans <= 35 KiB  (avg rec <~ 500 B)
+
+// ---- message table lookup --------------------------------------------------------------
+
+// exact reference binary search (offset_small/offset_big), returns end offset or -1
+template <class Src>
+__device__ __noinline__ long long table_search(const Src s, typename Src::pos_t tstart, uint32_t nent,
+                                               bool big, uint32_t tag) {
+    int left = 0, right = (int)nent - 1;
+    while (left <= right) {
+        int mid = (int)((unsigned)(left + right) >> 1);
+        uint32_t cur;
+        typename Src::pos_t p;
+        if (big) {
+            p = tstart + (typename Src::pos_t)mid * 6;
+            cur = (s.u8(p) << 8) | s.u8(p + 1);
+        } else {
+            p = tstart + (typename Src::pos_t)mid * 3;
+            cur = s.u8(p);
+        }
+        if (cur < tag) {
+            left = mid + 1;
+        } else if (cur > tag) {
+            right = mid - 1;
+        } else {
+            if (big)
+                return ((long long)s.u8(p + 2) << 24) | (s.u8(p + 3) << 16) | (s.u8(p + 4) << 8) | s.u8(p + 5);
+            return (s.u8(p + 1) << 8) | s.u8(p + 2);
+        }
+    }
+    return -1;
+}
+
+// ---- value decoders: field slice [lo, e), type at e-1 (internal/decode/...) ------------
+
+struct Val {
+    uint64_t v0, v1, v2, v3; // up to 32 bytes of column payload, little-endian
+};
+
+// Decode the value ending at e (field slice [lo, e), flen = e - lo > 0) from its 16-byte
+// tail window t; bin128/bin256 read their leading bytes from s.
+template <uint32_t KIND, class Src>
+__device__ __forceinline__ Val decode_tail_k(const Src &s, const Tail &t, typename Src::pos_t lo,
+                                             typename Src::pos_t e, long long to_stream) {
+    Val out = {0, 0, 0, 0};
+    const long long flen = (long long)(e - lo);
+    uint32_t type = (uint32_t)t.q0 & 0xff;
+    uint64_t R = tail_r(t);
+    uint32_t R2 = tail_r2(t);
+    long long avail = flen - 1; // bytes before the type byte
+    int m;
+    if constexpr (KIND == K_BOOL) { // DecodeBool, byte.go:38-51: true iff type == TypeTrue
+        out.v0 = type == T_TRUE;
+    } else if constexpr (KIND == K_BYTE) { // DecodeByte, byte.go:16-34
+        if (type == T_BYTE && flen >= 2) out.v0 = R & 0xff;
+    } else if constexpr (KIND == K_INT16 || KIND == K_INT32 || KIND == K_INT64) {
+        // DecodeInt16/32/64, int.go:16-135: 32-bit routine for Int16/Int32, 64-bit for Int64
+        long long x;
+        bool ok;
+        if (type == T_INT16 || type == T_INT32) {
+            uint32_t u = (uint32_t)rvarint<5>(R, R2, avail, m);
+            x = unzigzag32(u);
+            ok = m >= 0;
+        } else {
+            x = unzigzag64(rvarint<10>(R, R2, avail, m));
+            ok = type == T_INT64 && m >= 0;
+        }
+        if (KIND == K_INT16) ok = ok && x >= -32768 && x <= 32767;
+        if (KIND == K_INT32) ok = ok && (type != T_INT64 || (x >= INT32_MIN && x <= INT32_MAX));
+        out.v0 = ok ? (uint64_t)x : 0;
+        if (KIND == K_INT16) out.v0 &= 0xffff;
+        if (KIND == K_INT32) out.v0 &= 0xffffffffu;
+    } else if constexpr (KIND == K_UINT16 || KIND == K_UINT32 || KIND == K_UINT64) {
+        // DecodeUint16/32/64, uint.go:16-125
+        uint64_t x;
+        bool ok;
+        if (type == T_UINT16 || type == T_UINT32) {
+            x = rvarint<5>(R, R2, avail, m);
+            ok = m >= 0;
+        } else {
+            x = rvarint<10>(R, R2, avail, m);
+            ok = type == T_UINT64 && m >= 0;
+        }
+        if (KIND == K_UINT16) ok = ok && x <= 0xffffull;
+        if (KIND == K_UINT32) ok = ok && x <= 0xffffffffull;
+        out.v0 = ok ? x : 0;
+    } else if constexpr (KIND == K_FLOAT32) { // DecodeFloat32, float.go:15-32 (via float64 + range check)
+        if (type == T_FLOAT32) {
+            if (flen >= 5) {
+                uint32_t b = (uint32_t)(R & 0xffffffffu);
+                uint32_t ex = (b >> 23) & 0xff;
+                bool inf = ex == 0xff && (b & 0x7fffff) == 0; // +-Inf fails the +-MaxFloat32 check
+                if (ex == 0xff) b |= 0x00400000u;              // NaN: quieted by the float64 round trip
+                out.v0 = inf ? 0 : b;
+            }
+        } else if (type == T_FLOAT64) {
+            if (flen >= 9) {
+                uint64_t d = R;
+                uint32_t ex = (uint32_t)(d >> 52) & 0x7ff;
+                bool nan = ex == 0x7ff && (d & 0xfffffffffffffull);
+                // |d| > MaxFloat32 (0x47EFFFFFE0000000) => overflow error => 0
+                bool over = !nan && (d & 0x7fffffffffffffffull) > 0x47EFFFFFE0000000ull;
+                out.v0 = over ? 0 : f64_to_f32_bits(d);
+            }
+        }
+    } else if constexpr (KIND == K_FLOAT64) { // DecodeFloat64, float.go:34-78
+        if (type == T_FLOAT32) {
+            if (flen >= 5) out.v0 = f32_to_f64_bits((uint32_t)(R & 0xffffffffu));
+        } else if (type == T_FLOAT64) {
+            if (flen >= 9) out.v0 = R;
+        }
+    } else if constexpr (KIND == K_BIN64) { // DecodeBin64, bin.go:15-44: raw 8 bytes before the type byte
+        if (type == T_BIN64 && flen >= 9) out.v0 = __builtin_bswap64(R);
+    } else if constexpr (KIND == K_BIN128) {
+        if (type == T_BIN128 && flen >= 17) {
+            out.v0 = load_le64(s, e - 17);
+            out.v1 = __builtin_bswap64(R);
+        }
+    } else if constexpr (KIND == K_BIN256) {
+        if (type == T_BIN256 && flen >= 33) {
+            out.v0 = load_le64(s, e - 33);
+            out.v1 = load_le64(s, e - 25);
+            out.v2 = load_le64(s, e - 17);
+            out.v3 = __builtin_bswap64(R);
+        }
+    } else if constexpr (KIND == K_STRING || KIND == K_BYTES) {
+        // DecodeString (string.go:15-70) / DecodeBytes (bytes.go:14-58)
+        constexpr bool str = KIND == K_STRING;
+        if (type == (str ? T_STRING : T_BYTES)) {
+            uint32_t len = (uint32_t)rvarint<5>(R, R2, avail, m);
+            long long end = (long long)(e - 1) - m - (str ? 1 : 0); // skip the NUL for strings
+            long long off = end - (long long)len;
+            bool ok = m >= 0 && end >= (long long)lo && off >= (long long)lo && len;
+            if (ok) out.v0 = (uint64_t)(uint32_t)(off + to_stream) | ((uint64_t)len << 32);
+        }
+    }
+    return out;
+}
+
+template <uint32_t KIND, class Src>
+__device__ __forceinline__ Val decode_value_k(const Src &s, typename Src::pos_t lo, typename Src::pos_t e,
+                                              long long to_stream) {
+    if ((long long)(e - lo) <= 0) return Val{0, 0, 0, 0}; // empty => zero value, no error
+    return decode_tail_k<KIND>(s, load_tail(s, e), lo, e, to_stream);
+}
+
+template <uint32_t KIND>
+__device__ __forceinline__ void store_value_k(void *colp, uint64_t r, const Val &v) {
+    uint8_t *col = (uint8_t *)colp;
+    if constexpr (KIND == K_BOOL || KIND == K_BYTE) {
+        col[r] = (uint8_t)v.v0;
+    } else if constexpr (KIND == K_INT16 || KIND == K_UINT16) {
+        ((uint16_t *)col)[r] = (uint16_t)v.v0;
+    } else if constexpr (KIND == K_INT32 || KIND == K_UINT32 || KIND == K_FLOAT32) {
+        ((uint32_t *)col)[r] = (uint32_t)v.v0;
+    } else if constexpr (KIND == K_BIN128) {
+        ((ulonglong2 *)col)[r] = make_ulonglong2(v.v0, v.v1);
+    } else if constexpr (KIND == K_BIN256) {
+        ulonglong2 *c = (ulonglong2 *)col + 2 * r;
+        c[0] = make_ulonglong2(v.v0, v.v1);
+        c[1] = make_ulonglong2(v.v2, v.v3);
+    } else {
+        ((uint64_t *)col)[r] = v.v0;
+    }
+}
+
+// run-time kind dispatch for the generic path (wave-uniform switches around ONE shared
+// tail-window load, so the generic kernel stays compact)
+template <class Src>
+__device__ __forceinline__ void decode_store(const Src &s, uint32_t kind, typename Src::pos_t lo, long long end,
+                                             long long to_stream, void *col, uint64_t r) {
+    Val v = {0, 0, 0, 0};
+    if (end > 0) {
+        const typename Src::pos_t e = lo + (typename Src::pos_t)end;
+        const Tail t = load_tail(s, e);
+#define SPEC_CASE(K) \
+    case K: v = decode_tail_k<K>(s, t, lo, e, to_stream); break;
+        switch (kind) {
+            SPEC_CASE(K_BOOL)
+            SPEC_CASE(K_BYTE)
+            SPEC_CASE(K_INT16)
+            SPEC_CASE(K_INT32)
+            SPEC_CASE(K_INT64)
+            SPEC_CASE(K_UINT16)
+            SPEC_CASE(K_UINT32)
+            SPEC_CASE(K_UINT64)
+            SPEC_CASE(K_FLOAT32)
+            SPEC_CASE(K_FLOAT64)
+            SPEC_CASE(K_BIN64)
+            SPEC_CASE(K_BIN128)
+            SPEC_CASE(K_BIN256)
+            SPEC_CASE(K_STRING)
+            SPEC_CASE(K_BYTES)
+        }
+#undef SPEC_CASE
+    }
+    uint8_t *c = (uint8_t *)col;
+    switch (kind) {
+    case K_BOOL:
+    case K_BYTE: c[r] = (uint8_t)v.v0; break;
+    case K_INT16:
+    case K_UINT16: ((uint16_t *)c)[r] = (uint16_t)v.v0; break;
+    case K_INT32:
+    case K_UINT32:
+    case K_FLOAT32: ((uint32_t *)c)[r] = (uint32_t)v.v0; break;
+    case K_BIN128: store_value_k<K_BIN128>(col, r, v); break;
+    case K_BIN256: store_value_k<K_BIN256>(col, r, v); break;
+    default: ((uint64_t *)c)[r] = v.v0; break;
+    }
+}
+
+// ---- record trailer: DecodeMessageTable, internal/decode/msg.go:14-99 -------------------
+
+struct Trailer {
+    uint32_t st;     // spec_status
+    bool big;
+    long long tstart, dstart; // source positions
+    uint32_t dsize, tsize;
+};
+
+template <class Src>
+__device__ __forceinline__ Trailer parse_trailer(const Src &s, typename Src::pos_t rs, typename Src::pos_t re) {
+    Trailer tr = {ST_OK, false, 0, 0, 0, 0};
+    long long len = (long long)(re - rs);
+    Tail t = load_tail(s, re);
+    uint32_t type = (uint32_t)t.q0 & 0xff;
+    if (type != T_MESSAGE && type != T_BIG_MESSAGE) {
+        tr.st = ST_INVALID_TYPE;
+        return tr;
+    }
+    tr.big = type == T_BIG_MESSAGE;
+    uint64_t R = tail_r(t);
+    uint32_t R2 = tail_r2(t);
+    int m1, m2;
+    uint32_t tsz = (uint32_t)rvarint<5>(R, R2, len - 1, m1);
+    if (m1 < 0) {
+        tr.st = ST_INVALID_TABLE_SIZE;
+        return tr;
+    }
+    // the data-size varint ends m1 bytes further down: shift the window
+    uint64_t Rs = (R >> (8 * m1)) | ((uint64_t)R2 << (64 - 8 * m1));
+    uint32_t R2s = m1 >= 2 ? 0u : (R2 >> (8 * m1));
+    uint32_t dsz = (uint32_t)rvarint<5>(Rs, R2s, len - 1 - m1, m2);
+    if (m2 < 0) {
+        tr.st = ST_INVALID_DATA_SIZE;
+        return tr;
+    }
+    long long tend = (long long)(re - 1) - m1 - m2;
+    long long ts = tend - (long long)tsz;
+    if (ts < (long long)rs || tsz % (tr.big ? 6u : 3u) != 0) {
+        tr.st = ST_INVALID_TABLE;
+        return tr;
+    }
+    if (ts - (long long)dsz < (long long)rs) {
+        tr.st = ST_INVALID_DATA;
+        return tr;
+    }
+    tr.tstart = ts;
+    tr.dstart = ts - (long long)dsz;
+    tr.dsize = dsz;
+    tr.tsize = tsz;
+    return tr;
+}
+
+// ---- generic path: any record, run-time schema -----------------------------------------
+
+// Parse record r occupying [rs, re) of the source; to_stream converts a source position to a
+// stream offset (string/bytes spans).
+template <class Src>
+__device__ __forceinline__ void decode_record_generic(const Src &s, typename Src::pos_t rs, typename Src::pos_t re,
+                                                   uint64_t r, const DecodeArgs &a, long long to_stream) {
+    using pos_t = typename Src::pos_t;
+    bool ok = false, sorted = true;
+    Trailer tr = {ST_OK, false, 0, 0, 0, 0};
+    uint32_t nent = 0;
+    if (re > rs) {
+        tr = parse_trailer(s, rs, re);
+        ok = tr.st == ST_OK;
+        nent = tr.tsize / (tr.big ? 6u : 3u);
+    }
+    const pos_t tstart = (pos_t)tr.tstart, dstart = (pos_t)tr.dstart;
+    if (ok) {
+        // strictly increasing tags => a probe at the expected index is what binary search finds
+        uint32_t prev = 0;
+        for (uint32_t i = 0; i < nent; i++) {
+            pos_t p = tstart + (pos_t)i * (tr.big ? 6 : 3);
+            uint32_t tg = tr.big ? ((s.u8(p) << 8) | s.u8(p + 1)) : s.u8(p);
+            if (i > 0 && tg <= prev) sorted = false;
+            prev = tg;
+        }
+    }
+    if (a.status) a.status[r] = (uint8_t)tr.st;
+
+    for (uint32_t f = 0; f < a.nfields; f++) {
+        uint32_t tag = a.tags[f];
+        long long end = -1;
+        if (ok) {
+            uint32_t k = a.rank[f];
+            bool hit = false;
+            if (sorted && k < nent) {
+                if (tr.big) {
+                    pos_t p = tstart + (pos_t)k * 6;
+                    uint32_t tg = (s.u8(p) << 8) | s.u8(p + 1);
+                    if (tg == tag) {
+                        end = ((long long)s.u8(p + 2) << 24) | (s.u8(p + 3) << 16) | (s.u8(p + 4) << 8) | s.u8(p + 5);
+                        hit = true;
+                    }
+                } else {
+                    pos_t p = tstart + (pos_t)k * 3;
+                    if (s.u8(p) == tag) {
+                        end = (s.u8(p + 1) << 8) | s.u8(p + 2);
+                        hit = true;
+                    }
+                }
+            }
+            if (!hit) end = table_search(s, tstart, nent, tr.big, tag);
+            if (end > (long long)tr.dsize) end = -1; // m.field: end > dataSize => nil
+        }
+        decode_store(s, a.kinds[f], dstart, end, to_stream, a.cols[f], r);
+    }
+}
+
+// ---- fast path: compile-time schema ------------------------------------------------------
+
+// A run-time schema has no fast path.
+struct RuntimeSpec {
+    static constexpr int N = 0;
+};
+
+// Spec (generated by jit.cpp) provides:
+//   N              number of fields (1..FAST_MAX_FIELDS)
+//   kind[f], rank[f]  per schema field
+//   stag[k]        k-th tag of the table a Writer emits (strictly increasing, all <= 255)
+constexpr int FAST_MAX_FIELDS = 24;
+
+// Unrolled at compile time: field F's kind and table index are constants, so every
+// field is straight-line code and independent fields interleave.
+template <class Spec, int F>
+struct FieldLoop {
+    static __device__ __forceinline__ void run(const LdsSrc &s, int ds, const uint32_t *ends, uint32_t dsize,
+                                               long long to_stream, const DecodeArgs &a, uint64_t r) {
+        if constexpr (F < Spec::N) {
+            constexpr uint32_t K = Spec::kind[F];
+            constexpr int k = Spec::rank[F];
+            const uint32_t end = ends[k];
+            const int e = end <= dsize ? ds + (int)end : ds; // end > dataSize => nil => zero
+            store_value_k<K>(a.cols[F], r, decode_value_k<K>(s, ds, e, to_stream));
+            FieldLoop<Spec, F + 1>::run(s, ds, ends, dsize, to_stream, a, r);
+        }
+    }
+};
+
+// LdsSrc only.  Returns false (nothing written) when the record needs the generic path.
+template <class Spec>
+__device__ __forceinline__ bool decode_record_fast(const LdsSrc &s, int rs, int re, uint64_t r,
+                                                   const DecodeArgs &a, long long to_stream) {
+    constexpr int N = Spec::N;
+    if (re <= rs) return false;
+    Trailer tr = parse_trailer(s, rs, re);
+    if (tr.st != ST_OK || tr.big || tr.tsize != 3u * N) return false;
+    const int ts = (int)tr.tstart;
+    // the table's 3N bytes, re-aligned into dwords: w[i] = bytes [ts+4i, ts+4i+4)
+    constexpr int NW = (3 * N + 3) / 4;
+    constexpr int NQ = (3 * N + 7) / 8 + 1; // aligned qwords covering [ts & ~7, ts + 3N)
+    const int base = ts & ~7;
+    const uint32_t sh = (uint32_t)(ts & 7);
+    uint32_t d[2 * NQ + 1];
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+        uint64_t x = s.d64(base + 8 * q);
+        d[2 * q] = (uint32_t)x;
+        d[2 * q + 1] = (uint32_t)(x >> 32);
+    }
+    d[2 * NQ] = 0;
+    const bool hi = sh >= 4;
+    const uint32_t b = sh & 3;
+    uint32_t w[NW];
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        uint32_t a0 = hi ? d[i + 1] : d[i];
+        uint32_t a1 = hi ? d[i + 2] : d[i + 1];
+        w[i] = __builtin_amdgcn_alignbyte(a1, a0, b);
+    }
+    // entry k = bytes 3k (tag), 3k+1..3k+2 (end, big-endian)
+    auto byte_at = [&](int j) -> uint32_t { return (w[j >> 2] >> (8 * (j & 3))) & 0xff; };
+    bool hit = true;
+    uint32_t ends[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        hit = hit && byte_at(3 * k) == Spec::stag[k];
+        ends[k] = (byte_at(3 * k + 1) << 8) | byte_at(3 * k + 2);
+    }
+    if (!hit) return false;
+    if (a.status) a.status[r] = ST_OK;
+    FieldLoop<Spec, 0>::run(s, (int)tr.dstart, ends, tr.dsize, to_stream, a, r);
+    return true;
+}
+
+// ---- kernel body -------------------------------------------------------------------------
+
+template <int SLAB, class Spec>
+__device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const uint64_t base = ((uint64_t)blockIdx.x * DEC_WAVES + wave) * 64;
+    if (base >= a.n) return;
+    const uint64_t r = base + lane;
+    const bool valid = r < a.n;
+    const uint64_t last = (a.n - base) < 64 ? a.n - 1 : base + 63;
+
+    uint64_t rec_hi = valid ? a.ends[r] : 0;
+    uint64_t prev = __shfl_up(rec_hi, 1);
+    if (lane == 0) prev = base ? a.ends[base - 1] : 0;
+    const uint64_t rec_lo = prev;
+    const uint64_t span_lo = __builtin_amdgcn_readfirstlane((uint32_t)rec_lo) |
+                             ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(rec_lo >> 32)) << 32);
+    const uint64_t span_hi_v = __shfl(rec_hi, (int)(last - base));
+    const uint64_t span_hi = __builtin_amdgcn_readfirstlane((uint32_t)span_hi_v) |
+                             ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(span_hi_v >> 32)) << 32);
+
+    __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
+
+    const uint64_t aligned_lo = span_lo & ~15ull;
+    if constexpr (SLAB > 0) {
+        const uint64_t bytes = span_hi - aligned_lo;
+        const uint64_t chunks = (bytes + 1023) >> 10;
+        if (span_hi >= span_lo && SLAB_GUARD + chunks * 1024 + 16 <= (uint64_t)SLAB) {
+            uint8_t *slab = smem + wave * SLAB;
+            for (uint32_t c = 0; c < (uint32_t)chunks; c++) {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rsrc, (__attribute__((address_space(3))) void *)(slab + SLAB_GUARD + c * 1024), 16,
+                    (uint32_t)aligned_lo + c * 1024 + lane * 16, 0, 0, 0);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // the 16-byte chunk holding the stream's last bytes came back zeroed if it
+            // straddles the end (whole-access range check): refill it bytewise
+            const uint64_t tail = a.stream_len & ~15ull;
+            if (tail < a.stream_len && tail >= aligned_lo && tail < span_hi) {
+                if (lane < 16 && tail + lane < a.stream_len)
+                    slab[SLAB_GUARD + (tail - aligned_lo) + lane] =
+                        (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)(tail + lane), 0, 0);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            if (valid) {
+                LdsSrc s{(lds_u8 *)slab};
+                int rs = SLAB_GUARD + (int)(rec_lo - aligned_lo);
+                int re = SLAB_GUARD + (int)(rec_hi - aligned_lo);
+                if (rec_hi < rec_lo) re = rs; // malformed ends: treat as empty
+                const long long to_stream = (long long)aligned_lo - SLAB_GUARD;
+                bool done = false;
+                if constexpr (Spec::N > 0) done = decode_record_fast<Spec>(s, rs, re, r, a, to_stream);
+                if (!done) decode_record_generic(s, rs, re, r, a, to_stream);
+            }
+            return;
+        }
+    }
+    if (valid) {
+        GlobalSrc s{rsrc, a.stream_len};
+        long long rs = (long long)rec_lo, re = (long long)rec_hi;
+        if (re < rs) re = rs;
+        decode_record_generic(s, rs, re, r, a, 0);
+    }
+}
+
+// slab choice shared by the launchers (host) — average record size * 64 * margin
+__host__ __device__ inline int decode_slab_class(double avg_record) {
+    double span = avg_record * 64.0 * 1.08 + 64.0;
+    if (span <= 11 * 1024) return 0;
+    if (span <= 19 * 1024) return 1;
+    if (span <= 35 * 1024) return 2;
+    return 3;
+}
+
+} // namespace spec

@@ -1,0 +1,206 @@
+// jit.cpp — schema-specialised decode kernels, compiled at run time with hiprtc.
+//
+// The reference decodes through GENERATED code: `spec generate` emits one Go reader per
+// schema whose getters call Message.<Kind>(tag) with constant tags
+// (internal/lang/generator/message.go:97-186).  This is the MI355X analogue: the first time
+// a schema is decoded, decode_core.hpp's kernel body is instantiated for that schema (field
+// count, kinds, tags and table order as compile-time constants) and compiled for gfx950
+// with hiprtc; the code object is loaded with hipModuleLoadData and cached per (device,
+// schema, LDS slab class).  The generated kernel keeps the generic path for every record
+// its fast path rejects, so results are identical to the precompiled kernel's.
+//
+// Schemas without a fast path (more than FAST_MAX_FIELDS fields, repeated tags, tags >
+// 255) and SPEC_AMD_JIT=0 use the precompiled generic kernel (decode_flat.hip).
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <unordered_map>
+#include <vector>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "spec_internal.hpp"
+
+namespace {
+
+// the device sources, embedded at build time (Makefile -> build/rtc_sources.inc)
+#include "build/rtc_sources.inc"
+
+struct Entry {
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+    bool failed = false;
+};
+
+std::mutex g_mu;
+std::unordered_map<std::string, Entry> g_cache;
+int g_enabled = -1; // -1: read SPEC_AMD_JIT on first use
+
+bool enabled() {
+    if (g_enabled < 0) {
+        const char *e = getenv("SPEC_AMD_JIT");
+        g_enabled = (e && e[0] == '0') ? 0 : 1;
+    }
+    return g_enabled == 1;
+}
+
+bool debug() {
+    const char *e = getenv("SPEC_AMD_DEBUG");
+    return e && e[0] && e[0] != '0';
+}
+
+// Table order a Writer produces (insertion sort, internal/writer/stack_msg.go:37-61).
+void writer_order(const spec_schema *s, uint8_t *order, uint16_t *sorted) {
+    for (uint32_t f = 0; f < s->nfields; f++) {
+        sorted[f] = s->fields[f].tag;
+        order[f] = (uint8_t)f;
+        for (int i = (int)f; i > 0 && sorted[i - 1] >= sorted[i]; i--) {
+            std::swap(sorted[i - 1], sorted[i]);
+            std::swap(order[i - 1], order[i]);
+        }
+    }
+}
+
+// A fast path exists when the Writer's table is strictly increasing in tags <= 255.
+bool has_fast_path(const spec_schema *s) {
+    if (s->nfields == 0 || s->nfields > (uint32_t)spec::FAST_MAX_FIELDS) return false;
+    uint8_t order[SPEC_MAX_FIELDS];
+    uint16_t sorted[SPEC_MAX_FIELDS];
+    writer_order(s, order, sorted);
+    for (uint32_t k = 0; k < s->nfields; k++) {
+        if (sorted[k] > 255 || sorted[k] == 0) return false;
+        if (k && sorted[k] <= sorted[k - 1]) return false;
+    }
+    return true;
+}
+
+const int kSlab[3] = {spec::SLAB_S, spec::SLAB_M, spec::SLAB_L};
+
+std::string key_of(const spec_schema *s, int slab_class, int device) {
+    std::ostringstream k;
+    k << device << ':' << slab_class << ':';
+    for (uint32_t f = 0; f < s->nfields; f++) k << s->fields[f].tag << '/' << (int)s->fields[f].kind << ',';
+    return k.str();
+}
+
+std::string generate(const spec_schema *s, int slab) {
+    uint8_t order[SPEC_MAX_FIELDS];
+    uint16_t sorted[SPEC_MAX_FIELDS];
+    writer_order(s, order, sorted);
+    uint8_t rank[SPEC_MAX_FIELDS];
+    for (uint32_t k = 0; k < s->nfields; k++) rank[order[k]] = (uint8_t)k;
+    std::ostringstream o;
+    o << "#include \"decode_core.hpp\"\n"
+      << "struct GenSpec {\n  static constexpr int N = " << s->nfields << ";\n"
+      << "  static constexpr uint32_t kind[N] = {";
+    for (uint32_t f = 0; f < s->nfields; f++) o << (f ? "," : "") << (int)s->fields[f].kind;
+    o << "};\n  static constexpr int rank[N] = {";
+    for (uint32_t f = 0; f < s->nfields; f++) o << (f ? "," : "") << (int)rank[f];
+    o << "};\n  static constexpr uint32_t stag[N] = {";
+    for (uint32_t k = 0; k < s->nfields; k++) o << (k ? "," : "") << sorted[k];
+    o << "};\n};\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void spec_decode_flat_jit(spec::DecodeArgs a) {\n"
+      << "  spec::decode_flat_body<" << slab << ", GenSpec>(a);\n}\n";
+    return o.str();
+}
+
+// hiprtc compile only; returns the code object (empty on failure)
+std::vector<char> compile_code(const spec_schema *s, int slab) {
+    std::string src = generate(s, slab);
+    const char *hdr_src[2] = {kSpecDeviceHpp, kDecodeCoreHpp};
+    const char *hdr_name[2] = {"spec_device.hpp", "decode_core.hpp"};
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "spec_decode_flat_jit.hip", 2, hdr_src, hdr_name) != HIPRTC_SUCCESS)
+        return {};
+    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+    if (rc != HIPRTC_SUCCESS || debug()) {
+        size_t ls = 0;
+        hiprtcGetProgramLogSize(prog, &ls);
+        if (ls > 1) {
+            std::vector<char> log(ls + 1, 0);
+            hiprtcGetProgramLog(prog, log.data());
+            fprintf(stderr, "spec_amd jit: %s\n", log.data());
+        }
+    }
+    if (rc != HIPRTC_SUCCESS) {
+        hiprtcDestroyProgram(&prog);
+        return {};
+    }
+    size_t cs = 0;
+    hiprtcGetCodeSize(prog, &cs);
+    std::vector<char> code(cs);
+    hiprtcGetCode(prog, code.data());
+    hiprtcDestroyProgram(&prog);
+    return code;
+}
+
+Entry compile(const spec_schema *s, int slab) {
+    Entry e;
+    std::vector<char> code = compile_code(s, slab);
+    if (code.empty()) {
+        e.failed = true;
+        return e;
+    }
+    if (hipModuleLoadData(&e.mod, code.data()) != hipSuccess ||
+        hipModuleGetFunction(&e.fn, e.mod, "spec_decode_flat_jit") != hipSuccess) {
+        (void)hipGetLastError();
+        e.failed = true;
+        e.fn = nullptr;
+    }
+    return e;
+}
+
+// nullptr => use the generic kernel
+hipFunction_t lookup(const spec_schema *s, int slab_class) {
+    if (slab_class > 2 || !enabled() || !has_fast_path(s)) return nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::string k = key_of(s, slab_class, dev);
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_cache.find(k);
+    if (it == g_cache.end()) {
+        Entry e = compile(s, kSlab[slab_class]);
+        if (e.failed && debug()) fprintf(stderr, "spec_amd jit: compile/load failed, generic kernel in use\n");
+        it = g_cache.emplace(k, e).first;
+    }
+    return it->second.failed ? nullptr : it->second.fn;
+}
+
+} // namespace
+
+namespace spec {
+
+void jit_set_enabled(int on) { g_enabled = on ? 1 : 0; }
+
+long long jit_compile_only(const spec_schema *schema, double avg_record) {
+    const int cls = decode_slab_class(avg_record);
+    if (cls > 2 || !has_fast_path(schema)) return 0;
+    return (long long)compile_code(schema, kSlab[cls]).size();
+}
+
+int jit_prepare_decode_flat(const spec_schema *schema, double avg_record) {
+    return lookup(schema, decode_slab_class(avg_record)) ? 1 : 0;
+}
+
+int jit_launch_decode_flat(const spec_schema *schema, const DecodeArgs &a, double avg_record, hipStream_t stream) {
+    const int cls = decode_slab_class(avg_record);
+    hipFunction_t fn = lookup(schema, cls);
+    if (!fn) return 0;
+    uint64_t waves = (a.n + 63) / 64;
+    uint64_t blocks = (waves + DEC_WAVES - 1) / DEC_WAVES;
+    if (blocks == 0) return 1;
+    DecodeArgs args = a;
+    size_t size = sizeof(args);
+    void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
+                     HIP_LAUNCH_PARAM_END};
+    hipError_t e = hipModuleLaunchKernel(fn, (unsigned)blocks, 1, 1, 256, 1, 1, DEC_WAVES * kSlab[cls], stream,
+                                         nullptr, extra);
+    return e == hipSuccess ? 1 : -1;
+}
+
+} // namespace spec

@@ -15,8 +15,21 @@
 //     independently of the GPU's FP mode registers.
 #pragma once
 
+#ifdef __HIPCC_RTC__
+// compiled at run time by hiprtc (schema-specialised kernels, jit.cpp): no system headers
+typedef __hip_internal::uint8_t uint8_t;
+typedef __hip_internal::uint16_t uint16_t;
+typedef __hip_internal::uint32_t uint32_t;
+typedef __hip_internal::uint64_t uint64_t;
+typedef __hip_internal::int16_t int16_t;
+typedef __hip_internal::int32_t int32_t;
+typedef __hip_internal::int64_t int64_t;
+#define INT32_MIN (-2147483647 - 1)
+#define INT32_MAX 2147483647
+#else
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 namespace spec {
 

@@ -6,24 +6,12 @@
 #include <stdint.h>
 
 #include "../../include/spec_amd.h"
+#include "decode_core.hpp"
 
 namespace spec {
 
 // Passed by value as the kernel argument (lives in the kernarg segment => scalar loads,
 // the per-field loop branches are wave-uniform).
-struct DecodeArgs {
-    const uint8_t *stream;
-    uint64_t stream_len;
-    const uint64_t *ends;
-    uint64_t n;
-    uint8_t *status;
-    uint32_t nfields;
-    uint16_t tags[SPEC_MAX_FIELDS];
-    uint8_t kinds[SPEC_MAX_FIELDS];
-    uint8_t rank[SPEC_MAX_FIELDS]; // index of the field's tag in the sorted table a writer emits
-    void *cols[SPEC_MAX_FIELDS];
-};
-
 struct EncodeArgs {
     uint64_t n;
     uint32_t nfields;
@@ -44,6 +32,12 @@ struct EncodeArgs {
 };
 
 int launch_decode_flat(const DecodeArgs &a, double avg_record, hipStream_t stream);
+// jit.cpp: schema-specialised decode kernel (hiprtc); returns 1 if launched, 0 if the caller
+// should launch the generic kernel, <0 on a HIP error.
+int jit_launch_decode_flat(const spec_schema *schema, const DecodeArgs &a, double avg_record, hipStream_t stream);
+int jit_prepare_decode_flat(const spec_schema *schema, double avg_record);
+void jit_set_enabled(int on);
+long long jit_compile_only(const spec_schema *schema, double avg_record);
 int launch_encode_size(const EncodeArgs &a, hipStream_t stream);
 int launch_encode_write(const EncodeArgs &a, hipStream_t stream);
 

@@ -62,3 +62,16 @@ def test_schema_limits():
 
     with pytest.raises(ValueError):
         spec_amd.Schema([(i + 1, spec_amd.Kind.INT64) for i in range(65)])
+
+
+def test_jit_source_compiles_for_gfx950():
+    """The schema-specialised decode kernel (jit.cpp) compiles with hiprtc for gfx950 here
+    (compile only; loading needs the GPU)."""
+    L = spec_amd.lib()
+    s = spec_amd.FLAT16.c
+    assert L.spec_decode_flat_jit_compile(C.byref(s), 256 << 20, 1 << 20) > 1000
+    # no fast path: repeated tags / tags > 255 / too many fields => generic kernel, nothing compiled
+    dup = spec_amd.Schema([(5, spec_amd.Kind.INT32), (5, spec_amd.Kind.INT64)])
+    assert L.spec_decode_flat_jit_compile(C.byref(dup.c), 1000, 10) == 0
+    big = spec_amd.Schema([(300, spec_amd.Kind.INT32)])
+    assert L.spec_decode_flat_jit_compile(C.byref(big.c), 1000, 10) == 0

@@ -39,8 +39,16 @@ def write_record(fields):
     return data
 
 
+@pytest.fixture(params=["jit", "generic"])
+def kernel(request):
+    """Run a test with the schema-specialised kernels (hiprtc) and with the generic kernel."""
+    spec_amd.set_jit(request.param == "jit")
+    yield request.param
+    spec_amd.set_jit(True)
+
+
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 4096 + 17])
-def test_flat16_decode_parity(dev, n):
+def test_flat16_decode_parity(dev, kernel, n):
     cols, heaps = workload.flat16(n, seed=n)
     stream, ends = oracle_encode(FLAT16, cols, heaps, n)
     check_decode(dev, FLAT16, stream, ends, f"flat16 n={n}")
@@ -52,7 +60,7 @@ def test_flat16_encode_bitexact(dev, n):
     check_encode(dev, FLAT16, cols, heaps, n, f"flat16 n={n}")
 
 
-def test_flat16_full_size_parity(dev):
+def test_flat16_full_size_parity(dev, kernel):
     """BASELINE configs 2+3 at full size: 1M Flat16 records, encode bit-exact and decode
     identical to the oracle."""
     n = 1 << 20
@@ -123,7 +131,7 @@ def _extreme_values(kind, rng, m):
 
 
 @pytest.mark.parametrize("shift", range(1, len(ALL_KINDS)))
-def test_cross_kind_decode(dev, shift):
+def test_cross_kind_decode(dev, kernel, shift):
     """Values written as kind A, read back with the getter of kind B: the cross-width and
     range-check rules of internal/decode/{int,uint,float}.go, type mismatches => zero."""
     rng = np.random.default_rng(shift)
@@ -137,7 +145,7 @@ def test_cross_kind_decode(dev, shift):
     check_decode(dev, read, stream, ends, f"cross-kind shift={shift}")
 
 
-def test_same_kind_extremes(dev):
+def test_same_kind_extremes(dev, kernel):
     rng = np.random.default_rng(5)
     m = 80
     per_kind = {k: _extreme_values(k, rng, m) for k in ALL_KINDS}
@@ -147,7 +155,7 @@ def test_same_kind_extremes(dev):
     check_decode(dev, schema, stream, ends, "extremes")
 
 
-def test_float_widths_both_ways(dev):
+def test_float_widths_both_ways(dev, kernel):
     """float32 <-> float64 through the getters (float.go:15-78): NaN payloads, Inf, subnormal
     rounding, the MaxFloat32 boundary."""
     rng = np.random.default_rng(11)
@@ -163,7 +171,7 @@ def test_float_widths_both_ways(dev):
         check_decode(dev, schema, stream, ends, "float widths")
 
 
-def test_empty_and_zero_records(dev):
+def test_empty_and_zero_records(dev, kernel):
     recs = [b"", write_record([]), b"", write_record([(1, Kind.BOOL, True)]), b""]
     stream, ends = concat_records(recs)
     check_decode(dev, FLAT16, stream, ends, "empty records")
@@ -171,7 +179,7 @@ def test_empty_and_zero_records(dev):
     check_decode(dev, FLAT16, stream, ends, "all empty")
 
 
-def test_handcrafted_tables(dev):
+def test_handcrafted_tables(dev, kernel):
     """Unsorted, duplicate, missing and extra tags; end offsets beyond dataSize; big-format
     tables with small values; truncated trailers (msg_test.go:74-143 error classes)."""
     vals = [O.encode("int32", 7)[0], O.encode("string", "abc")[0], O.encode("int64", -5)[0],
@@ -214,7 +222,7 @@ def test_handcrafted_tables(dev):
 
 
 @pytest.mark.parametrize("seed", range(6))
-def test_fuzz_mutated_records(dev, seed):
+def test_fuzz_mutated_records(dev, kernel, seed):
     """Valid Flat16 records with random byte mutations, truncations and garbage records."""
     rng = np.random.default_rng(1000 + seed)
     n = 3000
@@ -244,7 +252,7 @@ def test_fuzz_mutated_records(dev, seed):
     check_decode(dev, FLAT16, s2, e2, f"fuzz seed={seed}")
 
 
-def test_large_records_global_path(dev):
+def test_large_records_global_path(dev, kernel):
     """Records too large for a wave's LDS slab take the direct-HBM path; big messages
     (dataSize > 65535) use the 6-byte table."""
     rng = np.random.default_rng(3)
