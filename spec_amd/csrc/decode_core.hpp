@@ -51,12 +51,15 @@ struct DecodeArgs {
 };
 
 constexpr int DEC_WAVES = 4; // waves per 256-thread block
-constexpr int SLAB_GUARD = 16;
+constexpr int SLAB_GUARD = 48; // >= the deepest read below a value end (bin256: 33 + 7)
 
-// slab bytes per wave for each instantiation (guard + DMA chunks + pad)
-constexpr int SLAB_S = SLAB_GUARD + 11 * 1024 + 16 + 16; // spans <= 11 KiB  (avg rec <~ 150 B)
-constexpr int SLAB_M = SLAB_GUARD + 19 * 1024 + 16 + 16; // spans <= 19 KiB  (avg rec <~ 270 B)
-constexpr int SLAB_L = SLAB_GUARD + 35 * 1024 + 16 + 16; // spans <= 35 KiB  (avg rec <~ 500 B)
+// LDS slab per wave: guard + the DMA chunks (1 KiB each) a span may need + pad.  Three size
+// classes per records-per-wave setting, chosen from the batch's average record size; a wave
+// whose span does not fit parses from HBM instead (GlobalSrc).
+__host__ __device__ constexpr int slab_chunks(int recs, int cls) {
+    return recs == 64 ? (cls == 0 ? 11 : cls == 1 ? 19 : 35) : (cls == 0 ? 6 : cls == 1 ? 10 : 18);
+}
+__host__ __device__ constexpr int slab_bytes(int recs, int cls) { return SLAB_GUARD + slab_chunks(recs, cls) * 1024 + 32; }
 
 // ---- message table lookup --------------------------------------------------------------
 
@@ -95,102 +98,103 @@ struct Val {
     uint64_t v0, v1, v2, v3; // up to 32 bytes of column payload, little-endian
 };
 
-// Decode the value ending at e (field slice [lo, e), flen = e - lo > 0) from its 16-byte
-// tail window t; bin128/bin256 read their leading bytes from s.
+// Decode the value ending at e (field slice [lo, e), flen = e - lo; flen <= 0 => zero value)
+// from its 16-byte tail window t; bin128/bin256 read their leading bytes from s.
+// Straight-line code (selects, no branches): every byte it reads lies within 40 bytes below
+// e, which callers keep inside the source even for an empty field.
+// The bytes a value's decode reads: its 16-byte tail window, plus for bin128/bin256 the
+// leading payload qwords.
+struct Win {
+    Tail t;
+    uint64_t x0, x1, x2;
+};
+
 template <uint32_t KIND, class Src>
-__device__ __forceinline__ Val decode_tail_k(const Src &s, const Tail &t, typename Src::pos_t lo,
-                                             typename Src::pos_t e, long long to_stream) {
+__device__ __forceinline__ Win load_win(const Src &s, typename Src::pos_t e) {
+    Win w;
+    w.t = load_tail(s, e);
+    w.x0 = w.x1 = w.x2 = 0;
+    if constexpr (KIND == K_BIN128) {
+        w.x0 = load_le64(s, e - 17);
+    } else if constexpr (KIND == K_BIN256) {
+        w.x0 = load_le64(s, e - 33);
+        w.x1 = load_le64(s, e - 25);
+        w.x2 = load_le64(s, e - 17);
+    }
+    return w;
+}
+
+template <uint32_t KIND, class Pos>
+__device__ __forceinline__ Val decode_tail_k(const Win &w, Pos lo, Pos e, long long to_stream) {
+    const Tail &t = w.t;
     Val out = {0, 0, 0, 0};
     const long long flen = (long long)(e - lo);
-    uint32_t type = (uint32_t)t.q0 & 0xff;
-    uint64_t R = tail_r(t);
-    uint32_t R2 = tail_r2(t);
-    long long avail = flen - 1; // bytes before the type byte
+    const uint32_t type = (uint32_t)t.q0 & 0xff;
+    const uint64_t R = tail_r(t);
+    const uint32_t R2 = tail_r2(t);
+    const long long avail = flen - 1; // bytes before the type byte
     int m;
     if constexpr (KIND == K_BOOL) { // DecodeBool, byte.go:38-51: true iff type == TypeTrue
-        out.v0 = type == T_TRUE;
+        out.v0 = ((flen > 0) & (type == T_TRUE)) ? 1 : 0;
     } else if constexpr (KIND == K_BYTE) { // DecodeByte, byte.go:16-34
-        if (type == T_BYTE && flen >= 2) out.v0 = R & 0xff;
-    } else if constexpr (KIND == K_INT16 || KIND == K_INT32 || KIND == K_INT64) {
+        out.v0 = ((type == T_BYTE) & (flen >= 2)) ? (R & 0xff) : 0;
+    } else if constexpr (KIND == K_INT16 | KIND == K_INT32 | KIND == K_INT64) {
         // DecodeInt16/32/64, int.go:16-135: 32-bit routine for Int16/Int32, 64-bit for Int64
-        long long x;
-        bool ok;
-        if (type == T_INT16 || type == T_INT32) {
-            uint32_t u = (uint32_t)rvarint<5>(R, R2, avail, m);
-            x = unzigzag32(u);
-            ok = m >= 0;
-        } else {
-            x = unzigzag64(rvarint<10>(R, R2, avail, m));
-            ok = type == T_INT64 && m >= 0;
-        }
-        if (KIND == K_INT16) ok = ok && x >= -32768 && x <= 32767;
-        if (KIND == K_INT32) ok = ok && (type != T_INT64 || (x >= INT32_MIN && x <= INT32_MAX));
+        const bool w32 = (type == T_INT16) | (type == T_INT32);
+        const uint64_t u = rvarint_bf(R, R2, avail, w32 ? 5 : 10, m);
+        const long long x = w32 ? (long long)unzigzag32((uint32_t)u) : (long long)unzigzag64(u);
+        bool ok = (flen > 0) & (w32 | (type == T_INT64)) & (m >= 0);
+        if (KIND == K_INT16) ok = ok & (x >= -32768) & (x <= 32767);
+        if (KIND == K_INT32) ok = ok & (w32 | ((x >= INT32_MIN) & (x <= INT32_MAX)));
         out.v0 = ok ? (uint64_t)x : 0;
         if (KIND == K_INT16) out.v0 &= 0xffff;
         if (KIND == K_INT32) out.v0 &= 0xffffffffu;
-    } else if constexpr (KIND == K_UINT16 || KIND == K_UINT32 || KIND == K_UINT64) {
+    } else if constexpr (KIND == K_UINT16 | KIND == K_UINT32 | KIND == K_UINT64) {
         // DecodeUint16/32/64, uint.go:16-125
-        uint64_t x;
-        bool ok;
-        if (type == T_UINT16 || type == T_UINT32) {
-            x = rvarint<5>(R, R2, avail, m);
-            ok = m >= 0;
-        } else {
-            x = rvarint<10>(R, R2, avail, m);
-            ok = type == T_UINT64 && m >= 0;
-        }
-        if (KIND == K_UINT16) ok = ok && x <= 0xffffull;
-        if (KIND == K_UINT32) ok = ok && x <= 0xffffffffull;
+        const bool w32 = (type == T_UINT16) | (type == T_UINT32);
+        const uint64_t x = rvarint_bf(R, R2, avail, w32 ? 5 : 10, m);
+        bool ok = (flen > 0) & (w32 | (type == T_UINT64)) & (m >= 0);
+        if (KIND == K_UINT16) ok = ok & (x <= 0xffffull);
+        if (KIND == K_UINT32) ok = ok & (x <= 0xffffffffull);
         out.v0 = ok ? x : 0;
     } else if constexpr (KIND == K_FLOAT32) { // DecodeFloat32, float.go:15-32 (via float64 + range check)
-        if (type == T_FLOAT32) {
-            if (flen >= 5) {
-                uint32_t b = (uint32_t)(R & 0xffffffffu);
-                uint32_t ex = (b >> 23) & 0xff;
-                bool inf = ex == 0xff && (b & 0x7fffff) == 0; // +-Inf fails the +-MaxFloat32 check
-                if (ex == 0xff) b |= 0x00400000u;              // NaN: quieted by the float64 round trip
-                out.v0 = inf ? 0 : b;
-            }
-        } else if (type == T_FLOAT64) {
-            if (flen >= 9) {
-                uint64_t d = R;
-                uint32_t ex = (uint32_t)(d >> 52) & 0x7ff;
-                bool nan = ex == 0x7ff && (d & 0xfffffffffffffull);
-                // |d| > MaxFloat32 (0x47EFFFFFE0000000) => overflow error => 0
-                bool over = !nan && (d & 0x7fffffffffffffffull) > 0x47EFFFFFE0000000ull;
-                out.v0 = over ? 0 : f64_to_f32_bits(d);
-            }
-        }
+        uint32_t b = (uint32_t)(R & 0xffffffffu);
+        const uint32_t ex = (b >> 23) & 0xff;
+        const bool inf = (ex == 0xff) & ((b & 0x7fffff) == 0); // +-Inf fails the +-MaxFloat32 check
+        b = ex == 0xff ? (b | 0x00400000u) : b;             // NaN: quieted by the float64 round trip
+        const uint64_t d = R;
+        const uint32_t dx = (uint32_t)(d >> 52) & 0x7ff;
+        const bool nan = (dx == 0x7ff) & ((d & 0xfffffffffffffull) != 0);
+        // |d| > MaxFloat32 (0x47EFFFFFE0000000) => overflow error => 0
+        const bool over = !nan & ((d & 0x7fffffffffffffffull) > 0x47EFFFFFE0000000ull);
+        const uint32_t from64 = f64_to_f32_bits_bf(d);
+        const bool ok32 = (type == T_FLOAT32) & (flen >= 5) & !inf, ok64 = (type == T_FLOAT64) & (flen >= 9) & !over;
+        out.v0 = ok32 ? b : (ok64 ? from64 : 0u);
     } else if constexpr (KIND == K_FLOAT64) { // DecodeFloat64, float.go:34-78
-        if (type == T_FLOAT32) {
-            if (flen >= 5) out.v0 = f32_to_f64_bits((uint32_t)(R & 0xffffffffu));
-        } else if (type == T_FLOAT64) {
-            if (flen >= 9) out.v0 = R;
-        }
+        const uint64_t from32 = f32_to_f64_bits_bf((uint32_t)(R & 0xffffffffu));
+        const bool ok32 = (type == T_FLOAT32) & (flen >= 5), ok64 = (type == T_FLOAT64) & (flen >= 9);
+        out.v0 = ok32 ? from32 : (ok64 ? R : 0ull);
     } else if constexpr (KIND == K_BIN64) { // DecodeBin64, bin.go:15-44: raw 8 bytes before the type byte
-        if (type == T_BIN64 && flen >= 9) out.v0 = __builtin_bswap64(R);
+        out.v0 = ((type == T_BIN64) & (flen >= 9)) ? __builtin_bswap64(R) : 0;
     } else if constexpr (KIND == K_BIN128) {
-        if (type == T_BIN128 && flen >= 17) {
-            out.v0 = load_le64(s, e - 17);
-            out.v1 = __builtin_bswap64(R);
-        }
+        const bool ok = (type == T_BIN128) & (flen >= 17);
+        out.v0 = ok ? w.x0 : 0;
+        out.v1 = ok ? __builtin_bswap64(R) : 0;
     } else if constexpr (KIND == K_BIN256) {
-        if (type == T_BIN256 && flen >= 33) {
-            out.v0 = load_le64(s, e - 33);
-            out.v1 = load_le64(s, e - 25);
-            out.v2 = load_le64(s, e - 17);
-            out.v3 = __builtin_bswap64(R);
-        }
-    } else if constexpr (KIND == K_STRING || KIND == K_BYTES) {
+        const bool ok = (type == T_BIN256) & (flen >= 33);
+        out.v0 = ok ? w.x0 : 0;
+        out.v1 = ok ? w.x1 : 0;
+        out.v2 = ok ? w.x2 : 0;
+        out.v3 = ok ? __builtin_bswap64(R) : 0;
+    } else if constexpr (KIND == K_STRING | KIND == K_BYTES) {
         // DecodeString (string.go:15-70) / DecodeBytes (bytes.go:14-58)
         constexpr bool str = KIND == K_STRING;
-        if (type == (str ? T_STRING : T_BYTES)) {
-            uint32_t len = (uint32_t)rvarint<5>(R, R2, avail, m);
-            long long end = (long long)(e - 1) - m - (str ? 1 : 0); // skip the NUL for strings
-            long long off = end - (long long)len;
-            bool ok = m >= 0 && end >= (long long)lo && off >= (long long)lo && len;
-            if (ok) out.v0 = (uint64_t)(uint32_t)(off + to_stream) | ((uint64_t)len << 32);
-        }
+        const uint32_t len = (uint32_t)rvarint_bf(R, R2, avail, 5, m);
+        const long long end = (long long)(e - 1) - m - (str ? 1 : 0); // skip the NUL for strings
+        const long long off = end - (long long)len;
+        const bool ok = (type == (str ? T_STRING : T_BYTES)) & (flen > 0) & (m >= 0) & (end >= (long long)lo) &
+                        (off >= (long long)lo) & (len != 0);
+        out.v0 = ok ? ((uint64_t)(uint32_t)(off + to_stream) | ((uint64_t)len << 32)) : 0;
     }
     return out;
 }
@@ -199,7 +203,7 @@ template <uint32_t KIND, class Src>
 __device__ __forceinline__ Val decode_value_k(const Src &s, typename Src::pos_t lo, typename Src::pos_t e,
                                               long long to_stream) {
     if ((long long)(e - lo) <= 0) return Val{0, 0, 0, 0}; // empty => zero value, no error
-    return decode_tail_k<KIND>(s, load_tail(s, e), lo, e, to_stream);
+    return decode_tail_k<KIND>(load_win<KIND>(s, e), lo, e, to_stream);
 }
 
 template <uint32_t KIND>
@@ -230,9 +234,8 @@ __device__ __forceinline__ void decode_store(const Src &s, uint32_t kind, typena
     Val v = {0, 0, 0, 0};
     if (end > 0) {
         const typename Src::pos_t e = lo + (typename Src::pos_t)end;
-        const Tail t = load_tail(s, e);
 #define SPEC_CASE(K) \
-    case K: v = decode_tail_k<K>(s, t, lo, e, to_stream); break;
+    case K: v = decode_tail_k<K>(load_win<K>(s, e), lo, e, to_stream); break;
         switch (kind) {
             SPEC_CASE(K_BOOL)
             SPEC_CASE(K_BYTE)
@@ -391,19 +394,45 @@ struct RuntimeSpec {
 //   stag[k]        k-th tag of the table a Writer emits (strictly increasing, all <= 255)
 constexpr int FAST_MAX_FIELDS = 24;
 
-// Unrolled at compile time: field F's kind and table index are constants, so every
-// field is straight-line code and independent fields interleave.
+// Unrolled at compile time: field F's kind and table index are constants, so every field
+// is straight-line code.  Phase 1 issues every field's LDS reads, phase 2 decodes and
+// stores, so the LDS latency is paid once per record, not once per field.
+template <class Spec>
+struct FastRec {
+    Win w[Spec::N];
+    int e[Spec::N], lo[Spec::N];
+};
+
 template <class Spec, int F>
-struct FieldLoop {
-    static __device__ __forceinline__ void run(const LdsSrc &s, int ds, const uint32_t *ends, uint32_t dsize,
-                                               long long to_stream, const DecodeArgs &a, uint64_t r) {
+struct FieldLoad {
+    static __device__ __forceinline__ void run(FastRec<Spec> &fr, const LdsSrc &s, int ds, const uint32_t *ends,
+                                               uint32_t dsize) {
         if constexpr (F < Spec::N) {
             constexpr uint32_t K = Spec::kind[F];
-            constexpr int k = Spec::rank[F];
-            const uint32_t end = ends[k];
-            const int e = end <= dsize ? ds + (int)end : ds; // end > dataSize => nil => zero
-            store_value_k<K>(a.cols[F], r, decode_value_k<K>(s, ds, e, to_stream));
-            FieldLoop<Spec, F + 1>::run(s, ds, ends, dsize, to_stream, a, r);
+            const uint32_t end = ends[Spec::rank[F]];
+            // end > dataSize => nil; an empty field decodes to zero: read a harmless window
+            const bool has = (end <= dsize) & (end > 0);
+            fr.e[F] = has ? ds + (int)end : SLAB_GUARD;
+            fr.lo[F] = has ? ds : SLAB_GUARD;
+            fr.w[F] = load_win<K>(s, fr.e[F]);
+            FieldLoad<Spec, F + 1>::run(fr, s, ds, ends, dsize);
+        }
+    }
+};
+
+template <class Spec, int F>
+struct FieldStore {
+    static __device__ __forceinline__ void run(const FastRec<Spec> &fr, long long to_stream, const DecodeArgs &a,
+                                               uint64_t r, uint64_t &acc) {
+        if constexpr (F < Spec::N) {
+            constexpr uint32_t K = Spec::kind[F];
+            const Val v = decode_tail_k<K>(fr.w[F], fr.lo[F], fr.e[F], to_stream);
+#if defined(SPEC_EXP) && SPEC_EXP == 3 // diagnostic: decode, no column stores
+            acc ^= v.v0 ^ v.v1 ^ v.v2 ^ v.v3;
+#else
+            store_value_k<K>(a.cols[F], r, v);
+#endif
+            FieldStore<Spec, F + 1>::run(fr, to_stream, a, r, acc);
         }
     }
 };
@@ -449,23 +478,35 @@ __device__ __forceinline__ bool decode_record_fast(const LdsSrc &s, int rs, int 
         ends[k] = (byte_at(3 * k + 1) << 8) | byte_at(3 * k + 2);
     }
     if (!hit) return false;
+#if defined(SPEC_EXP) && SPEC_EXP == 2 // diagnostic: trailer + table only
+    if (a.status) a.status[r] = (uint8_t)ends[N - 1];
+    return true;
+#endif
     if (a.status) a.status[r] = ST_OK;
-    FieldLoop<Spec, 0>::run(s, (int)tr.dstart, ends, tr.dsize, to_stream, a, r);
+    uint64_t acc = 0;
+    FastRec<Spec> fr;
+    FieldLoad<Spec, 0>::run(fr, s, (int)tr.dstart, ends, tr.dsize);
+    FieldStore<Spec, 0>::run(fr, to_stream, a, r, acc);
+#if defined(SPEC_EXP) && SPEC_EXP == 3
+    if (a.status) a.status[r] = (uint8_t)(acc ^ (acc >> 8) ^ (acc >> 16) ^ (acc >> 32));
+#endif
     return true;
 }
 
 // ---- kernel body -------------------------------------------------------------------------
 
-template <int SLAB, class Spec>
+// RECS records per wave (64: one per lane; 32: lanes 32..63 only stage bytes, which halves
+// the slab and doubles the waves a CU holds).
+template <int RECS, int SLAB, class Spec>
 __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const uint64_t base = ((uint64_t)blockIdx.x * DEC_WAVES + wave) * 64;
+    const uint64_t base = ((uint64_t)blockIdx.x * DEC_WAVES + wave) * RECS;
     if (base >= a.n) return;
     const uint64_t r = base + lane;
-    const bool valid = r < a.n;
-    const uint64_t last = (a.n - base) < 64 ? a.n - 1 : base + 63;
+    const bool valid = lane < RECS && r < a.n;
+    const uint64_t last = (a.n - base) < RECS ? a.n - 1 : base + RECS - 1;
 
     uint64_t rec_hi = valid ? a.ends[r] : 0;
     uint64_t prev = __shfl_up(rec_hi, 1);
@@ -503,6 +544,10 @@ __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
+#if defined(SPEC_EXP) && SPEC_EXP == 1 // diagnostic: staging only
+            if (valid && a.status) a.status[r] = slab[SLAB_GUARD + (rec_hi - aligned_lo) - 1];
+            return;
+#endif
             if (valid) {
                 LdsSrc s{(lds_u8 *)slab};
                 int rs = SLAB_GUARD + (int)(rec_lo - aligned_lo);
@@ -524,12 +569,11 @@ __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
     }
 }
 
-// slab choice shared by the launchers (host) — average record size * 64 * margin
-__host__ __device__ inline int decode_slab_class(double avg_record) {
-    double span = avg_record * 64.0 * 1.08 + 64.0;
-    if (span <= 11 * 1024) return 0;
-    if (span <= 19 * 1024) return 1;
-    if (span <= 35 * 1024) return 2;
+// slab class shared by the launchers (host): average record size * RECS * margin; 3 = none
+__host__ __device__ inline int decode_slab_class(double avg_record, int recs) {
+    double span = avg_record * recs * 1.08 + 64.0;
+    for (int c = 0; c < 3; c++)
+        if (span <= slab_chunks(recs, c) * 1024) return c;
     return 3;
 }
 

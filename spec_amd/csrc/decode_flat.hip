@@ -8,20 +8,23 @@
 
 namespace spec {
 
+constexpr int GENERIC_RECS = 64;
+
 template <int SLAB>
 __global__ __launch_bounds__(256) void decode_flat_kernel(DecodeArgs a) {
-    decode_flat_body<SLAB, RuntimeSpec>(a);
+    decode_flat_body<GENERIC_RECS, SLAB, RuntimeSpec>(a);
 }
 
 int launch_decode_flat(const DecodeArgs &a, double avg_record, hipStream_t stream) {
-    uint64_t waves = (a.n + 63) / 64;
+    constexpr int R = GENERIC_RECS;
+    uint64_t waves = (a.n + R - 1) / R;
     uint64_t blocks = (waves + DEC_WAVES - 1) / DEC_WAVES;
     if (blocks == 0) return 0;
     dim3 grid((unsigned)blocks), block(256);
-    switch (decode_slab_class(avg_record)) {
-    case 0: hipLaunchKernelGGL(decode_flat_kernel<SLAB_S>, grid, block, DEC_WAVES * SLAB_S, stream, a); break;
-    case 1: hipLaunchKernelGGL(decode_flat_kernel<SLAB_M>, grid, block, DEC_WAVES * SLAB_M, stream, a); break;
-    case 2: hipLaunchKernelGGL(decode_flat_kernel<SLAB_L>, grid, block, DEC_WAVES * SLAB_L, stream, a); break;
+    switch (decode_slab_class(avg_record, R)) {
+    case 0: hipLaunchKernelGGL(decode_flat_kernel<slab_bytes(R, 0)>, grid, block, DEC_WAVES * slab_bytes(R, 0), stream, a); break;
+    case 1: hipLaunchKernelGGL(decode_flat_kernel<slab_bytes(R, 1)>, grid, block, DEC_WAVES * slab_bytes(R, 1), stream, a); break;
+    case 2: hipLaunchKernelGGL(decode_flat_kernel<slab_bytes(R, 2)>, grid, block, DEC_WAVES * slab_bytes(R, 2), stream, a); break;
     default: hipLaunchKernelGGL(decode_flat_kernel<0>, grid, block, 0, stream, a); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;

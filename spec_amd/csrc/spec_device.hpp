@@ -206,6 +206,39 @@ __device__ __forceinline__ uint64_t rvarint(uint64_t r, uint32_t r2, long long a
     return w;
 }
 
+// Branch-free form of rvarint (same results) with a run-time MaxLen (5 or 10): every
+// intermediate is computed eagerly and combined with selects, so a specialised kernel's
+// fields stay straight-line code the compiler can interleave.
+__device__ __forceinline__ uint32_t ctz_or(uint32_t x, uint32_t none) { return __builtin_ctzg(x, (int)none); }
+
+__device__ __forceinline__ uint64_t rvarint_bf(uint64_t r, uint32_t r2, long long avail, int maxlen, int &n) {
+    const uint64_t t = ~r & 0x8080808080808080ull;
+    const uint32_t t2 = ~r2 & 0x8080u;
+    // index of the first byte with MSB clear: bit index / 8, 10 if none among the 10 bytes
+    const uint32_t b0 = ctz_or((uint32_t)t, 96u);
+    const uint32_t b1 = ctz_or((uint32_t)(t >> 32), 64u) + 32u;
+    const uint32_t b2 = ctz_or(t2, 16u) + 64u;
+    const int ta = (int)(__builtin_elementwise_min(__builtin_elementwise_min(b0, b1), b2) >> 3);
+    const long long lim = avail < maxlen ? avail : (long long)maxlen;
+    const bool incomplete = (long long)ta >= lim;
+    const uint64_t keep = ~0ull >> (56 - 8 * (ta < 7 ? ta : 7)); // bytes 0..ta (all 8 when ta >= 7)
+    uint64_t w = r & 0x7f7f7f7f7f7f7f7full & keep;
+    w = (w & 0x007f007f007f007full) | ((w & 0x7f007f007f007f00ull) >> 1);
+    w = (w & 0x00003fff00003fffull) | ((w & 0x3fff00003fff0000ull) >> 2);
+    w = (w & 0x000000000fffffffull) | ((w & 0x0fffffff00000000ull) >> 4);
+    const uint64_t h8 = (uint64_t)(r2 & 0x7f) << 56;
+    const uint64_t h9 = (uint64_t)((r2 >> 8) & 0x7f) << 63;
+    w |= (ta >= 8 ? h8 : 0ull) | (ta == 9 ? h9 : 0ull);
+    const uint32_t lo_last = (uint32_t)(r >> (8 * (ta & 7))) & 0xff;
+    const uint32_t hi_last = (r2 >> (8 * ((ta - 8) & 1))) & 0xff;
+    const uint32_t last = ta >= 8 ? hi_last : lo_last;
+    const uint32_t cap = maxlen == 10 ? 1u : 0x0fu;
+    const bool over = (ta == maxlen - 1) & (last > cap);
+    const int n_inc = -(int)(lim + 1), n_over = -(ta + 1), n_ok = ta + 1;
+    n = incomplete ? n_inc : (over ? n_over : n_ok);
+    return (incomplete | over) ? 0ull : w;
+}
+
 __device__ __forceinline__ int64_t unzigzag64(uint64_t u) { return (int64_t)(u >> 1) ^ -(int64_t)(u & 1); }
 __device__ __forceinline__ int32_t unzigzag32(uint32_t u) { return (int32_t)(u >> 1) ^ -(int32_t)(u & 1); }
 
@@ -255,6 +288,39 @@ __device__ __forceinline__ uint32_t f64_to_f32_bits(uint64_t d) {
     uint64_t half = 1ull << (r - 1);
     if (rem > half || (rem == half && (q & 1))) q += 1;
     return s | (base + (uint32_t)q); // mantissa carry rolls into the exponent correctly
+}
+
+// Branch-free forms of the two conversions above (same bits).
+__device__ __forceinline__ uint64_t f32_to_f64_bits_bf(uint32_t f) {
+    const uint64_t sgn = (uint64_t)(f >> 31) << 63;
+    const uint32_t e = (f >> 23) & 0xff, m = f & 0x7fffff;
+    const uint64_t norm = sgn | ((uint64_t)(e + 896) << 52) | ((uint64_t)m << 29);
+    const uint64_t qnan = 0x0008000000000000ull | ((uint64_t)m << 29);
+    const uint64_t infnan = sgn | 0x7ff0000000000000ull | (m != 0 ? qnan : 0ull);
+    const int p = 31 - (int)__builtin_clz(m | 1u);
+    const uint64_t sub = sgn | ((uint64_t)(p + 874) << 52) | (((uint64_t)m << (52 - p)) & 0xfffffffffffffull);
+    const uint64_t zs = m != 0 ? sub : sgn;
+    return e == 0xff ? infnan : (e == 0 ? zs : norm);
+}
+
+__device__ __forceinline__ uint32_t f64_to_f32_bits_bf(uint64_t d) {
+    const uint32_t sgn = (uint32_t)(d >> 63) << 31;
+    const int E = (int)((d >> 52) & 0x7ff);
+    const uint64_t M = d & 0xfffffffffffffull;
+    const int e = E - 1023;
+    const bool normal = e >= -126;
+    const int rr = normal ? 29 : 29 + (-126 - e);
+    const bool tiny = rr >= 64;
+    const int r = tiny ? 63 : rr;
+    const uint64_t sig = normal ? M : (M | (1ull << 52));
+    const uint32_t base = normal ? (uint32_t)(e + 127) << 23 : 0u;
+    uint64_t q = sig >> r;
+    const uint64_t rem = sig & ((1ull << r) - 1);
+    const uint64_t half = 1ull << (r - 1);
+    q += ((rem > half) | ((rem == half) & ((q & 1) != 0))) ? 1 : 0;
+    const uint32_t fin = tiny ? sgn : sgn | (base + (uint32_t)q);
+    const uint32_t nanr = sgn | 0x7fc00000u | (uint32_t)(M >> 29);
+    return E == 0x7ff ? nanr : (E == 0 ? sgn : fin);
 }
 
 // ---- tiny helpers ------------------------------------------------------------------------
