@@ -54,6 +54,8 @@ typedef enum spec_kind {
     SPEC_KIND_BIN256 = 13, /* 32 opaque bytes  Message.Bin256   / FieldWriter.Bin256  */
     SPEC_KIND_STRING = 14, /* spec_span        Message.String   / FieldWriter.String  */
     SPEC_KIND_BYTES = 15,  /* spec_span        Message.Bytes    / FieldWriter.Bytes   */
+    SPEC_KIND_LIST = 16,   /* list<message>: only in spec_nested_schema.outer; its column is
+                              the item_begin CSR index   Message.List / FieldWriter.List */
 } spec_kind;
 
 /* Per-record status: the error class OpenMessageErr returns for the record
@@ -96,11 +98,35 @@ typedef struct spec_schema {
     spec_field fields[SPEC_MAX_FIELDS];
 } spec_schema;
 
+/* A message with one list<message> field (BASELINE config 4, list_msg.go / writer_list_msg.go):
+ * `outer` lists the outer message's fields in write order, exactly one of kind SPEC_KIND_LIST;
+ * `item` the fields of each list item (flat kinds only). */
+typedef struct spec_nested_schema {
+    spec_schema outer;
+    spec_schema item;
+} spec_nested_schema;
+
 /* ---- introspection ---- */
 int spec_abi_version(void);
 int spec_kind_width(int kind);
 const char *spec_strerror(int rc);
 int spec_last_hip_error(void);
+
+/* ---- memory and streams ----
+ * Thin wrappers so a binding (cgo) needs only this header: device buffers,
+ * pinned host staging (hipHostMalloc; Go code sees it through unsafe.Slice and never hands Go
+ * memory to the device), streams and async copies.  All return SPEC_OK or SPEC_E_HIP. */
+int spec_set_device(int device);
+int spec_device_alloc(size_t bytes, void **ptr);
+int spec_device_free(void *ptr);
+int spec_host_alloc(size_t bytes, void **ptr);
+int spec_host_free(void *ptr);
+int spec_stream_create(void **stream);
+int spec_stream_destroy(void *stream);
+int spec_stream_sync(void *stream);
+int spec_copy_h2d(void *dst, const void *src, size_t bytes, void *stream);
+int spec_copy_d2h(void *dst, const void *src, size_t bytes, void *stream);
+int spec_copy_d2d(void *dst, const void *src, size_t bytes, void *stream);
 
 /* ---- decode ----
  * spec_decode_flat: for every record i, exactly
@@ -125,6 +151,28 @@ int spec_decode_flat_prepare(const spec_schema *schema, uint64_t stream_len, uin
 long long spec_decode_flat_jit_compile(const spec_schema *schema, uint64_t stream_len, uint64_t n);
 /* spec_set_jit: 0 forces the generic kernel (also: environment SPEC_AMD_JIT=0). */
 void spec_set_jit(int enabled);
+
+/* ---- nested decode (list<message>) ----
+ * For every record i, exactly what a generated reader does:
+ *     m, err := spec.OpenMessageErr(record_i); status[i] = class(err); outer getters as above
+ *     items := spec.NewMessageList(m.msg.List(list_tag), OpenItemErr)     list_msg.go:20-26,
+ *                                                      internal/types/msg.go:441-444
+ *     for j < items.Len(): item = items.Get(j) -> item getters             list_msg.go:88-92
+ * Items are stored in record order: record i's items are [item_begin[i], item_begin[i+1]).
+ * item_status[k] = class(OpenItemErr error), or SPEC_STATUS_PANIC where Go's
+ * List.GetBytes would panic (element start > end, internal/types/list.go:100-116).
+ * Two calls on the same workspace (spec_decode_nested_workspace_size(n) bytes):
+ *   spec_decode_nested_index  -> *total_items (device uint64): size the item columns,
+ *   spec_decode_nested        -> all columns; items beyond item_cap are not written.
+ * outer_columns[f] for the SPEC_KIND_LIST field is ignored (may be NULL). */
+size_t spec_decode_nested_workspace_size(uint64_t n);
+int spec_decode_nested_index(const spec_nested_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
+                             const uint64_t *ends, uint64_t n, void *workspace, size_t workspace_size,
+                             uint64_t *total_items, void *stream);
+int spec_decode_nested(const spec_nested_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
+                       const uint64_t *ends, uint64_t n, void *const *outer_columns, uint8_t *status,
+                       uint32_t *item_begin, void *const *item_columns, uint8_t *item_status, uint64_t item_cap,
+                       void *workspace, size_t workspace_size, void *stream);
 
 /* ---- encode ----
  * spec_encode_flat: for every record i, exactly

@@ -7,9 +7,11 @@ decoded into SoA columns / encoded from them by hand-written gfx950 kernels
 """
 from ._lib import LIB_PATH, SpecError, header_symbols, lib, set_jit
 from .batch import Columns, Decoder, Encoder, alloc_columns, decode_flat, encode_flat
-from .schema import FLAT16, Field, Kind, Schema
+from .nested import NestedColumns, NestedDecoder, decode_nested
+from .schema import FLAT16, NESTED, Field, Kind, NestedSchema, Schema
 
 __all__ = [
     "LIB_PATH", "SpecError", "header_symbols", "lib", "set_jit", "Columns", "Decoder", "Encoder", "alloc_columns",
     "decode_flat", "encode_flat", "FLAT16", "Field", "Kind", "Schema",
+    "NESTED", "NestedSchema", "NestedColumns", "NestedDecoder", "decode_nested",
 ]

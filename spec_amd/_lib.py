@@ -25,6 +25,10 @@ class SpecSchema(C.Structure):
     _fields_ = [("nfields", C.c_uint32), ("fields", SpecField * SPEC_MAX_FIELDS)]
 
 
+class SpecNestedSchema(C.Structure):
+    _fields_ = [("outer", SpecSchema), ("item", SpecSchema)]
+
+
 class SpecError(RuntimeError):
     def __init__(self, rc: int, what: str):
         self.rc = rc
@@ -59,6 +63,12 @@ def _declare(L):
     L.spec_set_jit.restype = None
     L.spec_decode_flat_jit_compile.argtypes = [C.POINTER(SpecSchema), C.c_uint64, C.c_uint64]
     L.spec_decode_flat_jit_compile.restype = C.c_longlong
+    L.spec_decode_nested_workspace_size.restype = C.c_size_t
+    L.spec_decode_nested_workspace_size.argtypes = [C.c_uint64]
+    L.spec_decode_nested_index.argtypes = [C.POINTER(SpecNestedSchema), vp, C.c_uint64, vp, C.c_uint64, vp,
+                                           C.c_size_t, vp, vp]
+    L.spec_decode_nested.argtypes = [C.POINTER(SpecNestedSchema), vp, C.c_uint64, vp, C.c_uint64,
+                                     C.POINTER(vp), vp, vp, C.POINTER(vp), vp, C.c_uint64, vp, C.c_size_t, vp]
     L.spec_encode_flat_workspace_size.restype = C.c_size_t
     L.spec_encode_flat_workspace_size.argtypes = [C.c_uint64]
     L.spec_encode_flat_size.argtypes = [C.POINTER(SpecSchema), C.POINTER(vp), C.c_uint64, vp,

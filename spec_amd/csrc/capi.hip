@@ -52,10 +52,39 @@ int check_schema(const spec_schema *s) {
     return SPEC_OK;
 }
 
+// outer schema of a nested decode: flat kinds plus exactly one SPEC_KIND_LIST; *list_f = its index
+int check_nested(const spec_nested_schema *s, uint32_t *list_f) {
+    if (!s || s->outer.nfields > SPEC_MAX_FIELDS || check_schema(&s->item)) return SPEC_E_INVALID_ARGUMENT;
+    int lists = 0;
+    for (uint32_t f = 0; f < s->outer.nfields; f++) {
+        if (s->outer.fields[f].kind == SPEC_KIND_LIST) {
+            lists++;
+            *list_f = f;
+        } else if (kind_width(s->outer.fields[f].kind) == 0) {
+            return SPEC_E_INVALID_ARGUMENT;
+        }
+    }
+    return lists == 1 ? SPEC_OK : SPEC_E_INVALID_ARGUMENT;
+}
+
 int hip_rc(hipError_t e) {
     if (e == hipSuccess) return SPEC_OK;
     g_last_hip_error = (int)e;
     return SPEC_E_HIP;
+}
+
+void fill_field_set(spec::FieldSet &fs, const spec_schema *schema, void *const *columns, uint8_t *status) {
+    memset(&fs, 0, sizeof(fs));
+    fs.status = status;
+    fs.nfields = schema->nfields;
+    uint8_t order[SPEC_MAX_FIELDS];
+    table_order(schema, order);
+    for (uint32_t j = 0; j < schema->nfields; j++) fs.rank[order[j]] = (uint8_t)j;
+    for (uint32_t f = 0; f < schema->nfields; f++) {
+        fs.tags[f] = schema->fields[f].tag;
+        fs.kinds[f] = schema->fields[f].kind;
+        fs.cols[f] = columns ? columns[f] : nullptr;
+    }
 }
 
 void fill_encode_args(spec::EncodeArgs &a, const spec_schema *schema, const void *const *columns, uint64_t n) {
@@ -94,6 +123,33 @@ const char *spec_strerror(int rc) {
     return "unknown error";
 }
 
+int spec_set_device(int device) { return hip_rc(hipSetDevice(device)); }
+int spec_device_alloc(size_t bytes, void **ptr) {
+    if (!ptr) return SPEC_E_INVALID_ARGUMENT;
+    return hip_rc(hipMalloc(ptr, bytes ? bytes : 1));
+}
+int spec_device_free(void *ptr) { return hip_rc(hipFree(ptr)); }
+int spec_host_alloc(size_t bytes, void **ptr) {
+    if (!ptr) return SPEC_E_INVALID_ARGUMENT;
+    return hip_rc(hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault));
+}
+int spec_host_free(void *ptr) { return hip_rc(hipHostFree(ptr)); }
+int spec_stream_create(void **stream) {
+    if (!stream) return SPEC_E_INVALID_ARGUMENT;
+    return hip_rc(hipStreamCreateWithFlags((hipStream_t *)stream, hipStreamNonBlocking));
+}
+int spec_stream_destroy(void *stream) { return hip_rc(hipStreamDestroy((hipStream_t)stream)); }
+int spec_stream_sync(void *stream) { return hip_rc(hipStreamSynchronize((hipStream_t)stream)); }
+int spec_copy_h2d(void *dst, const void *src, size_t bytes, void *stream) {
+    return hip_rc(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+}
+int spec_copy_d2h(void *dst, const void *src, size_t bytes, void *stream) {
+    return hip_rc(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+}
+int spec_copy_d2d(void *dst, const void *src, size_t bytes, void *stream) {
+    return hip_rc(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+}
+
 int spec_decode_flat(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
                      const uint64_t *ends, uint64_t n, void *const *columns, uint8_t *status,
                      void *stream) {
@@ -110,16 +166,7 @@ int spec_decode_flat(const spec_schema *schema, const uint8_t *stream_bytes, uin
     a.stream_len = stream_len;
     a.ends = ends;
     a.n = n;
-    a.status = status;
-    a.nfields = schema->nfields;
-    uint8_t order[SPEC_MAX_FIELDS];
-    table_order(schema, order);
-    for (uint32_t j = 0; j < schema->nfields; j++) a.rank[order[j]] = (uint8_t)j;
-    for (uint32_t f = 0; f < schema->nfields; f++) {
-        a.tags[f] = schema->fields[f].tag;
-        a.kinds[f] = schema->fields[f].kind;
-        a.cols[f] = columns[f];
-    }
+    fill_field_set(a.f, schema, columns, status);
     double avg = (double)stream_len / (double)n;
     int j = spec::jit_launch_decode_flat(schema, a, avg, (hipStream_t)stream);
     if (j < 0) return hip_rc(hipGetLastError());
@@ -141,6 +188,70 @@ long long spec_decode_flat_jit_compile(const spec_schema *schema, uint64_t strea
     if (rc) return rc;
     if (n == 0) return 0;
     return spec::jit_compile_only(schema, (double)stream_len / (double)n);
+}
+
+size_t spec_decode_nested_workspace_size(uint64_t n) { return (size_t)(((n + 63) / 64 + 1) * sizeof(uint64_t)); }
+
+static int nested_args(spec::NestedArgs &a, const spec_nested_schema *schema, const uint8_t *stream_bytes,
+                       uint64_t stream_len, const uint64_t *ends, uint64_t n, void *workspace,
+                       size_t workspace_size) {
+    uint32_t list_f = 0;
+    int rc = check_nested(schema, &list_f);
+    if (rc) return rc;
+    if (n && (!ends || (!stream_bytes && stream_len) || !workspace)) return SPEC_E_INVALID_ARGUMENT;
+    if (stream_len >= (1ull << 32)) return SPEC_E_TOO_LARGE;
+    if (workspace_size < spec_decode_nested_workspace_size(n)) return SPEC_E_WORKSPACE;
+    memset(&a, 0, sizeof(a));
+    a.stream = stream_bytes;
+    a.stream_len = stream_len;
+    a.ends = ends;
+    a.n = n;
+    fill_field_set(a.outer, &schema->outer, nullptr, nullptr);
+    fill_field_set(a.item, &schema->item, nullptr, nullptr);
+    a.list_tag = schema->outer.fields[list_f].tag;
+    a.list_rank = a.outer.rank[list_f];
+    a.group_base = (uint64_t *)workspace;
+    return SPEC_OK;
+}
+
+int spec_decode_nested_index(const spec_nested_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
+                             const uint64_t *ends, uint64_t n, void *workspace, size_t workspace_size,
+                             uint64_t *total_items, void *stream) {
+    spec::NestedArgs a;
+    int rc = nested_args(a, schema, stream_bytes, stream_len, ends, n, workspace, workspace_size);
+    if (rc) return rc;
+    if (!total_items) return SPEC_E_INVALID_ARGUMENT;
+    a.total = total_items;
+    double avg = n ? (double)stream_len / (double)n : 0.0;
+    if (spec::launch_nested_index(a, avg, (hipStream_t)stream)) return hip_rc(hipGetLastError());
+    return SPEC_OK;
+}
+
+int spec_decode_nested(const spec_nested_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
+                       const uint64_t *ends, uint64_t n, void *const *outer_columns, uint8_t *status,
+                       uint32_t *item_begin, void *const *item_columns, uint8_t *item_status, uint64_t item_cap,
+                       void *workspace, size_t workspace_size, void *stream) {
+    spec::NestedArgs a;
+    int rc = nested_args(a, schema, stream_bytes, stream_len, ends, n, workspace, workspace_size);
+    if (rc) return rc;
+    if (n == 0) return SPEC_OK;
+    if (!outer_columns || !item_begin || (item_cap && !item_columns)) return SPEC_E_INVALID_ARGUMENT;
+    for (uint32_t f = 0; f < schema->outer.nfields; f++) {
+        if (schema->outer.fields[f].kind == SPEC_KIND_LIST) continue;
+        if (!outer_columns[f]) return SPEC_E_INVALID_ARGUMENT;
+        a.outer.cols[f] = outer_columns[f];
+    }
+    for (uint32_t f = 0; f < schema->item.nfields && item_cap; f++) {
+        if (!item_columns[f]) return SPEC_E_INVALID_ARGUMENT;
+        a.item.cols[f] = item_columns[f];
+    }
+    a.outer.status = status;
+    a.item.status = item_cap ? item_status : nullptr;
+    a.item_begin = item_begin;
+    a.item_cap = item_cap;
+    double avg = (double)stream_len / (double)n;
+    if (spec::launch_nested_decode(a, avg, (hipStream_t)stream)) return hip_rc(hipGetLastError());
+    return SPEC_OK;
 }
 
 size_t spec_encode_flat_workspace_size(uint64_t n) {

@@ -35,13 +35,8 @@ namespace spec {
 #define SPEC_MAX_FIELDS 64
 #endif
 
-// Passed by value as the kernel argument (lives in the kernarg segment => scalar loads,
-// the per-field loop branches are wave-uniform).
-struct DecodeArgs {
-    const uint8_t *stream;
-    uint64_t stream_len;
-    const uint64_t *ends;
-    uint64_t n;
+// The fields a record decode produces: one column per schema field + the status column.
+struct FieldSet {
     uint8_t *status;
     uint32_t nfields;
     uint16_t tags[SPEC_MAX_FIELDS];
@@ -50,16 +45,39 @@ struct DecodeArgs {
     void *cols[SPEC_MAX_FIELDS];
 };
 
+// Passed by value as the kernel argument (lives in the kernarg segment => scalar loads,
+// the per-field loop branches are wave-uniform).
+struct DecodeArgs {
+    const uint8_t *stream;
+    uint64_t stream_len;
+    const uint64_t *ends;
+    uint64_t n;
+    FieldSet f;
+};
+
+// spec_decode_nested (decode_nested.hip): outer records with one list<message> field.
+struct NestedArgs {
+    const uint8_t *stream;
+    uint64_t stream_len;
+    const uint64_t *ends;
+    uint64_t n;
+    FieldSet outer; // the outer message; its K_LIST field is decoded into item_begin
+    FieldSet item;  // the list items
+    uint32_t list_tag, list_rank;
+    uint32_t *item_begin; // [n + 1]
+    uint64_t item_cap;    // item columns hold this many items
+    uint64_t *group_base; // workspace: per 64-record group item total, then exclusive offsets
+    uint64_t *total;      // device: total items
+};
+
 constexpr int DEC_WAVES = 4; // waves per 256-thread block
 constexpr int SLAB_GUARD = 48; // >= the deepest read below a value end (bin256: 33 + 7)
 
 // LDS slab per wave: guard + the DMA chunks (1 KiB each) a span may need + pad.  Three size
 // classes per records-per-wave setting, chosen from the batch's average record size; a wave
 // whose span does not fit parses from HBM instead (GlobalSrc).
-__host__ __device__ constexpr int slab_chunks(int recs, int cls) {
-    return recs == 64 ? (cls == 0 ? 11 : cls == 1 ? 19 : 35) : (cls == 0 ? 6 : cls == 1 ? 10 : 18);
-}
-__host__ __device__ constexpr int slab_bytes(int recs, int cls) { return SLAB_GUARD + slab_chunks(recs, cls) * 1024 + 32; }
+__host__ __device__ constexpr int slab_chunks(int cls) { return cls == 0 ? 11 : cls == 1 ? 19 : 35; }
+__host__ __device__ constexpr int slab_bytes(int cls) { return SLAB_GUARD + slab_chunks(cls) * 1024 + 32; }
 
 // ---- message table lookup --------------------------------------------------------------
 
@@ -279,17 +297,21 @@ struct Trailer {
     uint32_t dsize, tsize;
 };
 
-template <class Src>
+// LIST = false: DecodeMessageTable (internal/decode/msg.go:14-99), 3/6-byte entries;
+// LIST = true: DecodeListTable (internal/decode/list.go:14-98), 2/4-byte entries.
+template <bool LIST = false, class Src>
 __device__ __forceinline__ Trailer parse_trailer(const Src &s, typename Src::pos_t rs, typename Src::pos_t re) {
     Trailer tr = {ST_OK, false, 0, 0, 0, 0};
     long long len = (long long)(re - rs);
     Tail t = load_tail(s, re);
     uint32_t type = (uint32_t)t.q0 & 0xff;
-    if (type != T_MESSAGE && type != T_BIG_MESSAGE) {
+    const uint32_t T_SMALL = LIST ? T_LIST : T_MESSAGE, T_BIG = LIST ? T_BIG_LIST : T_BIG_MESSAGE;
+    const uint32_t ESMALL = LIST ? 2u : 3u, EBIG = LIST ? 4u : 6u;
+    if (type != T_SMALL && type != T_BIG) {
         tr.st = ST_INVALID_TYPE;
         return tr;
     }
-    tr.big = type == T_BIG_MESSAGE;
+    tr.big = type == T_BIG;
     uint64_t R = tail_r(t);
     uint32_t R2 = tail_r2(t);
     int m1, m2;
@@ -308,7 +330,7 @@ __device__ __forceinline__ Trailer parse_trailer(const Src &s, typename Src::pos
     }
     long long tend = (long long)(re - 1) - m1 - m2;
     long long ts = tend - (long long)tsz;
-    if (ts < (long long)rs || tsz % (tr.big ? 6u : 3u) != 0) {
+    if (ts < (long long)rs || tsz % (tr.big ? EBIG : ESMALL) != 0) {
         tr.st = ST_INVALID_TABLE;
         return tr;
     }
@@ -325,59 +347,84 @@ __device__ __forceinline__ Trailer parse_trailer(const Src &s, typename Src::pos
 
 // ---- generic path: any record, run-time schema -----------------------------------------
 
-// Parse record r occupying [rs, re) of the source; to_stream converts a source position to a
-// stream offset (string/bytes spans).
+// OpenMessageErr of one record: trailer + whether the table's tags are strictly increasing
+// (then a probe at a field's expected index finds what the reference's binary search finds).
+struct RecInfo {
+    Trailer tr;
+    bool ok, sorted;
+    uint32_t nent;
+};
+
 template <class Src>
-__device__ __forceinline__ void decode_record_generic(const Src &s, typename Src::pos_t rs, typename Src::pos_t re,
-                                                   uint64_t r, const DecodeArgs &a, long long to_stream) {
+__device__ __forceinline__ RecInfo rec_open(const Src &s, typename Src::pos_t rs, typename Src::pos_t re) {
     using pos_t = typename Src::pos_t;
-    bool ok = false, sorted = true;
-    Trailer tr = {ST_OK, false, 0, 0, 0, 0};
-    uint32_t nent = 0;
+    RecInfo ri;
+    ri.tr = Trailer{ST_OK, false, 0, 0, 0, 0};
+    ri.ok = false;
+    ri.sorted = true;
+    ri.nent = 0;
     if (re > rs) {
-        tr = parse_trailer(s, rs, re);
-        ok = tr.st == ST_OK;
-        nent = tr.tsize / (tr.big ? 6u : 3u);
+        ri.tr = parse_trailer(s, rs, re);
+        ri.ok = ri.tr.st == ST_OK;
+        ri.nent = ri.tr.tsize / (ri.tr.big ? 6u : 3u);
     }
-    const pos_t tstart = (pos_t)tr.tstart, dstart = (pos_t)tr.dstart;
-    if (ok) {
-        // strictly increasing tags => a probe at the expected index is what binary search finds
+    if (ri.ok) {
+        const pos_t tstart = (pos_t)ri.tr.tstart;
         uint32_t prev = 0;
-        for (uint32_t i = 0; i < nent; i++) {
-            pos_t p = tstart + (pos_t)i * (tr.big ? 6 : 3);
-            uint32_t tg = tr.big ? ((s.u8(p) << 8) | s.u8(p + 1)) : s.u8(p);
-            if (i > 0 && tg <= prev) sorted = false;
+        for (uint32_t i = 0; i < ri.nent; i++) {
+            pos_t p = tstart + (pos_t)i * (ri.tr.big ? 6 : 3);
+            uint32_t tg = ri.tr.big ? ((s.u8(p) << 8) | s.u8(p + 1)) : s.u8(p);
+            if (i > 0 && tg <= prev) ri.sorted = false;
             prev = tg;
         }
     }
-    if (a.status) a.status[r] = (uint8_t)tr.st;
+    return ri;
+}
 
-    for (uint32_t f = 0; f < a.nfields; f++) {
-        uint32_t tag = a.tags[f];
-        long long end = -1;
-        if (ok) {
-            uint32_t k = a.rank[f];
-            bool hit = false;
-            if (sorted && k < nent) {
-                if (tr.big) {
-                    pos_t p = tstart + (pos_t)k * 6;
-                    uint32_t tg = (s.u8(p) << 8) | s.u8(p + 1);
-                    if (tg == tag) {
-                        end = ((long long)s.u8(p + 2) << 24) | (s.u8(p + 3) << 16) | (s.u8(p + 4) << 8) | s.u8(p + 5);
-                        hit = true;
-                    }
-                } else {
-                    pos_t p = tstart + (pos_t)k * 3;
-                    if (s.u8(p) == tag) {
-                        end = (s.u8(p + 1) << 8) | s.u8(p + 2);
-                        hit = true;
-                    }
-                }
+// m.field(tag) (internal/types/msg.go:466-475): the field's end offset relative to the data
+// start, or -1 (absent, or end > dataSize).  k = the tag's index in a Writer's table.
+template <class Src>
+__device__ __forceinline__ long long rec_field_end(const Src &s, const RecInfo &ri, uint32_t tag, uint32_t k) {
+    using pos_t = typename Src::pos_t;
+    if (!ri.ok) return -1;
+    const pos_t tstart = (pos_t)ri.tr.tstart;
+    long long end = -1;
+    bool hit = false;
+    if (ri.sorted && k < ri.nent) {
+        if (ri.tr.big) {
+            pos_t p = tstart + (pos_t)k * 6;
+            uint32_t tg = (s.u8(p) << 8) | s.u8(p + 1);
+            if (tg == tag) {
+                end = ((long long)s.u8(p + 2) << 24) | (s.u8(p + 3) << 16) | (s.u8(p + 4) << 8) | s.u8(p + 5);
+                hit = true;
             }
-            if (!hit) end = table_search(s, tstart, nent, tr.big, tag);
-            if (end > (long long)tr.dsize) end = -1; // m.field: end > dataSize => nil
+        } else {
+            pos_t p = tstart + (pos_t)k * 3;
+            if (s.u8(p) == tag) {
+                end = (s.u8(p + 1) << 8) | s.u8(p + 2);
+                hit = true;
+            }
         }
-        decode_store(s, a.kinds[f], dstart, end, to_stream, a.cols[f], r);
+    }
+    if (!hit) end = table_search(s, tstart, ri.nent, ri.tr.big, tag);
+    if (end > (long long)ri.tr.dsize) end = -1; // m.field: end > dataSize => nil
+    return end;
+}
+
+// Parse record r occupying [rs, re) of the source into fs's columns; to_stream converts a
+// source position to a stream offset (string/bytes spans).  Kind K_LIST fields are skipped.
+template <class Src>
+__device__ __forceinline__ void decode_record_generic(const Src &s, typename Src::pos_t rs, typename Src::pos_t re,
+                                                      uint64_t r, const FieldSet &fs, long long to_stream) {
+    using pos_t = typename Src::pos_t;
+    const RecInfo ri = rec_open(s, rs, re);
+    if (fs.status) fs.status[r] = (uint8_t)ri.tr.st;
+    const pos_t dstart = (pos_t)ri.tr.dstart;
+    for (uint32_t f = 0; f < fs.nfields; f++) {
+        const uint32_t kind = fs.kinds[f];
+        if (kind == K_LIST) continue;
+        const long long end = rec_field_end(s, ri, fs.tags[f], fs.rank[f]);
+        decode_store(s, kind, dstart, end, to_stream, fs.cols[f], r);
     }
 }
 
@@ -430,21 +477,22 @@ struct FieldStore {
 #if defined(SPEC_EXP) && SPEC_EXP == 3 // diagnostic: decode, no column stores
             acc ^= v.v0 ^ v.v1 ^ v.v2 ^ v.v3;
 #else
-            store_value_k<K>(a.cols[F], r, v);
+            store_value_k<K>(a.f.cols[F], r, v);
 #endif
             FieldStore<Spec, F + 1>::run(fr, to_stream, a, r, acc);
         }
     }
 };
 
-// LdsSrc only.  Returns false (nothing written) when the record needs the generic path.
+// Fast path, part 1 (LdsSrc only): trailer, table check and every field's window read into
+// registers.  Returns false (nothing read into fr, nothing written) when the record needs
+// the generic path.  After it returns the record's LDS bytes are no longer needed.
 template <class Spec>
-__device__ __forceinline__ bool decode_record_fast(const LdsSrc &s, int rs, int re, uint64_t r,
-                                                   const DecodeArgs &a, long long to_stream) {
+__device__ __forceinline__ bool fast_prepare(const LdsSrc &s, int rs, int re, FastRec<Spec> &fr) {
     constexpr int N = Spec::N;
     if (re <= rs) return false;
     Trailer tr = parse_trailer(s, rs, re);
-    if (tr.st != ST_OK || tr.big || tr.tsize != 3u * N) return false;
+    if ((tr.st != ST_OK) | tr.big | (tr.tsize != 3u * N)) return false;
     const int ts = (int)tr.tstart;
     // the table's 3N bytes, re-aligned into dwords: w[i] = bytes [ts+4i, ts+4i+4)
     constexpr int NW = (3 * N + 3) / 4;
@@ -468,113 +516,186 @@ __device__ __forceinline__ bool decode_record_fast(const LdsSrc &s, int rs, int 
         uint32_t a1 = hi ? d[i + 2] : d[i + 1];
         w[i] = __builtin_amdgcn_alignbyte(a1, a0, b);
     }
-    // entry k = bytes 3k (tag), 3k+1..3k+2 (end, big-endian)
+    // entry k = bytes 3k (tag), 3k+1..3k+2 (end, big-endian): the table must hold exactly the
+    // Writer's tags (strictly increasing), so binary search would land on entry rank[f]
     auto byte_at = [&](int j) -> uint32_t { return (w[j >> 2] >> (8 * (j & 3))) & 0xff; };
     bool hit = true;
     uint32_t ends[N];
 #pragma unroll
     for (int k = 0; k < N; k++) {
-        hit = hit && byte_at(3 * k) == Spec::stag[k];
+        hit = hit & (byte_at(3 * k) == Spec::stag[k]);
         ends[k] = (byte_at(3 * k + 1) << 8) | byte_at(3 * k + 2);
     }
     if (!hit) return false;
-#if defined(SPEC_EXP) && SPEC_EXP == 2 // diagnostic: trailer + table only
-    if (a.status) a.status[r] = (uint8_t)ends[N - 1];
-    return true;
-#endif
-    if (a.status) a.status[r] = ST_OK;
-    uint64_t acc = 0;
-    FastRec<Spec> fr;
     FieldLoad<Spec, 0>::run(fr, s, (int)tr.dstart, ends, tr.dsize);
+    return true;
+}
+
+// Fast path, part 2: decode every field from registers and store the columns.
+template <class Spec>
+__device__ __forceinline__ void fast_finish(const FastRec<Spec> &fr, uint64_t r, const DecodeArgs &a,
+                                            long long to_stream) {
+    uint64_t acc = 0;
     FieldStore<Spec, 0>::run(fr, to_stream, a, r, acc);
 #if defined(SPEC_EXP) && SPEC_EXP == 3
-    if (a.status) a.status[r] = (uint8_t)(acc ^ (acc >> 8) ^ (acc >> 16) ^ (acc >> 32));
+    if (a.f.status) a.f.status[r] = (uint8_t)(acc ^ (acc >> 8) ^ (acc >> 16) ^ (acc >> 32));
+#else
+    if (a.f.status) a.f.status[r] = ST_OK;
 #endif
-    return true;
 }
 
 // ---- kernel body -------------------------------------------------------------------------
 
-// RECS records per wave (64: one per lane; 32: lanes 32..63 only stage bytes, which halves
-// the slab and doubles the waves a CU holds).
-template <int RECS, int SLAB, class Spec>
+// One wave's group of 64 consecutive records: per-lane record bounds and the wave's span.
+struct Group {
+    uint64_t rec_lo, rec_hi; // this lane's record [rec_lo, rec_hi) in the stream
+    uint64_t aligned_lo;     // span start rounded down to 16 (wave-uniform)
+    uint32_t chunks;         // 1 KiB DMA chunks covering the span (wave-uniform)
+    bool in_lds;             // span fits the slab (wave-uniform)
+};
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    return __builtin_amdgcn_readfirstlane((uint32_t)v) |
+           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+}
+
+// ends[] of group g, as (lo, hi) per lane: lo = ends[r-1] (0 for record 0), hi = ends[r].
+__device__ __forceinline__ void load_group_ends(const DecodeArgs &a, uint64_t base, int lane, uint64_t &lo,
+                                                uint64_t &hi) {
+    const uint64_t r = base + lane;
+    const uint64_t last = a.n - 1;
+    hi = a.ends[r < last ? r : last];
+    lo = r == 0 ? 0 : a.ends[(r - 1) < last ? r - 1 : last];
+}
+
+template <int SLAB>
+__device__ __forceinline__ Group make_group(const DecodeArgs &a, uint64_t base, int lane, uint64_t lo, uint64_t hi) {
+    Group gr;
+    gr.rec_lo = lo;
+    gr.rec_hi = hi < lo ? lo : hi; // malformed ends: treat as empty
+    const uint64_t nrec = a.n - base < 64 ? a.n - base : 64;
+    const uint64_t span_lo = uniform64(__shfl(lo, 0));
+    const uint64_t span_hi = uniform64(__shfl(hi, (int)nrec - 1));
+    gr.aligned_lo = span_lo & ~15ull;
+    const uint64_t bytes = span_hi > gr.aligned_lo ? span_hi - gr.aligned_lo : 0;
+    const uint64_t chunks = (bytes + 1023) >> 10;
+    gr.chunks = (uint32_t)chunks;
+    gr.in_lds = SLAB > 0 && span_hi >= span_lo && SLAB_GUARD + chunks * 1024 + 16 <= (uint64_t)SLAB;
+    return gr;
+}
+
+__device__ __forceinline__ void issue_dma(__amdgpu_buffer_rsrc_t rsrc, uint8_t *slab, const Group &gr, int lane) {
+    for (uint32_t c = 0; c < gr.chunks; c++) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rsrc, (__attribute__((address_space(3))) void *)(slab + SLAB_GUARD + c * 1024), 16,
+            (uint32_t)gr.aligned_lo + c * 1024 + lane * 16, 0, 0, 0);
+    }
+}
+
+// The DMA'd 16-byte chunk holding the stream's last bytes came back zeroed if it straddles
+// the end (whole-access range check): refill it bytewise.
+__device__ __forceinline__ void fix_stream_tail(const DecodeArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint8_t *slab,
+                                                const Group &gr, int lane) {
+    const uint64_t tail = a.stream_len & ~15ull;
+    const uint64_t span_end = gr.aligned_lo + (uint64_t)gr.chunks * 1024;
+    if (tail < a.stream_len && tail >= gr.aligned_lo && tail < span_end) {
+        if (lane < 16 && tail + lane < a.stream_len)
+            slab[SLAB_GUARD + (tail - gr.aligned_lo) + lane] =
+                (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)(tail + lane), 0, 0);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+// Persistent waves: wave w of the grid decodes groups w, w + W, w + 2W, ... (W = waves in the
+// grid, sized by the launcher to what the CUs hold at once).  Per group:
+//   wait for its DMA -> fast_prepare (trailer, table, all field windows into registers) and
+//   the generic path for any rejected record -> the slab is free: issue the NEXT group's DMA
+//   -> decode + store this group from registers while that DMA is in flight.
+template <int SLAB, class Spec>
 __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const uint64_t base = ((uint64_t)blockIdx.x * DEC_WAVES + wave) * RECS;
-    if (base >= a.n) return;
-    const uint64_t r = base + lane;
-    const bool valid = lane < RECS && r < a.n;
-    const uint64_t last = (a.n - base) < RECS ? a.n - 1 : base + RECS - 1;
-
-    uint64_t rec_hi = valid ? a.ends[r] : 0;
-    uint64_t prev = __shfl_up(rec_hi, 1);
-    if (lane == 0) prev = base ? a.ends[base - 1] : 0;
-    const uint64_t rec_lo = prev;
-    const uint64_t span_lo = __builtin_amdgcn_readfirstlane((uint32_t)rec_lo) |
-                             ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(rec_lo >> 32)) << 32);
-    const uint64_t span_hi_v = __shfl(rec_hi, (int)(last - base));
-    const uint64_t span_hi = __builtin_amdgcn_readfirstlane((uint32_t)span_hi_v) |
-                             ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(span_hi_v >> 32)) << 32);
-
+    const uint64_t ngroups = (a.n + 63) / 64;
+    const uint64_t stride = (uint64_t)gridDim.x * DEC_WAVES;
+    uint64_t g = (uint64_t)blockIdx.x * DEC_WAVES + wave;
+    if (g >= ngroups) return;
+    uint8_t *slab = smem + wave * (SLAB > 0 ? SLAB : 0);
     __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
 
-    const uint64_t aligned_lo = span_lo & ~15ull;
-    if constexpr (SLAB > 0) {
-        const uint64_t bytes = span_hi - aligned_lo;
-        const uint64_t chunks = (bytes + 1023) >> 10;
-        if (span_hi >= span_lo && SLAB_GUARD + chunks * 1024 + 16 <= (uint64_t)SLAB) {
-            uint8_t *slab = smem + wave * SLAB;
-            for (uint32_t c = 0; c < (uint32_t)chunks; c++) {
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rsrc, (__attribute__((address_space(3))) void *)(slab + SLAB_GUARD + c * 1024), 16,
-                    (uint32_t)aligned_lo + c * 1024 + lane * 16, 0, 0, 0);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            // the 16-byte chunk holding the stream's last bytes came back zeroed if it
-            // straddles the end (whole-access range check): refill it bytewise
-            const uint64_t tail = a.stream_len & ~15ull;
-            if (tail < a.stream_len && tail >= aligned_lo && tail < span_hi) {
-                if (lane < 16 && tail + lane < a.stream_len)
-                    slab[SLAB_GUARD + (tail - aligned_lo) + lane] =
-                        (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)(tail + lane), 0, 0);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
+    uint64_t lo, hi;
+    load_group_ends(a, g * 64, lane, lo, hi);
+    Group cur = make_group<SLAB>(a, g * 64, lane, lo, hi);
+    if (cur.in_lds) issue_dma(rsrc, slab, cur, lane);
+
+    while (true) {
+        const uint64_t base = g * 64;
+        const uint64_t r = base + lane;
+        const bool valid = r < a.n;
+        const uint64_t gn = g + stride;
+        const bool has_next = gn < ngroups;
+        uint64_t nlo = 0, nhi = 0;
+        if (has_next) load_group_ends(a, gn * 64, lane, nlo, nhi);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        Group nxt = make_group<SLAB>(a, has_next ? gn * 64 : base, lane, nlo, nhi);
+
+        if (cur.in_lds) {
+            fix_stream_tail(a, rsrc, slab, cur, lane);
+            LdsSrc s{(lds_u8 *)slab};
+            const int rs = SLAB_GUARD + (int)(cur.rec_lo - cur.aligned_lo);
+            const int re = SLAB_GUARD + (int)(cur.rec_hi - cur.aligned_lo);
+            const long long to_stream = (long long)cur.aligned_lo - SLAB_GUARD;
 #if defined(SPEC_EXP) && SPEC_EXP == 1 // diagnostic: staging only
-            if (valid && a.status) a.status[r] = slab[SLAB_GUARD + (rec_hi - aligned_lo) - 1];
-            return;
-#endif
-            if (valid) {
-                LdsSrc s{(lds_u8 *)slab};
-                int rs = SLAB_GUARD + (int)(rec_lo - aligned_lo);
-                int re = SLAB_GUARD + (int)(rec_hi - aligned_lo);
-                if (rec_hi < rec_lo) re = rs; // malformed ends: treat as empty
-                const long long to_stream = (long long)aligned_lo - SLAB_GUARD;
-                bool done = false;
-                if constexpr (Spec::N > 0) done = decode_record_fast<Spec>(s, rs, re, r, a, to_stream);
-                if (!done) decode_record_generic(s, rs, re, r, a, to_stream);
+            if (valid && a.f.status) a.f.status[r] = slab[re - 1];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (has_next && nxt.in_lds) issue_dma(rsrc, slab, nxt, lane);
+#else
+            if constexpr (Spec::N > 0) {
+                FastRec<Spec> fr;
+                bool fast = valid && fast_prepare<Spec>(s, rs, re, fr);
+                if (valid && !fast) decode_record_generic(s, rs, re, r, a.f, to_stream);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // every LDS read of this group done
+                if (has_next && nxt.in_lds) issue_dma(rsrc, slab, nxt, lane);
+                if (fast) fast_finish<Spec>(fr, r, a, to_stream);
+            } else {
+                if (valid) decode_record_generic(s, rs, re, r, a.f, to_stream);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (has_next && nxt.in_lds) issue_dma(rsrc, slab, nxt, lane);
             }
-            return;
+#endif
+        } else {
+            if (has_next && nxt.in_lds) issue_dma(rsrc, slab, nxt, lane);
+            if (valid) {
+                GlobalSrc s{rsrc, a.stream_len};
+                decode_record_generic(s, (long long)cur.rec_lo, (long long)cur.rec_hi, r, a.f, 0);
+            }
         }
-    }
-    if (valid) {
-        GlobalSrc s{rsrc, a.stream_len};
-        long long rs = (long long)rec_lo, re = (long long)rec_hi;
-        if (re < rs) re = rs;
-        decode_record_generic(s, rs, re, r, a, 0);
+        if (!has_next) break;
+        g = gn;
+        cur = nxt;
     }
 }
 
-// slab class shared by the launchers (host): average record size * RECS * margin; 3 = none
-__host__ __device__ inline int decode_slab_class(double avg_record, int recs) {
-    double span = avg_record * recs * 1.08 + 64.0;
+// slab class shared by the launchers (host): average record size * 64 * margin; 3 = none
+__host__ __device__ inline int decode_slab_class(double avg_record) {
+    double span = avg_record * 64 * 1.08 + 64.0;
     for (int c = 0; c < 3; c++)
-        if (span <= slab_chunks(recs, c) * 1024) return c;
+        if (span <= slab_chunks(c) * 1024) return c;
     return 3;
+}
+
+// Grid for the persistent decode: as many 4-wave blocks as the CUs hold at once (LDS-bound),
+// never more than the groups need.
+__host__ inline unsigned decode_grid(uint64_t n, int cus, int slab) {
+    const uint64_t groups = (n + 63) / 64;
+    const uint64_t need = (groups + DEC_WAVES - 1) / DEC_WAVES;
+    int per_cu = slab > 0 ? (160 * 1024) / (DEC_WAVES * slab) : 8;
+    per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
+    const uint64_t cap = (uint64_t)cus * per_cu;
+    return (unsigned)(need < cap ? need : cap);
 }
 
 } // namespace spec

@@ -8,23 +8,32 @@
 
 namespace spec {
 
-constexpr int GENERIC_RECS = 64;
-
 template <int SLAB>
 __global__ __launch_bounds__(256) void decode_flat_kernel(DecodeArgs a) {
-    decode_flat_body<GENERIC_RECS, SLAB, RuntimeSpec>(a);
+    decode_flat_body<SLAB, RuntimeSpec>(a);
+}
+
+int device_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev]) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        cus[dev] = v;
+    }
+    return cus[dev];
 }
 
 int launch_decode_flat(const DecodeArgs &a, double avg_record, hipStream_t stream) {
-    constexpr int R = GENERIC_RECS;
-    uint64_t waves = (a.n + R - 1) / R;
-    uint64_t blocks = (waves + DEC_WAVES - 1) / DEC_WAVES;
-    if (blocks == 0) return 0;
-    dim3 grid((unsigned)blocks), block(256);
-    switch (decode_slab_class(avg_record, R)) {
-    case 0: hipLaunchKernelGGL(decode_flat_kernel<slab_bytes(R, 0)>, grid, block, DEC_WAVES * slab_bytes(R, 0), stream, a); break;
-    case 1: hipLaunchKernelGGL(decode_flat_kernel<slab_bytes(R, 1)>, grid, block, DEC_WAVES * slab_bytes(R, 1), stream, a); break;
-    case 2: hipLaunchKernelGGL(decode_flat_kernel<slab_bytes(R, 2)>, grid, block, DEC_WAVES * slab_bytes(R, 2), stream, a); break;
+    if (a.n == 0) return 0;
+    const int cls = decode_slab_class(avg_record);
+    const int slab = cls < 3 ? slab_bytes(cls) : 0;
+    dim3 grid(decode_grid(a.n, device_cus(), slab)), block(256);
+    switch (cls) {
+    case 0: hipLaunchKernelGGL(decode_flat_kernel<slab_bytes(0)>, grid, block, DEC_WAVES * slab_bytes(0), stream, a); break;
+    case 1: hipLaunchKernelGGL(decode_flat_kernel<slab_bytes(1)>, grid, block, DEC_WAVES * slab_bytes(1), stream, a); break;
+    case 2: hipLaunchKernelGGL(decode_flat_kernel<slab_bytes(2)>, grid, block, DEC_WAVES * slab_bytes(2), stream, a); break;
     default: hipLaunchKernelGGL(decode_flat_kernel<0>, grid, block, 0, stream, a); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;

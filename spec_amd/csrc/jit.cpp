@@ -78,23 +78,14 @@ bool has_fast_path(const spec_schema *s) {
     return true;
 }
 
-// records per wave of the specialised kernels (SPEC_AMD_RECS=64|32, default 64)
-int recs_per_wave() {
-    static int r = [] {
-        const char *e = getenv("SPEC_AMD_RECS");
-        return (e && atoi(e) == 32) ? 32 : 64;
-    }();
-    return r;
-}
-
-std::string key_of(const spec_schema *s, int recs, int slab_class, int device) {
+std::string key_of(const spec_schema *s, int slab_class, int device) {
     std::ostringstream k;
-    k << device << ':' << recs << ':' << slab_class << ':';
+    k << device << ':' << slab_class << ':';
     for (uint32_t f = 0; f < s->nfields; f++) k << s->fields[f].tag << '/' << (int)s->fields[f].kind << ',';
     return k.str();
 }
 
-std::string generate(const spec_schema *s, int recs, int slab) {
+std::string generate(const spec_schema *s, int slab) {
     uint8_t order[SPEC_MAX_FIELDS];
     uint16_t sorted[SPEC_MAX_FIELDS];
     writer_order(s, order, sorted);
@@ -111,13 +102,13 @@ std::string generate(const spec_schema *s, int recs, int slab) {
     for (uint32_t k = 0; k < s->nfields; k++) o << (k ? "," : "") << sorted[k];
     o << "};\n};\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void spec_decode_flat_jit(spec::DecodeArgs a) {\n"
-      << "  spec::decode_flat_body<" << recs << ", " << slab << ", GenSpec>(a);\n}\n";
+      << "  spec::decode_flat_body<" << slab << ", GenSpec>(a);\n}\n";
     return o.str();
 }
 
 // hiprtc compile only; returns the code object (empty on failure)
-std::vector<char> compile_code(const spec_schema *s, int recs, int slab) {
-    std::string src = generate(s, recs, slab);
+std::vector<char> compile_code(const spec_schema *s, int slab) {
+    std::string src = generate(s, slab);
     const char *hdr_src[2] = {kSpecDeviceHpp, kDecodeCoreHpp};
     const char *hdr_name[2] = {"spec_device.hpp", "decode_core.hpp"};
     hiprtcProgram prog;
@@ -151,9 +142,9 @@ std::vector<char> compile_code(const spec_schema *s, int recs, int slab) {
     return code;
 }
 
-Entry compile(const spec_schema *s, int recs, int slab) {
+Entry compile(const spec_schema *s, int slab) {
     Entry e;
-    std::vector<char> code = compile_code(s, recs, slab);
+    std::vector<char> code = compile_code(s, slab);
     if (code.empty()) {
         e.failed = true;
         return e;
@@ -168,15 +159,15 @@ Entry compile(const spec_schema *s, int recs, int slab) {
 }
 
 // nullptr => use the generic kernel
-hipFunction_t lookup(const spec_schema *s, int recs, int slab_class) {
+hipFunction_t lookup(const spec_schema *s, int slab_class) {
     if (slab_class > 2 || !enabled() || !has_fast_path(s)) return nullptr;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::string k = key_of(s, recs, slab_class, dev);
+    std::string k = key_of(s, slab_class, dev);
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_cache.find(k);
     if (it == g_cache.end()) {
-        Entry e = compile(s, recs, spec::slab_bytes(recs, slab_class));
+        Entry e = compile(s, spec::slab_bytes(slab_class));
         if (e.failed && debug()) fprintf(stderr, "spec_amd jit: compile/load failed, generic kernel in use\n");
         it = g_cache.emplace(k, e).first;
     }
@@ -190,30 +181,26 @@ namespace spec {
 void jit_set_enabled(int on) { g_enabled = on ? 1 : 0; }
 
 long long jit_compile_only(const spec_schema *schema, double avg_record) {
-    const int recs = recs_per_wave();
-    const int cls = decode_slab_class(avg_record, recs);
+    const int cls = decode_slab_class(avg_record);
     if (cls > 2 || !has_fast_path(schema)) return 0;
-    return (long long)compile_code(schema, recs, slab_bytes(recs, cls)).size();
+    return (long long)compile_code(schema, slab_bytes(cls)).size();
 }
 
 int jit_prepare_decode_flat(const spec_schema *schema, double avg_record) {
-    const int recs = recs_per_wave();
-    return lookup(schema, recs, decode_slab_class(avg_record, recs)) ? 1 : 0;
+    return lookup(schema, decode_slab_class(avg_record)) ? 1 : 0;
 }
 
 int jit_launch_decode_flat(const spec_schema *schema, const DecodeArgs &a, double avg_record, hipStream_t stream) {
-    const int recs = recs_per_wave();
-    const int cls = decode_slab_class(avg_record, recs);
-    hipFunction_t fn = lookup(schema, recs, cls);
+    const int cls = decode_slab_class(avg_record);
+    hipFunction_t fn = lookup(schema, cls);
     if (!fn) return 0;
-    uint64_t waves = (a.n + recs - 1) / recs;
-    uint64_t blocks = (waves + DEC_WAVES - 1) / DEC_WAVES;
-    if (blocks == 0) return 1;
+    if (a.n == 0) return 1;
+    const unsigned blocks = decode_grid(a.n, device_cus(), slab_bytes(cls));
     DecodeArgs args = a;
     size_t size = sizeof(args);
     void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                      HIP_LAUNCH_PARAM_END};
-    hipError_t e = hipModuleLaunchKernel(fn, (unsigned)blocks, 1, 1, 256, 1, 1, DEC_WAVES * slab_bytes(recs, cls), stream,
+    hipError_t e = hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, DEC_WAVES * slab_bytes(cls), stream,
                                          nullptr, extra);
     return e == hipSuccess ? 1 : -1;
 }

@@ -50,6 +50,7 @@ enum : uint32_t {
 enum : uint32_t {
     K_BOOL = 1, K_BYTE, K_INT16, K_INT32, K_INT64, K_UINT16, K_UINT32, K_UINT64,
     K_FLOAT32, K_FLOAT64, K_BIN64, K_BIN128, K_BIN256, K_STRING, K_BYTES,
+    K_LIST, // list<message> field of a nested schema (spec_decode_nested); no flat column
 };
 
 // ---- record status (include/spec_amd.h spec_status)

@@ -32,6 +32,9 @@ struct EncodeArgs {
 };
 
 int launch_decode_flat(const DecodeArgs &a, double avg_record, hipStream_t stream);
+int device_cus(); // CUs of the current device (cached)
+int launch_nested_index(const NestedArgs &a, double avg_record, hipStream_t stream);
+int launch_nested_decode(const NestedArgs &a, double avg_record, hipStream_t stream);
 // jit.cpp: schema-specialised decode kernel (hiprtc); returns 1 if launched, 0 if the caller
 // should launch the generic kernel, <0 on a HIP error.
 int jit_launch_decode_flat(const spec_schema *schema, const DecodeArgs &a, double avg_record, hipStream_t stream);

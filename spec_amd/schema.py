@@ -31,12 +31,14 @@ class Kind(enum.IntEnum):
     BIN256 = 13
     STRING = 14
     BYTES = 15
+    LIST = 16  # list<message> field of a NestedSchema's outer message (column = item_begin)
 
 
 WIDTH = {
     Kind.BOOL: 1, Kind.BYTE: 1, Kind.INT16: 2, Kind.INT32: 4, Kind.INT64: 8,
     Kind.UINT16: 2, Kind.UINT32: 4, Kind.UINT64: 8, Kind.FLOAT32: 4, Kind.FLOAT64: 8,
     Kind.BIN64: 8, Kind.BIN128: 16, Kind.BIN256: 32, Kind.STRING: 8, Kind.BYTES: 8,
+    Kind.LIST: 0,
 }
 
 # numpy view of one column element (bins stay raw bytes)
@@ -45,7 +47,7 @@ NP_DTYPE = {
     Kind.INT64: np.int64, Kind.UINT16: np.uint16, Kind.UINT32: np.uint32,
     Kind.UINT64: np.uint64, Kind.FLOAT32: np.uint32, Kind.FLOAT64: np.uint64,
     Kind.BIN64: np.uint8, Kind.BIN128: np.uint8, Kind.BIN256: np.uint8,
-    Kind.STRING: np.uint32, Kind.BYTES: np.uint32,
+    Kind.STRING: np.uint32, Kind.BYTES: np.uint32, Kind.LIST: np.uint32,
 }
 
 VARLEN = (Kind.STRING, Kind.BYTES)
@@ -114,3 +116,30 @@ FLAT16 = Schema([
     Field(15, Kind.BYTES, "bytes"),
     Field(16, Kind.INT64, "int64b"),
 ])
+
+
+class NestedSchema:
+    """A message with one list<message> field (include/spec_amd.h spec_nested_schema):
+    `outer` in write order with exactly one Kind.LIST field, `item` the list items' fields."""
+
+    def __init__(self, outer, item):
+        from ._lib import SpecNestedSchema
+
+        self.outer = Schema(outer) if not isinstance(outer, Schema) else outer
+        self.item = Schema(item) if not isinstance(item, Schema) else item
+        lists = [i for i, f in enumerate(self.outer.fields) if f.kind == Kind.LIST]
+        if len(lists) != 1 or any(f.kind == Kind.LIST for f in self.item.fields):
+            raise ValueError("outer needs exactly one Kind.LIST field; items must be flat")
+        self.list_field = lists[0]
+        self.c = SpecNestedSchema()
+        self.c.outer = self.outer.c
+        self.c.item = self.item.c
+
+
+# SURVEY.md §8(d) "Nested" (config 4): outer {1 bin128 id, 2 int64 seq, 3 string name,
+# 4 list<Item>}, Item {1 int32 key, 2 float64 value, 3 string label}.
+NESTED = NestedSchema(
+    [Field(1, Kind.BIN128, "id"), Field(2, Kind.INT64, "seq"), Field(3, Kind.STRING, "name"),
+     Field(4, Kind.LIST, "items")],
+    [Field(1, Kind.INT32, "key"), Field(2, Kind.FLOAT64, "value"), Field(3, Kind.STRING, "label")],
+)

@@ -1,0 +1,160 @@
+"""GPU parity for list<message> decode (BASELINE config 4) against the CPU oracle: outer
+columns + status, the item_begin index and item columns + item status, bit for bit."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+import spec_amd
+from oracle import oracle as O
+from spec_amd import NESTED, Kind, workload
+from tests.gpu_helpers import concat_records, to_dev
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def check_nested(dev, stream, ends, label=""):
+    import torch
+
+    stream = np.ascontiguousarray(stream, dtype=np.uint8)
+    ends = np.ascontiguousarray(ends, dtype=np.uint64)
+    want = O.decode_nested_batch(stream, ends)
+    d_stream = to_dev(stream if stream.size else np.zeros(1, np.uint8), dev)[: stream.size]
+    got = spec_amd.decode_nested(NESTED, d_stream, to_dev(ends.view(np.int64), dev))
+    torch.cuda.synchronize()
+    n = len(ends)
+    assert np.array_equal(got.status.cpu().numpy(), want["status"]), label + ": status"
+    assert np.array_equal(got.item_begin.cpu().numpy().view(np.uint32), want["item_begin"]), label + ": item_begin"
+    m = int(want["item_begin"][-1]) if n else 0
+    assert got.total_items == m, label
+    assert np.array_equal(got.outer[0].cpu().numpy(), want["id"]), label + ": id"
+    assert np.array_equal(got.outer[1].cpu().numpy().view(np.int64).ravel(), want["seq"]), label + ": seq"
+    assert np.array_equal(got.outer[2].cpu().numpy().view(np.uint32), want["name"]), label + ": name"
+    if m:
+        assert np.array_equal(got.item_status.cpu().numpy()[:m], want["item_status"]), label + ": item_status"
+        assert np.array_equal(got.items[0].cpu().numpy().view(np.int32).ravel(), want["key"]), label + ": key"
+        assert np.array_equal(got.items[1].cpu().numpy().view(np.uint64).ravel(),
+                              want["value"].view(np.uint64)), label + ": value"
+        assert np.array_equal(got.items[2].cpu().numpy().view(np.uint32), want["label"]), label + ": label"
+    return got, want
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 5000])
+def test_nested_parity(dev, n):
+    w = workload.nested(n, seed=n)
+    stream, ends = O.encode_nested_batch(w)
+    check_nested(dev, stream, ends, f"nested n={n}")
+
+
+def test_nested_golden(dev):
+    g = np.load(os.path.join(GOLDEN, "nested_small.npz"), allow_pickle=False)
+    got, _ = check_nested(dev, g["stream"], g["ends"], "golden")
+    assert np.array_equal(got.item_begin.cpu().numpy().view(np.uint32), g["out_item_begin"])
+
+
+def test_nested_full_size(dev):
+    """BASELINE config 4 at full size: 1M records."""
+    n = 1 << 20
+    w = workload.nested(n)
+    stream, ends = O.encode_nested_batch(w)
+    check_nested(dev, stream, ends, "nested 1M")
+
+
+def _record(items, name="nm", list_tag=4, extra=None):
+    wr = O.Writer()
+    wr.message()
+    wr.field(1, "bin128", bytes(range(16)))
+    wr.field(2, "int64", -7)
+    wr.field(3, "string", name)
+    if items is not None:
+        wr.field_list(list_tag)
+        for k, v, lab in items:
+            wr.elem_message()
+            wr.field(1, "int32", k)
+            wr.field(2, "float64", v)
+            wr.field(3, "string", lab)
+            assert wr.end()[1] is None
+        assert wr.end()[1] is None
+    if extra:
+        for tag, kind, v in extra:
+            wr.field(tag, kind, v)
+    b, err = wr.end()
+    assert err is None, err
+    return b
+
+
+def test_nested_edge_cases(dev):
+    """No list field, empty list, a big list (> 255 items), the list under another tag, items
+    with missing/extra fields, garbage records and truncated records."""
+    recs = [
+        _record(None),
+        _record([]),
+        _record([(i, i * 0.5, "x" * (i % 7)) for i in range(300)]),
+        _record([(1, 1.0, "a")], list_tag=9),
+        _record([(2, 2.0, "bb"), (3, -3.0, "")], extra=[(5, "int32", 1)]),
+        b"",
+        bytes([1, 2, 3, 80]),
+    ]
+    good = _record([(4, 4.0, "cccc")] * 3)
+    recs.append(good[: len(good) // 2])
+    recs.append(good)
+    # item messages written by hand: item with only field 2, item that is an int64 not a message
+    wr = O.Writer()
+    wr.message()
+    wr.field_list(4)
+    wr.elem_message()
+    wr.field(2, "float64", 9.5)
+    wr.end()
+    wr.elem_int64(12345)
+    wr.end()
+    b, err = wr.end()
+    assert err is None
+    recs.append(b)
+    stream, ends = concat_records(recs * 20)
+    check_nested(dev, stream, ends, "edge")
+
+
+def test_nested_malformed_list_tables(dev):
+    """List tables whose element ends decrease (Go panics on the slice => SPEC_STATUS_PANIC
+    for that item) or exceed the list's data size (nil items)."""
+    item = _record([(1, 1.0, "a")])
+    # build list bytes by hand: two items, then a table with swapped ends
+    it1, _, _ = O.encode("int64", 5)
+    it2, _, _ = O.encode("int64", 6)
+    data = it1 + it2
+    for offs in ([len(data), len(it1)], [len(it1), len(data) + 100], [len(it1), len(data)]):
+        lst_trailer, _, err = O.encode_list_table(len(data), offs)
+        assert err is None
+        lst = data + lst_trailer
+        fields = [(4, len(lst))]
+        msg_trailer, _, _ = O.encode_message_table(len(lst), fields)
+        rec = lst + msg_trailer
+        stream, ends = concat_records([item, rec, item] * 30)
+        check_nested(dev, stream, ends, f"malformed {offs}")
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_nested_fuzz(dev, seed):
+    rng = np.random.default_rng(500 + seed)
+    n = 2000
+    w = workload.nested(n, seed=seed)
+    stream, ends = O.encode_nested_batch(w)
+    recs = [bytes(stream[(int(ends[i - 1]) if i else 0):int(ends[i])]) for i in range(n)]
+    out = []
+    for r in recs:
+        b = bytearray(r)
+        x = rng.integers(0, 5)
+        if x == 0:
+            for _ in range(rng.integers(1, 4)):
+                b[rng.integers(0, len(b))] = rng.integers(0, 256)
+        elif x == 1:
+            b = b[rng.integers(0, len(b)):]
+        elif x == 2:
+            b = b[:rng.integers(0, len(b))]
+        out.append(bytes(b))
+    s2, e2 = concat_records(out)
+    check_nested(dev, s2, e2, f"fuzz {seed}")
