@@ -139,6 +139,13 @@ int spec_decode_flat(const spec_schema *schema, const uint8_t *stream_bytes, uin
                      const uint64_t *ends, uint64_t n, void *const *columns, uint8_t *status,
                      void *stream);
 
+/* spec_decode_flat_range: records [r0, r1) of a batch only — stream_bytes/stream_len/ends
+ * describe the WHOLE batch (absolute offsets) and columns/status are indexed by record, so a
+ * host pipeline can decode chunk k while chunk k+1 is still being copied in. */
+int spec_decode_flat_range(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
+                           const uint64_t *ends, uint64_t r0, uint64_t r1, void *const *columns, uint8_t *status,
+                           void *stream);
+
 /* spec_decode_flat_prepare: compile (once per device, schema and record-size class) the
  * schema-specialised decode kernel that spec_decode_flat uses when one exists — the
  * analogue of the reference's generated readers (internal/lang/generator/message.go:97-186).
@@ -193,6 +200,22 @@ int spec_encode_flat(const spec_schema *schema, const void *const *columns,
                      const uint8_t *const *heaps, const uint64_t *heap_lens, uint64_t n,
                      uint8_t *out, uint64_t out_cap, uint64_t *ends, void *workspace,
                      size_t workspace_size, uint64_t *total, void *stream);
+
+/* ---- nested encode (list<message>) ----
+ * For every record i, what a generated Write() does (writer_list_msg.go:8-47): the outer
+ * fields in write order; at the SPEC_KIND_LIST field, w.Field(tag).List(), then for each
+ * item k in [item_begin[i], item_begin[i+1]) l.Add() + the item fields + End(); l.End();
+ * finally Build().  Items come from item_columns (nitems rows); string/bytes columns index
+ * the matching heaps.  Writes out[], ends[] and *total (device); with out == NULL only
+ * *total is computed.  If the total exceeds out_cap nothing is written; an encoder error
+ * (string/bytes > MaxSize or outside its heap, item_begin not monotonic or > nitems) makes
+ * *total all-ones.  Workspace: spec_encode_nested_workspace_size(n) bytes. */
+size_t spec_encode_nested_workspace_size(uint64_t n);
+int spec_encode_nested(const spec_nested_schema *schema, const void *const *outer_columns,
+                       const uint8_t *const *outer_heaps, const uint64_t *outer_heap_lens, const uint32_t *item_begin,
+                       const void *const *item_columns, const uint8_t *const *item_heaps,
+                       const uint64_t *item_heap_lens, uint64_t nitems, uint64_t n, uint8_t *out, uint64_t out_cap,
+                       uint64_t *ends, void *workspace, size_t workspace_size, uint64_t *total, void *stream);
 
 #ifdef __cplusplus
 }

@@ -7,11 +7,13 @@ decoded into SoA columns / encoded from them by hand-written gfx950 kernels
 """
 from ._lib import LIB_PATH, SpecError, header_symbols, lib, set_jit
 from .batch import Columns, Decoder, Encoder, alloc_columns, decode_flat, encode_flat
-from .nested import NestedColumns, NestedDecoder, decode_nested
+from .pipeline import HostDecoder
+from .nested import NestedColumns, NestedDecoder, NestedEncoder, decode_nested, encode_nested
 from .schema import FLAT16, NESTED, Field, Kind, NestedSchema, Schema
 
 __all__ = [
-    "LIB_PATH", "SpecError", "header_symbols", "lib", "set_jit", "Columns", "Decoder", "Encoder", "alloc_columns",
+    "HostDecoder", "LIB_PATH", "SpecError", "header_symbols", "lib", "set_jit", "Columns", "Decoder", "Encoder", "alloc_columns",
     "decode_flat", "encode_flat", "FLAT16", "Field", "Kind", "Schema",
-    "NESTED", "NestedSchema", "NestedColumns", "NestedDecoder", "decode_nested",
+    "NESTED", "NestedSchema", "NestedColumns", "NestedDecoder", "NestedEncoder", "decode_nested",
+    "encode_nested",
 ]

@@ -58,6 +58,8 @@ def _declare(L):
     L.spec_last_hip_error.restype = C.c_int
     L.spec_decode_flat.argtypes = [C.POINTER(SpecSchema), vp, C.c_uint64, vp, C.c_uint64,
                                    C.POINTER(vp), vp, vp]
+    L.spec_decode_flat_range.argtypes = [C.POINTER(SpecSchema), vp, C.c_uint64, vp, C.c_uint64, C.c_uint64,
+                                         C.POINTER(vp), vp, vp]
     L.spec_decode_flat_prepare.argtypes = [C.POINTER(SpecSchema), C.c_uint64, C.c_uint64]
     L.spec_set_jit.argtypes = [C.c_int]
     L.spec_set_jit.restype = None
@@ -69,6 +71,18 @@ def _declare(L):
                                            C.c_size_t, vp, vp]
     L.spec_decode_nested.argtypes = [C.POINTER(SpecNestedSchema), vp, C.c_uint64, vp, C.c_uint64,
                                      C.POINTER(vp), vp, vp, C.POINTER(vp), vp, C.c_uint64, vp, C.c_size_t, vp]
+    L.spec_encode_nested_workspace_size.restype = C.c_size_t
+    L.spec_encode_nested_workspace_size.argtypes = [C.c_uint64]
+    L.spec_encode_nested.argtypes = [C.POINTER(SpecNestedSchema), C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_uint64),
+                                     vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_uint64), C.c_uint64, C.c_uint64,
+                                     vp, C.c_uint64, vp, vp, C.c_size_t, vp, vp]
+    for name in ("spec_device_free", "spec_host_free", "spec_stream_destroy", "spec_stream_sync"):
+        getattr(L, name).argtypes = [vp]
+    L.spec_device_alloc.argtypes = [C.c_size_t, C.POINTER(vp)]
+    L.spec_host_alloc.argtypes = [C.c_size_t, C.POINTER(vp)]
+    L.spec_stream_create.argtypes = [C.POINTER(vp)]
+    for name in ("spec_copy_h2d", "spec_copy_d2h", "spec_copy_d2d"):
+        getattr(L, name).argtypes = [vp, vp, C.c_size_t, vp]
     L.spec_encode_flat_workspace_size.restype = C.c_size_t
     L.spec_encode_flat_workspace_size.argtypes = [C.c_uint64]
     L.spec_encode_flat_size.argtypes = [C.POINTER(SpecSchema), C.POINTER(vp), C.c_uint64, vp,

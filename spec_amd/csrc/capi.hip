@@ -87,17 +87,22 @@ void fill_field_set(spec::FieldSet &fs, const spec_schema *schema, void *const *
     }
 }
 
+void fill_enc_fields(spec::EncFields &e, const spec_schema *schema, const void *const *columns) {
+    memset(&e, 0, sizeof(e));
+    e.nfields = schema->nfields;
+    for (uint32_t f = 0; f < schema->nfields; f++) {
+        e.tags[f] = schema->fields[f].tag;
+        e.kinds[f] = schema->fields[f].kind;
+        e.cols[f] = columns ? columns[f] : nullptr;
+        if (schema->fields[f].tag > 255) e.table_big_forced = 1;
+    }
+    table_order(schema, e.order);
+}
+
 void fill_encode_args(spec::EncodeArgs &a, const spec_schema *schema, const void *const *columns, uint64_t n) {
     memset(&a, 0, sizeof(a));
     a.n = n;
-    a.nfields = schema->nfields;
-    for (uint32_t f = 0; f < schema->nfields; f++) {
-        a.tags[f] = schema->fields[f].tag;
-        a.kinds[f] = schema->fields[f].kind;
-        a.cols[f] = columns[f];
-        if (schema->fields[f].tag > 255) a.table_big_forced = 1;
-    }
-    table_order(schema, a.order);
+    fill_enc_fields(a.f, schema, columns);
     a.nblocks = (n + spec::ENC_BLOCK - 1) / spec::ENC_BLOCK;
 }
 
@@ -150,12 +155,13 @@ int spec_copy_d2d(void *dst, const void *src, size_t bytes, void *stream) {
     return hip_rc(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
 }
 
-int spec_decode_flat(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
-                     const uint64_t *ends, uint64_t n, void *const *columns, uint8_t *status,
-                     void *stream) {
+int spec_decode_flat_range(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
+                           const uint64_t *ends, uint64_t r0, uint64_t r1, void *const *columns, uint8_t *status,
+                           void *stream) {
     int rc = check_schema(schema);
     if (rc) return rc;
-    if (n == 0) return SPEC_OK;
+    if (r1 < r0) return SPEC_E_INVALID_ARGUMENT;
+    if (r1 == r0) return SPEC_OK;
     if (!ends || !columns || (!stream_bytes && stream_len)) return SPEC_E_INVALID_ARGUMENT;
     if (stream_len >= (1ull << 32)) return SPEC_E_TOO_LARGE;
     for (uint32_t f = 0; f < schema->nfields; f++)
@@ -165,13 +171,22 @@ int spec_decode_flat(const spec_schema *schema, const uint8_t *stream_bytes, uin
     a.stream = stream_bytes;
     a.stream_len = stream_len;
     a.ends = ends;
-    a.n = n;
+    a.n = r1;
+    a.r0 = r0;
     fill_field_set(a.f, schema, columns, status);
-    double avg = (double)stream_len / (double)n;
+    // slab class from the whole batch's mean record size (ends[r1-1] bytes over r1 records is
+    // not known on the host; stream_len / r1 is the same figure for a full batch)
+    double avg = (double)stream_len / (double)r1;
     int j = spec::jit_launch_decode_flat(schema, a, avg, (hipStream_t)stream);
     if (j < 0) return hip_rc(hipGetLastError());
     if (j == 0 && spec::launch_decode_flat(a, avg, (hipStream_t)stream)) return hip_rc(hipGetLastError());
     return SPEC_OK;
+}
+
+int spec_decode_flat(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
+                     const uint64_t *ends, uint64_t n, void *const *columns, uint8_t *status,
+                     void *stream) {
+    return spec_decode_flat_range(schema, stream_bytes, stream_len, ends, 0, n, columns, status, stream);
 }
 
 int spec_decode_flat_prepare(const spec_schema *schema, uint64_t stream_len, uint64_t n) {
@@ -254,6 +269,55 @@ int spec_decode_nested(const spec_nested_schema *schema, const uint8_t *stream_b
     return SPEC_OK;
 }
 
+size_t spec_encode_nested_workspace_size(uint64_t n) { return spec_encode_flat_workspace_size(n); }
+
+static int heaps_of(spec::EncFields &e, const spec_schema *s, const uint8_t *const *heaps, const uint64_t *lens) {
+    for (uint32_t f = 0; f < s->nfields; f++) {
+        int k = s->fields[f].kind;
+        if (k == SPEC_KIND_STRING || k == SPEC_KIND_BYTES) {
+            if (!heaps || !lens || (!heaps[f] && lens[f])) return SPEC_E_INVALID_ARGUMENT;
+            e.heaps[f] = heaps[f];
+            e.heap_lens[f] = lens[f];
+        }
+    }
+    return SPEC_OK;
+}
+
+int spec_encode_nested(const spec_nested_schema *schema, const void *const *outer_columns,
+                       const uint8_t *const *outer_heaps, const uint64_t *outer_heap_lens, const uint32_t *item_begin,
+                       const void *const *item_columns, const uint8_t *const *item_heaps,
+                       const uint64_t *item_heap_lens, uint64_t nitems, uint64_t n, uint8_t *out, uint64_t out_cap,
+                       uint64_t *ends, void *workspace, size_t workspace_size, uint64_t *total, void *stream) {
+    uint32_t list_f = 0;
+    int rc = check_nested(schema, &list_f);
+    if (rc) return rc;
+    if (!workspace || !total || (n && (!item_begin || !outer_columns))) return SPEC_E_INVALID_ARGUMENT;
+    if (nitems && !item_columns) return SPEC_E_INVALID_ARGUMENT;
+    if (out && !ends && n) return SPEC_E_INVALID_ARGUMENT;
+    if (workspace_size < spec_encode_nested_workspace_size(n)) return SPEC_E_WORKSPACE;
+    spec::NestedEncodeArgs a;
+    memset(&a, 0, sizeof(a));
+    a.n = n;
+    fill_enc_fields(a.outer, &schema->outer, outer_columns);
+    fill_enc_fields(a.item, &schema->item, nitems ? item_columns : nullptr);
+    for (uint32_t f = 0; f < schema->outer.nfields; f++)
+        if (f != list_f && !outer_columns[f]) return SPEC_E_INVALID_ARGUMENT;
+    a.outer.cols[list_f] = nullptr;
+    if ((rc = heaps_of(a.outer, &schema->outer, outer_heaps, outer_heap_lens))) return rc;
+    if ((rc = heaps_of(a.item, &schema->item, item_heaps, item_heap_lens))) return rc;
+    a.item_begin = item_begin;
+    a.nitems = nitems;
+    a.check_heaps = 1;
+    a.out = out;
+    a.out_cap = out ? out_cap : 0;
+    a.ends = ends;
+    a.block_sums = (uint64_t *)workspace;
+    a.nblocks = (n + spec::ENC_BLOCK - 1) / spec::ENC_BLOCK;
+    a.total = total;
+    if (spec::launch_nested_encode(a, out != nullptr, (hipStream_t)stream)) return hip_rc(hipGetLastError());
+    return SPEC_OK;
+}
+
 size_t spec_encode_flat_workspace_size(uint64_t n) {
     uint64_t nblocks = (n + spec::ENC_BLOCK - 1) / spec::ENC_BLOCK;
     return (size_t)((nblocks + 1) * sizeof(uint64_t));
@@ -287,8 +351,8 @@ int spec_encode_flat(const spec_schema *schema, const void *const *columns,
         int k = schema->fields[f].kind;
         if (k == SPEC_KIND_STRING || k == SPEC_KIND_BYTES) {
             if (!heaps || !heap_lens || (!heaps[f] && heap_lens[f])) return SPEC_E_INVALID_ARGUMENT;
-            a.heaps[f] = heaps[f];
-            a.heap_lens[f] = heap_lens[f];
+            a.f.heaps[f] = heaps[f];
+            a.f.heap_lens[f] = heap_lens[f];
         }
     }
     a.check_heaps = 1;

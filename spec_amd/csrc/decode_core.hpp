@@ -51,7 +51,8 @@ struct DecodeArgs {
     const uint8_t *stream;
     uint64_t stream_len;
     const uint64_t *ends;
-    uint64_t n;
+    uint64_t n;  // records [r0, n) of the batch are decoded (columns indexed by record)
+    uint64_t r0;
     FieldSet f;
 };
 
@@ -618,7 +619,7 @@ __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const uint64_t ngroups = (a.n + 63) / 64;
+    const uint64_t ngroups = (a.n - a.r0 + 63) / 64;
     const uint64_t stride = (uint64_t)gridDim.x * DEC_WAVES;
     uint64_t g = (uint64_t)blockIdx.x * DEC_WAVES + wave;
     if (g >= ngroups) return;
@@ -627,20 +628,20 @@ __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
         __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
 
     uint64_t lo, hi;
-    load_group_ends(a, g * 64, lane, lo, hi);
-    Group cur = make_group<SLAB>(a, g * 64, lane, lo, hi);
+    load_group_ends(a, a.r0 + g * 64, lane, lo, hi);
+    Group cur = make_group<SLAB>(a, a.r0 + g * 64, lane, lo, hi);
     if (cur.in_lds) issue_dma(rsrc, slab, cur, lane);
 
     while (true) {
-        const uint64_t base = g * 64;
+        const uint64_t base = a.r0 + g * 64;
         const uint64_t r = base + lane;
         const bool valid = r < a.n;
         const uint64_t gn = g + stride;
         const bool has_next = gn < ngroups;
         uint64_t nlo = 0, nhi = 0;
-        if (has_next) load_group_ends(a, gn * 64, lane, nlo, nhi);
+        if (has_next) load_group_ends(a, a.r0 + gn * 64, lane, nlo, nhi);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        Group nxt = make_group<SLAB>(a, has_next ? gn * 64 : base, lane, nlo, nhi);
+        Group nxt = make_group<SLAB>(a, has_next ? a.r0 + gn * 64 : base, lane, nlo, nhi);
 
         if (cur.in_lds) {
             fix_stream_tail(a, rsrc, slab, cur, lane);

@@ -26,10 +26,10 @@ int device_cus() {
 }
 
 int launch_decode_flat(const DecodeArgs &a, double avg_record, hipStream_t stream) {
-    if (a.n == 0) return 0;
+    if (a.n <= a.r0) return 0;
     const int cls = decode_slab_class(avg_record);
     const int slab = cls < 3 ? slab_bytes(cls) : 0;
-    dim3 grid(decode_grid(a.n, device_cus(), slab)), block(256);
+    dim3 grid(decode_grid(a.n - a.r0, device_cus(), slab)), block(256);
     switch (cls) {
     case 0: hipLaunchKernelGGL(decode_flat_kernel<slab_bytes(0)>, grid, block, DEC_WAVES * slab_bytes(0), stream, a); break;
     case 1: hipLaunchKernelGGL(decode_flat_kernel<slab_bytes(1)>, grid, block, DEC_WAVES * slab_bytes(1), stream, a); break;

@@ -7,6 +7,7 @@
 
 #include "../../include/spec_amd.h"
 #include "decode_core.hpp"
+#include "encode_core.hpp"
 
 namespace spec {
 
@@ -14,14 +15,7 @@ namespace spec {
 // the per-field loop branches are wave-uniform).
 struct EncodeArgs {
     uint64_t n;
-    uint32_t nfields;
-    uint16_t tags[SPEC_MAX_FIELDS];
-    uint8_t kinds[SPEC_MAX_FIELDS];
-    uint8_t order[SPEC_MAX_FIELDS]; // table order: order[j] = schema index of j-th table entry
-    const void *cols[SPEC_MAX_FIELDS];
-    const uint8_t *heaps[SPEC_MAX_FIELDS];
-    uint64_t heap_lens[SPEC_MAX_FIELDS];
-    uint32_t table_big_forced; // 1 if any tag > 255 (IsBigMessage holds for every record)
+    EncFields f;
     uint32_t check_heaps;      // 1 when heaps/heap_lens are known (full encode, not size-only)
     uint8_t *out;
     uint64_t out_cap;
@@ -31,6 +25,23 @@ struct EncodeArgs {
     uint64_t *total;
 };
 
+// encode_nested.hip
+struct NestedEncodeArgs {
+    uint64_t n;
+    EncFields outer; // its K_LIST field is written from item_begin + item
+    EncFields item;
+    const uint32_t *item_begin; // [n + 1]
+    uint64_t nitems;            // item columns hold this many items
+    uint32_t check_heaps;
+    uint8_t *out;
+    uint64_t out_cap;
+    uint64_t *ends;
+    uint64_t *block_sums;
+    uint64_t nblocks;
+    uint64_t *total;
+};
+
+int launch_nested_encode(const NestedEncodeArgs &a, bool write, hipStream_t stream);
 int launch_decode_flat(const DecodeArgs &a, double avg_record, hipStream_t stream);
 int device_cus(); // CUs of the current device (cached)
 int launch_nested_index(const NestedArgs &a, double avg_record, hipStream_t stream);

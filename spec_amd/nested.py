@@ -88,3 +88,59 @@ def decode_nested(schema: NestedSchema, stream: torch.Tensor, ends: torch.Tensor
     d.reserve(total)
     d.decode()
     return d.result()
+
+
+class NestedEncoder:
+    """Reusable encode state for spec_encode_nested (workspace + device total)."""
+
+    def __init__(self, schema: NestedSchema, n: int, device="cuda"):
+        self.schema, self.n = schema, n
+        ws = _lib.lib().spec_encode_nested_workspace_size(n)
+        self.workspace = torch.empty((ws + 7) // 8, dtype=torch.int64, device=device)
+        self.ws_bytes = ws
+        self.total = torch.zeros(1, dtype=torch.int64, device=device)
+
+    @staticmethod
+    def _ptrs(ts):
+        return (C.c_void_p * max(1, len(ts)))(*[t.data_ptr() if t is not None else 0 for t in ts])
+
+    @staticmethod
+    def _heaps(fields, heaps):
+        hp = (C.c_void_p * max(1, len(fields)))()
+        hl = (C.c_uint64 * max(1, len(fields)))()
+        for f, fld in enumerate(fields):
+            if fld.kind in (Kind.STRING, Kind.BYTES):
+                h = heaps[f]
+                _check_dev(h, f"heap {f}", torch.uint8)
+                hp[f] = h.data_ptr()
+                hl[f] = h.numel()
+        return hp, hl
+
+    def encode(self, outer_cols, outer_heaps, item_begin, item_cols, item_heaps, nitems, out=None, ends=None,
+               cuda_stream=None):
+        """outer_cols: one tensor per outer field (None for the list field); item_begin: int32/uint32
+        [n+1]; writes out/ends when given, always self.total."""
+        ohp, ohl = self._heaps(self.schema.outer.fields, outer_heaps)
+        ihp, ihl = self._heaps(self.schema.item.fields, item_heaps)
+        rc = _lib.lib().spec_encode_nested(
+            C.byref(self.schema.c), self._ptrs(outer_cols), ohp, ohl, _ptr(item_begin), self._ptrs(item_cols), ihp,
+            ihl, nitems, self.n, _ptr(out), out.numel() if out is not None else 0, _ptr(ends), _ptr(self.workspace),
+            self.ws_bytes, _ptr(self.total), _stream_handle(cuda_stream))
+        _lib.check(rc, "spec_encode_nested")
+        return self.total
+
+
+def encode_nested(schema: NestedSchema, outer_cols, outer_heaps, item_begin, item_cols, item_heaps, n: int,
+                  cuda_stream=None):
+    """-> (stream uint8[total], ends int64[n]) on the device."""
+    dev = item_begin.device
+    enc = NestedEncoder(schema, n, dev)
+    nitems = item_cols[0].shape[0] if item_cols else 0
+    total = int(enc.encode(outer_cols, outer_heaps, item_begin, item_cols, item_heaps, nitems,
+                           cuda_stream=cuda_stream).item())
+    if total < 0:
+        raise _lib.SpecError(-1, "spec_encode_nested: encoder error")
+    out = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+    ends = torch.empty(n, dtype=torch.int64, device=dev)
+    enc.encode(outer_cols, outer_heaps, item_begin, item_cols, item_heaps, nitems, out, ends, cuda_stream)
+    return out[:total], ends

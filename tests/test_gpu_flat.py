@@ -335,3 +335,37 @@ def test_zero_records(dev):
     e = torch.zeros(0, dtype=torch.int64, device=dev)
     got = spec_amd.decode_flat(FLAT16, s, e)
     assert got.status.numel() == 0
+
+
+def test_decode_range_and_host_pipeline(dev):
+    """spec_decode_flat_range over chunks == one full decode; the pinned-host pipeline
+    (HostDecoder: chunked H2D / decode / D2H on three streams) returns the same columns."""
+    import ctypes as C
+
+    import torch
+
+    n = 70_001
+    cols, heaps = workload.flat16(n, seed=4)
+    stream, ends = oracle_encode(FLAT16, cols, heaps, n)
+    want, wst = O.decode_flat_batch(FLAT16.tags, FLAT16.kinds, stream, ends, FLAT16.widths, nthreads=4)
+    d_stream = torch.from_numpy(stream).to(dev)
+    d_ends = torch.from_numpy(ends.view(np.int64)).to(dev)
+    out = spec_amd.alloc_columns(FLAT16, n, dev)
+    st = torch.full((n,), 7, dtype=torch.uint8, device=dev)
+    ptrs = (C.c_void_p * 16)(*[c.data_ptr() for c in out])
+    L = spec_amd.lib()
+    for r0, r1 in [(0, 1000), (1000, 1001), (1001, 33333), (33333, n)]:
+        rc = L.spec_decode_flat_range(C.byref(FLAT16.c), C.c_void_p(d_stream.data_ptr()), stream.size,
+                                      C.c_void_p(d_ends.data_ptr()), r0, r1, ptrs, C.c_void_p(st.data_ptr()), None)
+        assert rc == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), wst)
+    for f in range(16):
+        assert np.array_equal(out[f].cpu().numpy(), want[f]), f
+    hd = spec_amd.HostDecoder(FLAT16, n, stream.size, dev, chunks=5)
+    h_stream = torch.from_numpy(stream).pin_memory()
+    h_ends = torch.from_numpy(ends.view(np.int64)).pin_memory()
+    hcols, hst = hd.decode(h_stream, h_ends)
+    assert np.array_equal(hst.numpy()[:n], wst)
+    for f in range(16):
+        assert np.array_equal(hcols[f].numpy()[:n], want[f]), f

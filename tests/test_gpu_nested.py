@@ -158,3 +158,77 @@ def test_nested_fuzz(dev, seed):
         out.append(bytes(b))
     s2, e2 = concat_records(out)
     check_nested(dev, s2, e2, f"fuzz {seed}")
+
+
+def nested_device_inputs(w, dev):
+    """workload.nested arrays -> (outer_cols, outer_heaps, item_begin, item_cols, item_heaps) on dev."""
+    n = len(w["seq"])
+    outer = [to_dev(w["id"], dev), to_dev(w["seq"].view(np.uint8).reshape(n, 8), dev),
+             to_dev(w["name"].view(np.uint8).reshape(n, 8), dev), None]
+    m = len(w["key"])
+    items = [to_dev(w["key"].view(np.uint8).reshape(m, 4), dev), to_dev(w["value"].view(np.uint8).reshape(m, 8), dev),
+             to_dev(w["label"].view(np.uint8).reshape(m, 8), dev)]
+    return (outer, {2: to_dev(w["name_heap"], dev)}, to_dev(w["item_begin"].view(np.int32), dev), items,
+            {2: to_dev(w["label_heap"] if w["label_heap"].size else np.zeros(1, np.uint8), dev)})
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 5000])
+def test_nested_encode_bitexact(dev, n):
+    import torch
+
+    w = workload.nested(n, seed=n + 3)
+    want, want_ends = O.encode_nested_batch(w)
+    oc, oh, ib, ic, ih = nested_device_inputs(w, dev)
+    out, ends = spec_amd.encode_nested(NESTED, oc, oh, ib, ic, ih, n)
+    torch.cuda.synchronize()
+    assert np.array_equal(ends.cpu().numpy().view(np.uint64), want_ends)
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+def test_nested_encode_big_lists_and_empty(dev):
+    """Lists of 0 and > 255 items (IsBigList by count), long labels (big items / big lists by
+    offset), in one batch."""
+    import torch
+
+    w = workload.nested(300, seed=9, count=(0, 3))
+    counts = np.diff(w["item_begin"]).astype(np.int64)
+    counts[5] = 300
+    counts[7] = 0
+    counts[11] = 2
+    rng = np.random.default_rng(1)
+    m = int(counts.sum())
+    ib = np.zeros(len(counts) + 1, np.uint32)
+    np.cumsum(counts, out=ib[1:])
+    lens = rng.integers(0, 12, m).astype(np.uint32)
+    lens[ib[11]] = 70000  # one big item (data > 65535) => big item table, big list by offset
+    label = np.zeros((m, 2), np.uint32)
+    label[1:, 0] = np.cumsum(lens[:-1])
+    label[:, 1] = lens
+    w.update(item_begin=ib, key=rng.integers(-2**31, 2**31, m).astype(np.int32),
+             value=rng.standard_normal(m), label=label,
+             label_heap=rng.integers(32, 127, int(lens.sum()), dtype=np.uint8))
+    want, want_ends = O.encode_nested_batch(w)
+    oc, oh, ibd, ic, ih = nested_device_inputs(w, dev)
+    out, ends = spec_amd.encode_nested(NESTED, oc, oh, ibd, ic, ih, 300)
+    torch.cuda.synchronize()
+    assert np.array_equal(ends.cpu().numpy().view(np.uint64), want_ends)
+    assert np.array_equal(out.cpu().numpy(), want)
+    check_nested(dev, want, want_ends, "big lists decode")
+
+
+def test_nested_roundtrip_full_size(dev):
+    """config 4 at 1M records: GPU encode == oracle bytes, and GPU decode of them == inputs."""
+    import torch
+
+    n = 1 << 20
+    w = workload.nested(n)
+    want, want_ends = O.encode_nested_batch(w)
+    oc, oh, ib, ic, ih = nested_device_inputs(w, dev)
+    out, ends = spec_amd.encode_nested(NESTED, oc, oh, ib, ic, ih, n)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), want)
+    got = spec_amd.decode_nested(NESTED, out, ends)
+    assert int(got.status.sum()) == 0
+    assert np.array_equal(got.item_begin.cpu().numpy().view(np.uint32), w["item_begin"])
+    assert np.array_equal(got.items[0].cpu().numpy().view(np.int32).ravel(), w["key"])
+    assert np.array_equal(got.outer[1].cpu().numpy().view(np.int64).ravel(), w["seq"])
