@@ -49,8 +49,8 @@ def parse():
     p.add_argument("--verify", action="store_true", help="check a sample against the oracle")
     p.add_argument("--no-jit", action="store_true", help="generic decode kernel (no schema specialisation)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_decode_flat.json"),
-                   help="PMC traffic summary (tools/pmc_summary.py) used for roofline.traffic")
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                   help="PMC traffic per kernel (tools/pmc_traffic.py) used for roofline.traffic")
     return p.parse_args()
 
 
@@ -161,6 +161,72 @@ def cpu_baseline(stream_np, ends_np, seconds):
     return res, threads, n
 
 
+def nested_leg(n, seed, dev):
+    """BASELINE config 4: n Nested records (list<message>), GPU encode then GPU decode
+    (index + decode launches), device-resident; kernel time via HIP events."""
+    from spec_amd import NESTED
+
+    w = workload.nested(n, seed)
+    m = len(w["key"])
+    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    outer = [to(w["id"]), to(w["seq"].view(np.uint8).reshape(n, 8)), to(w["name"].view(np.uint8).reshape(n, 8)), None]
+    items = [to(w["key"].view(np.uint8).reshape(m, 4)), to(w["value"].view(np.uint8).reshape(m, 8)),
+             to(w["label"].view(np.uint8).reshape(m, 8))]
+    oh, ih, ib = {2: to(w["name_heap"])}, {2: to(w["label_heap"])}, to(w["item_begin"].view(np.int32))
+    stream, ends = spec_amd.encode_nested(NESTED, outer, oh, ib, items, ih, n)
+    torch.cuda.synchronize()
+    enc = spec_amd.NestedEncoder(NESTED, n, dev)
+    out = torch.empty_like(stream)
+    e2 = torch.empty_like(ends)
+    enc_ms, _ = kernel_time_events(lambda: enc.encode(outer, oh, ib, items, ih, m, out, e2), 10)
+    d = spec_amd.NestedDecoder(NESTED, stream, ends)
+    d.index()
+    d.reserve(int(d.total.item()))
+
+    def step():
+        d.index()
+        d.decode()
+
+    dec_ms, _ = kernel_time_events(step, 20)
+    torch.cuda.synchronize()
+    ok = torch.equal(out, stream) and int(d.status.sum()) == 0 and int(d.total.item()) == m
+    ok = ok and torch.equal(d.items[0], items[0]) and torch.equal(d.outer[1], outer[1])
+    sb = stream.numel()
+    dec_alg = sb + 8 * n + n * (16 + 8 + 8 + 1 + 4) + m * (4 + 8 + 8 + 1)
+    enc_alg = n * (16 + 8 + 8 + 4) + m * (4 + 8 + 8) + int(w["name_heap"].size + w["label_heap"].size) + sb + 8 * n
+    return {"records": n, "items": m, "mean_record_bytes": round(sb / n, 1),
+            "decode_mmsg_s": round(n / (dec_ms * 1e-3) / 1e6, 1), "decode_ms": round(dec_ms, 4),
+            "decode_gb_s": round(dec_alg / (dec_ms * 1e-3) / 1e9, 1),
+            "encode_mmsg_s": round(n / (enc_ms * 1e-3) / 1e6, 1), "encode_ms": round(enc_ms, 4),
+            "encode_gb_s": round(enc_alg / (enc_ms * 1e-3) / 1e9, 1), "roundtrip_ok": bool(ok)}
+
+
+def gather_leg(dec, dist, rank, world, n, steps):
+    """BASELINE config 5's collective: each rank decodes its shard, then every rank's columns
+    (+ status) go to rank 0 over RCCL (xGMI).  Times decode + gather per step (max over ranks)."""
+    from spec_amd.shard import gather_columns
+
+    cols = dec.cols + [dec.status.view(-1, 1)]
+
+    def step():
+        dec()
+        gather_columns(cols, dist)
+
+    for _ in range(2):
+        step()
+    barrier(dist)
+    t0 = time.perf_counter()
+    for _ in range(max(3, steps // 10)):
+        step()
+    barrier(dist)
+    dt = max_over_ranks(dist, (time.perf_counter() - t0) / max(3, steps // 10))
+    col_bytes = n * (COLUMN_BYTES + 1)
+    return {"ms": round(dt * 1e3, 3), "records_total": n * world,
+            "mmsg_s": round(n * world / dt / 1e6, 1),
+            "gathered_gb_s": round(col_bytes * (world - 1) / dt / 1e9, 1),
+            "note": "decode + RCCL gather of all columns to rank 0, per step"}
+
+
 def e2e_decode(stream_host, ends_host, dev, reps=5, chunks=8):
     """Pinned host -> H2D -> decode -> D2H of all columns + status, pipelined in record chunks
     over three streams (spec_amd.HostDecoder); whole-pipeline rate (Mmsg/s)."""
@@ -201,10 +267,13 @@ def main():
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
     read_only = (stream_bytes + 8 * n) / (avg_ms * 1e-3) / 1e9
 
+    # HBM bytes per launch from the committed rocprofv3 PMC passes (tools/pmc_traffic.py):
+    # FETCH_SIZE x 2 (gfx950 correction, MI355X_MICROARCH.md) + WRITE_SIZE, for this kernel
     traffic = None
+    kname = "spec_decode_flat_jit" if jit else "decode_flat_kernel"
     if os.path.exists(args.traffic):
         try:
-            t = json.load(open(args.traffic))
+            t = json.load(open(args.traffic)).get(kname, {})
             if t.get("records") == n:
                 traffic = t.get("hbm_bytes_per_launch")
         except Exception:
@@ -224,6 +293,10 @@ def main():
         extras["encode"] = {"mmsg_s": round(n / (enc_ms * 1e-3) / 1e6, 1),
                             "gb_s": round(enc_alg / (enc_ms * 1e-3) / 1e9, 1),
                             "ms": round(enc_ms, 4), "bit_exact_vs_decode_input": bool(ok)}
+        if world > 1:
+            extras["gather"] = gather_leg(dec, dist, rank, world, n, args.steps)
+        if rank == 0 and world == 1:
+            extras["nested"] = nested_leg(n, args.seed, dev)
         if rank == 0:
             sh = stream.cpu().pin_memory()
             eh = ends.cpu().pin_memory()
