@@ -688,11 +688,14 @@ __host__ __device__ inline int decode_slab_class(double avg_record) {
     return 3;
 }
 
-// Grid for the persistent decode: as many 4-wave blocks as the CUs hold at once (LDS-bound),
-// never more than the groups need.
-__host__ inline unsigned decode_grid(uint64_t n, int cus, int slab) {
+// Grid: one wave per group (default, measured faster on MI355X: a finished block frees its
+// LDS for the next one), or persistent — as many 4-wave blocks as the CUs hold at once
+// (LDS-bound), each wave looping over groups with the next group's DMA overlapping this
+// group's decode (SPEC_AMD_PERSIST=1).
+__host__ inline unsigned decode_grid(uint64_t n, int cus, int slab, bool persistent) {
     const uint64_t groups = (n + 63) / 64;
     const uint64_t need = (groups + DEC_WAVES - 1) / DEC_WAVES;
+    if (!persistent) return (unsigned)need; // one group per wave
     int per_cu = slab > 0 ? (160 * 1024) / (DEC_WAVES * slab) : 8;
     per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
     const uint64_t cap = (uint64_t)cus * per_cu;

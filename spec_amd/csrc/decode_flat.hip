@@ -2,6 +2,7 @@
 // The device code lives in decode_core.hpp; schema-specialised variants of the same body
 // are compiled at run time by jit.cpp.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "decode_core.hpp"
 #include "spec_internal.hpp"
@@ -11,6 +12,14 @@ namespace spec {
 template <int SLAB>
 __global__ __launch_bounds__(256) void decode_flat_kernel(DecodeArgs a) {
     decode_flat_body<SLAB, RuntimeSpec>(a);
+}
+
+bool persistent_decode() {
+    static int v = [] {
+        const char *e = getenv("SPEC_AMD_PERSIST");
+        return (e && e[0] == '1') ? 1 : 0;
+    }();
+    return v == 1;
 }
 
 int device_cus() {
@@ -29,7 +38,7 @@ int launch_decode_flat(const DecodeArgs &a, double avg_record, hipStream_t strea
     if (a.n <= a.r0) return 0;
     const int cls = decode_slab_class(avg_record);
     const int slab = cls < 3 ? slab_bytes(cls) : 0;
-    dim3 grid(decode_grid(a.n - a.r0, device_cus(), slab)), block(256);
+    dim3 grid(decode_grid(a.n - a.r0, device_cus(), slab, persistent_decode())), block(256);
     switch (cls) {
     case 0: hipLaunchKernelGGL(decode_flat_kernel<slab_bytes(0)>, grid, block, DEC_WAVES * slab_bytes(0), stream, a); break;
     case 1: hipLaunchKernelGGL(decode_flat_kernel<slab_bytes(1)>, grid, block, DEC_WAVES * slab_bytes(1), stream, a); break;

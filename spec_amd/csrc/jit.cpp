@@ -195,7 +195,7 @@ int jit_launch_decode_flat(const spec_schema *schema, const DecodeArgs &a, doubl
     hipFunction_t fn = lookup(schema, cls);
     if (!fn) return 0;
     if (a.n <= a.r0) return 1;
-    const unsigned blocks = decode_grid(a.n - a.r0, device_cus(), slab_bytes(cls));
+    const unsigned blocks = decode_grid(a.n - a.r0, device_cus(), slab_bytes(cls), persistent_decode());
     DecodeArgs args = a;
     size_t size = sizeof(args);
     void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
