@@ -146,6 +146,20 @@ int spec_decode_flat_range(const spec_schema *schema, const uint8_t *stream_byte
                            const uint64_t *ends, uint64_t r0, uint64_t r1, void *const *columns, uint8_t *status,
                            void *stream);
 
+/* ---- mpx frames (the path's source: mpx/conn_reader.go:179-194, conn_writer.go:84-97) ----
+ * An mpx connection carries frames [u32 big-endian size][message], back to back.
+ * spec_frames_index (HOST memory, CPU): walks the heads of buf[0, len) and writes ends[k] =
+ * offset just past frame k's message, for every complete frame (at most cap; SPEC_E_CAPACITY
+ * if more remain); *count = frames indexed, *consumed = bytes they span (an incomplete tail
+ * frame is left for the next read).
+ * spec_decode_frames: spec_decode_flat_range over the frames in place (each record starts 4
+ * bytes after the previous frame's end): no host-side compaction of the received bytes. */
+int spec_frames_index(const uint8_t *buf, uint64_t len, uint64_t *ends, uint64_t cap, uint64_t *count,
+                      uint64_t *consumed);
+int spec_decode_frames(const spec_schema *schema, const uint8_t *frames, uint64_t frames_len,
+                       const uint64_t *ends, uint64_t r0, uint64_t r1, void *const *columns, uint8_t *status,
+                       void *stream);
+
 /* spec_decode_flat_prepare: compile (once per device, schema and record-size class) the
  * schema-specialised decode kernel that spec_decode_flat uses when one exists — the
  * analogue of the reference's generated readers (internal/lang/generator/message.go:97-186).

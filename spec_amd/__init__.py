@@ -7,12 +7,13 @@ decoded into SoA columns / encoded from them by hand-written gfx950 kernels
 """
 from ._lib import LIB_PATH, SpecError, header_symbols, lib, set_jit
 from .batch import Columns, Decoder, Encoder, alloc_columns, decode_flat, encode_flat
+from .frames import decode_frames, frames_index, make_frames
 from .pipeline import HostDecoder
 from .nested import NestedColumns, NestedDecoder, NestedEncoder, decode_nested, encode_nested
 from .schema import FLAT16, NESTED, Field, Kind, NestedSchema, Schema
 
 __all__ = [
-    "HostDecoder", "LIB_PATH", "SpecError", "header_symbols", "lib", "set_jit", "Columns", "Decoder", "Encoder", "alloc_columns",
+    "HostDecoder", "decode_frames", "frames_index", "make_frames", "LIB_PATH", "SpecError", "header_symbols", "lib", "set_jit", "Columns", "Decoder", "Encoder", "alloc_columns",
     "decode_flat", "encode_flat", "FLAT16", "Field", "Kind", "Schema",
     "NESTED", "NestedSchema", "NestedColumns", "NestedDecoder", "NestedEncoder", "decode_nested",
     "encode_nested",

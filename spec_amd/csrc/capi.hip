@@ -155,9 +155,9 @@ int spec_copy_d2d(void *dst, const void *src, size_t bytes, void *stream) {
     return hip_rc(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
 }
 
-int spec_decode_flat_range(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
-                           const uint64_t *ends, uint64_t r0, uint64_t r1, void *const *columns, uint8_t *status,
-                           void *stream) {
+static int decode_flat_impl(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
+                            const uint64_t *ends, uint64_t r0, uint64_t r1, uint32_t head, void *const *columns,
+                            uint8_t *status, void *stream) {
     int rc = check_schema(schema);
     if (rc) return rc;
     if (r1 < r0) return SPEC_E_INVALID_ARGUMENT;
@@ -173,6 +173,7 @@ int spec_decode_flat_range(const spec_schema *schema, const uint8_t *stream_byte
     a.ends = ends;
     a.n = r1;
     a.r0 = r0;
+    a.head = head;
     fill_field_set(a.f, schema, columns, status);
     // slab class from the whole batch's mean record size (ends[r1-1] bytes over r1 records is
     // not known on the host; stream_len / r1 is the same figure for a full batch)
@@ -183,10 +184,45 @@ int spec_decode_flat_range(const spec_schema *schema, const uint8_t *stream_byte
     return SPEC_OK;
 }
 
+int spec_decode_flat_range(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
+                           const uint64_t *ends, uint64_t r0, uint64_t r1, void *const *columns, uint8_t *status,
+                           void *stream) {
+    return decode_flat_impl(schema, stream_bytes, stream_len, ends, r0, r1, 0, columns, status, stream);
+}
+
 int spec_decode_flat(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
                      const uint64_t *ends, uint64_t n, void *const *columns, uint8_t *status,
                      void *stream) {
-    return spec_decode_flat_range(schema, stream_bytes, stream_len, ends, 0, n, columns, status, stream);
+    return decode_flat_impl(schema, stream_bytes, stream_len, ends, 0, n, 0, columns, status, stream);
+}
+
+int spec_decode_frames(const spec_schema *schema, const uint8_t *frames, uint64_t frames_len,
+                       const uint64_t *ends, uint64_t r0, uint64_t r1, void *const *columns, uint8_t *status,
+                       void *stream) {
+    return decode_flat_impl(schema, frames, frames_len, ends, r0, r1, 4, columns, status, stream);
+}
+
+// mpx framing, mpx/conn_reader.go:179-194 (read) / mpx/conn_writer.go:84-97 (write):
+// [u32 big-endian size][size message bytes], back to back.
+int spec_frames_index(const uint8_t *buf, uint64_t len, uint64_t *ends, uint64_t cap, uint64_t *count,
+                      uint64_t *consumed) {
+    if ((!buf && len) || !count || !consumed || (cap && !ends)) return SPEC_E_INVALID_ARGUMENT;
+    uint64_t p = 0, k = 0;
+    while (p + 4 <= len) {
+        const uint64_t size = ((uint64_t)buf[p] << 24) | ((uint64_t)buf[p + 1] << 16) | ((uint64_t)buf[p + 2] << 8) |
+                              (uint64_t)buf[p + 3];
+        if (p + 4 + size > len) break; // incomplete frame: the caller reads more
+        if (k == cap) {
+            *count = k;
+            *consumed = p;
+            return SPEC_E_CAPACITY;
+        }
+        p += 4 + size;
+        ends[k++] = p;
+    }
+    *count = k;
+    *consumed = p;
+    return SPEC_OK;
 }
 
 int spec_decode_flat_prepare(const spec_schema *schema, uint64_t stream_len, uint64_t n) {

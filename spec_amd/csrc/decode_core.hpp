@@ -53,6 +53,7 @@ struct DecodeArgs {
     const uint64_t *ends;
     uint64_t n;  // records [r0, n) of the batch are decoded (columns indexed by record)
     uint64_t r0;
+    uint32_t head; // bytes before each record (mpx frame head = 4: [u32 BE size][message])
     FieldSet f;
 };
 
@@ -566,7 +567,7 @@ __device__ __forceinline__ void load_group_ends(const DecodeArgs &a, uint64_t ba
     const uint64_t r = base + lane;
     const uint64_t last = a.n - 1;
     hi = a.ends[r < last ? r : last];
-    lo = r == 0 ? 0 : a.ends[(r - 1) < last ? r - 1 : last];
+    lo = (r == 0 ? 0 : a.ends[(r - 1) < last ? r - 1 : last]) + a.head;
 }
 
 template <int SLAB>
@@ -678,6 +679,62 @@ __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
         g = gn;
         cur = nxt;
     }
+}
+
+// One group per wave (the default grid): stage, decode, done.  Same steps as one iteration of
+// decode_flat_body without the hand-off to a next group, so nothing fences the fast path's
+// LDS reads from its decode and stores.
+template <int SLAB, class Spec>
+__device__ __forceinline__ void decode_flat_once(const DecodeArgs &a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const uint64_t base = a.r0 + ((uint64_t)blockIdx.x * DEC_WAVES + wave) * 64;
+    if (base >= a.n) return;
+    const uint64_t r = base + lane;
+    const bool valid = r < a.n;
+    uint8_t *slab = smem + wave * (SLAB > 0 ? SLAB : 0);
+    __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
+    const uint64_t hi = a.ends[valid ? r : a.n - 1];
+    uint64_t lo = __shfl_up(hi, 1);
+    if (lane == 0) lo = r == 0 ? 0 : a.ends[r - 1];
+    lo += a.head;
+    const Group cur = make_group<SLAB>(a, base, lane, lo, hi);
+    if (cur.in_lds) {
+        issue_dma(rsrc, slab, cur, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        fix_stream_tail(a, rsrc, slab, cur, lane);
+        if (!valid) return;
+        LdsSrc s{(lds_u8 *)slab};
+        const int rs = SLAB_GUARD + (int)(cur.rec_lo - cur.aligned_lo);
+        const int re = SLAB_GUARD + (int)(cur.rec_hi - cur.aligned_lo);
+        const long long to_stream = (long long)cur.aligned_lo - SLAB_GUARD;
+#if defined(SPEC_EXP) && SPEC_EXP == 1 // diagnostic: staging only
+        if (a.f.status) a.f.status[r] = slab[re - 1];
+        return;
+#endif
+        if constexpr (Spec::N > 0) {
+            FastRec<Spec> fr;
+            if (fast_prepare<Spec>(s, rs, re, fr)) {
+                fast_finish<Spec>(fr, r, a, to_stream);
+                return;
+            }
+        }
+        decode_record_generic(s, rs, re, r, a.f, to_stream);
+    } else if (valid) {
+        GlobalSrc s{rsrc, a.stream_len};
+        decode_record_generic(s, (long long)cur.rec_lo, (long long)cur.rec_hi, r, a.f, 0);
+    }
+}
+
+// Kernel entry: PERSIST selects the persistent, software-pipelined loop.
+template <bool PERSIST, int SLAB, class Spec>
+__device__ __forceinline__ void decode_flat_entry(const DecodeArgs &a) {
+    if constexpr (PERSIST)
+        decode_flat_body<SLAB, Spec>(a);
+    else
+        decode_flat_once<SLAB, Spec>(a);
 }
 
 // slab class shared by the launchers (host): average record size * 64 * margin; 3 = none

@@ -11,7 +11,12 @@ namespace spec {
 
 template <int SLAB>
 __global__ __launch_bounds__(256) void decode_flat_kernel(DecodeArgs a) {
-    decode_flat_body<SLAB, RuntimeSpec>(a);
+    decode_flat_entry<false, SLAB, RuntimeSpec>(a);
+}
+
+template <int SLAB>
+__global__ __launch_bounds__(256) void decode_flat_kernel_persistent(DecodeArgs a) {
+    decode_flat_entry<true, SLAB, RuntimeSpec>(a);
 }
 
 bool persistent_decode() {
@@ -39,12 +44,19 @@ int launch_decode_flat(const DecodeArgs &a, double avg_record, hipStream_t strea
     const int cls = decode_slab_class(avg_record);
     const int slab = cls < 3 ? slab_bytes(cls) : 0;
     dim3 grid(decode_grid(a.n - a.r0, device_cus(), slab, persistent_decode())), block(256);
-    switch (cls) {
-    case 0: hipLaunchKernelGGL(decode_flat_kernel<slab_bytes(0)>, grid, block, DEC_WAVES * slab_bytes(0), stream, a); break;
-    case 1: hipLaunchKernelGGL(decode_flat_kernel<slab_bytes(1)>, grid, block, DEC_WAVES * slab_bytes(1), stream, a); break;
-    case 2: hipLaunchKernelGGL(decode_flat_kernel<slab_bytes(2)>, grid, block, DEC_WAVES * slab_bytes(2), stream, a); break;
-    default: hipLaunchKernelGGL(decode_flat_kernel<0>, grid, block, 0, stream, a); break;
+#define SPEC_LAUNCH(K)                                                                                          \
+    switch (cls) {                                                                                              \
+    case 0: hipLaunchKernelGGL(K<slab_bytes(0)>, grid, block, DEC_WAVES * slab_bytes(0), stream, a); break;     \
+    case 1: hipLaunchKernelGGL(K<slab_bytes(1)>, grid, block, DEC_WAVES * slab_bytes(1), stream, a); break;     \
+    case 2: hipLaunchKernelGGL(K<slab_bytes(2)>, grid, block, DEC_WAVES * slab_bytes(2), stream, a); break;     \
+    default: hipLaunchKernelGGL(K<0>, grid, block, 0, stream, a); break;                                        \
     }
+    if (persistent_decode()) {
+        SPEC_LAUNCH(decode_flat_kernel_persistent)
+    } else {
+        SPEC_LAUNCH(decode_flat_kernel)
+    }
+#undef SPEC_LAUNCH
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

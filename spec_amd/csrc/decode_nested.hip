@@ -93,6 +93,7 @@ __device__ __forceinline__ Group stage(const NestedArgs &a, __amdgpu_buffer_rsrc
     d.ends = a.ends;
     d.n = a.n;
     d.r0 = 0;
+    d.head = 0;
     load_group_ends(d, base, lane, lo, hi);
     Group gr = make_group<SLAB>(d, base, lane, lo, hi);
     if (gr.in_lds) {

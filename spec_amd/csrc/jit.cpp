@@ -80,7 +80,7 @@ bool has_fast_path(const spec_schema *s) {
 
 std::string key_of(const spec_schema *s, int slab_class, int device) {
     std::ostringstream k;
-    k << device << ':' << slab_class << ':';
+    k << device << ':' << slab_class << ':' << (spec::persistent_decode() ? 'p' : 'o') << ':';
     for (uint32_t f = 0; f < s->nfields; f++) k << s->fields[f].tag << '/' << (int)s->fields[f].kind << ',';
     return k.str();
 }
@@ -102,7 +102,8 @@ std::string generate(const spec_schema *s, int slab) {
     for (uint32_t k = 0; k < s->nfields; k++) o << (k ? "," : "") << sorted[k];
     o << "};\n};\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void spec_decode_flat_jit(spec::DecodeArgs a) {\n"
-      << "  spec::decode_flat_body<" << slab << ", GenSpec>(a);\n}\n";
+      << "  spec::decode_flat_entry<" << (spec::persistent_decode() ? "true" : "false") << ", " << slab
+      << ", GenSpec>(a);\n}\n";
     return o.str();
 }
 

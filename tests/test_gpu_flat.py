@@ -369,3 +369,28 @@ def test_decode_range_and_host_pipeline(dev):
     assert np.array_equal(hst.numpy()[:n], wst)
     for f in range(16):
         assert np.array_equal(hcols[f].numpy()[:n], want[f]), f
+
+
+def test_decode_frames_in_place(dev, kernel):
+    """mpx frames decoded in place == the same records decoded from a compact stream (spans
+    shifted by the 4-byte heads before them)."""
+    import torch
+
+    n = 3001
+    cols, heaps = workload.flat16(n, seed=12)
+    stream, ends = oracle_encode(FLAT16, cols, heaps, n)
+    want, wst = O.decode_flat_batch(FLAT16.tags, FLAT16.kinds, stream, ends, FLAT16.widths, nthreads=4)
+    fr = spec_amd.make_frames(stream, ends)
+    fends, used = spec_amd.frames_index(fr)
+    assert used == fr.size
+    got = spec_amd.decode_frames(FLAT16, torch.from_numpy(fr).to(dev), torch.from_numpy(fends.view(np.int64)).to(dev))
+    torch.cuda.synchronize()
+    assert np.array_equal(got.status.cpu().numpy(), wst)
+    shift = 4 * (np.arange(n, dtype=np.uint32) + 1)
+    for f, fld in enumerate(FLAT16.fields):
+        g = got.cols[f].cpu().numpy()
+        w = want[f].copy()
+        if fld.kind in (Kind.STRING, Kind.BYTES):
+            wv = w.view(np.uint32)
+            wv[:, 0] = np.where(wv[:, 1] > 0, wv[:, 0] + shift, 0)
+        assert np.array_equal(g, w), fld
