@@ -54,6 +54,7 @@ struct DecodeArgs {
     uint64_t n;  // records [r0, n) of the batch are decoded (columns indexed by record)
     uint64_t r0;
     uint32_t head; // bytes before each record (mpx frame head = 4: [u32 BE size][message])
+    uint32_t slab; // LDS bytes per wave (0: every wave parses from HBM)
     FieldSet f;
 };
 
@@ -70,16 +71,22 @@ struct NestedArgs {
     uint64_t item_cap;    // item columns hold this many items
     uint64_t *group_base; // workspace: per 64-record group item total, then exclusive offsets
     uint64_t *total;      // device: total items
+    uint32_t slab;        // LDS bytes per wave
 };
 
-constexpr int DEC_WAVES = 4; // waves per 256-thread block
+constexpr int DEC_WAVES = 4; // waves per block of the nested kernels
 constexpr int SLAB_GUARD = 48; // >= the deepest read below a value end (bin256: 33 + 7)
 
-// LDS slab per wave: guard + the DMA chunks (1 KiB each) a span may need + pad.  Three size
-// classes per records-per-wave setting, chosen from the batch's average record size; a wave
-// whose span does not fit parses from HBM instead (GlobalSrc).
-__host__ __device__ constexpr int slab_chunks(int cls) { return cls == 0 ? 11 : cls == 1 ? 19 : 35; }
-__host__ __device__ constexpr int slab_bytes(int cls) { return SLAB_GUARD + slab_chunks(cls) * 1024 + 32; }
+// LDS slab per wave: guard + the 1 KiB DMA chunks a 64-record span needs + pad.  Sized at
+// launch from the batch's mean record size with a 4 % margin; a wave whose span does not
+// fit parses from HBM instead (GlobalSrc), so the margin only affects speed.
+constexpr int SLAB_MAX_CHUNKS = 40;
+__host__ __device__ inline uint32_t decode_slab_bytes(double avg_record) {
+    const double span = avg_record * 64 * 1.04;
+    int chunks = (int)(span / 1024.0) + 1;
+    if (chunks > SLAB_MAX_CHUNKS) return 0;
+    return (uint32_t)(SLAB_GUARD + chunks * 1024 + 32);
+}
 
 // ---- message table lookup --------------------------------------------------------------
 
@@ -570,8 +577,8 @@ __device__ __forceinline__ void load_group_ends(const DecodeArgs &a, uint64_t ba
     lo = (r == 0 ? 0 : a.ends[(r - 1) < last ? r - 1 : last]) + a.head;
 }
 
-template <int SLAB>
-__device__ __forceinline__ Group make_group(const DecodeArgs &a, uint64_t base, int lane, uint64_t lo, uint64_t hi) {
+__device__ __forceinline__ Group make_group(const DecodeArgs &a, uint64_t base, int lane, uint64_t lo, uint64_t hi,
+                                            uint32_t slab) {
     Group gr;
     gr.rec_lo = lo;
     gr.rec_hi = hi < lo ? lo : hi; // malformed ends: treat as empty
@@ -582,7 +589,7 @@ __device__ __forceinline__ Group make_group(const DecodeArgs &a, uint64_t base, 
     const uint64_t bytes = span_hi > gr.aligned_lo ? span_hi - gr.aligned_lo : 0;
     const uint64_t chunks = (bytes + 1023) >> 10;
     gr.chunks = (uint32_t)chunks;
-    gr.in_lds = SLAB > 0 && span_hi >= span_lo && SLAB_GUARD + chunks * 1024 + 16 <= (uint64_t)SLAB;
+    gr.in_lds = slab > 0 && span_hi >= span_lo && SLAB_GUARD + chunks * 1024 + 16 <= (uint64_t)slab;
     return gr;
 }
 
@@ -615,22 +622,23 @@ __device__ __forceinline__ void fix_stream_tail(const DecodeArgs &a, __amdgpu_bu
 //   wait for its DMA -> fast_prepare (trailer, table, all field windows into registers) and
 //   the generic path for any rejected record -> the slab is free: issue the NEXT group's DMA
 //   -> decode + store this group from registers while that DMA is in flight.
-template <int SLAB, class Spec>
+template <class Spec>
 __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int nw = blockDim.x >> 6;
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const uint64_t ngroups = (a.n - a.r0 + 63) / 64;
-    const uint64_t stride = (uint64_t)gridDim.x * DEC_WAVES;
-    uint64_t g = (uint64_t)blockIdx.x * DEC_WAVES + wave;
+    const uint64_t stride = (uint64_t)gridDim.x * nw;
+    uint64_t g = (uint64_t)blockIdx.x * nw + wave;
     if (g >= ngroups) return;
-    uint8_t *slab = smem + wave * (SLAB > 0 ? SLAB : 0);
+    uint8_t *slab = smem + wave * a.slab;
     __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
 
     uint64_t lo, hi;
     load_group_ends(a, a.r0 + g * 64, lane, lo, hi);
-    Group cur = make_group<SLAB>(a, a.r0 + g * 64, lane, lo, hi);
+    Group cur = make_group(a, a.r0 + g * 64, lane, lo, hi, a.slab);
     if (cur.in_lds) issue_dma(rsrc, slab, cur, lane);
 
     while (true) {
@@ -642,7 +650,7 @@ __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
         uint64_t nlo = 0, nhi = 0;
         if (has_next) load_group_ends(a, a.r0 + gn * 64, lane, nlo, nhi);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        Group nxt = make_group<SLAB>(a, has_next ? a.r0 + gn * 64 : base, lane, nlo, nhi);
+        Group nxt = make_group(a, has_next ? a.r0 + gn * 64 : base, lane, nlo, nhi, a.slab);
 
         if (cur.in_lds) {
             fix_stream_tail(a, rsrc, slab, cur, lane);
@@ -684,23 +692,23 @@ __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
 // One group per wave (the default grid): stage, decode, done.  Same steps as one iteration of
 // decode_flat_body without the hand-off to a next group, so nothing fences the fast path's
 // LDS reads from its decode and stores.
-template <int SLAB, class Spec>
+template <class Spec>
 __device__ __forceinline__ void decode_flat_once(const DecodeArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const uint64_t base = a.r0 + ((uint64_t)blockIdx.x * DEC_WAVES + wave) * 64;
+    const uint64_t base = a.r0 + ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * 64;
     if (base >= a.n) return;
     const uint64_t r = base + lane;
     const bool valid = r < a.n;
-    uint8_t *slab = smem + wave * (SLAB > 0 ? SLAB : 0);
+    uint8_t *slab = smem + wave * a.slab;
     __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
     const uint64_t hi = a.ends[valid ? r : a.n - 1];
     uint64_t lo = __shfl_up(hi, 1);
     if (lane == 0) lo = r == 0 ? 0 : a.ends[r - 1];
     lo += a.head;
-    const Group cur = make_group<SLAB>(a, base, lane, lo, hi);
+    const Group cur = make_group(a, base, lane, lo, hi, a.slab);
     if (cur.in_lds) {
         issue_dma(rsrc, slab, cur, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -729,34 +737,40 @@ __device__ __forceinline__ void decode_flat_once(const DecodeArgs &a) {
 }
 
 // Kernel entry: PERSIST selects the persistent, software-pipelined loop.
-template <bool PERSIST, int SLAB, class Spec>
+template <bool PERSIST, class Spec>
 __device__ __forceinline__ void decode_flat_entry(const DecodeArgs &a) {
     if constexpr (PERSIST)
-        decode_flat_body<SLAB, Spec>(a);
+        decode_flat_body<Spec>(a);
     else
-        decode_flat_once<SLAB, Spec>(a);
+        decode_flat_once<Spec>(a);
 }
 
-// slab class shared by the launchers (host): average record size * 64 * margin; 3 = none
-__host__ __device__ inline int decode_slab_class(double avg_record) {
-    double span = avg_record * 64 * 1.08 + 64.0;
-    for (int c = 0; c < 3; c++)
-        if (span <= slab_chunks(c) * 1024) return c;
-    return 3;
-}
+// Launch shape of the flat decode: per-wave slab, waves per block, grid.
+struct DecodeLaunch {
+    uint32_t slab;   // bytes per wave
+    unsigned wpb;    // waves per block
+    unsigned blocks;
+    size_t lds;      // dynamic LDS per block
+};
 
-// Grid: one wave per group (default, measured faster on MI355X: a finished block frees its
-// LDS for the next one), or persistent — as many 4-wave blocks as the CUs hold at once
-// (LDS-bound), each wave looping over groups with the next group's DMA overlapping this
-// group's decode (SPEC_AMD_PERSIST=1).
-__host__ inline unsigned decode_grid(uint64_t n, int cus, int slab, bool persistent) {
-    const uint64_t groups = (n + 63) / 64;
-    const uint64_t need = (groups + DEC_WAVES - 1) / DEC_WAVES;
-    if (!persistent) return (unsigned)need; // one group per wave
-    int per_cu = slab > 0 ? (160 * 1024) / (DEC_WAVES * slab) : 8;
-    per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
-    const uint64_t cap = (uint64_t)cus * per_cu;
-    return (unsigned)(need < cap ? need : cap);
+// One group per wave (default): `wpb` waves per block (1 packs the most slabs per CU: LDS
+// is the occupancy limit).  Persistent: as many blocks as the CUs hold at once, each wave
+// looping over groups with the next group's DMA overlapping this group's decode.
+__host__ inline DecodeLaunch decode_launch(uint64_t nrec, double avg_record, int cus, bool persistent, unsigned wpb) {
+    DecodeLaunch L;
+    L.slab = decode_slab_bytes(avg_record);
+    L.wpb = wpb < 1 ? 1 : (wpb > 4 ? 4 : wpb);
+    const uint64_t groups = (nrec + 63) / 64;
+    uint64_t need = (groups + L.wpb - 1) / L.wpb;
+    if (persistent) {
+        int per_cu = L.slab > 0 ? (int)((160 * 1024) / (L.wpb * L.slab)) : 8;
+        per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
+        const uint64_t cap = (uint64_t)cus * per_cu;
+        need = need < cap ? need : cap;
+    }
+    L.blocks = (unsigned)need;
+    L.lds = (size_t)L.wpb * L.slab;
+    return L;
 }
 
 } // namespace spec

@@ -9,14 +9,10 @@
 
 namespace spec {
 
-template <int SLAB>
-__global__ __launch_bounds__(256) void decode_flat_kernel(DecodeArgs a) {
-    decode_flat_entry<false, SLAB, RuntimeSpec>(a);
-}
+__global__ __launch_bounds__(256) void decode_flat_kernel(DecodeArgs a) { decode_flat_entry<false, RuntimeSpec>(a); }
 
-template <int SLAB>
 __global__ __launch_bounds__(256) void decode_flat_kernel_persistent(DecodeArgs a) {
-    decode_flat_entry<true, SLAB, RuntimeSpec>(a);
+    decode_flat_entry<true, RuntimeSpec>(a);
 }
 
 bool persistent_decode() {
@@ -25,6 +21,15 @@ bool persistent_decode() {
         return (e && e[0] == '1') ? 1 : 0;
     }();
     return v == 1;
+}
+
+unsigned decode_wpb() {
+    static unsigned v = [] {
+        const char *e = getenv("SPEC_AMD_WPB");
+        int w = e ? atoi(e) : 1;
+        return (unsigned)(w >= 1 && w <= 4 ? w : 1);
+    }();
+    return v;
 }
 
 int device_cus() {
@@ -39,24 +44,15 @@ int device_cus() {
     return cus[dev];
 }
 
-int launch_decode_flat(const DecodeArgs &a, double avg_record, hipStream_t stream) {
+int launch_decode_flat(DecodeArgs a, double avg_record, hipStream_t stream) {
     if (a.n <= a.r0) return 0;
-    const int cls = decode_slab_class(avg_record);
-    const int slab = cls < 3 ? slab_bytes(cls) : 0;
-    dim3 grid(decode_grid(a.n - a.r0, device_cus(), slab, persistent_decode())), block(256);
-#define SPEC_LAUNCH(K)                                                                                          \
-    switch (cls) {                                                                                              \
-    case 0: hipLaunchKernelGGL(K<slab_bytes(0)>, grid, block, DEC_WAVES * slab_bytes(0), stream, a); break;     \
-    case 1: hipLaunchKernelGGL(K<slab_bytes(1)>, grid, block, DEC_WAVES * slab_bytes(1), stream, a); break;     \
-    case 2: hipLaunchKernelGGL(K<slab_bytes(2)>, grid, block, DEC_WAVES * slab_bytes(2), stream, a); break;     \
-    default: hipLaunchKernelGGL(K<0>, grid, block, 0, stream, a); break;                                        \
-    }
-    if (persistent_decode()) {
-        SPEC_LAUNCH(decode_flat_kernel_persistent)
-    } else {
-        SPEC_LAUNCH(decode_flat_kernel)
-    }
-#undef SPEC_LAUNCH
+    const DecodeLaunch L = decode_launch(a.n - a.r0, avg_record, device_cus(), persistent_decode(), decode_wpb());
+    a.slab = L.slab;
+    dim3 grid(L.blocks), block(64 * L.wpb);
+    if (persistent_decode())
+        hipLaunchKernelGGL(decode_flat_kernel_persistent, grid, block, L.lds, stream, a);
+    else
+        hipLaunchKernelGGL(decode_flat_kernel, grid, block, L.lds, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

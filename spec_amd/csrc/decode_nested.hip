@@ -83,7 +83,6 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 
 // Stage one wave's group (records [base, base+64)) into its slab: returns the group; if
 // gr.in_lds the bytes are in LDS when this returns.
-template <int SLAB>
 __device__ __forceinline__ Group stage(const NestedArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint8_t *slab, uint64_t base,
                                        int lane) {
     uint64_t lo, hi;
@@ -95,7 +94,7 @@ __device__ __forceinline__ Group stage(const NestedArgs &a, __amdgpu_buffer_rsrc
     d.r0 = 0;
     d.head = 0;
     load_group_ends(d, base, lane, lo, hi);
-    Group gr = make_group<SLAB>(d, base, lane, lo, hi);
+    Group gr = make_group(d, base, lane, lo, hi, a.slab);
     if (gr.in_lds) {
         issue_dma(rsrc, slab, gr, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -169,17 +168,16 @@ __device__ __forceinline__ void decode_group(const Src &s, long long rs, long lo
     }
 }
 
-template <int SLAB>
 __global__ __launch_bounds__(256) void nested_count_kernel(NestedArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t g = (uint64_t)blockIdx.x * DEC_WAVES + wave;
     const uint64_t base = g * 64;
     if (base >= a.n) return;
-    uint8_t *slab = smem + wave * (SLAB > 0 ? SLAB : 0);
+    uint8_t *slab = smem + wave * a.slab;
     __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
-    const Group gr = stage<SLAB>(a, rsrc, slab, base, lane);
+    const Group gr = stage(a, rsrc, slab, base, lane);
     const bool valid = base + lane < a.n;
     uint32_t cnt = 0;
     if (valid) {
@@ -231,17 +229,16 @@ __global__ __launch_bounds__(1024) void nested_scan_kernel(NestedArgs a) {
     if (t == 0) *a.total = carry;
 }
 
-template <int SLAB>
 __global__ __launch_bounds__(256) void nested_decode_kernel(NestedArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t g = (uint64_t)blockIdx.x * DEC_WAVES + wave;
     const uint64_t base = g * 64;
     if (base >= a.n) return;
-    uint8_t *slab = smem + wave * (SLAB > 0 ? SLAB : 0);
+    uint8_t *slab = smem + wave * a.slab;
     __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
-    const Group gr = stage<SLAB>(a, rsrc, slab, base, lane);
+    const Group gr = stage(a, rsrc, slab, base, lane);
     const uint64_t r = base + lane;
     const bool valid = r < a.n;
     const uint64_t item_base = a.group_base[g];
@@ -258,34 +255,26 @@ __global__ __launch_bounds__(256) void nested_decode_kernel(NestedArgs a) {
 
 } // namespace
 
-int launch_nested_index(const NestedArgs &a, double avg_record, hipStream_t stream) {
+int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream) {
     if (a.n == 0) {
         (void)hipMemsetAsync(a.total, 0, sizeof(uint64_t), stream);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
+    a.slab = decode_slab_bytes(avg_record);
     const uint64_t groups = (a.n + 63) / 64;
-    dim3 grid((unsigned)((groups + DEC_WAVES - 1) / DEC_WAVES)), block(256);
-    switch (decode_slab_class(avg_record)) {
-    case 0: hipLaunchKernelGGL(nested_count_kernel<slab_bytes(0)>, grid, block, DEC_WAVES * slab_bytes(0), stream, a); break;
-    case 1: hipLaunchKernelGGL(nested_count_kernel<slab_bytes(1)>, grid, block, DEC_WAVES * slab_bytes(1), stream, a); break;
-    case 2: hipLaunchKernelGGL(nested_count_kernel<slab_bytes(2)>, grid, block, DEC_WAVES * slab_bytes(2), stream, a); break;
-    default: hipLaunchKernelGGL(nested_count_kernel<0>, grid, block, 0, stream, a); break;
-    }
+    dim3 grid((unsigned)((groups + DEC_WAVES - 1) / DEC_WAVES)), block(64 * DEC_WAVES);
+    hipLaunchKernelGGL(nested_count_kernel, grid, block, (size_t)DEC_WAVES * a.slab, stream, a);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(nested_scan_kernel, dim3(1), dim3(1024), 0, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_nested_decode(const NestedArgs &a, double avg_record, hipStream_t stream) {
+int launch_nested_decode(NestedArgs a, double avg_record, hipStream_t stream) {
     if (a.n == 0) return 0;
+    a.slab = decode_slab_bytes(avg_record);
     const uint64_t groups = (a.n + 63) / 64;
-    dim3 grid((unsigned)((groups + DEC_WAVES - 1) / DEC_WAVES)), block(256);
-    switch (decode_slab_class(avg_record)) {
-    case 0: hipLaunchKernelGGL(nested_decode_kernel<slab_bytes(0)>, grid, block, DEC_WAVES * slab_bytes(0), stream, a); break;
-    case 1: hipLaunchKernelGGL(nested_decode_kernel<slab_bytes(1)>, grid, block, DEC_WAVES * slab_bytes(1), stream, a); break;
-    case 2: hipLaunchKernelGGL(nested_decode_kernel<slab_bytes(2)>, grid, block, DEC_WAVES * slab_bytes(2), stream, a); break;
-    default: hipLaunchKernelGGL(nested_decode_kernel<0>, grid, block, 0, stream, a); break;
-    }
+    dim3 grid((unsigned)((groups + DEC_WAVES - 1) / DEC_WAVES)), block(64 * DEC_WAVES);
+    hipLaunchKernelGGL(nested_decode_kernel, grid, block, (size_t)DEC_WAVES * a.slab, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -78,14 +78,14 @@ bool has_fast_path(const spec_schema *s) {
     return true;
 }
 
-std::string key_of(const spec_schema *s, int slab_class, int device) {
+std::string key_of(const spec_schema *s, int device) {
     std::ostringstream k;
-    k << device << ':' << slab_class << ':' << (spec::persistent_decode() ? 'p' : 'o') << ':';
+    k << device << ':' << (spec::persistent_decode() ? 'p' : 'o') << ':';
     for (uint32_t f = 0; f < s->nfields; f++) k << s->fields[f].tag << '/' << (int)s->fields[f].kind << ',';
     return k.str();
 }
 
-std::string generate(const spec_schema *s, int slab) {
+std::string generate(const spec_schema *s) {
     uint8_t order[SPEC_MAX_FIELDS];
     uint16_t sorted[SPEC_MAX_FIELDS];
     writer_order(s, order, sorted);
@@ -102,14 +102,13 @@ std::string generate(const spec_schema *s, int slab) {
     for (uint32_t k = 0; k < s->nfields; k++) o << (k ? "," : "") << sorted[k];
     o << "};\n};\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void spec_decode_flat_jit(spec::DecodeArgs a) {\n"
-      << "  spec::decode_flat_entry<" << (spec::persistent_decode() ? "true" : "false") << ", " << slab
-      << ", GenSpec>(a);\n}\n";
+      << "  spec::decode_flat_entry<" << (spec::persistent_decode() ? "true" : "false") << ", GenSpec>(a);\n}\n";
     return o.str();
 }
 
 // hiprtc compile only; returns the code object (empty on failure)
-std::vector<char> compile_code(const spec_schema *s, int slab) {
-    std::string src = generate(s, slab);
+std::vector<char> compile_code(const spec_schema *s) {
+    std::string src = generate(s);
     const char *hdr_src[2] = {kSpecDeviceHpp, kDecodeCoreHpp};
     const char *hdr_name[2] = {"spec_device.hpp", "decode_core.hpp"};
     hiprtcProgram prog;
@@ -143,9 +142,9 @@ std::vector<char> compile_code(const spec_schema *s, int slab) {
     return code;
 }
 
-Entry compile(const spec_schema *s, int slab) {
+Entry compile(const spec_schema *s) {
     Entry e;
-    std::vector<char> code = compile_code(s, slab);
+    std::vector<char> code = compile_code(s);
     if (code.empty()) {
         e.failed = true;
         return e;
@@ -160,15 +159,15 @@ Entry compile(const spec_schema *s, int slab) {
 }
 
 // nullptr => use the generic kernel
-hipFunction_t lookup(const spec_schema *s, int slab_class) {
-    if (slab_class > 2 || !enabled() || !has_fast_path(s)) return nullptr;
+hipFunction_t lookup(const spec_schema *s) {
+    if (!enabled() || !has_fast_path(s)) return nullptr;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::string k = key_of(s, slab_class, dev);
+    std::string k = key_of(s, dev);
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_cache.find(k);
     if (it == g_cache.end()) {
-        Entry e = compile(s, spec::slab_bytes(slab_class));
+        Entry e = compile(s);
         if (e.failed && debug()) fprintf(stderr, "spec_amd jit: compile/load failed, generic kernel in use\n");
         it = g_cache.emplace(k, e).first;
     }
@@ -181,28 +180,25 @@ namespace spec {
 
 void jit_set_enabled(int on) { g_enabled = on ? 1 : 0; }
 
-long long jit_compile_only(const spec_schema *schema, double avg_record) {
-    const int cls = decode_slab_class(avg_record);
-    if (cls > 2 || !has_fast_path(schema)) return 0;
-    return (long long)compile_code(schema, slab_bytes(cls)).size();
+long long jit_compile_only(const spec_schema *schema, double) {
+    if (!has_fast_path(schema)) return 0;
+    return (long long)compile_code(schema).size();
 }
 
-int jit_prepare_decode_flat(const spec_schema *schema, double avg_record) {
-    return lookup(schema, decode_slab_class(avg_record)) ? 1 : 0;
-}
+int jit_prepare_decode_flat(const spec_schema *schema, double) { return lookup(schema) ? 1 : 0; }
 
 int jit_launch_decode_flat(const spec_schema *schema, const DecodeArgs &a, double avg_record, hipStream_t stream) {
-    const int cls = decode_slab_class(avg_record);
-    hipFunction_t fn = lookup(schema, cls);
+    if (decode_slab_bytes(avg_record) == 0) return 0; // records too large for LDS: generic kernel
+    hipFunction_t fn = lookup(schema);
     if (!fn) return 0;
     if (a.n <= a.r0) return 1;
-    const unsigned blocks = decode_grid(a.n - a.r0, device_cus(), slab_bytes(cls), persistent_decode());
+    const DecodeLaunch L = decode_launch(a.n - a.r0, avg_record, device_cus(), persistent_decode(), decode_wpb());
     DecodeArgs args = a;
+    args.slab = L.slab;
     size_t size = sizeof(args);
     void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                      HIP_LAUNCH_PARAM_END};
-    hipError_t e = hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, DEC_WAVES * slab_bytes(cls), stream,
-                                         nullptr, extra);
+    hipError_t e = hipModuleLaunchKernel(fn, L.blocks, 1, 1, 64 * L.wpb, 1, 1, L.lds, stream, nullptr, extra);
     return e == hipSuccess ? 1 : -1;
 }
 

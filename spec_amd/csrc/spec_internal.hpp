@@ -42,11 +42,12 @@ struct NestedEncodeArgs {
 };
 
 int launch_nested_encode(const NestedEncodeArgs &a, bool write, hipStream_t stream);
-int launch_decode_flat(const DecodeArgs &a, double avg_record, hipStream_t stream);
+int launch_decode_flat(DecodeArgs a, double avg_record, hipStream_t stream);
 int device_cus(); // CUs of the current device (cached)
 bool persistent_decode(); // SPEC_AMD_PERSIST=1
-int launch_nested_index(const NestedArgs &a, double avg_record, hipStream_t stream);
-int launch_nested_decode(const NestedArgs &a, double avg_record, hipStream_t stream);
+unsigned decode_wpb();     // SPEC_AMD_WPB (waves per block, default 1)
+int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream);
+int launch_nested_decode(NestedArgs a, double avg_record, hipStream_t stream);
 // jit.cpp: schema-specialised decode kernel (hiprtc); returns 1 if launched, 0 if the caller
 // should launch the generic kernel, <0 on a HIP error.
 int jit_launch_decode_flat(const spec_schema *schema, const DecodeArgs &a, double avg_record, hipStream_t stream);
