@@ -69,6 +69,8 @@ typedef enum spec_status {
     SPEC_STATUS_INVALID_TABLE = 4,      /* "decode message: invalid table"      */
     SPEC_STATUS_INVALID_DATA = 5,       /* "decode message: invalid data"       */
     SPEC_STATUS_PANIC = 6,              /* the reference would panic (malformed list table) */
+    SPEC_STATUS_INVALID_VALUE = 7,      /* spec_parse_messages: a nested value failed to parse */
+    SPEC_STATUS_TOO_DEEP = 8,           /* spec_parse_messages: nesting deeper than 32 levels */
 } spec_status;
 
 typedef enum spec_rc {
@@ -159,6 +161,19 @@ int spec_frames_index(const uint8_t *buf, uint64_t len, uint64_t *ends, uint64_t
 int spec_decode_frames(const spec_schema *schema, const uint8_t *frames, uint64_t frames_len,
                        const uint64_t *ends, uint64_t r0, uint64_t r1, void *const *columns, uint8_t *status,
                        void *stream);
+
+/* ---- recursive validation ----
+ * spec_parse_messages: for every record, spec.ParseMessage (msg.go:29-32 ->
+ * internal/types/msg.go:58-82): the message table, then ParseValue on every non-empty field,
+ * recursing into lists and messages (internal/types/list.go:35-53, value.go:49-113) — what
+ * mpx runs on each received frame (mpx/conn_reader.go:119).  status[i]: SPEC_STATUS_OK, the
+ * top-level trailer class (1-5), SPEC_STATUS_PANIC (a list element whose start > end: Go
+ * panics), SPEC_STATUS_INVALID_VALUE (any nested error), or SPEC_STATUS_TOO_DEEP (more than
+ * 32 nested containers; the reference recurses without a bound).  sizes[i] (optional) =
+ * ParseMessage's size (bytes of the message), 0 on error.  head = bytes before each record
+ * (4 for mpx frames, see spec_frames_index). */
+int spec_parse_messages(const uint8_t *stream_bytes, uint64_t stream_len, const uint64_t *ends, uint64_t n,
+                        uint32_t head, uint8_t *status, uint32_t *sizes, void *stream);
 
 /* spec_decode_flat_prepare: compile (once per device, schema and record-size class) the
  * schema-specialised decode kernel that spec_decode_flat uses when one exists — the

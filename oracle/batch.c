@@ -284,3 +284,28 @@ int so_decode_nested_batch(const uint8_t *stream, const uint64_t *ends, uint64_t
     }
     return 0;
 }
+
+/* ---- ParseMessage over a batch (spec_parse_messages semantics) ---- */
+int so_parse_batch(const uint8_t *stream, const uint64_t *ends, uint64_t n, uint32_t head, uint8_t *status,
+                   uint32_t *sizes) {
+    for (uint64_t r = 0; r < n; r++) {
+        uint64_t s = (r ? ends[r - 1] : 0) + head;
+        uint64_t e = ends[r] < s ? s : ends[r];
+        so_message m;
+        sizes[r] = 0;
+        so_err err = so_open_message_err(stream + s, (size_t)(e - s), &m);
+        if (err) {
+            status[r] = classify(err);
+            continue;
+        }
+        int size = 0;
+        err = so_parse_message(stream + s, (size_t)(e - s), &m, &size);
+        if (err) {
+            status[r] = strstr(err, "index out of range") ? ST_PANIC : 7;
+            continue;
+        }
+        status[r] = 0;
+        sizes[r] = (uint32_t)size;
+    }
+    return 0;
+}

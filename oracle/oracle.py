@@ -217,6 +217,7 @@ def _declare(L):
                                                             C.c_void_p]
     L.so_decode_nested_counts.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
     L.so_decode_nested_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64] + [C.c_void_p] * 9
+    L.so_parse_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]
 
 
 def _e(err):
@@ -593,3 +594,14 @@ def decode_nested_batch(stream: np.ndarray, ends: np.ndarray):
     for k in ("key", "value", "label", "item_status"):
         out[k] = out[k][:m]
     return out
+
+
+def parse_batch(stream: np.ndarray, ends: np.ndarray, head: int = 0):
+    """ParseMessage per record -> (status uint8[n], sizes uint32[n]) (spec_parse_messages semantics)."""
+    n = len(ends)
+    stream = np.ascontiguousarray(stream, dtype=np.uint8)
+    ends = np.ascontiguousarray(ends, dtype=np.uint64)
+    st = np.zeros(n, np.uint8)
+    sz = np.zeros(n, np.uint32)
+    lib().so_parse_batch(_ptr(stream), _ptr(ends), n, head, _ptr(st), _ptr(sz))
+    return st, sz

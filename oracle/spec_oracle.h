@@ -321,6 +321,12 @@ int so_decode_nested_batch(const uint8_t *stream, const uint64_t *ends, uint64_t
                            uint32_t *name, int32_t *key, double *value, uint32_t *label,
                            uint8_t *item_status, uint8_t *status);
 
+/* ParseMessage per record (spec_parse_messages semantics): status 0 ok, 1-5 trailer class,
+ * 6 panic (list element start > end), 7 nested value error; sizes = message bytes or 0.
+ * head = bytes before each record (4 for mpx frames). */
+int so_parse_batch(const uint8_t *stream, const uint64_t *ends, uint64_t n, uint32_t head, uint8_t *status,
+                   uint32_t *sizes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -6,7 +6,7 @@ decoded into SoA columns / encoded from them by hand-written gfx950 kernels
 (spec_amd/csrc, C ABI in include/spec_amd.h).  See DESIGN.md.
 """
 from ._lib import LIB_PATH, SpecError, header_symbols, lib, set_jit
-from .batch import Columns, Decoder, Encoder, alloc_columns, decode_flat, encode_flat
+from .batch import Columns, Decoder, Encoder, alloc_columns, decode_flat, encode_flat, parse_messages
 from .frames import decode_frames, frames_index, make_frames
 from .pipeline import HostDecoder
 from .nested import NestedColumns, NestedDecoder, NestedEncoder, decode_nested, encode_nested
@@ -14,7 +14,7 @@ from .schema import FLAT16, NESTED, Field, Kind, NestedSchema, Schema
 
 __all__ = [
     "HostDecoder", "decode_frames", "frames_index", "make_frames", "LIB_PATH", "SpecError", "header_symbols", "lib", "set_jit", "Columns", "Decoder", "Encoder", "alloc_columns",
-    "decode_flat", "encode_flat", "FLAT16", "Field", "Kind", "Schema",
+    "decode_flat", "encode_flat", "parse_messages", "FLAT16", "Field", "Kind", "Schema",
     "NESTED", "NestedSchema", "NestedColumns", "NestedDecoder", "NestedEncoder", "decode_nested",
     "encode_nested",
 ]

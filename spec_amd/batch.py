@@ -179,3 +179,17 @@ def encode_flat(schema: Schema, cols, heaps: dict, n: int | None = None, cuda_st
     if int(enc.total.item()) != total:  # heap-range check failed in the full pass
         raise _lib.SpecError(-1, "spec_encode_flat: encoder error (span outside its heap)")
     return out[:total], ends
+
+
+def parse_messages(stream: torch.Tensor, ends: torch.Tensor, head: int = 0, sizes: bool = True, cuda_stream=None):
+    """spec_parse_messages: spec.ParseMessage (recursive validation) of every record.
+    Returns (status uint8 [n], sizes int32 view of uint32 [n] or None)."""
+    _check_dev(stream, "stream", torch.uint8)
+    _check_dev(ends, "ends", torch.int64)
+    n = ends.numel()
+    st = torch.empty(n, dtype=torch.uint8, device=stream.device)
+    sz = torch.empty(n, dtype=torch.int32, device=stream.device) if sizes else None
+    rc = _lib.lib().spec_parse_messages(_ptr(stream), stream.numel(), _ptr(ends), n, head, _ptr(st), _ptr(sz),
+                                        _stream_handle(cuda_stream))
+    _lib.check(rc, "spec_parse_messages")
+    return st, sz

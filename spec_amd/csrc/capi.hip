@@ -225,6 +225,24 @@ int spec_frames_index(const uint8_t *buf, uint64_t len, uint64_t *ends, uint64_t
     return SPEC_OK;
 }
 
+int spec_parse_messages(const uint8_t *stream_bytes, uint64_t stream_len, const uint64_t *ends, uint64_t n,
+                        uint32_t head, uint8_t *status, uint32_t *sizes, void *stream) {
+    if (n == 0) return SPEC_OK;
+    if (!ends || !status || (!stream_bytes && stream_len)) return SPEC_E_INVALID_ARGUMENT;
+    if (stream_len >= (1ull << 32)) return SPEC_E_TOO_LARGE;
+    spec::DecodeArgs a;
+    memset(&a, 0, sizeof(a));
+    a.stream = stream_bytes;
+    a.stream_len = stream_len;
+    a.ends = ends;
+    a.n = n;
+    a.head = head;
+    a.f.status = status;
+    if (spec::launch_parse(a, sizes, (double)stream_len / (double)n, (hipStream_t)stream))
+        return hip_rc(hipGetLastError());
+    return SPEC_OK;
+}
+
 int spec_decode_flat_prepare(const spec_schema *schema, uint64_t stream_len, uint64_t n) {
     int rc = check_schema(schema);
     if (rc) return rc;

@@ -56,7 +56,7 @@ enum : uint32_t {
 // ---- record status (include/spec_amd.h spec_status)
 enum : uint32_t {
     ST_OK = 0, ST_INVALID_TYPE = 1, ST_INVALID_TABLE_SIZE = 2, ST_INVALID_DATA_SIZE = 3,
-    ST_INVALID_TABLE = 4, ST_INVALID_DATA = 5, ST_PANIC = 6,
+    ST_INVALID_TABLE = 4, ST_INVALID_DATA = 5, ST_PANIC = 6, ST_INVALID_VALUE = 7, ST_TOO_DEEP = 8,
 };
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }

@@ -46,6 +46,7 @@ int launch_decode_flat(DecodeArgs a, double avg_record, hipStream_t stream);
 int device_cus(); // CUs of the current device (cached)
 bool persistent_decode(); // SPEC_AMD_PERSIST=1
 unsigned decode_wpb();     // SPEC_AMD_WPB (waves per block, default 1)
+int launch_parse(DecodeArgs a, uint32_t *sizes, double avg_record, hipStream_t stream);
 int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream);
 int launch_nested_decode(NestedArgs a, double avg_record, hipStream_t stream);
 // jit.cpp: schema-specialised decode kernel (hiprtc); returns 1 if launched, 0 if the caller

@@ -1,0 +1,175 @@
+// validate.hip — bulk ParseMessage: recursive validation of every record.
+//
+// What mpx runs on every received frame (mpx/conn_reader.go:119: pmpx.ParseMessage):
+//   ParseMessage(b)  internal/types/msg.go:58-82  — DecodeMessageTable, then ParseValue on
+//                    every non-empty field slice m.bytes[:end_i] in table order (fieldAt,
+//                    msg.go:477-486: end > dataSize => nil, skipped)
+//   ParseList(b)     internal/types/list.go:35-53 — DecodeListTable, then ParseValue on every
+//                    non-empty element (GetBytes: end > dataSize => nil; start > end panics)
+//   ParseValue(b)    internal/types/value.go:49-113 — per type: the decoder's error checks,
+//                    recursion into lists/messages, "unsupported type" otherwise.
+// One lane per record, depth-first with an explicit stack (the reference recurses; nesting
+// deeper than VAL_MAX_DEPTH reports SPEC_STATUS_TOO_DEEP).  Records are staged in LDS like
+// the decoders'; larger spans parse from HBM.
+#include <hip/hip_runtime.h>
+
+#include "decode_core.hpp"
+#include "spec_internal.hpp"
+
+namespace spec {
+
+namespace {
+
+constexpr int VAL_MAX_DEPTH = 32;
+
+struct Frame {
+    long long base, tstart; // data start, table start (source positions)
+    uint32_t nent, i, dsize;
+    uint8_t list, big;
+};
+
+// The decoder error checks ParseValue runs for a scalar of type `type` ending at e.
+template <class Src>
+__device__ __forceinline__ bool scalar_ok(const Src &s, uint32_t type, long long lo, long long e) {
+    const long long flen = e - lo;
+    const Tail t = load_tail(s, (typename Src::pos_t)e);
+    const uint64_t R = tail_r(t);
+    const uint32_t R2 = tail_r2(t);
+    const long long avail = flen - 1;
+    int m;
+    switch (type) {
+    case T_TRUE:
+    case T_FALSE: return true;
+    case T_BYTE: return flen >= 2;                                   // byte.go:16-34
+    case T_INT16: {                                                  // int.go:16-62
+        const int32_t x = unzigzag32((uint32_t)rvarint_bf(R, R2, avail, 5, m));
+        return m >= 0 && x >= -32768 && x <= 32767;
+    }
+    case T_INT32:
+    case T_UINT32: rvarint_bf(R, R2, avail, 5, m); return m >= 0;   // int.go:64-103, uint.go:58-95
+    case T_INT64:
+    case T_UINT64: rvarint_bf(R, R2, avail, 10, m); return m >= 0;  // int.go:105-135, uint.go:97-125
+    case T_UINT16: {                                                 // uint.go:16-56
+        const uint64_t x = rvarint_bf(R, R2, avail, 5, m);
+        return m >= 0 && x <= 0xffff;
+    }
+    case T_BIN64: return flen >= 9;                                  // bin.go:15-112
+    case T_BIN128: return flen >= 17;
+    case T_BIN256: return flen >= 33;
+    case T_FLOAT32: {                                                // float.go:15-32: +-Inf > MaxFloat32
+        const uint32_t b = (uint32_t)(R & 0xffffffffu);
+        return flen >= 5 && (b & 0x7fffffffu) != 0x7f800000u;
+    }
+    case T_FLOAT64: return flen >= 9;                                // float.go:34-49
+    case T_BYTES: {                                                  // bytes.go:14-58
+        const uint32_t ds = (uint32_t)rvarint_bf(R, R2, avail, 5, m);
+        return m >= 0 && (e - 1 - m) - (long long)ds >= lo;
+    }
+    case T_STRING: {                                                 // string.go:15-47 (+1: the NUL)
+        const uint32_t ds = (uint32_t)rvarint_bf(R, R2, avail, 5, m);
+        const long long end = e - 1 - m - 1;
+        return m >= 0 && end >= lo && end - (long long)ds >= lo;
+    }
+    case T_STRUCT: rvarint_bf(R, R2, avail, 5, m); return m >= 0;   // struct.go:14-42 (no bound check)
+    }
+    return false; // "unsupported type", value.go:103-104
+}
+
+template <class Src>
+__device__ __forceinline__ uint32_t be_at(const Src &s, long long p, int bytes) {
+    uint32_t v = 0;
+    for (int k = 0; k < bytes; k++) v = (v << 8) | s.u8((typename Src::pos_t)(p + k));
+    return v;
+}
+
+// ParseMessage of record [rs, re): status and size (message bytes, 0 on error).
+template <class Src>
+__device__ __forceinline__ uint32_t parse_record(const Src &s, long long rs, long long re, uint32_t &size) {
+    using pos_t = typename Src::pos_t;
+    size = 0;
+    if (re <= rs) return ST_OK; // empty input: zero message, no error
+    const Trailer top = parse_trailer<false>(s, (pos_t)rs, (pos_t)re);
+    if (top.st != ST_OK) return top.st;
+    Frame stk[VAL_MAX_DEPTH];
+    int sp = 0;
+    stk[sp++] = Frame{top.dstart, top.tstart, top.tsize / (top.big ? 6u : 3u), 0, top.dsize, 0, (uint8_t)top.big};
+    while (sp > 0) {
+        Frame &f = stk[sp - 1];
+        if (f.i >= f.nent) {
+            sp--;
+            continue;
+        }
+        const uint32_t i = f.i++;
+        long long lo = f.base, e;
+        if (!f.list) { // fieldAt(i): table entry i's end
+            const uint32_t end = f.big ? be_at(s, f.tstart + 6ll * i + 2, 4) : be_at(s, f.tstart + 3ll * i + 1, 2);
+            if (end > f.dsize) continue; // nil
+            e = f.base + end;
+        } else { // GetBytes(i)
+            const int w = f.big ? 4 : 2;
+            const uint32_t end = be_at(s, f.tstart + (long long)w * i, w);
+            const uint32_t start = i ? be_at(s, f.tstart + (long long)w * (i - 1), w) : 0;
+            if (end > f.dsize) continue; // nil
+            if (start > end) return ST_PANIC; // Go: slice bounds out of range
+            lo = f.base + start;
+            e = f.base + end;
+        }
+        if (e <= lo) continue; // empty value: skipped
+        const uint32_t type = s.u8((pos_t)(e - 1));
+        if (type == T_LIST || type == T_BIG_LIST || type == T_MESSAGE || type == T_BIG_MESSAGE) {
+            const bool list = type == T_LIST || type == T_BIG_LIST;
+            const Trailer tr = list ? parse_trailer<true>(s, (pos_t)lo, (pos_t)e) : parse_trailer<false>(s, (pos_t)lo, (pos_t)e);
+            if (tr.st != ST_OK) return ST_INVALID_VALUE;
+            if (sp == VAL_MAX_DEPTH) return ST_TOO_DEEP;
+            const uint32_t es = list ? (tr.big ? 4u : 2u) : (tr.big ? 6u : 3u);
+            stk[sp++] = Frame{tr.dstart, tr.tstart, tr.tsize / es, 0, tr.dsize, (uint8_t)list, (uint8_t)tr.big};
+        } else if (!scalar_ok(s, type, lo, e)) {
+            return ST_INVALID_VALUE;
+        }
+    }
+    size = (uint32_t)(re - top.dstart);
+    return ST_OK;
+}
+
+__global__ __launch_bounds__(256) void parse_kernel(DecodeArgs a, uint32_t *sizes) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t base = a.r0 + ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * 64;
+    if (base >= a.n) return;
+    const uint64_t r = base + lane;
+    const bool valid = r < a.n;
+    uint8_t *slab = smem + wave * a.slab;
+    __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
+    uint64_t lo, hi;
+    load_group_ends(a, base, lane, lo, hi);
+    const Group gr = make_group(a, base, lane, lo, hi, a.slab);
+    uint32_t st = ST_OK, size = 0;
+    if (gr.in_lds) {
+        issue_dma(rsrc, slab, gr, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        fix_stream_tail(a, rsrc, slab, gr, lane);
+        if (!valid) return;
+        LdsSrc s{(lds_u8 *)slab};
+        st = parse_record(s, SLAB_GUARD + (long long)(gr.rec_lo - gr.aligned_lo),
+                          SLAB_GUARD + (long long)(gr.rec_hi - gr.aligned_lo), size);
+    } else {
+        if (!valid) return;
+        GlobalSrc s{rsrc, a.stream_len};
+        st = parse_record(s, (long long)gr.rec_lo, (long long)gr.rec_hi, size);
+    }
+    a.f.status[r] = (uint8_t)st;
+    if (sizes) sizes[r] = size;
+}
+
+} // namespace
+
+int launch_parse(DecodeArgs a, uint32_t *sizes, double avg_record, hipStream_t stream) {
+    if (a.n <= a.r0) return 0;
+    const DecodeLaunch L = decode_launch(a.n - a.r0, avg_record, device_cus(), false, 1);
+    a.slab = L.slab;
+    hipLaunchKernelGGL(parse_kernel, dim3(L.blocks), dim3(64 * L.wpb), L.lds, stream, a, sizes);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+} // namespace spec
