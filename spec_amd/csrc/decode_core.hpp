@@ -640,17 +640,19 @@ __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
     load_group_ends(a, a.r0 + g * 64, lane, lo, hi);
     Group cur = make_group(a, a.r0 + g * 64, lane, lo, hi, a.slab);
     if (cur.in_lds) issue_dma(rsrc, slab, cur, lane);
+    // the next group's ends are always one iteration ahead
+    uint64_t gn = g + stride, nlo = 0, nhi = 0;
+    if (gn < ngroups) load_group_ends(a, a.r0 + gn * 64, lane, nlo, nhi);
 
     while (true) {
         const uint64_t base = a.r0 + g * 64;
         const uint64_t r = base + lane;
         const bool valid = r < a.n;
-        const uint64_t gn = g + stride;
         const bool has_next = gn < ngroups;
-        uint64_t nlo = 0, nhi = 0;
-        if (has_next) load_group_ends(a, a.r0 + gn * 64, lane, nlo, nhi);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        Group nxt = make_group(a, has_next ? a.r0 + gn * 64 : base, lane, nlo, nhi, a.slab);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this group's DMA, the next group's ends
+        const Group nxt = make_group(a, has_next ? a.r0 + gn * 64 : base, lane, nlo, nhi, a.slab);
+        const uint64_t g2 = gn + stride;
+        uint64_t lo2 = 0, hi2 = 0;
 
         if (cur.in_lds) {
             fix_stream_tail(a, rsrc, slab, cur, lane);
@@ -658,26 +660,23 @@ __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
             const int rs = SLAB_GUARD + (int)(cur.rec_lo - cur.aligned_lo);
             const int re = SLAB_GUARD + (int)(cur.rec_hi - cur.aligned_lo);
             const long long to_stream = (long long)cur.aligned_lo - SLAB_GUARD;
-#if defined(SPEC_EXP) && SPEC_EXP == 1 // diagnostic: staging only
-            if (valid && a.f.status) a.f.status[r] = slab[re - 1];
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (has_next && nxt.in_lds) issue_dma(rsrc, slab, nxt, lane);
-#else
             if constexpr (Spec::N > 0) {
                 FastRec<Spec> fr;
                 bool fast = valid && fast_prepare<Spec>(s, rs, re, fr);
                 if (valid && !fast) decode_record_generic(s, rs, re, r, a.f, to_stream);
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // every LDS read of this group done
                 if (has_next && nxt.in_lds) issue_dma(rsrc, slab, nxt, lane);
+                if (g2 < ngroups) load_group_ends(a, a.r0 + g2 * 64, lane, lo2, hi2);
                 if (fast) fast_finish<Spec>(fr, r, a, to_stream);
             } else {
                 if (valid) decode_record_generic(s, rs, re, r, a.f, to_stream);
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 if (has_next && nxt.in_lds) issue_dma(rsrc, slab, nxt, lane);
+                if (g2 < ngroups) load_group_ends(a, a.r0 + g2 * 64, lane, lo2, hi2);
             }
-#endif
         } else {
             if (has_next && nxt.in_lds) issue_dma(rsrc, slab, nxt, lane);
+            if (g2 < ngroups) load_group_ends(a, a.r0 + g2 * 64, lane, lo2, hi2);
             if (valid) {
                 GlobalSrc s{rsrc, a.stream_len};
                 decode_record_generic(s, (long long)cur.rec_lo, (long long)cur.rec_hi, r, a.f, 0);
@@ -685,7 +684,10 @@ __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
         }
         if (!has_next) break;
         g = gn;
+        gn = g2;
         cur = nxt;
+        nlo = lo2;
+        nhi = hi2;
     }
 }
 

@@ -1,19 +1,19 @@
 #!/bin/bash
-# One GPU-box pass: parity tests, smoke, bench, rocprofv3 kernel stats.
-# Usage (from this container): gpurun --timeout 900 -- bash tools/gpu_round.sh TAG [quick]
+# One GPU-box pass: parity tests, smoke, bench, rocprofv3 kernel stats, PMC traffic.
+# Usage (from this container): gpurun --timeout 1100 -- bash tools/gpu_round.sh TAG [quick|full]
 set -o pipefail
 TAG=${1:-dev}
 MODE=${2:-full}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+export TMPDIR=/tmp
 echo "== pytest -m gpu"
 timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1
 rc=$?; tail -n 3 $OUT/pytest_gpu.log; echo "pytest_rc=$rc"
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 echo "== smoke"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -n 20 $OUT/smoke.log; exit 1; }
-tail -n 2 $OUT/smoke.log
+tail -n 1 $OUT/smoke.log
 echo "== bench"
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -n 20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
@@ -21,4 +21,7 @@ cat $OUT/bench.json
 echo "== rocprofv3 stats"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu > $OUT/prof.log 2>&1 || { tail -n 20 $OUT/prof.log; exit 1; }
 find $OUT/prof -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats.csv \;
-cut -d, -f1-4 $OUT/kernel_stats.csv | head -n 12
+cut -d, -f1-4 $OUT/kernel_stats.csv | head -n 14
+echo "== pmc traffic"
+bash tools/pmc.sh $OUT/pmc "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT" -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-extras > $OUT/pmc.log 2>&1 || { tail -n 20 $OUT/pmc.log; exit 1; }
+python3 tools/pmc_traffic.py $OUT/pmc 1048576 $OUT/pmc_traffic.json > /dev/null && cat $OUT/pmc_traffic.json
