@@ -209,10 +209,37 @@ struct Emit {
         put4((uint32_t)w);
         put4((uint32_t)(w >> 32));
     }
+    // k (0..8) bytes of v, lowest byte first, merged into the pending dword
+    __device__ __forceinline__ void put_n(uint64_t v, uint32_t k) {
+        const uint32_t ph = (uint32_t)(pos & 3), sh = 8 * ph;
+        const uint64_t lo64 = (uint64_t)acc | (v << sh);
+        const uint32_t hi32 = sh ? (uint32_t)(v >> (64 - sh)) : 0u;
+        const uint32_t total = ph + k;
+        const Pos d = pos & ~(Pos)3;
+        if (total >= 4) flush_dword(d, (uint32_t)lo64);
+        if (total >= 8) flush_dword(d + 4, (uint32_t)(lo64 >> 32));
+        const uint32_t full = total >> 2;
+        const uint32_t rest = full == 0 ? (uint32_t)lo64 : (full == 1 ? (uint32_t)(lo64 >> 32) : hi32);
+        const uint32_t keep = total & 3;
+        acc = keep ? (rest & (0xffffffffu >> (32 - 8 * keep))) : 0u;
+        pos += k;
+    }
     // reverse varint (oracle/compactint.c so_put_reverse_*): top group first, MSB clear;
-    // following groups carry 0x80; the least-significant group is the last byte
+    // following groups carry 0x80; the least-significant group is the last byte.  Up to 8
+    // bytes (values < 2^56) are built in a register and appended at once.
     __device__ __forceinline__ void rvarint(uint64_t v) {
-        uint32_t L = vlen64(v);
+        const uint32_t L = vlen64(v);
+        if (L <= 8) {
+            uint64_t x = v & 0x00ffffffffffffffull; // 7-bit groups -> bytes (inverse of rvarint_bf)
+            x = (x & 0x000000000fffffffull) | ((x << 4) & 0x0fffffff00000000ull);
+            x = (x & 0x00003fff00003fffull) | ((x << 2) & 0x3fff00003fff0000ull);
+            x = (x & 0x007f007f007f007full) | ((x << 1) & 0x7f007f007f007f00ull);
+            const uint32_t drop = 8 * (8 - L);
+            uint64_t out = __builtin_bswap64(x) >> drop;        // byte i = group L-1-i
+            const uint64_t cont = (0x8080808080808080ull >> drop) & ~0xffull; // all but the first byte
+            put_n(out | cont, L);
+            return;
+        }
         for (uint32_t i = 0; i < L; i++) {
             uint32_t g = (uint32_t)(v >> (7 * (L - 1 - i))) & 0x7f;
             put1(g | (i ? 0x80 : 0));
