@@ -55,6 +55,7 @@ struct DecodeArgs {
     uint64_t r0;
     uint32_t head; // bytes before each record (mpx frame head = 4: [u32 BE size][message])
     uint32_t slab; // LDS bytes per wave (0: every wave parses from HBM)
+    uint32_t xcd;  // 1: XCD-aware block order (consecutive groups on one XCD's L2)
     FieldSet f;
 };
 
@@ -699,7 +700,15 @@ __device__ __forceinline__ void decode_flat_once(const DecodeArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const uint64_t base = a.r0 + ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * 64;
+    // blocks are dealt round-robin to the 8 XCDs: with xcd = 1, block b takes the b/8-th slot
+    // of XCD b%8's contiguous share of the groups, so neighbouring groups (which share the
+    // narrow columns' cache lines) are written through one L2
+    uint64_t blk = blockIdx.x;
+    if (a.xcd) {
+        const uint64_t per = (gridDim.x + 7) / 8;
+        blk = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    }
+    const uint64_t base = a.r0 + (blk * (blockDim.x >> 6) + wave) * 64;
     if (base >= a.n) return;
     const uint64_t r = base + lane;
     const bool valid = r < a.n;
@@ -747,6 +756,8 @@ __device__ __forceinline__ void decode_flat_entry(const DecodeArgs &a) {
         decode_flat_once<Spec>(a);
 }
 
+bool xcd_swizzle_decode(); // SPEC_AMD_XCD=1 (decode_flat.hip)
+
 // Launch shape of the flat decode: per-wave slab, waves per block, grid.
 struct DecodeLaunch {
     uint32_t slab;   // bytes per wave
@@ -764,6 +775,7 @@ __host__ inline DecodeLaunch decode_launch(uint64_t nrec, double avg_record, int
     L.wpb = wpb < 1 ? 1 : (wpb > 4 ? 4 : wpb);
     const uint64_t groups = (nrec + 63) / 64;
     uint64_t need = (groups + L.wpb - 1) / L.wpb;
+    if (xcd_swizzle_decode() && !persistent) need = (need + 7) / 8 * 8; // 8 equal XCD shares
     if (persistent) {
         int per_cu = L.slab > 0 ? (int)((160 * 1024) / (L.wpb * L.slab)) : 8;
         per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);

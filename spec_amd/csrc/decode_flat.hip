@@ -23,6 +23,14 @@ bool persistent_decode() {
     return v == 1;
 }
 
+bool xcd_swizzle_decode() {
+    static int v = [] {
+        const char *e = getenv("SPEC_AMD_XCD");
+        return (e && e[0] == '1') ? 1 : 0;
+    }();
+    return v == 1;
+}
+
 unsigned decode_wpb() {
     static unsigned v = [] {
         const char *e = getenv("SPEC_AMD_WPB");
@@ -48,6 +56,7 @@ int launch_decode_flat(DecodeArgs a, double avg_record, hipStream_t stream) {
     if (a.n <= a.r0) return 0;
     const DecodeLaunch L = decode_launch(a.n - a.r0, avg_record, device_cus(), persistent_decode(), decode_wpb());
     a.slab = L.slab;
+    a.xcd = xcd_swizzle_decode() && !persistent_decode();
     dim3 grid(L.blocks), block(64 * L.wpb);
     if (persistent_decode())
         hipLaunchKernelGGL(decode_flat_kernel_persistent, grid, block, L.lds, stream, a);

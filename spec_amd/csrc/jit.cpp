@@ -195,6 +195,7 @@ int jit_launch_decode_flat(const spec_schema *schema, const DecodeArgs &a, doubl
     const DecodeLaunch L = decode_launch(a.n - a.r0, avg_record, device_cus(), persistent_decode(), decode_wpb());
     DecodeArgs args = a;
     args.slab = L.slab;
+    args.xcd = xcd_swizzle_decode() && !persistent_decode();
     size_t size = sizeof(args);
     void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                      HIP_LAUNCH_PARAM_END};
