@@ -161,14 +161,14 @@ TEST(TestMessageBatchWriter__should_write_records_like_writer) {
 TEST(TestParseMessageBatch__should_validate_records) {
     spec::Stream s;
     HostRecords h = test_records(1000);
-    h.stream[h.ends[10] - 1] = 0x63; // record 11's type byte: unsupported
+    h.stream[h.ends[10] - 1] = 0x63; // record 10: its type byte -> not a message
     spec::Batch b = upload(h.stream, h.ends, s);
     auto st = spec::ParseMessageBatch(b, s).ToHost<uint8_t>(s);
     std::vector<uint8_t> want(h.n);
     std::vector<uint32_t> sizes(h.n);
     so_parse_batch(h.stream.data(), h.ends.data(), h.n, 0, want.data(), sizes.data());
     REQUIRE(std::memcmp(st.data(), want.data(), h.n) == 0);
-    REQUIRE(st[11] == SPEC_STATUS_INVALID_TYPE && st[0] == SPEC_STATUS_OK);
+    REQUIRE(st[10] == SPEC_STATUS_INVALID_TYPE && st[0] == SPEC_STATUS_OK);
 }
 
 TEST(TestError__should_carry_rc) {
