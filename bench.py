@@ -40,8 +40,8 @@ COLUMN_BYTES = FLAT16.column_bytes  # 122
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--records", type=int, default=1 << 20, help="records per GPU")
     p.add_argument("--seed", type=int, default=workload.SEED)
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -112,20 +112,37 @@ def time_decode(dec, steps, warmup, dist):
 
 
 def kernel_time_events(fn, reps):
-    """Average per-launch duration from HIP events recorded on the launch stream.  The stream
-    is first parked behind a spin kernel so every launch and event is queued before the GPU
-    reaches them: the intervals measure the kernel, not host submission latency."""
+    """Average per-launch duration from HIP events on the launch stream: one event pair around
+    `reps` back-to-back launches (an event between every launch adds ~10 us of marker/flush to
+    each interval, which the kernel trace does not see), plus the median of per-launch pairs.
+    The stream is first parked behind a spin kernel so every launch is queued before the GPU
+    reaches them: the interval measures the GPU, not host submission."""
     s = torch.cuda.current_stream()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     if hasattr(torch.cuda, "_sleep"):
         torch.cuda._sleep(int(2e8))  # ~0.1 s of GPU spin while the host enqueues
-    for a, b in evs:
-        a.record(s)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(reps):
         fn()
-        b.record(s)
+    b.record(s)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for x, y in evs:
+        x.record(s)
+        fn()
+        y.record(s)
     torch.cuda.synchronize()
-    ms = sorted(a.elapsed_time(b) for a, b in evs)
-    return sum(ms) / len(ms), ms[len(ms) // 2]
+    ms = sorted(x.elapsed_time(y) for x, y in evs)
+    return a.elapsed_time(b) / reps, ms[len(ms) // 2]
+
+
+def gpu_prewarm(fn, seconds=0.3):
+    """Bring the GPU out of its idle clock state before any timing (MI355X idles at a low sclk;
+    the first ~20 ms of launches run slower)."""
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(20):
+            fn()
+        torch.cuda.synchronize()
 
 
 def cpu_baseline(stream_np, ends_np, seconds):
@@ -255,6 +272,7 @@ def main():
     jit = spec_amd.lib().spec_decode_flat_prepare(FLAT16.c, stream_bytes, n) == 1
     dec = spec_amd.Decoder(FLAT16, stream, ends)
     out_cols, status = dec.cols, dec.status
+    gpu_prewarm(dec)
     elapsed = time_decode(dec, args.steps, args.warmup, dist)
     elapsed = max_over_ranks(dist, elapsed)
     total_records = sum_over_ranks(dist, float(n)) * args.steps
@@ -262,7 +280,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     # per-launch kernel time on the launch stream (HIP events)
-    avg_ms, med_ms = kernel_time_events(dec, max(10, args.steps))
+    avg_ms, med_ms = kernel_time_events(dec, max(20, args.steps))
     alg_bytes = stream_bytes + n * (8 + COLUMN_BYTES + 1)
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
     read_only = (stream_bytes + 8 * n) / (avg_ms * 1e-3) / 1e9

@@ -143,10 +143,11 @@ int spec_decode_flat(const spec_schema *schema, const uint8_t *stream_bytes, uin
 
 /* spec_decode_flat_range: records [r0, r1) of a batch only — stream_bytes/stream_len/ends
  * describe the WHOLE batch (absolute offsets) and columns/status are indexed by record, so a
- * host pipeline can decode chunk k while chunk k+1 is still being copied in. */
+ * host pipeline can decode chunk k while chunk k+1 is still being copied in.  range_bytes =
+ * bytes the range spans (sizes the per-wave LDS staging; 0 = use stream_len / r1). */
 int spec_decode_flat_range(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
-                           const uint64_t *ends, uint64_t r0, uint64_t r1, void *const *columns, uint8_t *status,
-                           void *stream);
+                           const uint64_t *ends, uint64_t r0, uint64_t r1, uint64_t range_bytes, void *const *columns,
+                           uint8_t *status, void *stream);
 
 /* ---- mpx frames (the path's source: mpx/conn_reader.go:179-194, conn_writer.go:84-97) ----
  * An mpx connection carries frames [u32 big-endian size][message], back to back.
@@ -159,8 +160,8 @@ int spec_decode_flat_range(const spec_schema *schema, const uint8_t *stream_byte
 int spec_frames_index(const uint8_t *buf, uint64_t len, uint64_t *ends, uint64_t cap, uint64_t *count,
                       uint64_t *consumed);
 int spec_decode_frames(const spec_schema *schema, const uint8_t *frames, uint64_t frames_len,
-                       const uint64_t *ends, uint64_t r0, uint64_t r1, void *const *columns, uint8_t *status,
-                       void *stream);
+                       const uint64_t *ends, uint64_t r0, uint64_t r1, uint64_t range_bytes, void *const *columns,
+                       uint8_t *status, void *stream);
 
 /* ---- recursive validation ----
  * spec_parse_messages: for every record, spec.ParseMessage (msg.go:29-32 ->

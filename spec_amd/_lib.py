@@ -59,7 +59,7 @@ def _declare(L):
     L.spec_decode_flat.argtypes = [C.POINTER(SpecSchema), vp, C.c_uint64, vp, C.c_uint64,
                                    C.POINTER(vp), vp, vp]
     L.spec_decode_flat_range.argtypes = [C.POINTER(SpecSchema), vp, C.c_uint64, vp, C.c_uint64, C.c_uint64,
-                                         C.POINTER(vp), vp, vp]
+                                         C.c_uint64, C.POINTER(vp), vp, vp]
     L.spec_decode_frames.argtypes = L.spec_decode_flat_range.argtypes
     L.spec_frames_index.argtypes = [vp, C.c_uint64, vp, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.spec_parse_messages.argtypes = [vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, vp, vp, vp]

@@ -156,8 +156,8 @@ int spec_copy_d2d(void *dst, const void *src, size_t bytes, void *stream) {
 }
 
 static int decode_flat_impl(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
-                            const uint64_t *ends, uint64_t r0, uint64_t r1, uint32_t head, void *const *columns,
-                            uint8_t *status, void *stream) {
+                            const uint64_t *ends, uint64_t r0, uint64_t r1, uint64_t range_bytes, uint32_t head,
+                            void *const *columns, uint8_t *status, void *stream) {
     int rc = check_schema(schema);
     if (rc) return rc;
     if (r1 < r0) return SPEC_E_INVALID_ARGUMENT;
@@ -175,9 +175,9 @@ static int decode_flat_impl(const spec_schema *schema, const uint8_t *stream_byt
     a.r0 = r0;
     a.head = head;
     fill_field_set(a.f, schema, columns, status);
-    // slab class from the whole batch's mean record size (ends[r1-1] bytes over r1 records is
-    // not known on the host; stream_len / r1 is the same figure for a full batch)
-    double avg = (double)stream_len / (double)r1;
+    // LDS slab from the mean record size of the range (the caller knows the range's bytes;
+    // for a whole batch it is stream_len / n)
+    double avg = range_bytes ? (double)range_bytes / (double)(r1 - r0) : (double)stream_len / (double)r1;
     int j = spec::jit_launch_decode_flat(schema, a, avg, (hipStream_t)stream);
     if (j < 0) return hip_rc(hipGetLastError());
     if (j == 0 && spec::launch_decode_flat(a, avg, (hipStream_t)stream)) return hip_rc(hipGetLastError());
@@ -185,21 +185,21 @@ static int decode_flat_impl(const spec_schema *schema, const uint8_t *stream_byt
 }
 
 int spec_decode_flat_range(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
-                           const uint64_t *ends, uint64_t r0, uint64_t r1, void *const *columns, uint8_t *status,
-                           void *stream) {
-    return decode_flat_impl(schema, stream_bytes, stream_len, ends, r0, r1, 0, columns, status, stream);
+                           const uint64_t *ends, uint64_t r0, uint64_t r1, uint64_t range_bytes, void *const *columns,
+                           uint8_t *status, void *stream) {
+    return decode_flat_impl(schema, stream_bytes, stream_len, ends, r0, r1, range_bytes, 0, columns, status, stream);
 }
 
 int spec_decode_flat(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
                      const uint64_t *ends, uint64_t n, void *const *columns, uint8_t *status,
                      void *stream) {
-    return decode_flat_impl(schema, stream_bytes, stream_len, ends, 0, n, 0, columns, status, stream);
+    return decode_flat_impl(schema, stream_bytes, stream_len, ends, 0, n, 0, 0, columns, status, stream);
 }
 
 int spec_decode_frames(const spec_schema *schema, const uint8_t *frames, uint64_t frames_len,
-                       const uint64_t *ends, uint64_t r0, uint64_t r1, void *const *columns, uint8_t *status,
-                       void *stream) {
-    return decode_flat_impl(schema, frames, frames_len, ends, r0, r1, 4, columns, status, stream);
+                       const uint64_t *ends, uint64_t r0, uint64_t r1, uint64_t range_bytes, void *const *columns,
+                       uint8_t *status, void *stream) {
+    return decode_flat_impl(schema, frames, frames_len, ends, r0, r1, range_bytes, 4, columns, status, stream);
 }
 
 // mpx framing, mpx/conn_reader.go:179-194 (read) / mpx/conn_writer.go:84-97 (write):

@@ -57,7 +57,7 @@ def decode_frames(schema: Schema, frames: torch.Tensor, ends: torch.Tensor, r0: 
     if status is None:
         status = torch.empty(n, dtype=torch.uint8, device=frames.device)
     ptrs = (C.c_void_p * max(1, len(cols)))(*[c.data_ptr() for c in cols])
-    rc = _lib.lib().spec_decode_frames(C.byref(schema.c), _ptr(frames), frames.numel(), _ptr(ends), r0, r1, ptrs,
-                                       _ptr(status), _stream_handle(cuda_stream))
+    rc = _lib.lib().spec_decode_frames(C.byref(schema.c), _ptr(frames), frames.numel(), _ptr(ends), r0, r1, 0,
+                                       ptrs, _ptr(status), _stream_handle(cuda_stream))
     _lib.check(rc, "spec_decode_frames")
     return Columns(schema, cols, status)

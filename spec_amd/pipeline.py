@@ -54,7 +54,7 @@ class HostDecoder:
                 ev_in.record(self.s_in)
             self.s_dec.wait_event(ev_in)
             rc = L.spec_decode_flat_range(C.byref(self.schema.c), _ptr(self.d_stream), stream_len,
-                                          _ptr(self.d_ends), r0, r1, self._colptrs, _ptr(self.d_status),
+                                          _ptr(self.d_ends), r0, r1, b1 - b0, self._colptrs, _ptr(self.d_status),
                                           C.c_void_p(self.s_dec.cuda_stream))
             _lib.check(rc, "spec_decode_flat_range")
             ev_dec.record(self.s_dec)

@@ -355,8 +355,10 @@ def test_decode_range_and_host_pipeline(dev):
     ptrs = (C.c_void_p * 16)(*[c.data_ptr() for c in out])
     L = spec_amd.lib()
     for r0, r1 in [(0, 1000), (1000, 1001), (1001, 33333), (33333, n)]:
+        b0 = int(ends[r0 - 1]) if r0 else 0
         rc = L.spec_decode_flat_range(C.byref(FLAT16.c), C.c_void_p(d_stream.data_ptr()), stream.size,
-                                      C.c_void_p(d_ends.data_ptr()), r0, r1, ptrs, C.c_void_p(st.data_ptr()), None)
+                                      C.c_void_p(d_ends.data_ptr()), r0, r1, int(ends[r1 - 1]) - b0, ptrs,
+                                      C.c_void_p(st.data_ptr()), None)
         assert rc == 0
     torch.cuda.synchronize()
     assert np.array_equal(st.cpu().numpy(), wst)
