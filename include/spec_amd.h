@@ -186,6 +186,11 @@ int spec_decode_flat_prepare(const spec_schema *schema, uint64_t stream_len, uin
 /* spec_decode_flat_jit_compile: diagnostic — run only the hiprtc compile of that kernel
  * (no device needed); returns the code-object size, 0 if the schema has no fast path. */
 long long spec_decode_flat_jit_compile(const spec_schema *schema, uint64_t stream_len, uint64_t n);
+/* spec_encode_flat_jit_compile: diagnostic — the hiprtc compile of the schema-specialised
+ * encode kernels spec_encode_flat_size/spec_encode_flat use (analogue of the generated
+ * Write(), internal/lang/generator/message.go:319-439); code-object size, 0 if the schema
+ * has none (list fields, more than 32 fields). */
+long long spec_encode_flat_jit_compile(const spec_schema *schema);
 /* spec_set_jit: 0 forces the generic kernel (also: environment SPEC_AMD_JIT=0). */
 void spec_set_jit(int enabled);
 

@@ -68,6 +68,8 @@ def _declare(L):
     L.spec_set_jit.restype = None
     L.spec_decode_flat_jit_compile.argtypes = [C.POINTER(SpecSchema), C.c_uint64, C.c_uint64]
     L.spec_decode_flat_jit_compile.restype = C.c_longlong
+    L.spec_encode_flat_jit_compile.argtypes = [C.POINTER(SpecSchema)]
+    L.spec_encode_flat_jit_compile.restype = C.c_longlong
     L.spec_decode_nested_workspace_size.restype = C.c_size_t
     L.spec_decode_nested_workspace_size.argtypes = [C.c_uint64]
     L.spec_decode_nested_index.argtypes = [C.POINTER(SpecNestedSchema), vp, C.c_uint64, vp, C.c_uint64, vp,

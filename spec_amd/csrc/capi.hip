@@ -259,6 +259,12 @@ long long spec_decode_flat_jit_compile(const spec_schema *schema, uint64_t strea
     return spec::jit_compile_only(schema, (double)stream_len / (double)n);
 }
 
+long long spec_encode_flat_jit_compile(const spec_schema *schema) {
+    int rc = check_schema(schema);
+    if (rc) return rc;
+    return spec::jit_compile_only_encode(schema);
+}
+
 size_t spec_decode_nested_workspace_size(uint64_t n) { return (size_t)(((n + 63) / 64 + 1) * sizeof(uint64_t)); }
 
 static int nested_args(spec::NestedArgs &a, const spec_nested_schema *schema, const uint8_t *stream_bytes,
@@ -387,7 +393,7 @@ int spec_encode_flat_size(const spec_schema *schema, const void *const *columns,
     fill_encode_args(a, schema, columns, n);
     a.block_sums = (uint64_t *)workspace;
     a.total = total;
-    if (spec::launch_encode_size(a, (hipStream_t)stream)) return hip_rc(hipGetLastError());
+    if (spec::launch_encode_size(schema, a, (hipStream_t)stream)) return hip_rc(hipGetLastError());
     return SPEC_OK;
 }
 
@@ -415,8 +421,8 @@ int spec_encode_flat(const spec_schema *schema, const void *const *columns,
     a.ends = ends;
     a.block_sums = (uint64_t *)workspace;
     a.total = total;
-    if (spec::launch_encode_size(a, (hipStream_t)stream)) return hip_rc(hipGetLastError());
-    if (spec::launch_encode_write(a, (hipStream_t)stream)) return hip_rc(hipGetLastError());
+    if (spec::launch_encode_size(schema, a, (hipStream_t)stream)) return hip_rc(hipGetLastError());
+    if (spec::launch_encode_write(schema, a, (hipStream_t)stream)) return hip_rc(hipGetLastError());
     return SPEC_OK;
 }
 

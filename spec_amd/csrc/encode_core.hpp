@@ -26,6 +26,24 @@ struct EncFields {
     uint32_t table_big_forced; // 1 if any tag > 255 (IsBigMessage holds for every record)
 };
 
+// Passed by value as the kernel argument (lives in the kernarg segment => scalar loads,
+// the per-field loop branches are wave-uniform).
+struct EncodeArgs {
+    uint64_t n;
+    EncFields f;
+    uint32_t check_heaps;  // 1 when heaps/heap_lens are known (full encode, not size-only)
+    uint8_t *out;
+    uint64_t out_cap;
+    uint64_t *ends;
+    uint64_t *block_sums;  // workspace: per-block encoded bytes, then exclusive offsets
+    uint64_t nblocks;
+    uint64_t *total;
+};
+
+constexpr int ENC_BLOCK = 256;            // records per encode block (4 waves, one record per lane)
+constexpr int ENC_SLAB = 20 * 1024 - 128; // per-wave output staging (LDS)
+constexpr int ENC_LDS_HEAD = 128;         // write kernel LDS header: wave sums + inverse table order
+
 constexpr uint64_t MAX_SIZE = 2147483647ull; // format.MaxSize, type.go:14
 
 __device__ __forceinline__ uint32_t vlen64(uint64_t v) {
@@ -385,5 +403,336 @@ __device__ __forceinline__ Pos emit_message(const EncFields &a, const Sink &k, P
     tr.finish();
     return tr.pos;
 }
+
+// ---- kernel bodies shared by the precompiled and the schema-specialised encoders -------
+//
+// A record policy P supplies
+//   P::Rec                         the record's column values, loaded by
+//   P::load(a, r)                  (all loads of a lane issued together)
+//   P::size(a, rec, r, check, err) RecSize of the record
+//   P::emit(a, sink, pos, r, rec, rs, inv_order)   the record's bytes
+// RuntimeEnc reads the schema from the kernel arguments (one switch per field);
+// SpecEnc<Spec> has it as compile-time constants (jit.cpp).
+
+struct RuntimeEnc {
+    struct Rec {};
+    static __device__ __forceinline__ Rec load(const EncodeArgs &, uint64_t) { return Rec{}; }
+    static __device__ __forceinline__ RecSize size(const EncodeArgs &a, const Rec &, uint64_t r, bool check,
+                                                   bool &err) {
+        return record_size(a.f, r, check, err);
+    }
+    template <class Sink, class Pos>
+    static __device__ __forceinline__ void emit(const EncodeArgs &a, const Sink &k, Pos p, uint64_t r, const Rec &,
+                                                const RecSize &rs, const uint8_t *inv_order) {
+        emit_message(a.f, k, p, r, rs, inv_order);
+    }
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t heap_rsrc(const EncFields &f, int i) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)f.heaps[i], (short)0,
+                                             (int)(uint32_t)(f.heap_lens[i] > 0xffffffffull ? 0xffffffffull
+                                                                                             : f.heap_lens[i]),
+                                             0x00020000);
+}
+
+// Spec: N (1..), kind[N], tag[N] in write order, order[N] (table order, as EncFields.order),
+// big_forced (some tag > 255).  Every per-field step is instantiated per field index
+// (template recursion), so the record lives in registers.
+template <class Spec>
+struct SpecEnc {
+    static constexpr int N = Spec::N;
+    template <int F>
+    static constexpr bool heap_kind() { return Spec::kind[F] == K_STRING || Spec::kind[F] == K_BYTES; }
+    struct Rec {
+        uint64_t v[N][4]; // raw column bits (string/bytes: off | len << 32)
+        uint32_t h[N][20]; // string/bytes: first 80 heap bytes from off & ~3
+        uint32_t end[N];  // emit: end offset of each field
+    };
+
+    template <int F>
+    static __device__ __forceinline__ void load_col(const EncodeArgs &a, uint64_t r, Rec &x) {
+        if constexpr (F < N) {
+            const void *col = a.f.cols[F];
+            constexpr uint32_t k = Spec::kind[F];
+            if constexpr (k == K_BOOL || k == K_BYTE) {
+                x.v[F][0] = ((const uint8_t *)col)[r];
+            } else if constexpr (k == K_INT16 || k == K_UINT16) {
+                x.v[F][0] = ((const uint16_t *)col)[r];
+            } else if constexpr (k == K_INT32 || k == K_UINT32 || k == K_FLOAT32) {
+                x.v[F][0] = ((const uint32_t *)col)[r];
+            } else if constexpr (k == K_BIN128) {
+                const ulonglong2 q = ((const ulonglong2 *)col)[r];
+                x.v[F][0] = q.x;
+                x.v[F][1] = q.y;
+            } else if constexpr (k == K_BIN256) {
+                const ulonglong2 *c = (const ulonglong2 *)col + 2 * r;
+                const ulonglong2 q0 = c[0], q1 = c[1];
+                x.v[F][0] = q0.x;
+                x.v[F][1] = q0.y;
+                x.v[F][2] = q1.x;
+                x.v[F][3] = q1.y;
+            } else { // 64-bit kinds, string/bytes spans
+                x.v[F][0] = ((const uint64_t *)col)[r];
+            }
+            load_col<F + 1>(a, r, x);
+        }
+    }
+
+    template <int F>
+    static __device__ __forceinline__ void load_heap(const EncodeArgs &a, Rec &x) {
+        if constexpr (F < N) {
+            if constexpr (heap_kind<F>()) {
+                const __amdgpu_buffer_rsrc_t hr = heap_rsrc(a.f, F);
+                const uint32_t off = (uint32_t)x.v[F][0] & ~3u;
+#pragma unroll
+                for (int q = 0; q < 5; q++) {
+                    const uint4 w = heap_ld128(hr, off + 16 * q, a.f.heap_lens[F]);
+                    x.h[F][4 * q] = w.x;
+                    x.h[F][4 * q + 1] = w.y;
+                    x.h[F][4 * q + 2] = w.z;
+                    x.h[F][4 * q + 3] = w.w;
+                }
+            }
+            load_heap<F + 1>(a, x);
+        }
+    }
+
+    // every column load of the record, then the heap loads they address, all in flight at once
+    static __device__ __forceinline__ Rec load(const EncodeArgs &a, uint64_t r) {
+        Rec x;
+        load_col<0>(a, r, x);
+        load_heap<0>(a, x);
+        return x;
+    }
+
+    template <int F>
+    static __device__ __forceinline__ uint64_t data_size(const EncodeArgs &a, const Rec &x, bool check, bool &err) {
+        if constexpr (F >= N) {
+            return 0;
+        } else {
+            const uint64_t v = x.v[F][0];
+            constexpr uint32_t k = Spec::kind[F];
+            uint64_t s;
+            if constexpr (k == K_BOOL) s = 1;
+            else if constexpr (k == K_BYTE) s = 2;
+            else if constexpr (k == K_INT16) s = vlen32(zigzag32((int16_t)v)) + 1;
+            else if constexpr (k == K_INT32) s = vlen32(zigzag32((int32_t)v)) + 1;
+            else if constexpr (k == K_INT64) s = vlen64(zigzag64((int64_t)v)) + 1;
+            else if constexpr (k == K_UINT16 || k == K_UINT32 || k == K_UINT64) s = vlen64(v) + 1;
+            else if constexpr (k == K_FLOAT32) s = 5;
+            else if constexpr (k == K_FLOAT64 || k == K_BIN64) s = 9;
+            else if constexpr (k == K_BIN128) s = 17;
+            else if constexpr (k == K_BIN256) s = 33;
+            else {
+                const uint32_t off = (uint32_t)v, len = (uint32_t)(v >> 32);
+                err |= ((uint64_t)len > MAX_SIZE) | (check & ((uint64_t)off + len > a.f.heap_lens[F]));
+                s = (uint64_t)len + vlen32(len) + 1 + (k == K_STRING ? 1 : 0);
+            }
+            return s + data_size<F + 1>(a, x, check, err);
+        }
+    }
+
+    static __device__ __forceinline__ RecSize size(const EncodeArgs &a, const Rec &x, uint64_t, bool check,
+                                                   bool &err) {
+        const uint64_t data = data_size<0>(a, x, check, err);
+        const bool big = Spec::big_forced | (data > 65535); // IsBigMessage, internal/format/msg.go:43-61
+        const uint64_t tsize = (uint64_t)N * (big ? 6 : 3);
+        err |= data > MAX_SIZE;
+        RecSize s;
+        s.data = data;
+        s.big = big;
+        s.total = data + tsize + vlen32((uint32_t)data) + vlen32((uint32_t)tsize) + 1;
+        return s;
+    }
+
+    template <int F, class E>
+    static __device__ __forceinline__ void emit_values(const EncodeArgs &a, E &em, Rec &x, decltype(em.pos) start) {
+        if constexpr (F < N) {
+            const uint64_t v = x.v[F][0];
+            constexpr uint32_t k = Spec::kind[F];
+            if constexpr (k == K_BOOL) {
+                em.put1(v ? T_TRUE : T_FALSE);
+            } else if constexpr (k == K_BYTE) {
+                em.put_n(v | (T_BYTE << 8), 2);
+            } else if constexpr (k == K_INT16) {
+                em.rvarint(zigzag32((int16_t)v));
+                em.put1(T_INT16);
+            } else if constexpr (k == K_INT32) {
+                em.rvarint(zigzag32((int32_t)v));
+                em.put1(T_INT32);
+            } else if constexpr (k == K_INT64) {
+                em.rvarint(zigzag64((int64_t)v));
+                em.put1(T_INT64);
+            } else if constexpr (k == K_UINT16 || k == K_UINT32 || k == K_UINT64) {
+                em.rvarint(v);
+                em.put1(k == K_UINT16 ? T_UINT16 : (k == K_UINT32 ? T_UINT32 : T_UINT64));
+            } else if constexpr (k == K_FLOAT32) {
+                em.put4(bswap32((uint32_t)v));
+                em.put1(T_FLOAT32);
+            } else if constexpr (k == K_FLOAT64) {
+                em.put4(bswap32((uint32_t)(v >> 32)));
+                em.put4(bswap32((uint32_t)v));
+                em.put1(T_FLOAT64);
+            } else if constexpr (k == K_BIN64) {
+                em.put8(v);
+                em.put1(T_BIN64);
+            } else if constexpr (k == K_BIN128) {
+                em.put8(v);
+                em.put8(x.v[F][1]);
+                em.put1(T_BIN128);
+            } else if constexpr (k == K_BIN256) {
+                em.put8(v);
+                em.put8(x.v[F][1]);
+                em.put8(x.v[F][2]);
+                em.put8(x.v[F][3]);
+                em.put1(T_BIN256);
+            } else { // string/bytes: the prefetched 64 bytes, then the rest from the heap
+                const uint32_t off = (uint32_t)v, len = (uint32_t)(v >> 32), sh = off & 3;
+                const uint32_t n = len < 64 ? len : 64;
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    const uint32_t w = __builtin_amdgcn_alignbyte(x.h[F][j + 1], x.h[F][j], sh);
+                    if ((uint32_t)(4 * j + 4) <= n) {
+                        em.put4(w);
+                    } else if ((uint32_t)(4 * j) < n) {
+                        em.put_n(w, n - 4 * j);
+                    }
+                }
+                if (len > 64) emit_heap(em, heap_rsrc(a.f, F), a.f.heap_lens[F], off + 64, len - 64);
+                if constexpr (k == K_STRING) em.put1(0);
+                em.rvarint(len);
+                em.put1(k == K_STRING ? T_STRING : T_BYTES);
+            }
+            x.end[F] = (uint32_t)(em.pos - start);
+            emit_values<F + 1>(a, em, x, start);
+        }
+    }
+
+    // table (internal/encode/msg.go:58-72): small {u8 tag, u16 end}, big {u16 tag, u32 end}
+    template <int J, class E>
+    static __device__ __forceinline__ void emit_table(E &em, const Rec &x, bool big) {
+        if constexpr (J < N) {
+            constexpr int f = Spec::order[J];
+            constexpr uint32_t tag = Spec::tag[f];
+            const uint32_t e = x.end[f];
+            const uint64_t small = (tag & 0xff) | ((uint64_t)(__builtin_bswap16((uint16_t)e)) << 8);
+            const uint64_t bigv = (uint64_t)__builtin_bswap16((uint16_t)tag) | ((uint64_t)bswap32(e) << 16);
+            em.put_n(big ? bigv : small, big ? 6 : 3);
+            emit_table<J + 1>(em, x, big);
+        }
+    }
+
+    // The record as one sequential byte run: values in write order, the table entries in
+    // table order (their ends kept in registers), the trailer.
+    template <class Sink, class Pos>
+    static __device__ __forceinline__ void emit(const EncodeArgs &a, const Sink &k, Pos start, uint64_t,
+                                                const Rec &rec, const RecSize &rs, const uint8_t *) {
+        Rec x = rec;
+        Emit<Sink, Pos> em(k, start);
+        emit_values<0>(a, em, x, start);
+        emit_table<0>(em, x, rs.big);
+        // trailer: rvarint(dataSize) | rvarint(tableSize) | type (internal/encode/msg.go:36-39)
+        em.rvarint((uint32_t)rs.data);
+        em.rvarint((uint32_t)(N * (rs.big ? 6 : 3)));
+        em.put1(rs.big ? T_BIG_MESSAGE : T_MESSAGE);
+        em.finish();
+    }
+};
+
+// Pass 1: per-block encoded bytes (all-ones on an encoder error).
+template <class P>
+__device__ __forceinline__ void encode_size_body(const EncodeArgs &a) {
+    __shared__ uint64_t part[ENC_BLOCK / 64];
+    __shared__ int errs;
+    if (threadIdx.x == 0) errs = 0;
+    __syncthreads();
+    const uint64_t r = (uint64_t)blockIdx.x * ENC_BLOCK + threadIdx.x;
+    const bool valid = r < a.n;
+    const typename P::Rec rec = P::load(a, valid ? r : a.n - 1);
+    bool err = false;
+    const RecSize rs = P::size(a, rec, r, a.check_heaps, err);
+    if (valid & err) errs = 1;
+    uint64_t s = valid ? rs.total : 0;
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int w = 0; w < ENC_BLOCK / 64; w++) t += part[w];
+        a.block_sums[blockIdx.x] = errs ? ~0ull : t;
+    }
+}
+
+// Copy slab [head, lim) -> gbase[head, lim) (gbase 16-B aligned), one 16-B store per lane.
+__device__ __forceinline__ void copy_slab_out(const uint8_t *slab, uint8_t *gbase, uint64_t head, uint64_t lim,
+                                              int lane) {
+    for (uint64_t c = 0; c < lim; c += 1024) {
+        const uint64_t p = c + (uint64_t)lane * 16;
+        if (p >= lim) break;
+        if (p >= head && p + 16 <= lim) {
+            *(uint4 *)(gbase + p) = *(const uint4 *)(slab + p);
+        } else {
+            for (int i = 0; i < 16; i++)
+                if (p + i >= head && p + i < lim) gbase[p + i] = slab[p + i];
+        }
+    }
+}
+
+// Pass 3: block scan of the recomputed sizes -> record offsets; each lane emits its record
+// into the wave's LDS slab, the wave copies the slab to HBM with 16-byte stores; ends[]
+// written coalesced.  A wave whose output span does not fit the slab emits straight to HBM.
+// smem: ENC_LDS_HEAD bytes of header, then ENC_BLOCK / 64 slabs of ENC_SLAB bytes.
+template <class P>
+__device__ __forceinline__ void encode_write_body(const EncodeArgs &a, uint8_t *smem) {
+    uint64_t *wsum = (uint64_t *)smem;
+    uint8_t *inv_order = smem + 8 * (ENC_BLOCK / 64);
+    const uint64_t total = a.block_sums[a.nblocks];
+    if (total > a.out_cap) return; // capacity error or encoder error (total == ~0)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x < a.f.nfields) inv_order[a.f.order[threadIdx.x]] = (uint8_t)threadIdx.x;
+
+    const uint64_t r = (uint64_t)blockIdx.x * ENC_BLOCK + threadIdx.x;
+    const bool valid = r < a.n;
+    const typename P::Rec rec = P::load(a, valid ? r : a.n - 1);
+    bool err = false;
+    RecSize rs = P::size(a, rec, r, false, err);
+    if (!valid) rs.total = 0;
+    uint64_t x = rs.total; // block exclusive scan of sizes
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint64_t pre = a.block_sums[blockIdx.x];
+    for (int w = 0; w < wave; w++) pre += wsum[w];
+    const uint64_t start = pre + x - rs.total;
+    if (valid) a.ends[r] = start + rs.total;
+
+    // wave output span [S, E)
+    const uint64_t wbase = (uint64_t)blockIdx.x * ENC_BLOCK + wave * 64;
+    if (wbase >= a.n) return;
+    const uint64_t S = __builtin_amdgcn_readfirstlane((uint32_t)start) |
+                       ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(start >> 32)) << 32);
+    const int last = (int)((a.n - wbase) < 64 ? a.n - wbase - 1 : 63);
+    const uint64_t Ev = __shfl(start + rs.total, last);
+    const uint64_t E = __builtin_amdgcn_readfirstlane((uint32_t)Ev) |
+                       ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(Ev >> 32)) << 32);
+    const uint64_t head = ((uint64_t)(a.out + S)) & 15; // slab pos of byte S keeps 16-B phase
+    if (head + (E - S) + 16 <= (uint64_t)ENC_SLAB) {
+        uint8_t *slab = smem + ENC_LDS_HEAD + wave * ENC_SLAB;
+        LdsSink k{slab};
+        if (valid) P::emit(a, k, (int)(head + (start - S)), r, rec, rs, inv_order);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        copy_slab_out(slab, a.out + S - head, head, head + (E - S), lane);
+    } else if (valid) {
+        GlobalSink k{a.out};
+        P::emit(a, k, (long long)start, r, rec, rs, inv_order);
+    }
+}
+
+constexpr size_t enc_write_lds_bytes() { return ENC_LDS_HEAD + (size_t)(ENC_BLOCK / 64) * ENC_SLAB; }
 
 } // namespace spec

@@ -21,6 +21,8 @@
 //                            emitter), then the wave copies the slab to HBM with 16-byte
 //                            stores; ends[] written coalesced.  A wave whose output span does
 //                            not fit the slab emits straight to HBM.
+// Passes 1 and 3 are, for schemas jit.cpp accepts, schema-specialised kernels compiled at run
+// time (all column loads of a record issued together, the table emitted from registers).
 #include <hip/hip_runtime.h>
 
 #include "../../include/spec_amd.h"
@@ -29,116 +31,32 @@
 
 namespace spec {
 
-// ---- pass 1: block sums ------------------------------------------------------------------
+// Kernel bodies: encode_core.hpp (RuntimeEnc here; jit.cpp instantiates them per schema).
 
-__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
-__global__ __launch_bounds__(ENC_BLOCK) void encode_size_kernel(EncodeArgs a) {
-    __shared__ uint64_t part[ENC_BLOCK / 64];
-    __shared__ int errs;
-    if (threadIdx.x == 0) errs = 0;
-    __syncthreads();
-    uint64_t r = (uint64_t)blockIdx.x * ENC_BLOCK + threadIdx.x;
-    uint64_t sz = 0;
-    bool err = false;
-    if (r < a.n) sz = record_size(a.f, r, a.check_heaps, err).total;
-    if (err) errs = 1;
-    uint64_t s = wave_sum(sz);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t t = 0;
-        for (int w = 0; w < ENC_BLOCK / 64; w++) t += part[w];
-        a.block_sums[blockIdx.x] = errs ? ~0ull : t;
-    }
-}
-
-// ---- pass 2: exclusive scan of block sums (one workgroup), total ----------------------
+__global__ __launch_bounds__(ENC_BLOCK) void encode_size_kernel(EncodeArgs a) { encode_size_body<RuntimeEnc>(a); }
 
 __global__ __launch_bounds__(1024) void encode_scan_kernel(EncodeArgs a) { scan_block_sums(a.block_sums, a.nblocks, a.total); }
 
-// ---- pass 3: write ------------------------------------------------------------------------
-
-constexpr int ENC_SLAB = 20 * 1024 - 128; // per-wave output staging
-
 __global__ __launch_bounds__(ENC_BLOCK) void encode_write_kernel(EncodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ uint64_t wsum[ENC_BLOCK / 64];
-    __shared__ uint8_t inv_order[SPEC_MAX_FIELDS];
-    const uint64_t total = a.block_sums[a.nblocks];
-    if (total > a.out_cap) return; // capacity error or encoder error (total == ~0)
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (threadIdx.x < a.f.nfields) inv_order[a.f.order[threadIdx.x]] = (uint8_t)threadIdx.x;
-
-    const uint64_t r = (uint64_t)blockIdx.x * ENC_BLOCK + threadIdx.x;
-    const bool valid = r < a.n;
-    bool err = false;
-    RecSize rs = {0, 0, false};
-    if (valid) rs = record_size(a.f, r, a.check_heaps, err);
-    // block exclusive scan of sizes
-    uint64_t x = rs.total;
-    for (int o = 1; o < 64; o <<= 1) {
-        uint64_t y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    uint64_t pre = a.block_sums[blockIdx.x];
-    for (int w = 0; w < wave; w++) pre += wsum[w];
-    const uint64_t start = pre + x - rs.total;
-    if (valid) a.ends[r] = start + rs.total;
-
-    // wave output span [S, E)
-    if ((uint64_t)blockIdx.x * ENC_BLOCK + wave * 64 >= a.n) return;
-    const uint64_t S = __builtin_amdgcn_readfirstlane((uint32_t)start) |
-                       ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(start >> 32)) << 32);
-    const int last = (int)((a.n - ((uint64_t)blockIdx.x * ENC_BLOCK + wave * 64)) < 64
-                               ? a.n - ((uint64_t)blockIdx.x * ENC_BLOCK + wave * 64) - 1
-                               : 63);
-    const uint64_t Ev = __shfl(start + rs.total, last);
-    const uint64_t E = __builtin_amdgcn_readfirstlane((uint32_t)Ev) |
-                       ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(Ev >> 32)) << 32);
-    const uint64_t head = ((uintptr_t)(a.out + S)) & 15; // slab pos of byte S keeps 16-B phase
-    if (head + (E - S) + 16 <= (uint64_t)ENC_SLAB) {
-        uint8_t *slab = smem + wave * ENC_SLAB;
-        LdsSink k{slab};
-        if (valid) emit_message(a.f, k, (int)(head + (start - S)), r, rs, inv_order);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // copy slab [head, head + E - S) -> out[S, E) with 16-B stores
-        uint8_t *gbase = a.out + S - head; // 16-B aligned
-        const uint64_t lim = head + (E - S);
-        for (uint64_t c = 0; c < lim; c += 1024) {
-            uint64_t p = c + (uint64_t)lane * 16;
-            if (p >= lim) break;
-            if (p >= head && p + 16 <= lim) {
-                *(uint4 *)(gbase + p) = *(const uint4 *)(slab + p);
-            } else {
-                for (int i = 0; i < 16; i++)
-                    if (p + i >= head && p + i < lim) gbase[p + i] = slab[p + i];
-            }
-        }
-    } else if (valid) {
-        GlobalSink k{a.out};
-        emit_message(a.f, k, (long long)start, r, rs, inv_order);
-    }
+    encode_write_body<RuntimeEnc>(a, smem);
 }
 
-static size_t enc_lds_bytes() { return (size_t)(ENC_BLOCK / 64) * ENC_SLAB; }
-
-int launch_encode_size(const EncodeArgs &a, hipStream_t stream) {
-    if (a.nblocks) hipLaunchKernelGGL(encode_size_kernel, dim3((unsigned)a.nblocks), dim3(ENC_BLOCK), 0, stream, a);
+int launch_encode_size(const spec_schema *schema, const EncodeArgs &a, hipStream_t stream) {
+    int j = a.nblocks ? jit_launch_encode(schema, a, false, stream) : 1;
+    if (j < 0) return -1;
+    if (j == 0) hipLaunchKernelGGL(encode_size_kernel, dim3((unsigned)a.nblocks), dim3(ENC_BLOCK), 0, stream, a);
     hipLaunchKernelGGL(encode_scan_kernel, dim3(1), dim3(1024), 0, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_encode_write(const EncodeArgs &a, hipStream_t stream) {
-    if (a.nblocks)
-        hipLaunchKernelGGL(encode_write_kernel, dim3((unsigned)a.nblocks), dim3(ENC_BLOCK), enc_lds_bytes(), stream, a);
+int launch_encode_write(const spec_schema *schema, const EncodeArgs &a, hipStream_t stream) {
+    if (!a.nblocks) return 0;
+    int j = jit_launch_encode(schema, a, true, stream);
+    if (j < 0) return -1;
+    if (j == 0)
+        hipLaunchKernelGGL(encode_write_kernel, dim3((unsigned)a.nblocks), dim3(ENC_BLOCK), enc_write_lds_bytes(),
+                           stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

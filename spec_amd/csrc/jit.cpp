@@ -1,4 +1,4 @@
-// jit.cpp — schema-specialised decode kernels, compiled at run time with hiprtc.
+// jit.cpp — schema-specialised decode and encode kernels, compiled at run time with hiprtc.
 //
 // The reference decodes through GENERATED code: `spec generate` emits one Go reader per
 // schema whose getters call Message.<Kind>(tag) with constant tags
@@ -6,11 +6,16 @@
 // a schema is decoded, decode_core.hpp's kernel body is instantiated for that schema (field
 // count, kinds, tags and table order as compile-time constants) and compiled for gfx950
 // with hiprtc; the code object is loaded with hipModuleLoadData and cached per (device,
-// schema, LDS slab class).  The generated kernel keeps the generic path for every record
-// its fast path rejects, so results are identical to the precompiled kernel's.
+// schema).  The generated kernel keeps the generic path for every record its fast path
+// rejects, so results are identical to the precompiled kernel's.
 //
 // Schemas without a fast path (more than FAST_MAX_FIELDS fields, repeated tags, tags >
 // 255) and SPEC_AMD_JIT=0 use the precompiled generic kernel (decode_flat.hip).
+//
+// Encode: the generated Write() (internal/lang/generator/message.go:319-439) likewise —
+// encode_core.hpp's size and write bodies over SpecEnc<schema> (every column load of a
+// record issued at once, the table built from registers); any schema of 1..ENC_MAX_FIELDS
+// non-list fields.
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
@@ -32,7 +37,7 @@ namespace {
 
 struct Entry {
     hipModule_t mod = nullptr;
-    hipFunction_t fn = nullptr;
+    hipFunction_t fn[2] = {nullptr, nullptr};
     bool failed = false;
 };
 
@@ -78,14 +83,25 @@ bool has_fast_path(const spec_schema *s) {
     return true;
 }
 
-std::string key_of(const spec_schema *s, int device) {
+// A schema-specialised encoder exists for 1..ENC_MAX_FIELDS fields without list fields.
+constexpr uint32_t ENC_MAX_FIELDS = 32;
+bool has_encoder(const spec_schema *s) {
+    if (s->nfields == 0 || s->nfields > ENC_MAX_FIELDS) return false;
+    for (uint32_t f = 0; f < s->nfields; f++)
+        if (s->fields[f].kind == SPEC_KIND_LIST) return false;
+    return true;
+}
+
+enum Prog { DECODE = 0, ENCODE = 1 };
+
+std::string key_of(const spec_schema *s, int device, Prog p) {
     std::ostringstream k;
-    k << device << ':' << (spec::persistent_decode() ? 'p' : 'o') << ':';
+    k << (p == ENCODE ? "enc:" : "dec:") << device << ':' << (spec::persistent_decode() ? 'p' : 'o') << ':';
     for (uint32_t f = 0; f < s->nfields; f++) k << s->fields[f].tag << '/' << (int)s->fields[f].kind << ',';
     return k.str();
 }
 
-std::string generate(const spec_schema *s) {
+std::string generate_decode(const spec_schema *s) {
     uint8_t order[SPEC_MAX_FIELDS];
     uint16_t sorted[SPEC_MAX_FIELDS];
     writer_order(s, order, sorted);
@@ -106,13 +122,43 @@ std::string generate(const spec_schema *s) {
     return o.str();
 }
 
+// The generated Write() of internal/lang/generator/message.go:319-439 as constants: fields in
+// write order, the Writer's table order, IsBigMessage forced by a tag > 255.
+std::string generate_encode(const spec_schema *s) {
+    uint8_t order[SPEC_MAX_FIELDS];
+    uint16_t sorted[SPEC_MAX_FIELDS];
+    writer_order(s, order, sorted);
+    bool big = false;
+    std::ostringstream o;
+    o << "#include \"encode_core.hpp\"\n"
+      << "struct GenEnc {\n  static constexpr int N = " << s->nfields << ";\n"
+      << "  static constexpr uint32_t kind[N] = {";
+    for (uint32_t f = 0; f < s->nfields; f++) o << (f ? "," : "") << (int)s->fields[f].kind;
+    o << "};\n  static constexpr uint32_t tag[N] = {";
+    for (uint32_t f = 0; f < s->nfields; f++) {
+        o << (f ? "," : "") << s->fields[f].tag;
+        big |= s->fields[f].tag > 255;
+    }
+    o << "};\n  static constexpr int order[N] = {";
+    for (uint32_t k = 0; k < s->nfields; k++) o << (k ? "," : "") << (int)order[k];
+    o << "};\n  static constexpr bool big_forced = " << (big ? "true" : "false") << ";\n};\n"
+      << "using P = spec::SpecEnc<GenEnc>;\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void spec_encode_size_jit(spec::EncodeArgs a) {\n"
+      << "  spec::encode_size_body<P>(a);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void spec_encode_write_jit(spec::EncodeArgs a) {\n"
+      << "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+      << "  spec::encode_write_body<P>(a, smem);\n}\n";
+    return o.str();
+}
+
 // hiprtc compile only; returns the code object (empty on failure)
-std::vector<char> compile_code(const spec_schema *s) {
-    std::string src = generate(s);
-    const char *hdr_src[2] = {kSpecDeviceHpp, kDecodeCoreHpp};
-    const char *hdr_name[2] = {"spec_device.hpp", "decode_core.hpp"};
+std::vector<char> compile_code(const spec_schema *s, Prog p) {
+    std::string src = p == ENCODE ? generate_encode(s) : generate_decode(s);
+    const char *hdr_src[3] = {kSpecDeviceHpp, kDecodeCoreHpp, kEncodeCoreHpp};
+    const char *hdr_name[3] = {"spec_device.hpp", "decode_core.hpp", "encode_core.hpp"};
     hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), "spec_decode_flat_jit.hip", 2, hdr_src, hdr_name) != HIPRTC_SUCCESS)
+    if (hiprtcCreateProgram(&prog, src.c_str(), p == ENCODE ? "spec_encode_jit.hip" : "spec_decode_flat_jit.hip", 3,
+                            hdr_src, hdr_name) != HIPRTC_SUCCESS)
         return {};
     // SPEC_AMD_EXP=n: diagnostic variants of the kernel body (decode_core.hpp), timing only
     static std::string exp = [] {
@@ -139,39 +185,54 @@ std::vector<char> compile_code(const spec_schema *s) {
     std::vector<char> code(cs);
     hiprtcGetCode(prog, code.data());
     hiprtcDestroyProgram(&prog);
+    // SPEC_AMD_JIT_DUMP=prefix: write the source and code object (ISA inspection)
+    if (const char *d = getenv("SPEC_AMD_JIT_DUMP")) {
+        std::string base = std::string(d) + (p == ENCODE ? "encode" : "decode");
+        if (FILE *f = fopen((base + ".hip").c_str(), "w")) {
+            fwrite(src.data(), 1, src.size(), f);
+            fclose(f);
+        }
+        if (FILE *f = fopen((base + ".co").c_str(), "wb")) {
+            fwrite(code.data(), 1, code.size(), f);
+            fclose(f);
+        }
+    }
     return code;
 }
 
-Entry compile(const spec_schema *s) {
+Entry compile(const spec_schema *s, Prog p) {
     Entry e;
-    std::vector<char> code = compile_code(s);
+    std::vector<char> code = compile_code(s, p);
     if (code.empty()) {
         e.failed = true;
         return e;
     }
-    if (hipModuleLoadData(&e.mod, code.data()) != hipSuccess ||
-        hipModuleGetFunction(&e.fn, e.mod, "spec_decode_flat_jit") != hipSuccess) {
+    const char *names[2][2] = {{"spec_decode_flat_jit", nullptr}, {"spec_encode_size_jit", "spec_encode_write_jit"}};
+    bool ok = hipModuleLoadData(&e.mod, code.data()) == hipSuccess;
+    for (int i = 0; ok && i < 2; i++)
+        if (names[p][i]) ok = hipModuleGetFunction(&e.fn[i], e.mod, names[p][i]) == hipSuccess;
+    if (!ok) {
         (void)hipGetLastError();
         e.failed = true;
-        e.fn = nullptr;
+        e.fn[0] = e.fn[1] = nullptr;
     }
     return e;
 }
 
 // nullptr => use the generic kernel
-hipFunction_t lookup(const spec_schema *s) {
-    if (!enabled() || !has_fast_path(s)) return nullptr;
+const Entry *lookup(const spec_schema *s, Prog p) {
+    if (!enabled() || !(p == ENCODE ? has_encoder(s) : has_fast_path(s))) return nullptr;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::string k = key_of(s, dev);
+    std::string k = key_of(s, dev, p);
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_cache.find(k);
     if (it == g_cache.end()) {
-        Entry e = compile(s);
+        Entry e = compile(s, p);
         if (e.failed && debug()) fprintf(stderr, "spec_amd jit: compile/load failed, generic kernel in use\n");
         it = g_cache.emplace(k, e).first;
     }
-    return it->second.failed ? nullptr : it->second.fn;
+    return it->second.failed ? nullptr : &it->second;
 }
 
 } // namespace
@@ -182,15 +243,21 @@ void jit_set_enabled(int on) { g_enabled = on ? 1 : 0; }
 
 long long jit_compile_only(const spec_schema *schema, double) {
     if (!has_fast_path(schema)) return 0;
-    return (long long)compile_code(schema).size();
+    return (long long)compile_code(schema, DECODE).size();
 }
 
-int jit_prepare_decode_flat(const spec_schema *schema, double) { return lookup(schema) ? 1 : 0; }
+long long jit_compile_only_encode(const spec_schema *schema) {
+    if (!has_encoder(schema)) return 0;
+    return (long long)compile_code(schema, ENCODE).size();
+}
+
+int jit_prepare_decode_flat(const spec_schema *schema, double) { return lookup(schema, DECODE) ? 1 : 0; }
 
 int jit_launch_decode_flat(const spec_schema *schema, const DecodeArgs &a, double avg_record, hipStream_t stream) {
     if (decode_slab_bytes(avg_record) == 0) return 0; // records too large for LDS: generic kernel
-    hipFunction_t fn = lookup(schema);
-    if (!fn) return 0;
+    const Entry *ent = lookup(schema, DECODE);
+    if (!ent) return 0;
+    hipFunction_t fn = ent->fn[0];
     if (a.n <= a.r0) return 1;
     const DecodeLaunch L = decode_launch(a.n - a.r0, avg_record, device_cus(), persistent_decode(), decode_wpb());
     DecodeArgs args = a;
@@ -201,6 +268,18 @@ int jit_launch_decode_flat(const spec_schema *schema, const DecodeArgs &a, doubl
                      HIP_LAUNCH_PARAM_END};
     hipError_t e = hipModuleLaunchKernel(fn, L.blocks, 1, 1, 64 * L.wpb, 1, 1, L.lds, stream, nullptr, extra);
     return e == hipSuccess ? 1 : -1;
+}
+
+int jit_launch_encode(const spec_schema *schema, const EncodeArgs &a, bool write, hipStream_t stream) {
+    const Entry *e = lookup(schema, ENCODE);
+    if (!e) return 0;
+    EncodeArgs args = a;
+    size_t size = sizeof(args);
+    void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
+                     HIP_LAUNCH_PARAM_END};
+    hipError_t rc = hipModuleLaunchKernel(e->fn[write ? 1 : 0], (unsigned)a.nblocks, 1, 1, ENC_BLOCK, 1, 1,
+                                          write ? (unsigned)enc_write_lds_bytes() : 0, stream, nullptr, extra);
+    return rc == hipSuccess ? 1 : -1;
 }
 
 } // namespace spec

@@ -11,20 +11,6 @@
 
 namespace spec {
 
-// Passed by value as the kernel argument (lives in the kernarg segment => scalar loads,
-// the per-field loop branches are wave-uniform).
-struct EncodeArgs {
-    uint64_t n;
-    EncFields f;
-    uint32_t check_heaps;      // 1 when heaps/heap_lens are known (full encode, not size-only)
-    uint8_t *out;
-    uint64_t out_cap;
-    uint64_t *ends;
-    uint64_t *block_sums;  // workspace: per-block encoded bytes, then exclusive offsets
-    uint64_t nblocks;
-    uint64_t *total;
-};
-
 // encode_nested.hip
 struct NestedEncodeArgs {
     uint64_t n;
@@ -55,9 +41,12 @@ int jit_launch_decode_flat(const spec_schema *schema, const DecodeArgs &a, doubl
 int jit_prepare_decode_flat(const spec_schema *schema, double avg_record);
 void jit_set_enabled(int on);
 long long jit_compile_only(const spec_schema *schema, double avg_record);
-int launch_encode_size(const EncodeArgs &a, hipStream_t stream);
-int launch_encode_write(const EncodeArgs &a, hipStream_t stream);
+long long jit_compile_only_encode(const spec_schema *schema);
+int launch_encode_size(const spec_schema *schema, const EncodeArgs &a, hipStream_t stream);
+int launch_encode_write(const spec_schema *schema, const EncodeArgs &a, hipStream_t stream);
+// jit.cpp: schema-specialised encode pass 1 (write=false) or 3; 1 launched, 0 use the
+// precompiled kernel, <0 HIP error.
+int jit_launch_encode(const spec_schema *schema, const EncodeArgs &a, bool write, hipStream_t stream);
 
-constexpr int ENC_BLOCK = 256; // records per encode block (4 waves, one record per lane)
 
 } // namespace spec

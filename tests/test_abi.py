@@ -75,3 +75,14 @@ def test_jit_source_compiles_for_gfx950():
     assert L.spec_decode_flat_jit_compile(C.byref(dup.c), 1000, 10) == 0
     big = spec_amd.Schema([(300, spec_amd.Kind.INT32)])
     assert L.spec_decode_flat_jit_compile(C.byref(big.c), 1000, 10) == 0
+
+
+def test_encode_jit_source_compiles_for_gfx950():
+    """The schema-specialised encode kernels (jit.cpp over encode_core.hpp) compile with hiprtc."""
+    L = spec_amd.lib()
+    assert L.spec_encode_flat_jit_compile(C.byref(spec_amd.FLAT16.c)) > 1000
+    # tags > 255 and repeated tags are fine for the encoder (big table / Writer tie order)
+    odd = spec_amd.Schema([(300, spec_amd.Kind.INT32), (5, spec_amd.Kind.STRING), (5, spec_amd.Kind.BOOL)])
+    assert L.spec_encode_flat_jit_compile(C.byref(odd.c)) > 1000
+    many = spec_amd.Schema([(i + 1, spec_amd.Kind.INT64) for i in range(33)])
+    assert L.spec_encode_flat_jit_compile(C.byref(many.c)) == 0

@@ -55,7 +55,7 @@ def test_flat16_decode_parity(dev, kernel, n):
 
 
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 4096 + 17])
-def test_flat16_encode_bitexact(dev, n):
+def test_flat16_encode_bitexact(dev, kernel, n):
     cols, heaps = workload.flat16(n, seed=n + 1)
     check_encode(dev, FLAT16, cols, heaps, n, f"flat16 n={n}")
 
@@ -273,7 +273,7 @@ def _cols_for(schema, n, seed, str_len=(30, 62)):
 
 @pytest.mark.parametrize("case", ["all_kinds", "unsorted_tags", "dup_tags", "big_tags", "long_strings",
                                   "empty_strings", "single", "no_fields"])
-def test_encode_schemas(dev, case):
+def test_encode_schemas(dev, kernel, case):
     n = 777
     if case == "all_kinds":
         schema = Schema([(t + 1, k) for t, k in enumerate(ALL_KINDS)])
@@ -305,7 +305,7 @@ def test_encode_schemas(dev, case):
     check_decode(dev, schema, stream, ends, case + "/decode")
 
 
-def test_encode_capacity_and_errors(dev):
+def test_encode_capacity_and_errors(dev, kernel):
     import torch
 
     schema = Schema([(1, Kind.STRING)])
