@@ -111,15 +111,16 @@ def time_decode(dec, steps, warmup, dist):
     return time.perf_counter() - t0
 
 
-def kernel_time_events(fn, reps):
+def kernel_time_events(fn, reps, lead=None):
     """Average per-launch duration from HIP events on the launch stream: one event pair around
     `reps` back-to-back launches (an event between every launch adds ~10 us of marker/flush to
     each interval, which the kernel trace does not see), plus the median of per-launch pairs.
-    The stream is first parked behind a spin kernel so every launch is queued before the GPU
-    reaches them: the interval measures the GPU, not host submission."""
+    `lead` untimed launches go first: the GPU is busy (and at its working clock) on them while
+    the host enqueues the timed ones, so the interval measures the GPU, not host submission.
+    (A spin kernel in front instead lets the chip drop its clock during the spin.)"""
     s = torch.cuda.current_stream()
-    if hasattr(torch.cuda, "_sleep"):
-        torch.cuda._sleep(int(2e8))  # ~0.1 s of GPU spin while the host enqueues
+    for _ in range(reps if lead is None else lead):
+        fn()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record(s)
     for _ in range(reps):
