@@ -152,12 +152,24 @@ __device__ __forceinline__ Win load_win(const Src &s, typename Src::pos_t e) {
     return w;
 }
 
-template <uint32_t KIND, class Pos>
+// The type a Writer emits for a column kind, for the kinds whose getter also accepts other
+// types (ints of other widths, float32 <-> float64); 0 for kinds that accept one type only.
+__host__ __device__ constexpr uint32_t cross_kind_type(uint32_t k) {
+    return k == K_INT16 ? T_INT16 : k == K_INT32 ? T_INT32 : k == K_INT64 ? T_INT64
+         : k == K_UINT16 ? T_UINT16 : k == K_UINT32 ? T_UINT32 : k == K_UINT64 ? T_UINT64
+         : k == K_FLOAT32 ? T_FLOAT32 : k == K_FLOAT64 ? T_FLOAT64 : 0u;
+}
+
+// NAT = true: the caller has checked that the value's type byte is cross_kind_type(KIND) (or
+// the field is empty), so the cross-width branches fold away; results are those of NAT = false
+// for such values.
+template <uint32_t KIND, bool NAT = false, class Pos>
 __device__ __forceinline__ Val decode_tail_k(const Win &w, Pos lo, Pos e, long long to_stream) {
     const Tail &t = w.t;
     Val out = {0, 0, 0, 0};
     const long long flen = (long long)(e - lo);
-    const uint32_t type = (uint32_t)t.q0 & 0xff;
+    constexpr uint32_t NT = cross_kind_type(KIND);
+    const uint32_t type = (NAT && NT) ? NT : (uint32_t)t.q0 & 0xff;
     const uint64_t R = tail_r(t);
     const uint32_t R2 = tail_r2(t);
     const long long avail = flen - 1; // bytes before the type byte
@@ -477,13 +489,28 @@ struct FieldLoad {
     }
 };
 
+// true iff every int/float field F is empty or has type cross_kind_type(kind[F])
+template <class Spec, int F>
+struct FieldNat {
+    static __device__ __forceinline__ bool ok(const FastRec<Spec> &fr) {
+        if constexpr (F >= Spec::N) {
+            return true;
+        } else {
+            constexpr uint32_t NT = cross_kind_type(Spec::kind[F]);
+            bool good = true;
+            if constexpr (NT != 0) good = (fr.e[F] <= fr.lo[F]) | (((uint32_t)fr.w[F].t.q0 & 0xff) == NT);
+            return good & FieldNat<Spec, F + 1>::ok(fr);
+        }
+    }
+};
+
 template <class Spec, int F>
 struct FieldStore {
     static __device__ __forceinline__ void run(const FastRec<Spec> &fr, long long to_stream, const DecodeArgs &a,
                                                uint64_t r, uint64_t &acc) {
         if constexpr (F < Spec::N) {
             constexpr uint32_t K = Spec::kind[F];
-            const Val v = decode_tail_k<K>(fr.w[F], fr.lo[F], fr.e[F], to_stream);
+            const Val v = decode_tail_k<K, true>(fr.w[F], fr.lo[F], fr.e[F], to_stream);
 #if defined(SPEC_EXP) && SPEC_EXP == 3 // diagnostic: decode, no column stores
             acc ^= v.v0 ^ v.v1 ^ v.v2 ^ v.v3;
 #else
@@ -504,31 +531,23 @@ __device__ __forceinline__ bool fast_prepare(const LdsSrc &s, int rs, int re, Fa
     Trailer tr = parse_trailer(s, rs, re);
     if ((tr.st != ST_OK) | tr.big | (tr.tsize != 3u * N)) return false;
     const int ts = (int)tr.tstart;
-    // the table's 3N bytes, re-aligned into dwords: w[i] = bytes [ts+4i, ts+4i+4)
-    constexpr int NW = (3 * N + 3) / 4;
-    constexpr int NQ = (3 * N + 7) / 8 + 1; // aligned qwords covering [ts & ~7, ts + 3N)
+    // the table's 3N bytes, re-aligned into qwords: c[j] = bytes [ts+8j, ts+8j+8), each a
+    // 64-bit funnel shift of two aligned qwords.  (No select between array elements here: in
+    // the not-yet-unrolled loop LLVM folds `hi ? d[i+1] : d[i]` into a load at a variable
+    // index, which after unrolling is a 2N-deep v_cndmask chain per dword.)
+    constexpr int NC = (3 * N + 7) / 8;  // realigned qwords holding the table
+    constexpr int NQ = NC + 1;           // aligned qwords covering [ts & ~7, ts + 3N)
     const int base = ts & ~7;
-    const uint32_t sh = (uint32_t)(ts & 7);
-    uint32_t d[2 * NQ + 1];
+    const uint32_t sh = 8u * (uint32_t)(ts & 7);
+    uint64_t q[NQ];
 #pragma unroll
-    for (int q = 0; q < NQ; q++) {
-        uint64_t x = s.d64(base + 8 * q);
-        d[2 * q] = (uint32_t)x;
-        d[2 * q + 1] = (uint32_t)(x >> 32);
-    }
-    d[2 * NQ] = 0;
-    const bool hi = sh >= 4;
-    const uint32_t b = sh & 3;
-    uint32_t w[NW];
+    for (int j = 0; j < NQ; j++) q[j] = s.d64(base + 8 * j);
+    uint64_t c[NC];
 #pragma unroll
-    for (int i = 0; i < NW; i++) {
-        uint32_t a0 = hi ? d[i + 1] : d[i];
-        uint32_t a1 = hi ? d[i + 2] : d[i + 1];
-        w[i] = __builtin_amdgcn_alignbyte(a1, a0, b);
-    }
+    for (int j = 0; j < NC; j++) c[j] = (q[j] >> sh) | ((q[j + 1] << 1) << (63 - sh));
     // entry k = bytes 3k (tag), 3k+1..3k+2 (end, big-endian): the table must hold exactly the
     // Writer's tags (strictly increasing), so binary search would land on entry rank[f]
-    auto byte_at = [&](int j) -> uint32_t { return (w[j >> 2] >> (8 * (j & 3))) & 0xff; };
+    auto byte_at = [&](int j) -> uint32_t { return (uint32_t)(c[j >> 3] >> (8 * (j & 7))) & 0xff; };
     bool hit = true;
     uint32_t ends[N];
 #pragma unroll
@@ -538,7 +557,10 @@ __device__ __forceinline__ bool fast_prepare(const LdsSrc &s, int rs, int re, Fa
     }
     if (!hit) return false;
     FieldLoad<Spec, 0>::run(fr, s, (int)tr.dstart, ends, tr.dsize);
-    return true;
+    // every int/float field holds the type the Writer emits for its kind (or is empty): the
+    // decode needs no cross-width branches (a record written under another schema version
+    // takes the generic path)
+    return FieldNat<Spec, 0>::ok(fr);
 }
 
 // Fast path, part 2: decode every field from registers and store the columns.
