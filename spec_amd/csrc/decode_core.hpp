@@ -137,9 +137,25 @@ struct Win {
     uint64_t x0, x1, x2;
 };
 
-template <uint32_t KIND, class Src>
+// Kinds whose value, once its type is the one the Writer emits (cross_kind_type), ends in at
+// most 8 bytes: type byte + <= 5-byte reverse varint (32-bit ints, string/bytes lengths),
+// 4-byte float32, byte, bool.  The fast path reads an 8-byte window for them (2 LDS reads,
+// not 3); bytes below the window read as 0, which a <= 5-byte varint never looks at.
+template <uint32_t KIND>
+__host__ __device__ constexpr bool narrow_kind() {
+    return KIND == K_BOOL || KIND == K_BYTE || KIND == K_INT16 || KIND == K_INT32 || KIND == K_UINT16 ||
+           KIND == K_UINT32 || KIND == K_FLOAT32 || KIND == K_STRING || KIND == K_BYTES;
+}
+
+template <uint32_t KIND, bool NARROW = false, class Src>
 __device__ __forceinline__ Win load_win(const Src &s, typename Src::pos_t e) {
     Win w;
+    if constexpr (NARROW && narrow_kind<KIND>()) {
+        w.t.q0 = __builtin_bswap64(load_le64(s, e - 8)); // BE64([e-8, e))
+        w.t.q1 = 0;
+        w.x0 = w.x1 = w.x2 = 0;
+        return w;
+    }
     w.t = load_tail(s, e);
     w.x0 = w.x1 = w.x2 = 0;
     if constexpr (KIND == K_BIN128) {
@@ -483,7 +499,8 @@ struct FieldLoad {
             const bool has = (end <= dsize) & (end > 0);
             fr.e[F] = has ? ds + (int)end : SLAB_GUARD;
             fr.lo[F] = has ? ds : SLAB_GUARD;
-            fr.w[F] = load_win<K>(s, fr.e[F]);
+            // narrow windows are valid because fast_prepare only accepts natural-type records
+            fr.w[F] = load_win<K, true>(s, fr.e[F]);
             FieldLoad<Spec, F + 1>::run(fr, s, ds, ends, dsize);
         }
     }
