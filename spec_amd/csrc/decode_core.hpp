@@ -147,6 +147,33 @@ __host__ __device__ constexpr bool narrow_kind() {
            KIND == K_UINT32 || KIND == K_FLOAT32 || KIND == K_STRING || KIND == K_BYTES;
 }
 
+// Fixed-width payloads (bin64/128/256, float64): NQ payload qwords [e-1-8NQ, e-1) and the
+// type byte at e-1, from the NQ+1 aligned qwords that cover them (a 16-byte tail window plus
+// separate payload reads would take 3 / 5 / 9 reads for 8 / 16 / 32 bytes; this takes 2 / 3 / 5).
+// Packed as a Win: x0.. = leading payload qwords (little-endian), t = the tail view decode_tail_k
+// reads (type byte + the last 8 payload bytes, big-endian).
+template <int NQ, class Src>
+__device__ __forceinline__ Win load_fixed(const Src &s, typename Src::pos_t e) {
+    using pos_t = typename Src::pos_t;
+    const pos_t p = e - 1 - 8 * NQ;
+    const pos_t base = p & ~(pos_t)7;
+    const uint32_t sh = 8u * (uint32_t)(p - base);
+    uint64_t q[NQ + 1], c[NQ];
+#pragma unroll
+    for (int j = 0; j <= NQ; j++) q[j] = s.d64(base + 8 * j);
+#pragma unroll
+    for (int j = 0; j < NQ; j++) c[j] = (q[j] >> sh) | ((q[j + 1] << 1) << (63 - sh));
+    const uint32_t type = (uint32_t)(q[NQ] >> sh) & 0xff;
+    const uint64_t B = __builtin_bswap64(c[NQ - 1]);
+    Win w;
+    w.t.q0 = (B << 8) | type;
+    w.t.q1 = B >> 56;
+    w.x0 = NQ > 1 ? c[0] : 0;
+    w.x1 = NQ > 2 ? c[1 % NQ] : 0;
+    w.x2 = NQ > 3 ? c[2 % NQ] : 0;
+    return w;
+}
+
 template <uint32_t KIND, bool NARROW = false, class Src>
 __device__ __forceinline__ Win load_win(const Src &s, typename Src::pos_t e) {
     Win w;
@@ -155,6 +182,12 @@ __device__ __forceinline__ Win load_win(const Src &s, typename Src::pos_t e) {
         w.t.q1 = 0;
         w.x0 = w.x1 = w.x2 = 0;
         return w;
+    } else if constexpr (NARROW && (KIND == K_FLOAT64 || KIND == K_BIN64)) {
+        return load_fixed<1>(s, e);
+    } else if constexpr (NARROW && KIND == K_BIN128) {
+        return load_fixed<2>(s, e);
+    } else if constexpr (NARROW && KIND == K_BIN256) {
+        return load_fixed<4>(s, e);
     }
     w.t = load_tail(s, e);
     w.x0 = w.x1 = w.x2 = 0;
@@ -262,9 +295,38 @@ __device__ __forceinline__ Val decode_value_k(const Src &s, typename Src::pos_t 
     return decode_tail_k<KIND>(load_win<KIND>(s, e), lo, e, to_stream);
 }
 
+template <class T>
+__device__ __forceinline__ void col_store(T *p, T v) {
+#if !defined(SPEC_CACHED_STORE)
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 template <uint32_t KIND>
 __device__ __forceinline__ void store_value_k(void *colp, uint64_t r, const Val &v) {
     uint8_t *col = (uint8_t *)colp;
+#if !defined(SPEC_CACHED_STORE)
+    if constexpr (KIND == K_BOOL || KIND == K_BYTE) {
+        col_store(col + r, (uint8_t)v.v0);
+    } else if constexpr (KIND == K_INT16 || KIND == K_UINT16) {
+        col_store((uint16_t *)col + r, (uint16_t)v.v0);
+    } else if constexpr (KIND == K_INT32 || KIND == K_UINT32 || KIND == K_FLOAT32) {
+        col_store((uint32_t *)col + r, (uint32_t)v.v0);
+    } else if constexpr (KIND == K_BIN128) {
+        col_store((uint64_t *)col + 2 * r, v.v0);
+        col_store((uint64_t *)col + 2 * r + 1, v.v1);
+    } else if constexpr (KIND == K_BIN256) {
+        col_store((uint64_t *)col + 4 * r, v.v0);
+        col_store((uint64_t *)col + 4 * r + 1, v.v1);
+        col_store((uint64_t *)col + 4 * r + 2, v.v2);
+        col_store((uint64_t *)col + 4 * r + 3, v.v3);
+    } else {
+        col_store((uint64_t *)col + r, v.v0);
+    }
+    return;
+#endif
     if constexpr (KIND == K_BOOL || KIND == K_BYTE) {
         col[r] = (uint8_t)v.v0;
     } else if constexpr (KIND == K_INT16 || KIND == K_UINT16) {

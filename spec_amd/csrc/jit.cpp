@@ -165,8 +165,23 @@ std::vector<char> compile_code(const spec_schema *s, Prog p) {
         const char *e = getenv("SPEC_AMD_EXP");
         return std::string(e && e[0] ? std::string("-DSPEC_EXP=") + e : std::string("-DSPEC_EXP=0"));
     }();
-    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", exp.c_str()};
-    hiprtcResult rc = hiprtcCompileProgram(prog, 4, opts);
+    // SPEC_AMD_JIT_DEFS="A=1,B": extra -D options (kernel variants for A/B timing)
+    static std::vector<std::string> defs = [] {
+        std::vector<std::string> v;
+        const char *e = getenv("SPEC_AMD_JIT_DEFS");
+        std::string s = e ? e : "";
+        size_t p = 0;
+        while (p < s.size()) {
+            size_t q = s.find(',', p);
+            if (q == std::string::npos) q = s.size();
+            if (q > p) v.push_back("-D" + s.substr(p, q - p));
+            p = q + 1;
+        }
+        return v;
+    }();
+    std::vector<const char *> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", exp.c_str()};
+    for (const std::string &d : defs) opts.push_back(d.c_str());
+    hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
     if (rc != HIPRTC_SUCCESS || debug()) {
         size_t ls = 0;
         hiprtcGetProgramLogSize(prog, &ls);
