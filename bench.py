@@ -205,16 +205,27 @@ def nested_leg(n, seed, dev):
         d.index()
         d.decode()
 
-    dec_ms, _ = kernel_time_events(step, 20)
+    two_ms, _ = kernel_time_events(step, 20)
     torch.cuda.synchronize()
     ok = torch.equal(out, stream) and int(d.status.sum()) == 0 and int(d.total.item()) == m
     ok = ok and torch.equal(d.items[0], items[0]) and torch.equal(d.outer[1], outer[1])
+    # one pass (spec_decode_nested_onepass): item columns sized from the index above
+    d.item_begin.zero_()
+    d.items[0].zero_()
+    dec_ms, _ = kernel_time_events(d.decode_onepass, 20)
+    torch.cuda.synchronize()
+    ok = ok and int(d.status.sum()) == 0 and int(d.total.item()) == m and int(d.item_status[:m].sum()) == 0
+    # label spans: lengths equal the input's (offsets point into the stream, not the heap)
+    ok = ok and torch.equal(d.items[0], items[0]) and torch.equal(d.items[2][:, 4:], items[2][:, 4:])
+    ok = ok and torch.equal(d.item_begin, ib)
     sb = stream.numel()
     dec_alg = sb + 8 * n + n * (16 + 8 + 8 + 1 + 4) + m * (4 + 8 + 8 + 1)
     enc_alg = n * (16 + 8 + 8 + 4) + m * (4 + 8 + 8) + int(w["name_heap"].size + w["label_heap"].size) + sb + 8 * n
     return {"records": n, "items": m, "mean_record_bytes": round(sb / n, 1),
             "decode_mmsg_s": round(n / (dec_ms * 1e-3) / 1e6, 1), "decode_ms": round(dec_ms, 4),
             "decode_gb_s": round(dec_alg / (dec_ms * 1e-3) / 1e9, 1),
+            "decode_note": "spec_decode_nested_onepass (one launch + a workspace memset)",
+            "decode_twopass_ms": round(two_ms, 4),
             "encode_mmsg_s": round(n / (enc_ms * 1e-3) / 1e6, 1), "encode_ms": round(enc_ms, 4),
             "encode_gb_s": round(enc_alg / (enc_ms * 1e-3) / 1e9, 1), "roundtrip_ok": bool(ok)}
 

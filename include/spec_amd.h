@@ -215,6 +215,21 @@ int spec_decode_nested(const spec_nested_schema *schema, const uint8_t *stream_b
                        const uint64_t *ends, uint64_t n, void *const *outer_columns, uint8_t *status,
                        uint32_t *item_begin, void *const *item_columns, uint8_t *item_status, uint64_t item_cap,
                        void *workspace, size_t workspace_size, void *stream);
+/* spec_decode_nested_onepass: the same outputs in ONE pass over the stream (no index call):
+ * each 64-record group publishes its item count and finds its first item by looking back over
+ * the groups before it.  Writes *total_items (device uint64); items at index >= item_cap are not
+ * written — if *total_items > item_cap, call again with item columns of that size (the stream
+ * bytes bound it: every item has a list-table entry of at least 2 bytes, so stream_len / 2
+ * always suffices).
+ * Same workspace size as spec_decode_nested; its contents are overwritten. */
+int spec_decode_nested_onepass(const spec_nested_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
+                               const uint64_t *ends, uint64_t n, void *const *outer_columns, uint8_t *status,
+                               uint32_t *item_begin, void *const *item_columns, uint8_t *item_status,
+                               uint64_t item_cap, void *workspace, size_t workspace_size, uint64_t *total_items,
+                               void *stream);
+/* spec_decode_nested_jit_compile: compile (hiprtc, no GPU needed) the schema-specialised one-pass
+ * kernel; code-object size, 0 if neither schema has a fast path. */
+long long spec_decode_nested_jit_compile(const spec_nested_schema *schema);
 
 /* ---- encode ----
  * spec_encode_flat: for every record i, exactly

@@ -76,6 +76,11 @@ def _declare(L):
                                            C.c_size_t, vp, vp]
     L.spec_decode_nested.argtypes = [C.POINTER(SpecNestedSchema), vp, C.c_uint64, vp, C.c_uint64,
                                      C.POINTER(vp), vp, vp, C.POINTER(vp), vp, C.c_uint64, vp, C.c_size_t, vp]
+    L.spec_decode_nested_onepass.argtypes = [C.POINTER(SpecNestedSchema), vp, C.c_uint64, vp, C.c_uint64,
+                                             C.POINTER(vp), vp, vp, C.POINTER(vp), vp, C.c_uint64, vp, C.c_size_t,
+                                             vp, vp]
+    L.spec_decode_nested_jit_compile.argtypes = [C.POINTER(SpecNestedSchema)]
+    L.spec_decode_nested_jit_compile.restype = C.c_longlong
     L.spec_encode_nested_workspace_size.restype = C.c_size_t
     L.spec_encode_nested_workspace_size.argtypes = [C.c_uint64]
     L.spec_encode_nested.argtypes = [C.POINTER(SpecNestedSchema), C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_uint64),

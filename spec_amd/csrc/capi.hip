@@ -329,6 +329,44 @@ int spec_decode_nested(const spec_nested_schema *schema, const uint8_t *stream_b
     return SPEC_OK;
 }
 
+int spec_decode_nested_onepass(const spec_nested_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
+                               const uint64_t *ends, uint64_t n, void *const *outer_columns, uint8_t *status,
+                               uint32_t *item_begin, void *const *item_columns, uint8_t *item_status,
+                               uint64_t item_cap, void *workspace, size_t workspace_size, uint64_t *total_items,
+                               void *stream) {
+    spec::NestedArgs a;
+    int rc = nested_args(a, schema, stream_bytes, stream_len, ends, n, workspace, workspace_size);
+    if (rc) return rc;
+    if (!total_items) return SPEC_E_INVALID_ARGUMENT;
+    a.total = total_items;
+    if (n) {
+        if (!outer_columns || !item_begin || (item_cap && !item_columns)) return SPEC_E_INVALID_ARGUMENT;
+        for (uint32_t f = 0; f < schema->outer.nfields; f++) {
+            if (schema->outer.fields[f].kind == SPEC_KIND_LIST) continue;
+            if (!outer_columns[f]) return SPEC_E_INVALID_ARGUMENT;
+            a.outer.cols[f] = outer_columns[f];
+        }
+        for (uint32_t f = 0; f < schema->item.nfields && item_cap; f++) {
+            if (!item_columns[f]) return SPEC_E_INVALID_ARGUMENT;
+            a.item.cols[f] = item_columns[f];
+        }
+    }
+    a.outer.status = status;
+    a.item.status = item_cap ? item_status : nullptr;
+    a.item_begin = item_begin;
+    a.item_cap = item_cap;
+    double avg = n ? (double)stream_len / (double)n : 0.0;
+    if (spec::launch_nested_onepass(schema, a, avg, (hipStream_t)stream)) return hip_rc(hipGetLastError());
+    return SPEC_OK;
+}
+
+long long spec_decode_nested_jit_compile(const spec_nested_schema *schema) {
+    uint32_t list_f = 0;
+    int rc = check_nested(schema, &list_f);
+    if (rc) return rc;
+    return spec::jit_compile_only_nested(schema);
+}
+
 size_t spec_encode_nested_workspace_size(uint64_t n) { return spec_encode_flat_workspace_size(n); }
 
 static int heaps_of(spec::EncFields &e, const spec_schema *s, const uint8_t *const *heaps, const uint64_t *lens) {

@@ -559,10 +559,16 @@ struct FieldLoad {
             const uint32_t end = ends[Spec::rank[F]];
             // end > dataSize => nil; an empty field decodes to zero: read a harmless window
             const bool has = (end <= dsize) & (end > 0);
-            fr.e[F] = has ? ds + (int)end : SLAB_GUARD;
-            fr.lo[F] = has ? ds : SLAB_GUARD;
-            // narrow windows are valid because fast_prepare only accepts natural-type records
-            fr.w[F] = load_win<K, true>(s, fr.e[F]);
+            if constexpr (K == K_LIST) {
+                // list<message> of a nested schema: only its extent [lo, e) (empty if absent)
+                fr.lo[F] = ds;
+                fr.e[F] = has ? ds + (int)end : ds;
+            } else {
+                fr.e[F] = has ? ds + (int)end : SLAB_GUARD;
+                fr.lo[F] = has ? ds : SLAB_GUARD;
+                // narrow windows are valid because fast_prepare only accepts natural-type records
+                fr.w[F] = load_win<K, true>(s, fr.e[F]);
+            }
             FieldLoad<Spec, F + 1>::run(fr, s, ds, ends, dsize);
         }
     }
@@ -585,17 +591,19 @@ struct FieldNat {
 
 template <class Spec, int F>
 struct FieldStore {
-    static __device__ __forceinline__ void run(const FastRec<Spec> &fr, long long to_stream, const DecodeArgs &a,
+    static __device__ __forceinline__ void run(const FastRec<Spec> &fr, long long to_stream, const FieldSet &fs,
                                                uint64_t r, uint64_t &acc) {
         if constexpr (F < Spec::N) {
             constexpr uint32_t K = Spec::kind[F];
-            const Val v = decode_tail_k<K, true>(fr.w[F], fr.lo[F], fr.e[F], to_stream);
+            if constexpr (K != K_LIST) {
+                const Val v = decode_tail_k<K, true>(fr.w[F], fr.lo[F], fr.e[F], to_stream);
 #if defined(SPEC_EXP) && SPEC_EXP == 3 // diagnostic: decode, no column stores
-            acc ^= v.v0 ^ v.v1 ^ v.v2 ^ v.v3;
+                acc ^= v.v0 ^ v.v1 ^ v.v2 ^ v.v3;
 #else
-            store_value_k<K>(a.f.cols[F], r, v);
+                store_value_k<K>(fs.cols[F], r, v);
 #endif
-            FieldStore<Spec, F + 1>::run(fr, to_stream, a, r, acc);
+            }
+            FieldStore<Spec, F + 1>::run(fr, to_stream, fs, r, acc);
         }
     }
 };
@@ -644,14 +652,14 @@ __device__ __forceinline__ bool fast_prepare(const LdsSrc &s, int rs, int re, Fa
 
 // Fast path, part 2: decode every field from registers and store the columns.
 template <class Spec>
-__device__ __forceinline__ void fast_finish(const FastRec<Spec> &fr, uint64_t r, const DecodeArgs &a,
+__device__ __forceinline__ void fast_finish(const FastRec<Spec> &fr, uint64_t r, const FieldSet &fs,
                                             long long to_stream) {
     uint64_t acc = 0;
-    FieldStore<Spec, 0>::run(fr, to_stream, a, r, acc);
+    FieldStore<Spec, 0>::run(fr, to_stream, fs, r, acc);
 #if defined(SPEC_EXP) && SPEC_EXP == 3
-    if (a.f.status) a.f.status[r] = (uint8_t)(acc ^ (acc >> 8) ^ (acc >> 16) ^ (acc >> 32));
+    if (fs.status) fs.status[r] = (uint8_t)(acc ^ (acc >> 8) ^ (acc >> 16) ^ (acc >> 32));
 #else
-    if (a.f.status) a.f.status[r] = ST_OK;
+    if (fs.status) fs.status[r] = ST_OK;
 #endif
 }
 
@@ -769,7 +777,7 @@ __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // every LDS read of this group done
                 if (has_next && nxt.in_lds) issue_dma(rsrc, slab, nxt, lane);
                 if (g2 < ngroups) load_group_ends(a, a.r0 + g2 * 64, lane, lo2, hi2);
-                if (fast) fast_finish<Spec>(fr, r, a, to_stream);
+                if (fast) fast_finish<Spec>(fr, r, a.f, to_stream);
             } else {
                 if (valid) decode_record_generic(s, rs, re, r, a.f, to_stream);
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -837,7 +845,7 @@ __device__ __forceinline__ void decode_flat_once(const DecodeArgs &a) {
         if constexpr (Spec::N > 0) {
             FastRec<Spec> fr;
             if (fast_prepare<Spec>(s, rs, re, fr)) {
-                fast_finish<Spec>(fr, r, a, to_stream);
+                fast_finish<Spec>(fr, r, a.f, to_stream);
                 return;
             }
         }

@@ -1,0 +1,353 @@
+// decode_nested_core.hpp — device code of the list<message> decoder (BASELINE config 4),
+// shared by the precompiled kernels (decode_nested.hip, run-time schema) and the
+// schema-specialised one-pass kernel jit.cpp compiles with hiprtc.
+//
+// Per record the reference runs (generated reader, internal/lang/generator/message.go:154-162):
+//   m, err := spec.OpenMessageErr(b)                       internal/types/msg.go:43-55
+//   outer getters as for a flat message                     internal/types/msg.go:219-475
+//   items := spec.NewMessageList(m.msg.List(tag), OpenItemErr)   list_msg.go:20-26
+//     m.List(tag) = OpenList(m.field(tag))                  internal/types/msg.go:441-444 (errors => empty list)
+//     items.Len() = table.Len()                             list_msg.go:67-69, internal/types/list.go:70-72
+//     items.Get(i) = open(List.GetBytes(i))                 list_msg.go:88-92, internal/types/list.go:100-116
+//       GetBytes: start = end(i-1) (0 for i = 0), end = end(i); end > dataSize => nil;
+//       start > end panics in Go (slice bounds) => item status SPEC_STATUS_PANIC here
+//     item getters on the opened item message
+// Output: outer columns [n] + status; item_begin [n+1] (CSR, uint32); item columns [m] +
+// item status, items in record order.
+//
+// A wave decodes a group of 64 consecutive records: stage the span into LDS (as the flat
+// decoder), decode each outer record (one lane per record), wave prefix-sum of the item
+// counts, then the group's items ITEM-PARALLEL: item j of the group goes to lane j % 64 (owner
+// record found by a binary search over the lanes' prefix sums), so item columns are written
+// coalesced and no lane idles on a short list.  Outer records and items take the
+// schema-specialised fast path (decode_core.hpp) when the kernel has one (OSpec / ISpec), the
+// generic path otherwise.
+//
+// Where the group's first item goes:
+//   * two-pass (spec_decode_nested_index + spec_decode_nested): a count kernel and a scan
+//     kernel write every group's item offset first;
+//   * one pass (spec_decode_nested_onepass): groups are taken in order from an atomic ticket
+//     and publish their item count, then their inclusive prefix, in a per-group state word;
+//     a group finds its offset by looking back over its predecessors' words (decoupled
+//     look-back: a window of 64 predecessors per step, one per lane).
+#pragma once
+
+#include "decode_core.hpp"
+
+namespace spec {
+
+// What OpenList(m.field(tag)) gives: count and where the table / data are (source positions).
+struct ListInfo {
+    uint32_t count;
+    long long dstart, tstart; // list data start, table start
+    uint32_t dsize;
+    bool big;
+};
+
+// OpenList over the list value [lo, e) (e <= lo: absent or empty => empty list)
+template <class Src>
+__device__ __forceinline__ ListInfo list_at(const Src &s, typename Src::pos_t lo, typename Src::pos_t e) {
+    ListInfo li = {0, 0, 0, 0, false};
+    if (e <= lo) return li;
+    const Trailer lt = parse_trailer<true>(s, lo, e);
+    if (lt.st != ST_OK) return li; // OpenList: error => List{}
+    li.big = lt.big;
+    li.count = lt.tsize / (lt.big ? 4u : 2u);
+    li.dstart = lt.dstart;
+    li.tstart = lt.tstart;
+    li.dsize = lt.dsize;
+    return li;
+}
+
+template <class Src>
+__device__ __forceinline__ ListInfo list_open(const Src &s, const RecInfo &ri, const NestedArgs &a) {
+    const long long end = rec_field_end(s, ri, a.list_tag, a.list_rank);
+    using pos_t = typename Src::pos_t;
+    const pos_t lo = (pos_t)ri.tr.dstart;
+    return list_at(s, lo, end <= 0 ? lo : lo + (pos_t)end);
+}
+
+template <class Src>
+__device__ __forceinline__ uint32_t be16_at(const Src &s, long long p) {
+    return (s.u8((typename Src::pos_t)p) << 8) | s.u8((typename Src::pos_t)p + 1);
+}
+template <class Src>
+__device__ __forceinline__ uint32_t be32_at(const Src &s, long long p) {
+    typename Src::pos_t q = (typename Src::pos_t)p;
+    return (s.u8(q) << 24) | (s.u8(q + 1) << 16) | (s.u8(q + 2) << 8) | s.u8(q + 3);
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t t = __shfl_up(v, d);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    return v;
+}
+
+// Stage one wave's group (records [base, base+64)) into its slab: returns the group; if
+// gr.in_lds the bytes are in LDS when this returns.
+__device__ __forceinline__ Group nested_stage(const NestedArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint8_t *slab,
+                                              uint64_t base, int lane) {
+    uint64_t lo, hi;
+    DecodeArgs d;
+    d.stream = a.stream;
+    d.stream_len = a.stream_len;
+    d.ends = a.ends;
+    d.n = a.n;
+    d.r0 = 0;
+    d.head = 0;
+    load_group_ends(d, base, lane, lo, hi);
+    Group gr = make_group(d, base, lane, lo, hi, a.slab);
+    if (gr.in_lds) {
+        issue_dma(rsrc, slab, gr, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        fix_stream_tail(d, rsrc, slab, gr, lane);
+    }
+    return gr;
+}
+
+// Item count of record [rs, re) (generic path).
+template <class Src>
+__device__ __forceinline__ uint32_t record_count(const Src &s, long long rs, long long re, const NestedArgs &a) {
+    const RecInfo ri = rec_open(s, (typename Src::pos_t)rs, (typename Src::pos_t)re);
+    return list_open(s, ri, a).count;
+}
+
+// index of the K_LIST field in a compile-time outer schema
+template <class Spec>
+__host__ __device__ constexpr int list_field() {
+    for (int f = 0; f < Spec::N; f++)
+        if (Spec::kind[f] == K_LIST) return f;
+    return -1;
+}
+
+// Outer record r at [rs, re): its columns + status, and its list.
+template <class OSpec, class Src>
+__device__ __forceinline__ ListInfo decode_outer(const Src &s, long long rs, long long re, uint64_t r,
+                                                 long long to_stream, const NestedArgs &a) {
+    using pos_t = typename Src::pos_t;
+    if constexpr (OSpec::N > 0 && __is_same(Src, LdsSrc)) {
+        FastRec<OSpec> fr;
+        if (fast_prepare<OSpec>(s, (int)rs, (int)re, fr)) {
+            constexpr int LF = list_field<OSpec>();
+            const ListInfo li = list_at(s, fr.lo[LF], fr.e[LF]);
+            fast_finish<OSpec>(fr, r, a.outer, to_stream);
+            return li;
+        }
+    }
+    decode_record_generic(s, (pos_t)rs, (pos_t)re, r, a.outer, to_stream);
+    const RecInfo ri = rec_open(s, (pos_t)rs, (pos_t)re);
+    return list_open(s, ri, a);
+}
+
+// Item `out` = List.GetBytes(i) of the list li (internal/types/list.go:100-116 with
+// format.ListTable.Offset), opened and decoded.
+template <class ISpec, class Src>
+__device__ __forceinline__ void decode_item(const Src &s, const ListInfo &li, uint32_t i, uint64_t out,
+                                            long long to_stream, const NestedArgs &a) {
+    using pos_t = typename Src::pos_t;
+    uint32_t start, end;
+    if (li.big) {
+        end = be32_at(s, li.tstart + 4ll * i);
+        start = i ? be32_at(s, li.tstart + 4ll * (i - 1)) : 0;
+    } else {
+        end = be16_at(s, li.tstart + 2ll * i);
+        start = i ? be16_at(s, li.tstart + 2ll * (i - 1)) : 0;
+    }
+    if (end > li.dsize) {
+        // nil item => OpenItemErr(nil): empty message, zero fields, no error
+        decode_record_generic(s, (pos_t)0, (pos_t)0, out, a.item, to_stream);
+        return;
+    }
+    if (start > end) {
+        decode_record_generic(s, (pos_t)0, (pos_t)0, out, a.item, to_stream);
+        if (a.item.status) a.item.status[out] = ST_PANIC;
+        return;
+    }
+    const pos_t ib = (pos_t)(li.dstart + start), ie = (pos_t)(li.dstart + end);
+    if constexpr (ISpec::N > 0 && __is_same(Src, LdsSrc)) {
+        FastRec<ISpec> fr;
+        if (fast_prepare<ISpec>(s, (int)ib, (int)ie, fr)) {
+            fast_finish<ISpec>(fr, out, a.item, to_stream);
+            return;
+        }
+    }
+    decode_record_generic(s, ib, ie, out, a.item, to_stream);
+}
+
+// The group's items, item-parallel: item j of the group (j = excl[owner] + i) on lane j % 64.
+template <class ISpec, class Src>
+__device__ __forceinline__ void decode_group_items(const Src &s, const ListInfo &li, uint32_t excl, uint32_t total,
+                                                   uint64_t item_base, int lane, long long to_stream,
+                                                   const NestedArgs &a) {
+    for (uint32_t j0 = 0; j0 < total; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        // owner: the largest lane whose exclusive prefix is <= j (it has count > 0)
+        int l = 0;
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1) {
+            const uint32_t ex = __shfl(excl, l + step < 64 ? l + step : 63);
+            if (l + step < 64 && ex <= j) l += step;
+        }
+        ListInfo own;
+        const uint32_t i = j - __shfl(excl, l);
+        own.dstart = __shfl(li.dstart, l);
+        own.tstart = __shfl(li.tstart, l);
+        own.dsize = __shfl(li.dsize, l);
+        own.big = __shfl((int)li.big, l) != 0;
+        own.count = 0;
+        if (j >= total) continue;
+        const uint64_t out = item_base + j;
+        if (out >= a.item_cap) continue;
+        decode_item<ISpec>(s, own, i, out, to_stream, a);
+    }
+}
+
+// ---- decoupled look-back (one pass) ------------------------------------------------------
+
+constexpr uint64_t LB_AGG = 1ull << 62;       // word holds the group's own item count
+constexpr uint64_t LB_PRE = 2ull << 62;       // word holds the inclusive prefix (items up to and incl. the group)
+constexpr uint64_t LB_VAL = (1ull << 62) - 1;
+
+__device__ __forceinline__ uint64_t lb_load(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    return v;
+}
+
+// Publish group g's item count `agg`, return the items of groups [0, g).  Every group < g
+// holds a ticket taken before g's, so its wave is resident and will publish: the wait ends.
+__device__ __forceinline__ uint64_t lookback(uint64_t *state, uint64_t g, uint64_t agg, int lane) {
+    if (lane == 0) lb_store(&state[g], (g == 0 ? LB_PRE : LB_AGG) | agg);
+    if (g == 0) return 0;
+    uint64_t excl = 0;
+    long long hi = (long long)g - 1; // window: groups hi, hi-1, ..., hi-63 on lanes 0..63
+    while (true) {
+        const long long j = hi - lane;
+        const uint64_t v = j >= 0 ? lb_load(&state[j]) : LB_PRE; // before group 0: prefix 0
+        const uint64_t pre = __ballot((v >> 62) == 2);
+        const uint64_t none = __ballot((v >> 62) == 0);
+        const int first = pre ? __builtin_ctzll(pre) : 64; // nearest inclusive prefix
+        const uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1); // lanes 0..first
+        if (none & upto) { // a nearer group has not published yet
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        excl += wave_sum64((upto >> lane) & 1 ? (v & LB_VAL) : 0);
+        if (first < 64) break;
+        hi -= 64;
+    }
+    if (lane == 0) lb_store(&state[g], LB_PRE | (excl + agg));
+    return excl;
+}
+
+// Decode a group: outer records (lane = record), then items (item-parallel).  item_base =
+// the group's first item; ONEPASS: item_base is found here by look-back (state = a.group_base).
+template <class OSpec, class ISpec, bool ONEPASS, class Src>
+__device__ __forceinline__ void nested_group_body(const Src &s, long long rs, long long re, bool valid, uint64_t r,
+                                                  uint64_t g, uint64_t item_base, int lane, long long to_stream,
+                                                  const NestedArgs &a) {
+    ListInfo li = {0, 0, 0, 0, false};
+    if (valid) li = decode_outer<OSpec>(s, rs, re, r, to_stream, a);
+    const uint32_t incl = wave_incl_scan(li.count, lane);
+    const uint32_t excl = incl - li.count;
+    const uint32_t total = __shfl(incl, 63);
+    if constexpr (ONEPASS) {
+#if defined(SPEC_EXP) && (SPEC_EXP == 5 || SPEC_EXP == 6) // diagnostic (timing only): no look-back
+        item_base = 0;
+#else
+        item_base = uniform64(lookback(a.group_base, g, total, lane));
+#endif
+        if (g == (a.n - 1) / 64 && lane == 0) *a.total = item_base + total;
+    }
+    if (valid) {
+        a.item_begin[r] = (uint32_t)(item_base + excl);
+        if (r == a.n - 1) a.item_begin[a.n] = (uint32_t)(item_base + incl);
+    }
+    decode_group_items<ISpec>(s, li, excl, total, item_base, lane, to_stream, a);
+}
+
+// Kernel body for one group per wave.  ONEPASS: group = ticket order (a.group_base = state
+// words, ticket at state[ngroups], both zeroed by the launcher); else group = wave index and
+// a.group_base holds the exclusive item offsets from the index kernels.
+template <class OSpec, class ISpec, bool ONEPASS>
+__device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t ngroups = (a.n + 63) / 64;
+    uint64_t g;
+    if constexpr (ONEPASS) {
+#if defined(SPEC_EXP) && SPEC_EXP == 5 // diagnostic (timing only): no ticket
+        g = blockIdx.x;
+#else
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd((unsigned int *)&a.group_base[ngroups], 1u);
+        g = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
+#endif
+    } else {
+        g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    }
+    const uint64_t base = g * 64;
+    if (base >= a.n) return;
+    uint8_t *slab = smem + wave * a.slab;
+    __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
+    const Group gr = nested_stage(a, rsrc, slab, base, lane);
+    const uint64_t r = base + lane;
+    const bool valid = r < a.n;
+    const uint64_t item_base = ONEPASS ? 0 : a.group_base[g];
+    if (gr.in_lds) {
+        LdsSrc s{(lds_u8 *)slab};
+        nested_group_body<OSpec, ISpec, ONEPASS>(s, SLAB_GUARD + (long long)(gr.rec_lo - gr.aligned_lo),
+                                                 SLAB_GUARD + (long long)(gr.rec_hi - gr.aligned_lo), valid, r, g,
+                                                 item_base, lane, (long long)gr.aligned_lo - SLAB_GUARD, a);
+    } else {
+        GlobalSrc s{rsrc, a.stream_len};
+        nested_group_body<OSpec, ISpec, ONEPASS>(s, (long long)gr.rec_lo, (long long)gr.rec_hi, valid, r, g,
+                                                 item_base, lane, 0, a);
+    }
+}
+
+// Count kernel of the two-pass index: per group, the item total.
+__device__ __forceinline__ void nested_count_body(const NestedArgs &a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    const uint64_t base = g * 64;
+    if (base >= a.n) return;
+    uint8_t *slab = smem + wave * a.slab;
+    __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
+    const Group gr = nested_stage(a, rsrc, slab, base, lane);
+    const bool valid = base + lane < a.n;
+    uint32_t cnt = 0;
+    if (valid) {
+        if (gr.in_lds) {
+            LdsSrc s{(lds_u8 *)slab};
+            cnt = record_count(s, SLAB_GUARD + (long long)(gr.rec_lo - gr.aligned_lo),
+                               SLAB_GUARD + (long long)(gr.rec_hi - gr.aligned_lo), a);
+        } else {
+            GlobalSrc s{rsrc, a.stream_len};
+            cnt = record_count(s, (long long)gr.rec_lo, (long long)gr.rec_hi, a);
+        }
+    }
+    const uint32_t sum = wave_sum(cnt);
+    if (lane == 0) a.group_base[g] = sum;
+}
+
+} // namespace spec

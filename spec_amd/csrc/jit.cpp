@@ -92,7 +92,7 @@ bool has_encoder(const spec_schema *s) {
     return true;
 }
 
-enum Prog { DECODE = 0, ENCODE = 1 };
+enum Prog { DECODE = 0, ENCODE = 1, NESTED = 2 };
 
 std::string key_of(const spec_schema *s, int device, Prog p) {
     std::ostringstream k;
@@ -101,24 +101,42 @@ std::string key_of(const spec_schema *s, int device, Prog p) {
     return k.str();
 }
 
-std::string generate_decode(const spec_schema *s) {
+// struct <name> { N, kind[], rank[], stag[] }: the fast-path schema of decode_core.hpp
+void emit_spec(std::ostringstream &o, const char *name, const spec_schema *s) {
     uint8_t order[SPEC_MAX_FIELDS];
     uint16_t sorted[SPEC_MAX_FIELDS];
     writer_order(s, order, sorted);
     uint8_t rank[SPEC_MAX_FIELDS];
     for (uint32_t k = 0; k < s->nfields; k++) rank[order[k]] = (uint8_t)k;
-    std::ostringstream o;
-    o << "#include \"decode_core.hpp\"\n"
-      << "struct GenSpec {\n  static constexpr int N = " << s->nfields << ";\n"
+    o << "struct " << name << " {\n  static constexpr int N = " << s->nfields << ";\n"
       << "  static constexpr uint32_t kind[N] = {";
     for (uint32_t f = 0; f < s->nfields; f++) o << (f ? "," : "") << (int)s->fields[f].kind;
     o << "};\n  static constexpr int rank[N] = {";
     for (uint32_t f = 0; f < s->nfields; f++) o << (f ? "," : "") << (int)rank[f];
     o << "};\n  static constexpr uint32_t stag[N] = {";
     for (uint32_t k = 0; k < s->nfields; k++) o << (k ? "," : "") << sorted[k];
-    o << "};\n};\n"
-      << "extern \"C\" __global__ __launch_bounds__(256) void spec_decode_flat_jit(spec::DecodeArgs a) {\n"
+    o << "};\n};\n";
+}
+
+std::string generate_decode(const spec_schema *s) {
+    std::ostringstream o;
+    o << "#include \"decode_core.hpp\"\n";
+    emit_spec(o, "GenSpec", s);
+    o << "extern \"C\" __global__ __launch_bounds__(256) void spec_decode_flat_jit(spec::DecodeArgs a) {\n"
       << "  spec::decode_flat_entry<" << (spec::persistent_decode() ? "true" : "false") << ", GenSpec>(a);\n}\n";
+    return o.str();
+}
+
+// One-pass nested decode: outer and item fast paths where the schema has one.
+std::string generate_nested(const spec_nested_schema *s) {
+    std::ostringstream o;
+    o << "#include \"decode_nested_core.hpp\"\n";
+    const bool fo = has_fast_path(&s->outer), fi = has_fast_path(&s->item);
+    if (fo) emit_spec(o, "GenOuter", &s->outer);
+    if (fi) emit_spec(o, "GenItem", &s->item);
+    o << "extern \"C\" __global__ __launch_bounds__(64) void spec_decode_nested_jit(spec::NestedArgs a) {\n"
+      << "  spec::nested_decode_body<" << (fo ? "GenOuter" : "spec::RuntimeSpec") << ", "
+      << (fi ? "GenItem" : "spec::RuntimeSpec") << ", true>(a);\n}\n";
     return o.str();
 }
 
@@ -151,15 +169,16 @@ std::string generate_encode(const spec_schema *s) {
     return o.str();
 }
 
+const char *prog_name(Prog p) {
+    return p == ENCODE ? "spec_encode_jit.hip" : p == NESTED ? "spec_decode_nested_jit.hip" : "spec_decode_flat_jit.hip";
+}
+
 // hiprtc compile only; returns the code object (empty on failure)
-std::vector<char> compile_code(const spec_schema *s, Prog p) {
-    std::string src = p == ENCODE ? generate_encode(s) : generate_decode(s);
-    const char *hdr_src[3] = {kSpecDeviceHpp, kDecodeCoreHpp, kEncodeCoreHpp};
-    const char *hdr_name[3] = {"spec_device.hpp", "decode_core.hpp", "encode_core.hpp"};
+std::vector<char> compile_source(const std::string &src, Prog p) {
+    const char *hdr_src[4] = {kSpecDeviceHpp, kDecodeCoreHpp, kEncodeCoreHpp, kDecodeNestedCoreHpp};
+    const char *hdr_name[4] = {"spec_device.hpp", "decode_core.hpp", "encode_core.hpp", "decode_nested_core.hpp"};
     hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), p == ENCODE ? "spec_encode_jit.hip" : "spec_decode_flat_jit.hip", 3,
-                            hdr_src, hdr_name) != HIPRTC_SUCCESS)
-        return {};
+    if (hiprtcCreateProgram(&prog, src.c_str(), prog_name(p), 4, hdr_src, hdr_name) != HIPRTC_SUCCESS) return {};
     // SPEC_AMD_EXP=n: diagnostic variants of the kernel body (decode_core.hpp), timing only
     static std::string exp = [] {
         const char *e = getenv("SPEC_AMD_EXP");
@@ -202,7 +221,7 @@ std::vector<char> compile_code(const spec_schema *s, Prog p) {
     hiprtcDestroyProgram(&prog);
     // SPEC_AMD_JIT_DUMP=prefix: write the source and code object (ISA inspection)
     if (const char *d = getenv("SPEC_AMD_JIT_DUMP")) {
-        std::string base = std::string(d) + (p == ENCODE ? "encode" : "decode");
+        std::string base = std::string(d) + (p == ENCODE ? "encode" : p == NESTED ? "nested" : "decode");
         if (FILE *f = fopen((base + ".hip").c_str(), "w")) {
             fwrite(src.data(), 1, src.size(), f);
             fclose(f);
@@ -215,14 +234,19 @@ std::vector<char> compile_code(const spec_schema *s, Prog p) {
     return code;
 }
 
-Entry compile(const spec_schema *s, Prog p) {
+std::vector<char> compile_code(const spec_schema *s, Prog p) {
+    return compile_source(p == ENCODE ? generate_encode(s) : generate_decode(s), p);
+}
+
+Entry load(const std::vector<char> &code, Prog p) {
     Entry e;
-    std::vector<char> code = compile_code(s, p);
     if (code.empty()) {
         e.failed = true;
         return e;
     }
-    const char *names[2][2] = {{"spec_decode_flat_jit", nullptr}, {"spec_encode_size_jit", "spec_encode_write_jit"}};
+    const char *names[3][2] = {{"spec_decode_flat_jit", nullptr},
+                               {"spec_encode_size_jit", "spec_encode_write_jit"},
+                               {"spec_decode_nested_jit", nullptr}};
     bool ok = hipModuleLoadData(&e.mod, code.data()) == hipSuccess;
     for (int i = 0; ok && i < 2; i++)
         if (names[p][i]) ok = hipModuleGetFunction(&e.fn[i], e.mod, names[p][i]) == hipSuccess;
@@ -234,20 +258,35 @@ Entry compile(const spec_schema *s, Prog p) {
     return e;
 }
 
-// nullptr => use the generic kernel
-const Entry *lookup(const spec_schema *s, Prog p) {
-    if (!enabled() || !(p == ENCODE ? has_encoder(s) : has_fast_path(s))) return nullptr;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::string k = key_of(s, dev, p);
+// cached per key; make() returns the code object. nullptr => use the generic kernel
+template <class Make>
+const Entry *lookup_key(const std::string &k, Prog p, Make make) {
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_cache.find(k);
     if (it == g_cache.end()) {
-        Entry e = compile(s, p);
+        Entry e = load(make(), p);
         if (e.failed && debug()) fprintf(stderr, "spec_amd jit: compile/load failed, generic kernel in use\n");
         it = g_cache.emplace(k, e).first;
     }
     return it->second.failed ? nullptr : &it->second;
+}
+
+const Entry *lookup(const spec_schema *s, Prog p) {
+    if (!enabled() || !(p == ENCODE ? has_encoder(s) : has_fast_path(s))) return nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    return lookup_key(key_of(s, dev, p), p, [&] { return compile_code(s, p); });
+}
+
+// a nested kernel is worth compiling when the outer or the item schema has a fast path
+bool has_nested_fast_path(const spec_nested_schema *s) { return has_fast_path(&s->outer) || has_fast_path(&s->item); }
+
+const Entry *lookup_nested(const spec_nested_schema *s) {
+    if (!enabled() || !has_nested_fast_path(s)) return nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    const std::string k = key_of(&s->outer, dev, NESTED) + "|" + key_of(&s->item, dev, NESTED);
+    return lookup_key(k, NESTED, [&] { return compile_source(generate_nested(s), NESTED); });
 }
 
 } // namespace
@@ -294,6 +333,24 @@ int jit_launch_encode(const spec_schema *schema, const EncodeArgs &a, bool write
                      HIP_LAUNCH_PARAM_END};
     hipError_t rc = hipModuleLaunchKernel(e->fn[write ? 1 : 0], (unsigned)a.nblocks, 1, 1, ENC_BLOCK, 1, 1,
                                           write ? (unsigned)enc_write_lds_bytes() : 0, stream, nullptr, extra);
+    return rc == hipSuccess ? 1 : -1;
+}
+
+long long jit_compile_only_nested(const spec_nested_schema *schema) {
+    if (!has_nested_fast_path(schema)) return 0;
+    return (long long)compile_source(generate_nested(schema), NESTED).size();
+}
+
+int jit_launch_nested_onepass(const spec_nested_schema *schema, const NestedArgs &a, hipStream_t stream) {
+    if (a.slab == 0) return 0; // records too large for LDS: generic kernel
+    const Entry *e = lookup_nested(schema);
+    if (!e) return 0;
+    NestedArgs args = a;
+    size_t size = sizeof(args);
+    void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
+                     HIP_LAUNCH_PARAM_END};
+    const unsigned groups = (unsigned)((a.n + 63) / 64);
+    hipError_t rc = hipModuleLaunchKernel(e->fn[0], groups, 1, 1, 64, 1, 1, a.slab, stream, nullptr, extra);
     return rc == hipSuccess ? 1 : -1;
 }
 

@@ -76,14 +76,37 @@ class NestedDecoder:
                                            self.ws_bytes, _stream_handle(self.cuda_stream))
         _lib.check(rc, "spec_decode_nested")
 
+    def decode_onepass(self) -> torch.Tensor:
+        """spec_decode_nested_onepass into the reserved item columns (no index call); returns the
+        device total.  Items beyond the reserved capacity are not written: if total > capacity,
+        reserve(total) and call again."""
+        outer = (C.c_void_p * max(1, len(self.outer)))(*[c.data_ptr() if c is not None else 0 for c in self.outer])
+        items = (C.c_void_p * max(1, len(self.items)))(*[c.data_ptr() for c in self.items])
+        rc = _lib.lib().spec_decode_nested_onepass(
+            C.byref(self.schema.c), _ptr(self.stream), self.stream.numel(), _ptr(self.ends), self.n, outer,
+            _ptr(self.status), _ptr(self.item_begin), items, _ptr(self.item_status), self.item_cap,
+            _ptr(self.workspace), self.ws_bytes, _ptr(self.total), _stream_handle(self.cuda_stream))
+        _lib.check(rc, "spec_decode_nested_onepass")
+        return self.total
+
     def result(self) -> NestedColumns:
         return NestedColumns(self.schema, self.outer, self.status, self.item_begin, self.items, self.item_status,
                              int(self.total.item()))
 
 
-def decode_nested(schema: NestedSchema, stream: torch.Tensor, ends: torch.Tensor, cuda_stream=None) -> NestedColumns:
-    """Index, size the item columns from the device total, decode."""
+def decode_nested(schema: NestedSchema, stream: torch.Tensor, ends: torch.Tensor, cuda_stream=None,
+                  onepass: bool = False, item_cap: int | None = None) -> NestedColumns:
+    """Two-pass: index, size the item columns from the device total, decode.  onepass: decode
+    into item_cap items (default 4 per record) in one pass; if the batch holds more, grow the
+    item columns to the reported total and decode again."""
     d = NestedDecoder(schema, stream, ends, cuda_stream)
+    if onepass:
+        d.reserve(max(1, item_cap if item_cap is not None else 4 * d.n))
+        total = int(d.decode_onepass().item())
+        if total > d.item_cap:
+            d.reserve(total)
+            d.decode_onepass()
+        return d.result()
     total = int(d.index().item())
     d.reserve(total)
     d.decode()

@@ -17,16 +17,35 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def check_nested(dev, stream, ends, label=""):
-    import torch
+@pytest.fixture(params=["jit", "generic"])
+def kernel(request):
+    """Schema-specialised one-pass kernel (hiprtc) and the precompiled generic kernels."""
+    spec_amd.set_jit(request.param == "jit")
+    yield request.param
+    spec_amd.set_jit(True)
 
+
+def check_nested(dev, stream, ends, label="", modes=("twopass", "onepass", "onepass-small-cap")):
+    """Every decode mode against the oracle: index + decode, one pass with room for every
+    item, one pass that first runs out of item room (and decodes again with the total)."""
     stream = np.ascontiguousarray(stream, dtype=np.uint8)
     ends = np.ascontiguousarray(ends, dtype=np.uint64)
     want = O.decode_nested_batch(stream, ends)
     d_stream = to_dev(stream if stream.size else np.zeros(1, np.uint8), dev)[: stream.size]
-    got = spec_amd.decode_nested(NESTED, d_stream, to_dev(ends.view(np.int64), dev))
+    d_ends = to_dev(ends.view(np.int64), dev)
+    got = None
+    for mode in modes:
+        cap = 1 if mode == "onepass-small-cap" else None
+        got = _check_nested_mode(dev, d_stream, d_ends, want, len(ends), f"{label} [{mode}]",
+                                 onepass=mode != "twopass", item_cap=cap)
+    return got, want
+
+
+def _check_nested_mode(dev, d_stream, d_ends, want, n, label, onepass, item_cap):
+    import torch
+
+    got = spec_amd.decode_nested(NESTED, d_stream, d_ends, onepass=onepass, item_cap=item_cap)
     torch.cuda.synchronize()
-    n = len(ends)
     assert np.array_equal(got.status.cpu().numpy(), want["status"]), label + ": status"
     assert np.array_equal(got.item_begin.cpu().numpy().view(np.uint32), want["item_begin"]), label + ": item_begin"
     m = int(want["item_begin"][-1]) if n else 0
@@ -36,15 +55,15 @@ def check_nested(dev, stream, ends, label=""):
     assert np.array_equal(got.outer[2].cpu().numpy().view(np.uint32), want["name"]), label + ": name"
     if m:
         assert np.array_equal(got.item_status.cpu().numpy()[:m], want["item_status"]), label + ": item_status"
-        assert np.array_equal(got.items[0].cpu().numpy().view(np.int32).ravel(), want["key"]), label + ": key"
-        assert np.array_equal(got.items[1].cpu().numpy().view(np.uint64).ravel(),
+        assert np.array_equal(got.items[0][:m].cpu().numpy().view(np.int32).ravel(), want["key"]), label + ": key"
+        assert np.array_equal(got.items[1][:m].cpu().numpy().view(np.uint64).ravel(),
                               want["value"].view(np.uint64)), label + ": value"
-        assert np.array_equal(got.items[2].cpu().numpy().view(np.uint32), want["label"]), label + ": label"
-    return got, want
+        assert np.array_equal(got.items[2][:m].cpu().numpy().view(np.uint32), want["label"]), label + ": label"
+    return got
 
 
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 5000])
-def test_nested_parity(dev, n):
+def test_nested_parity(dev, kernel, n):
     w = workload.nested(n, seed=n)
     stream, ends = O.encode_nested_batch(w)
     check_nested(dev, stream, ends, f"nested n={n}")
@@ -87,7 +106,7 @@ def _record(items, name="nm", list_tag=4, extra=None):
     return b
 
 
-def test_nested_edge_cases(dev):
+def test_nested_edge_cases(dev, kernel):
     """No list field, empty list, a big list (> 255 items), the list under another tag, items
     with missing/extra fields, garbage records and truncated records."""
     recs = [
@@ -118,7 +137,7 @@ def test_nested_edge_cases(dev):
     check_nested(dev, stream, ends, "edge")
 
 
-def test_nested_malformed_list_tables(dev):
+def test_nested_malformed_list_tables(dev, kernel):
     """List tables whose element ends decrease (Go panics on the slice => SPEC_STATUS_PANIC
     for that item) or exceed the list's data size (nil items)."""
     item = _record([(1, 1.0, "a")])
@@ -138,7 +157,7 @@ def test_nested_malformed_list_tables(dev):
 
 
 @pytest.mark.parametrize("seed", range(4))
-def test_nested_fuzz(dev, seed):
+def test_nested_fuzz(dev, kernel, seed):
     rng = np.random.default_rng(500 + seed)
     n = 2000
     w = workload.nested(n, seed=seed)
@@ -227,8 +246,13 @@ def test_nested_roundtrip_full_size(dev):
     out, ends = spec_amd.encode_nested(NESTED, oc, oh, ib, ic, ih, n)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), want)
-    got = spec_amd.decode_nested(NESTED, out, ends)
-    assert int(got.status.sum()) == 0
-    assert np.array_equal(got.item_begin.cpu().numpy().view(np.uint32), w["item_begin"])
-    assert np.array_equal(got.items[0].cpu().numpy().view(np.int32).ravel(), w["key"])
-    assert np.array_equal(got.outer[1].cpu().numpy().view(np.int64).ravel(), w["seq"])
+    m = len(w["key"])
+    for onepass in (False, True):
+        got = spec_amd.decode_nested(NESTED, out, ends, onepass=onepass)
+        assert int(got.status.sum()) == 0
+        assert got.total_items == m
+        assert np.array_equal(got.item_begin.cpu().numpy().view(np.uint32), w["item_begin"])
+        assert np.array_equal(got.items[0][:m].cpu().numpy().view(np.int32).ravel(), w["key"])
+        assert np.array_equal(got.items[1][:m].cpu().numpy().view(np.uint64).ravel(), w["value"].view(np.uint64))
+        assert int(got.item_status[:m].sum()) == 0
+        assert np.array_equal(got.outer[1].cpu().numpy().view(np.int64).ravel(), w["seq"])

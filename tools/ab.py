@@ -1,5 +1,8 @@
-"""A/B decode variants in separate processes (env vars select kernel variants), interleaved
-rounds to cancel box drift.  Usage: python tools/ab.py 'NAME=ENV=VAL,ENV=VAL' ... [--rounds R]"""
+"""A/B kernel variants in separate processes (env vars select kernel variants), interleaved
+rounds to cancel box drift.
+Usage: python tools/ab.py 'NAME=ENV=VAL,ENV=VAL' ... [--rounds=R] [--tool=flat|nested]
+  flat:   tools/bench_variants.py jit  (1M Flat16 decode, median per-launch ms)
+  nested: tools/bench_nested.py        (1M Nested one-pass decode, ms per launch)"""
 import json
 import os
 import subprocess
@@ -7,10 +10,13 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
-rounds = 3
+rounds, tool = 3, "flat"
 for a in sys.argv[1:]:
     if a.startswith("--rounds="):
         rounds = int(a.split("=")[1])
+    if a.startswith("--tool="):
+        tool = a.split("=")[1]
+cmd, key = {"flat": (["bench_variants.py", "jit"], "jit"), "nested": (["bench_nested.py"], "nested")}[tool]
 variants = []
 for a in args:
     name, _, envs = a.partition("=")
@@ -20,14 +26,16 @@ for a in args:
         env[k] = v
     variants.append((name, env))
 res = {name: [] for name, _ in variants}
+extra = {}
 for _ in range(rounds):
     for name, env in variants:
-        out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bench_variants.py"), "jit"],
+        out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", cmd[0])] + cmd[1:],
                              env=env, capture_output=True, text=True, timeout=300)
         if out.returncode != 0:
             print(out.stderr[-2000:])
             sys.exit(1)
         d = json.loads(out.stdout.strip().splitlines()[-1])
-        res[name].append(d["jit"]["med"])
-summary = {k: {"median_ms": sorted(v)[len(v) // 2], "all": v} for k, v in res.items()}
+        res[name].append(d[key]["med"])
+        extra[name] = d[key]
+summary = {k: {"median_ms": sorted(v)[len(v) // 2], "all": v, "last": extra[k]} for k, v in res.items()}
 print(json.dumps(summary))

@@ -1,0 +1,47 @@
+"""Nested (config 4) decode timing on one GPU: one-pass and two-pass, per launch (HIP events).
+Prints one JSON line; env variables (SPEC_AMD_JIT, SPEC_AMD_EXP, SPEC_AMD_JIT_DEFS) select
+kernel variants, so tools/ab.py-style interleaved runs compare them."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import spec_amd  # noqa: E402
+from spec_amd import NESTED, workload  # noqa: E402
+import bench  # noqa: E402
+
+
+def main():
+    n = int(os.environ.get("N", 1 << 20))
+    dev = torch.device("cuda", 0)
+    w = workload.nested(n, workload.SEED)
+    m = len(w["key"])
+    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    outer = [to(w["id"]), to(w["seq"].view(np.uint8).reshape(n, 8)), to(w["name"].view(np.uint8).reshape(n, 8)), None]
+    items = [to(w["key"].view(np.uint8).reshape(m, 4)), to(w["value"].view(np.uint8).reshape(m, 8)),
+             to(w["label"].view(np.uint8).reshape(m, 8))]
+    oh, ih, ib = {2: to(w["name_heap"])}, {2: to(w["label_heap"])}, to(w["item_begin"].view(np.int32))
+    stream, ends = spec_amd.encode_nested(NESTED, outer, oh, ib, items, ih, n)
+    d = spec_amd.NestedDecoder(NESTED, stream, ends)
+    d.index()
+    d.reserve(int(d.total.item()))
+
+    def two():
+        d.index()
+        d.decode()
+
+    res = {}
+    two_ms, _ = bench.kernel_time_events(two, 20)
+    one_ms, _ = bench.kernel_time_events(d.decode_onepass, 20)
+    torch.cuda.synchronize()
+    ok = int(d.total.item()) == m and torch.equal(d.items[0], items[0]) and torch.equal(d.item_begin, ib)
+    res["nested"] = {"onepass_ms": round(one_ms, 4), "twopass_ms": round(two_ms, 4), "ok": bool(ok),
+                     "med": round(one_ms, 4)}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
