@@ -325,7 +325,7 @@ int spec_decode_nested(const spec_nested_schema *schema, const uint8_t *stream_b
     a.item_begin = item_begin;
     a.item_cap = item_cap;
     double avg = (double)stream_len / (double)n;
-    if (spec::launch_nested_decode(a, avg, (hipStream_t)stream)) return hip_rc(hipGetLastError());
+    if (spec::launch_nested_decode(schema, a, avg, (hipStream_t)stream)) return hip_rc(hipGetLastError());
     return SPEC_OK;
 }
 

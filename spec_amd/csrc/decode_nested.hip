@@ -9,6 +9,7 @@
 //   spec_decode_nested_onepass: nested_onepass_kernel alone (decoupled look-back over the
 //     groups' item counts), after zeroing the look-back words.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "decode_nested_core.hpp"
 #include "spec_internal.hpp"
@@ -19,36 +20,43 @@ namespace {
 
 __global__ __launch_bounds__(256) void nested_count_kernel(NestedArgs a) { nested_count_body(a); }
 
-// Exclusive scan of the group totals (one 1024-thread workgroup, chunked) + total items.
+// Exclusive scan of the group totals + total items: one 1024-thread workgroup, tiles of
+// 16 consecutive totals per thread (thread sums -> wave scans -> wave totals in LDS).
 __global__ __launch_bounds__(1024) void nested_scan_kernel(NestedArgs a) {
-    __shared__ uint64_t part[1024 / 64];
-    __shared__ uint64_t carry;
+    constexpr int PER = 16;
+    __shared__ uint64_t wsum[1024 / 64];
     const uint64_t ngroups = (a.n + 63) / 64;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    if (t == 0) carry = 0;
-    __syncthreads();
-    for (uint64_t c0 = 0; c0 < ngroups; c0 += 1024) {
-        const uint64_t i = c0 + t;
-        const uint64_t v = i < ngroups ? a.group_base[i] : 0;
-        uint64_t x = v;
+    uint64_t carry = 0;
+    for (uint64_t tile = 0; tile < ngroups; tile += 1024 * PER) {
+        const uint64_t b = tile + (uint64_t)t * PER;
+        uint64_t v[PER], sum = 0;
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            v[i] = b + i < ngroups ? a.group_base[b + i] : 0;
+            sum += v[i];
+        }
+        uint64_t x = sum; // inclusive wave scan of the thread sums
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
-            uint64_t y = __shfl_up(x, d);
+            const uint64_t y = __shfl_up(x, d);
             if (lane >= d) x += y;
         }
-        if (lane == 63) part[w] = x;
+        if (lane == 63) wsum[w] = x;
         __syncthreads();
-        if (t == 0) {
-            uint64_t run = carry;
-            for (int k = 0; k < 1024 / 64; k++) {
-                uint64_t p = part[k];
-                part[k] = run;
-                run += p;
-            }
-            carry = run;
+        uint64_t before = 0, tile_total = 0;
+#pragma unroll
+        for (int k = 0; k < 1024 / 64; k++) {
+            before += k < w ? wsum[k] : 0;
+            tile_total += wsum[k];
         }
-        __syncthreads();
-        if (i < ngroups) a.group_base[i] = part[w] + x - v;
+        uint64_t run = carry + before + x - sum;
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            if (b + i < ngroups) a.group_base[b + i] = run;
+            run += v[i];
+        }
+        carry += tile_total;
         __syncthreads();
     }
     if (t == 0) *a.total = carry;
@@ -78,26 +86,43 @@ int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_nested_decode(NestedArgs a, double avg_record, hipStream_t stream) {
+int launch_nested_decode(const spec_nested_schema *schema, NestedArgs a, double avg_record, hipStream_t stream) {
     if (a.n == 0) return 0;
     a.slab = decode_slab_bytes(avg_record);
+    const int j = jit_launch_nested(schema, a, false, stream);
+    if (j != 0) return j > 0 ? 0 : -1;
     const uint64_t groups = (a.n + 63) / 64;
     dim3 grid((unsigned)((groups + DEC_WAVES - 1) / DEC_WAVES)), block(64 * DEC_WAVES);
     hipLaunchKernelGGL(nested_decode_kernel, grid, block, (size_t)DEC_WAVES * a.slab, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// One wave per block (one group per wave, in ticket order).  The look-back words and the
-// ticket (group_base[0 .. ngroups]) are zeroed first, on the same stream.
+bool nested_lookback() {
+    static int v = [] {
+        const char *e = getenv("SPEC_AMD_LOOKBACK");
+        return (e && e[0] == '1') ? 1 : 0;
+    }();
+    return v == 1;
+}
+
+// spec_decode_nested_onepass: by default the index kernels + the decode kernel back to back
+// (no host round trip; measured faster on MI355X than the look-back kernel, whose global
+// ticket and look-back words cross the XCDs through memory); SPEC_AMD_LOOKBACK=1: one wave
+// per block, one group per wave in ticket order, look-back words and ticket
+// (group_base[0 .. ngroups]) zeroed first, on the same stream.
 int launch_nested_onepass(const spec_nested_schema *schema, NestedArgs a, double avg_record, hipStream_t stream) {
     if (a.n == 0) {
         (void)hipMemsetAsync(a.total, 0, sizeof(uint64_t), stream);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
+    if (!nested_lookback()) {
+        if (launch_nested_index(a, avg_record, stream)) return -1;
+        return launch_nested_decode(schema, a, avg_record, stream);
+    }
     a.slab = decode_slab_bytes(avg_record);
     const uint64_t groups = (a.n + 63) / 64;
     if (hipMemsetAsync(a.group_base, 0, (groups + 1) * sizeof(uint64_t), stream) != hipSuccess) return -1;
-    const int j = jit_launch_nested_onepass(schema, a, stream);
+    const int j = jit_launch_nested(schema, a, true, stream);
     if (j < 0) return -1;
     if (j == 0) hipLaunchKernelGGL(nested_onepass_kernel, dim3((unsigned)groups), dim3(64), (size_t)a.slab, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -134,9 +134,12 @@ std::string generate_nested(const spec_nested_schema *s) {
     const bool fo = has_fast_path(&s->outer), fi = has_fast_path(&s->item);
     if (fo) emit_spec(o, "GenOuter", &s->outer);
     if (fi) emit_spec(o, "GenItem", &s->item);
+    const std::string specs = std::string(fo ? "GenOuter" : "spec::RuntimeSpec") + ", " +
+                              (fi ? "GenItem" : "spec::RuntimeSpec");
     o << "extern \"C\" __global__ __launch_bounds__(64) void spec_decode_nested_jit(spec::NestedArgs a) {\n"
-      << "  spec::nested_decode_body<" << (fo ? "GenOuter" : "spec::RuntimeSpec") << ", "
-      << (fi ? "GenItem" : "spec::RuntimeSpec") << ", true>(a);\n}\n";
+      << "  spec::nested_decode_body<" << specs << ", true>(a);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(64) void spec_decode_nested2_jit(spec::NestedArgs a) {\n"
+      << "  spec::nested_decode_body<" << specs << ", false>(a);\n}\n";
     return o.str();
 }
 
@@ -246,7 +249,7 @@ Entry load(const std::vector<char> &code, Prog p) {
     }
     const char *names[3][2] = {{"spec_decode_flat_jit", nullptr},
                                {"spec_encode_size_jit", "spec_encode_write_jit"},
-                               {"spec_decode_nested_jit", nullptr}};
+                               {"spec_decode_nested_jit", "spec_decode_nested2_jit"}};
     bool ok = hipModuleLoadData(&e.mod, code.data()) == hipSuccess;
     for (int i = 0; ok && i < 2; i++)
         if (names[p][i]) ok = hipModuleGetFunction(&e.fn[i], e.mod, names[p][i]) == hipSuccess;
@@ -341,7 +344,7 @@ long long jit_compile_only_nested(const spec_nested_schema *schema) {
     return (long long)compile_source(generate_nested(schema), NESTED).size();
 }
 
-int jit_launch_nested_onepass(const spec_nested_schema *schema, const NestedArgs &a, hipStream_t stream) {
+int jit_launch_nested(const spec_nested_schema *schema, const NestedArgs &a, bool onepass, hipStream_t stream) {
     if (a.slab == 0) return 0; // records too large for LDS: generic kernel
     const Entry *e = lookup_nested(schema);
     if (!e) return 0;
@@ -350,7 +353,8 @@ int jit_launch_nested_onepass(const spec_nested_schema *schema, const NestedArgs
     void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                      HIP_LAUNCH_PARAM_END};
     const unsigned groups = (unsigned)((a.n + 63) / 64);
-    hipError_t rc = hipModuleLaunchKernel(e->fn[0], groups, 1, 1, 64, 1, 1, a.slab, stream, nullptr, extra);
+    hipError_t rc = hipModuleLaunchKernel(e->fn[onepass ? 0 : 1], groups, 1, 1, 64, 1, 1, a.slab, stream, nullptr,
+                                          extra);
     return rc == hipSuccess ? 1 : -1;
 }
 

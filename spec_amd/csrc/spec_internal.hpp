@@ -34,11 +34,13 @@ bool persistent_decode(); // SPEC_AMD_PERSIST=1
 unsigned decode_wpb();     // SPEC_AMD_WPB (waves per block, default 1)
 int launch_parse(DecodeArgs a, uint32_t *sizes, double avg_record, hipStream_t stream);
 int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream);
-int launch_nested_decode(NestedArgs a, double avg_record, hipStream_t stream);
+int launch_nested_decode(const spec_nested_schema *schema, NestedArgs a, double avg_record, hipStream_t stream);
 int launch_nested_onepass(const spec_nested_schema *schema, NestedArgs a, double avg_record, hipStream_t stream);
-// jit.cpp: one-pass nested decode specialised to the outer and item schemas; 1 launched,
-// 0 use the precompiled kernel, <0 HIP error.  a.slab must be set.
-int jit_launch_nested_onepass(const spec_nested_schema *schema, const NestedArgs &a, hipStream_t stream);
+// jit.cpp: nested decode specialised to the outer and item schemas (onepass: look-back kernel,
+// else the decode pass after the index kernels); 1 launched, 0 use the precompiled kernel,
+// <0 HIP error.  a.slab must be set.
+int jit_launch_nested(const spec_nested_schema *schema, const NestedArgs &a, bool onepass, hipStream_t stream);
+bool nested_lookback(); // SPEC_AMD_LOOKBACK=1: spec_decode_nested_onepass runs the look-back kernel
 long long jit_compile_only_nested(const spec_nested_schema *schema);
 // jit.cpp: schema-specialised decode kernel (hiprtc); returns 1 if launched, 0 if the caller
 // should launch the generic kernel, <0 on a HIP error.
