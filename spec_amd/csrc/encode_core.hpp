@@ -168,12 +168,17 @@ __device__ __forceinline__ void scan_block_sums(uint64_t *block_sums, uint64_t n
 // Byte sinks.  Positions are in sink coordinates; `lo` is the first byte this lane owns (a
 // dword straddling lo is written bytewise so neighbouring records are never clobbered).
 struct LdsSink {
+    // An emitter that owns a record from its first to its last byte (SpecEnc::emit) may store
+    // its first dword whole even when it starts below the record (HEAD_ST4 below): the bytes
+    // below belong to the previous lane's record, which writes them later, in its finish().
+    static constexpr bool kHeadSt4 = true;
     uint8_t *slab;
     __device__ __forceinline__ void st1(int p, uint32_t b) const { slab[p] = (uint8_t)b; }
     __device__ __forceinline__ void st4a(int p, uint32_t w) const { *(uint32_t *)(slab + p) = w; }
 };
 
 struct GlobalSink {
+    static constexpr bool kHeadSt4 = false;
     uint8_t *out;
     __device__ __forceinline__ void st1(long long p, uint32_t b) const { out[p] = (uint8_t)b; }
     __device__ __forceinline__ void st4a(long long p, uint32_t w) const {
@@ -185,7 +190,10 @@ struct GlobalSink {
 };
 
 // Sequential emitter that merges bytes into dwords (aligned in sink coordinates).
-template <class Sink, class Pos>
+// HEAD_ST4: the dword straddling `lo` is stored whole (no per-byte path, no divergent branch
+// per flush) — only for an emitter that writes a whole record in one sequence, in lockstep
+// with its neighbours (see LdsSink::kHeadSt4); otherwise bytes below `lo` are never written.
+template <class Sink, class Pos, bool HEAD_ST4 = false>
 struct Emit {
     const Sink &k;
     Pos pos;   // next byte position
@@ -195,7 +203,7 @@ struct Emit {
     __device__ __forceinline__ Emit(const Sink &sink, Pos p) : k(sink), pos(p), lo(p), acc(0) {}
 
     __device__ __forceinline__ void flush_dword(Pos d, uint32_t w) {
-        if (d >= lo) {
+        if (HEAD_ST4 || d >= lo) {
             k.st4a(d, w);
         } else {
             for (int i = 0; i < 4; i++)
@@ -628,7 +636,7 @@ struct SpecEnc {
     static __device__ __forceinline__ void emit(const EncodeArgs &a, const Sink &k, Pos start, uint64_t,
                                                 const Rec &rec, const RecSize &rs, const uint8_t *) {
         Rec x = rec;
-        Emit<Sink, Pos> em(k, start);
+        Emit<Sink, Pos, Sink::kHeadSt4> em(k, start);
         emit_values<0>(a, em, x, start);
         emit_table<0>(em, x, rs.big);
         // trailer: rvarint(dataSize) | rvarint(tableSize) | type (internal/encode/msg.go:36-39)

@@ -16,7 +16,8 @@ for a in sys.argv[1:]:
         rounds = int(a.split("=")[1])
     if a.startswith("--tool="):
         tool = a.split("=")[1]
-cmd, key = {"flat": (["bench_variants.py", "jit"], "jit"), "nested": (["bench_nested.py"], "nested")}[tool]
+cmd, key = {"flat": (["bench_variants.py", "jit"], "jit"), "nested": (["bench_nested.py"], "nested"),
+            "encode": (["bench_encode.py"], "flat")}[tool]
 variants = []
 for a in args:
     name, _, envs = a.partition("=")
