@@ -173,8 +173,11 @@ struct LdsSink {
     // below belong to the previous lane's record, which writes them later, in its finish().
     static constexpr bool kHeadSt4 = true;
     uint8_t *slab;
+    int dummy; // slab-relative dword nobody reads: target of the stores a HEAD_ST4 emitter skips
     __device__ __forceinline__ void st1(int p, uint32_t b) const { slab[p] = (uint8_t)b; }
     __device__ __forceinline__ void st4a(int p, uint32_t w) const { *(uint32_t *)(slab + p) = w; }
+    // store w at p if c, else at the dummy dword: one store, no divergent branch
+    __device__ __forceinline__ void st4a_if(bool c, int p, uint32_t w) const { st4a(c ? p : dummy, w); }
 };
 
 struct GlobalSink {
@@ -187,6 +190,9 @@ struct GlobalSink {
         out[p + 2] = (uint8_t)(w >> 16);
         out[p + 3] = (uint8_t)(w >> 24);
     }
+    __device__ __forceinline__ void st4a_if(bool c, long long p, uint32_t w) const {
+        if (c) st4a(p, w);
+    }
 };
 
 // Sequential emitter that merges bytes into dwords (aligned in sink coordinates).
@@ -195,6 +201,7 @@ struct GlobalSink {
 // with its neighbours (see LdsSink::kHeadSt4); otherwise bytes below `lo` are never written.
 template <class Sink, class Pos, bool HEAD_ST4 = false>
 struct Emit {
+    static constexpr bool kHeadSt4 = HEAD_ST4;
     const Sink &k;
     Pos pos;   // next byte position
     Pos lo;    // first owned byte
@@ -214,7 +221,11 @@ struct Emit {
         uint32_t sh = (uint32_t)(pos & 3) * 8;
         acc |= (b & 0xff) << sh;
         pos++;
-        if ((pos & 3) == 0) {
+        if constexpr (HEAD_ST4) {
+            const bool full = (pos & 3) == 0;
+            k.st4a_if(full, pos - 4, acc);
+            acc = full ? 0u : acc;
+        } else if ((pos & 3) == 0) {
             flush_dword(pos - 4, acc);
             acc = 0;
         }
@@ -222,7 +233,11 @@ struct Emit {
     // 4 bytes in memory order packed little-endian
     __device__ __forceinline__ void put4(uint32_t w) {
         uint32_t k4 = (uint32_t)(pos & 3);
-        if (k4 == 0) {
+        if constexpr (HEAD_ST4) {
+            const uint32_t sh = 8 * k4;
+            k.st4a(pos - k4, acc | (w << sh));
+            acc = k4 ? (w >> (32 - sh)) : 0u;
+        } else if (k4 == 0) {
             flush_dword(pos, w);
         } else {
             uint32_t sh = 8 * k4;
@@ -236,19 +251,24 @@ struct Emit {
         put4((uint32_t)(w >> 32));
     }
     // k (0..8) bytes of v, lowest byte first, merged into the pending dword
-    __device__ __forceinline__ void put_n(uint64_t v, uint32_t k) {
+    __device__ __forceinline__ void put_n(uint64_t v, uint32_t nb) {
         const uint32_t ph = (uint32_t)(pos & 3), sh = 8 * ph;
         const uint64_t lo64 = (uint64_t)acc | (v << sh);
         const uint32_t hi32 = sh ? (uint32_t)(v >> (64 - sh)) : 0u;
-        const uint32_t total = ph + k;
+        const uint32_t total = ph + nb;
         const Pos d = pos & ~(Pos)3;
-        if (total >= 4) flush_dword(d, (uint32_t)lo64);
-        if (total >= 8) flush_dword(d + 4, (uint32_t)(lo64 >> 32));
+        if constexpr (HEAD_ST4) {
+            k.st4a_if(total >= 4, d, (uint32_t)lo64);
+            k.st4a_if(total >= 8, d + 4, (uint32_t)(lo64 >> 32));
+        } else {
+            if (total >= 4) flush_dword(d, (uint32_t)lo64);
+            if (total >= 8) flush_dword(d + 4, (uint32_t)(lo64 >> 32));
+        }
         const uint32_t full = total >> 2;
         const uint32_t rest = full == 0 ? (uint32_t)lo64 : (full == 1 ? (uint32_t)(lo64 >> 32) : hi32);
         const uint32_t keep = total & 3;
         acc = keep ? (rest & (0xffffffffu >> (32 - 8 * keep))) : 0u;
-        pos += k;
+        pos += nb;
     }
     // reverse varint (oracle/compactint.c so_put_reverse_*): top group first, MSB clear;
     // following groups carry 0x80; the least-significant group is the last byte.  Up to 8
@@ -600,7 +620,10 @@ struct SpecEnc {
 #pragma unroll
                 for (int j = 0; j < 16; j++) {
                     const uint32_t w = __builtin_amdgcn_alignbyte(x.h[F][j + 1], x.h[F][j], sh);
-                    if ((uint32_t)(4 * j + 4) <= n) {
+                    if constexpr (E::kHeadSt4) { // straight-line: 0..4 bytes per dword
+                        const uint32_t left = n > (uint32_t)(4 * j) ? n - 4 * j : 0u;
+                        em.put_n(w, left < 4 ? left : 4u);
+                    } else if ((uint32_t)(4 * j + 4) <= n) {
                         em.put4(w);
                     } else if ((uint32_t)(4 * j) < n) {
                         em.put_n(w, n - 4 * j);
@@ -729,7 +752,7 @@ __device__ __forceinline__ void encode_write_body(const EncodeArgs &a, uint8_t *
     const uint64_t head = ((uint64_t)(a.out + S)) & 15; // slab pos of byte S keeps 16-B phase
     if (head + (E - S) + 16 <= (uint64_t)ENC_SLAB) {
         uint8_t *slab = smem + ENC_LDS_HEAD + wave * ENC_SLAB;
-        LdsSink k{slab};
+        LdsSink k{slab, (int)(smem + ENC_LDS_HEAD - 4 - slab)}; // dummy: last header dword (unused)
         if (valid) P::emit(a, k, (int)(head + (start - S)), r, rec, rs, inv_order);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();

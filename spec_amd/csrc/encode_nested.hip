@@ -169,7 +169,7 @@ __global__ __launch_bounds__(ENC_BLOCK) void nested_enc_write_kernel(NestedEncod
     const uint64_t head = ((uintptr_t)(a.out + S)) & 15;
     if (head + (E - S) + 16 <= (uint64_t)NENC_SLAB) {
         uint8_t *slab = smem + wave * NENC_SLAB;
-        LdsSink k{slab};
+        LdsSink k{slab, 0}; // emit_message never uses the dummy (no HEAD_ST4 emitter)
         if (valid) {
             ListEmitter<LdsSink, int> le{&a, &k, inv_item};
             emit_message(a.outer, k, (int)(head + (start - S)), r, rs, inv_outer, le);
