@@ -270,6 +270,47 @@ struct Emit {
         acc = keep ? (rest & (0xffffffffu >> (32 - 8 * keep))) : 0u;
         pos += nb;
     }
+    // HEAD_ST4 only: n (<= 64) bytes whose first is heap byte `off`, from h[0..19] = the heap
+    // dwords starting at off & ~3.  Output dword m of the run (byte d0 + 4m, d0 = pos & ~3) is
+    // one funnel shift of two heap dwords, so a 64-byte string costs 17 shifts and 17 dword
+    // stores instead of 16 byte-merging appends.
+    template <class H>
+    __device__ __forceinline__ void put_heap64(const H &h, uint32_t off, uint32_t n) {
+        static_assert(HEAD_ST4, "put_heap64: whole-record emitters only");
+        const uint32_t ph = (uint32_t)(pos & 3);
+        const Pos d0 = pos & ~(Pos)3;
+        const uint32_t s = (off & 3) + 4 - ph; // g-byte of output byte d0, g = [0, h0, h1, ...]
+        const bool hi = s >= 4;
+        const uint32_t b = s & 3;
+        const uint32_t total = ph + n, full = total >> 2;
+        uint32_t v[17];
+#pragma unroll
+        for (int m = 0; m < 17; m++) {
+            const uint32_t g0 = m == 0 ? 0u : h[m - 1], g1 = h[m], g2 = h[m + 1];
+            v[m] = hi ? __builtin_amdgcn_alignbyte(g2, g1, b) : __builtin_amdgcn_alignbyte(g1, g0, b);
+        }
+        v[0] = (v[0] & (0xffffffffu << (8 * ph))) | acc;
+#pragma unroll
+        for (int m = 0; m < 17; m++) k.st4a_if((uint32_t)m < full, d0 + 4 * m, v[m]);
+        // the pending (partial) dword: v[full], by a select tree on full's bits
+        uint32_t t[17];
+#pragma unroll
+        for (int m = 0; m < 17; m++) t[m] = v[m];
+        asm("" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]), "+v"(t[7]),
+            "+v"(t[8]), "+v"(t[9]), "+v"(t[10]), "+v"(t[11]), "+v"(t[12]), "+v"(t[13]), "+v"(t[14]), "+v"(t[15]),
+            "+v"(t[16]));
+        const uint32_t l1[9] = {full & 1 ? t[1] : t[0],   full & 1 ? t[3] : t[2],   full & 1 ? t[5] : t[4],
+                                full & 1 ? t[7] : t[6],   full & 1 ? t[9] : t[8],   full & 1 ? t[11] : t[10],
+                                full & 1 ? t[13] : t[12], full & 1 ? t[15] : t[14], t[16]};
+        const uint32_t l2[5] = {full & 2 ? l1[1] : l1[0], full & 2 ? l1[3] : l1[2], full & 2 ? l1[5] : l1[4],
+                                full & 2 ? l1[7] : l1[6], l1[8]};
+        const uint32_t l3[3] = {full & 4 ? l2[1] : l2[0], full & 4 ? l2[3] : l2[2], l2[4]};
+        const uint32_t l4[2] = {full & 8 ? l3[1] : l3[0], l3[2]};
+        const uint32_t last = full & 16 ? l4[1] : l4[0];
+        const uint32_t keep = total & 3;
+        acc = keep ? (last & (0xffffffffu >> (32 - 8 * keep))) : 0u;
+        pos += n;
+    }
     // reverse varint (oracle/compactint.c so_put_reverse_*): top group first, MSB clear;
     // following groups carry 0x80; the least-significant group is the last byte.  Up to 8
     // bytes (values < 2^56) are built in a register and appended at once.
@@ -617,16 +658,17 @@ struct SpecEnc {
             } else { // string/bytes: the prefetched 64 bytes, then the rest from the heap
                 const uint32_t off = (uint32_t)v, len = (uint32_t)(v >> 32), sh = off & 3;
                 const uint32_t n = len < 64 ? len : 64;
+                if constexpr (E::kHeadSt4) {
+                    em.put_heap64(x.h[F], off, n);
+                } else {
 #pragma unroll
-                for (int j = 0; j < 16; j++) {
-                    const uint32_t w = __builtin_amdgcn_alignbyte(x.h[F][j + 1], x.h[F][j], sh);
-                    if constexpr (E::kHeadSt4) { // straight-line: 0..4 bytes per dword
-                        const uint32_t left = n > (uint32_t)(4 * j) ? n - 4 * j : 0u;
-                        em.put_n(w, left < 4 ? left : 4u);
-                    } else if ((uint32_t)(4 * j + 4) <= n) {
-                        em.put4(w);
-                    } else if ((uint32_t)(4 * j) < n) {
-                        em.put_n(w, n - 4 * j);
+                    for (int j = 0; j < 16; j++) {
+                        const uint32_t w = __builtin_amdgcn_alignbyte(x.h[F][j + 1], x.h[F][j], sh);
+                        if ((uint32_t)(4 * j + 4) <= n) {
+                            em.put4(w);
+                        } else if ((uint32_t)(4 * j) < n) {
+                            em.put_n(w, n - 4 * j);
+                        }
                     }
                 }
                 if (len > 64) emit_heap(em, heap_rsrc(a.f, F), a.f.heap_lens[F], off + 64, len - 64);
