@@ -485,15 +485,15 @@ __device__ __forceinline__ Pos emit_message(const EncFields &a, const Sink &k, P
 
 struct RuntimeEnc {
     struct Rec {};
-    static __device__ __forceinline__ Rec load(const EncodeArgs &, uint64_t) { return Rec{}; }
-    static __device__ __forceinline__ RecSize size(const EncodeArgs &a, const Rec &, uint64_t r, bool check,
+    static __device__ __forceinline__ Rec load(const EncFields &, uint64_t) { return Rec{}; }
+    static __device__ __forceinline__ RecSize size(const EncFields &f, const Rec &, uint64_t r, bool check,
                                                    bool &err) {
-        return record_size(a.f, r, check, err);
+        return record_size(f, r, check, err);
     }
     template <class Sink, class Pos>
-    static __device__ __forceinline__ void emit(const EncodeArgs &a, const Sink &k, Pos p, uint64_t r, const Rec &,
+    static __device__ __forceinline__ void emit(const EncFields &f, const Sink &k, Pos p, uint64_t r, const Rec &,
                                                 const RecSize &rs, const uint8_t *inv_order) {
-        emit_message(a.f, k, p, r, rs, inv_order);
+        emit_message(f, k, p, r, rs, inv_order);
     }
 };
 
@@ -519,9 +519,9 @@ struct SpecEnc {
     };
 
     template <int F>
-    static __device__ __forceinline__ void load_col(const EncodeArgs &a, uint64_t r, Rec &x) {
+    static __device__ __forceinline__ void load_col(const EncFields &f, uint64_t r, Rec &x) {
         if constexpr (F < N) {
-            const void *col = a.f.cols[F];
+            const void *col = f.cols[F];
             constexpr uint32_t k = Spec::kind[F];
             if constexpr (k == K_BOOL || k == K_BYTE) {
                 x.v[F][0] = ((const uint8_t *)col)[r];
@@ -543,39 +543,39 @@ struct SpecEnc {
             } else { // 64-bit kinds, string/bytes spans
                 x.v[F][0] = ((const uint64_t *)col)[r];
             }
-            load_col<F + 1>(a, r, x);
+            load_col<F + 1>(f, r, x);
         }
     }
 
     template <int F>
-    static __device__ __forceinline__ void load_heap(const EncodeArgs &a, Rec &x) {
+    static __device__ __forceinline__ void load_heap(const EncFields &f, Rec &x) {
         if constexpr (F < N) {
             if constexpr (heap_kind<F>()) {
-                const __amdgpu_buffer_rsrc_t hr = heap_rsrc(a.f, F);
+                const __amdgpu_buffer_rsrc_t hr = heap_rsrc(f, F);
                 const uint32_t off = (uint32_t)x.v[F][0] & ~3u;
 #pragma unroll
                 for (int q = 0; q < 5; q++) {
-                    const uint4 w = heap_ld128(hr, off + 16 * q, a.f.heap_lens[F]);
+                    const uint4 w = heap_ld128(hr, off + 16 * q, f.heap_lens[F]);
                     x.h[F][4 * q] = w.x;
                     x.h[F][4 * q + 1] = w.y;
                     x.h[F][4 * q + 2] = w.z;
                     x.h[F][4 * q + 3] = w.w;
                 }
             }
-            load_heap<F + 1>(a, x);
+            load_heap<F + 1>(f, x);
         }
     }
 
     // every column load of the record, then the heap loads they address, all in flight at once
-    static __device__ __forceinline__ Rec load(const EncodeArgs &a, uint64_t r) {
+    static __device__ __forceinline__ Rec load(const EncFields &f, uint64_t r) {
         Rec x;
-        load_col<0>(a, r, x);
-        load_heap<0>(a, x);
+        load_col<0>(f, r, x);
+        load_heap<0>(f, x);
         return x;
     }
 
     template <int F>
-    static __device__ __forceinline__ uint64_t data_size(const EncodeArgs &a, const Rec &x, bool check, bool &err) {
+    static __device__ __forceinline__ uint64_t data_size(const EncFields &f, const Rec &x, bool check, bool &err) {
         if constexpr (F >= N) {
             return 0;
         } else {
@@ -594,16 +594,16 @@ struct SpecEnc {
             else if constexpr (k == K_BIN256) s = 33;
             else {
                 const uint32_t off = (uint32_t)v, len = (uint32_t)(v >> 32);
-                err |= ((uint64_t)len > MAX_SIZE) | (check & ((uint64_t)off + len > a.f.heap_lens[F]));
+                err |= ((uint64_t)len > MAX_SIZE) | (check & ((uint64_t)off + len > f.heap_lens[F]));
                 s = (uint64_t)len + vlen32(len) + 1 + (k == K_STRING ? 1 : 0);
             }
-            return s + data_size<F + 1>(a, x, check, err);
+            return s + data_size<F + 1>(f, x, check, err);
         }
     }
 
-    static __device__ __forceinline__ RecSize size(const EncodeArgs &a, const Rec &x, uint64_t, bool check,
+    static __device__ __forceinline__ RecSize size(const EncFields &f, const Rec &x, uint64_t, bool check,
                                                    bool &err) {
-        const uint64_t data = data_size<0>(a, x, check, err);
+        const uint64_t data = data_size<0>(f, x, check, err);
         const bool big = Spec::big_forced | (data > 65535); // IsBigMessage, internal/format/msg.go:43-61
         const uint64_t tsize = (uint64_t)N * (big ? 6 : 3);
         err |= data > MAX_SIZE;
@@ -615,7 +615,7 @@ struct SpecEnc {
     }
 
     template <int F, class E>
-    static __device__ __forceinline__ void emit_values(const EncodeArgs &a, E &em, Rec &x, decltype(em.pos) start) {
+    static __device__ __forceinline__ void emit_values(const EncFields &f, E &em, Rec &x, decltype(em.pos) start) {
         if constexpr (F < N) {
             const uint64_t v = x.v[F][0];
             constexpr uint32_t k = Spec::kind[F];
@@ -671,13 +671,13 @@ struct SpecEnc {
                         }
                     }
                 }
-                if (len > 64) emit_heap(em, heap_rsrc(a.f, F), a.f.heap_lens[F], off + 64, len - 64);
+                if (len > 64) emit_heap(em, heap_rsrc(f, F), f.heap_lens[F], off + 64, len - 64);
                 if constexpr (k == K_STRING) em.put1(0);
                 em.rvarint(len);
                 em.put1(k == K_STRING ? T_STRING : T_BYTES);
             }
             x.end[F] = (uint32_t)(em.pos - start);
-            emit_values<F + 1>(a, em, x, start);
+            emit_values<F + 1>(f, em, x, start);
         }
     }
 
@@ -698,11 +698,11 @@ struct SpecEnc {
     // The record as one sequential byte run: values in write order, the table entries in
     // table order (their ends kept in registers), the trailer.
     template <class Sink, class Pos>
-    static __device__ __forceinline__ void emit(const EncodeArgs &a, const Sink &k, Pos start, uint64_t,
+    static __device__ __forceinline__ void emit(const EncFields &f, const Sink &k, Pos start, uint64_t,
                                                 const Rec &rec, const RecSize &rs, const uint8_t *) {
         Rec x = rec;
         Emit<Sink, Pos, Sink::kHeadSt4> em(k, start);
-        emit_values<0>(a, em, x, start);
+        emit_values<0>(f, em, x, start);
         emit_table<0>(em, x, rs.big);
         // trailer: rvarint(dataSize) | rvarint(tableSize) | type (internal/encode/msg.go:36-39)
         em.rvarint((uint32_t)rs.data);
@@ -721,9 +721,9 @@ __device__ __forceinline__ void encode_size_body(const EncodeArgs &a) {
     __syncthreads();
     const uint64_t r = (uint64_t)blockIdx.x * ENC_BLOCK + threadIdx.x;
     const bool valid = r < a.n;
-    const typename P::Rec rec = P::load(a, valid ? r : a.n - 1);
+    const typename P::Rec rec = P::load(a.f, valid ? r : a.n - 1);
     bool err = false;
-    const RecSize rs = P::size(a, rec, r, a.check_heaps, err);
+    const RecSize rs = P::size(a.f, rec, r, a.check_heaps, err);
     if (valid & err) errs = 1;
     uint64_t s = valid ? rs.total : 0;
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
@@ -766,9 +766,9 @@ __device__ __forceinline__ void encode_write_body(const EncodeArgs &a, uint8_t *
 
     const uint64_t r = (uint64_t)blockIdx.x * ENC_BLOCK + threadIdx.x;
     const bool valid = r < a.n;
-    const typename P::Rec rec = P::load(a, valid ? r : a.n - 1);
+    const typename P::Rec rec = P::load(a.f, valid ? r : a.n - 1);
     bool err = false;
-    RecSize rs = P::size(a, rec, r, false, err);
+    RecSize rs = P::size(a.f, rec, r, false, err);
     if (!valid) rs.total = 0;
     uint64_t x = rs.total; // block exclusive scan of sizes
     for (int o = 1; o < 64; o <<= 1) {
@@ -795,14 +795,14 @@ __device__ __forceinline__ void encode_write_body(const EncodeArgs &a, uint8_t *
     if (head + (E - S) + 16 <= (uint64_t)ENC_SLAB) {
         uint8_t *slab = smem + ENC_LDS_HEAD + wave * ENC_SLAB;
         LdsSink k{slab, (int)(smem + ENC_LDS_HEAD - 4 - slab)}; // dummy: last header dword (unused)
-        if (valid) P::emit(a, k, (int)(head + (start - S)), r, rec, rs, inv_order);
+        if (valid) P::emit(a.f, k, (int)(head + (start - S)), r, rec, rs, inv_order);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         copy_slab_out(slab, a.out + S - head, head, head + (E - S), lane);
     } else if (valid) {
         GlobalSink k{a.out};
-        P::emit(a, k, (long long)start, r, rec, rs, inv_order);
+        P::emit(a.f, k, (long long)start, r, rec, rs, inv_order);
     }
 }
 
