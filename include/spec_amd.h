@@ -268,6 +268,9 @@ int spec_encode_nested(const spec_nested_schema *schema, const void *const *oute
                        const void *const *item_columns, const uint8_t *const *item_heaps,
                        const uint64_t *item_heap_lens, uint64_t nitems, uint64_t n, uint8_t *out, uint64_t out_cap,
                        uint64_t *ends, void *workspace, size_t workspace_size, uint64_t *total, void *stream);
+/* spec_encode_nested_jit_compile: diagnostic — the hiprtc compile (no GPU needed) of the
+ * schema-specialised nested encode kernels; code-object size, 0 if neither schema has one. */
+long long spec_encode_nested_jit_compile(const spec_nested_schema *schema);
 
 #ifdef __cplusplus
 }

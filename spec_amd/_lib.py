@@ -81,6 +81,8 @@ def _declare(L):
                                              vp, vp]
     L.spec_decode_nested_jit_compile.argtypes = [C.POINTER(SpecNestedSchema)]
     L.spec_decode_nested_jit_compile.restype = C.c_longlong
+    L.spec_encode_nested_jit_compile.argtypes = [C.POINTER(SpecNestedSchema)]
+    L.spec_encode_nested_jit_compile.restype = C.c_longlong
     L.spec_encode_nested_workspace_size.restype = C.c_size_t
     L.spec_encode_nested_workspace_size.argtypes = [C.c_uint64]
     L.spec_encode_nested.argtypes = [C.POINTER(SpecNestedSchema), C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_uint64),

@@ -367,6 +367,13 @@ long long spec_decode_nested_jit_compile(const spec_nested_schema *schema) {
     return spec::jit_compile_only_nested(schema);
 }
 
+long long spec_encode_nested_jit_compile(const spec_nested_schema *schema) {
+    uint32_t list_f = 0;
+    int rc = check_nested(schema, &list_f);
+    if (rc) return rc;
+    return spec::jit_compile_only_nested_encode(schema);
+}
+
 size_t spec_encode_nested_workspace_size(uint64_t n) { return spec_encode_flat_workspace_size(n); }
 
 static int heaps_of(spec::EncFields &e, const spec_schema *s, const uint8_t *const *heaps, const uint64_t *lens) {
@@ -412,7 +419,8 @@ int spec_encode_nested(const spec_nested_schema *schema, const void *const *oute
     a.block_sums = (uint64_t *)workspace;
     a.nblocks = (n + spec::ENC_BLOCK - 1) / spec::ENC_BLOCK;
     a.total = total;
-    if (spec::launch_nested_encode(a, out != nullptr, (hipStream_t)stream)) return hip_rc(hipGetLastError());
+    if (spec::launch_nested_encode(schema, a, out != nullptr, (hipStream_t)stream))
+        return hip_rc(hipGetLastError());
     return SPEC_OK;
 }
 

@@ -486,14 +486,16 @@ __device__ __forceinline__ Pos emit_message(const EncFields &a, const Sink &k, P
 struct RuntimeEnc {
     struct Rec {};
     static __device__ __forceinline__ Rec load(const EncFields &, uint64_t) { return Rec{}; }
+    template <class Lists = NoLists>
     static __device__ __forceinline__ RecSize size(const EncFields &f, const Rec &, uint64_t r, bool check,
-                                                   bool &err) {
-        return record_size(f, r, check, err);
+                                                   bool &err, const Lists &lists = Lists()) {
+        return record_size(f, r, check, err, lists);
     }
-    template <class Sink, class Pos>
+    template <class Sink, class Pos, class Lists = NoListEmit>
     static __device__ __forceinline__ void emit(const EncFields &f, const Sink &k, Pos p, uint64_t r, const Rec &,
-                                                const RecSize &rs, const uint8_t *inv_order) {
-        emit_message(f, k, p, r, rs, inv_order);
+                                                const RecSize &rs, const uint8_t *inv_order,
+                                                const Lists &lists = Lists()) {
+        emit_message(f, k, p, r, rs, inv_order, lists);
     }
 };
 
@@ -510,6 +512,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t heap_rsrc(const EncFields &f, 
 template <class Spec>
 struct SpecEnc {
     static constexpr int N = Spec::N;
+    static constexpr bool has_list() {
+        for (int f = 0; f < N; f++)
+            if (Spec::kind[f] == K_LIST) return true;
+        return false;
+    }
+    static constexpr bool kHasList = has_list();
     template <int F>
     static constexpr bool heap_kind() { return Spec::kind[F] == K_STRING || Spec::kind[F] == K_BYTES; }
     struct Rec {
@@ -523,7 +531,9 @@ struct SpecEnc {
         if constexpr (F < N) {
             const void *col = f.cols[F];
             constexpr uint32_t k = Spec::kind[F];
-            if constexpr (k == K_BOOL || k == K_BYTE) {
+            if constexpr (k == K_LIST) {
+                // no column: written from the item columns by the nested encoder's list hook
+            } else if constexpr (k == K_BOOL || k == K_BYTE) {
                 x.v[F][0] = ((const uint8_t *)col)[r];
             } else if constexpr (k == K_INT16 || k == K_UINT16) {
                 x.v[F][0] = ((const uint16_t *)col)[r];
@@ -574,15 +584,17 @@ struct SpecEnc {
         return x;
     }
 
-    template <int F>
-    static __device__ __forceinline__ uint64_t data_size(const EncFields &f, const Rec &x, bool check, bool &err) {
+    template <int F, class Lists>
+    static __device__ __forceinline__ uint64_t data_size(const EncFields &f, const Rec &x, uint64_t r, bool check,
+                                                         bool &err, const Lists &lists) {
         if constexpr (F >= N) {
             return 0;
         } else {
             const uint64_t v = x.v[F][0];
             constexpr uint32_t k = Spec::kind[F];
             uint64_t s;
-            if constexpr (k == K_BOOL) s = 1;
+            if constexpr (k == K_LIST) s = lists((uint32_t)F, r);
+            else if constexpr (k == K_BOOL) s = 1;
             else if constexpr (k == K_BYTE) s = 2;
             else if constexpr (k == K_INT16) s = vlen32(zigzag32((int16_t)v)) + 1;
             else if constexpr (k == K_INT32) s = vlen32(zigzag32((int32_t)v)) + 1;
@@ -597,13 +609,14 @@ struct SpecEnc {
                 err |= ((uint64_t)len > MAX_SIZE) | (check & ((uint64_t)off + len > f.heap_lens[F]));
                 s = (uint64_t)len + vlen32(len) + 1 + (k == K_STRING ? 1 : 0);
             }
-            return s + data_size<F + 1>(f, x, check, err);
+            return s + data_size<F + 1>(f, x, r, check, err, lists);
         }
     }
 
-    static __device__ __forceinline__ RecSize size(const EncFields &f, const Rec &x, uint64_t, bool check,
-                                                   bool &err) {
-        const uint64_t data = data_size<0>(f, x, check, err);
+    template <class Lists = NoLists>
+    static __device__ __forceinline__ RecSize size(const EncFields &f, const Rec &x, uint64_t r, bool check,
+                                                   bool &err, const Lists &lists = Lists()) {
+        const uint64_t data = data_size<0>(f, x, r, check, err, lists);
         const bool big = Spec::big_forced | (data > 65535); // IsBigMessage, internal/format/msg.go:43-61
         const uint64_t tsize = (uint64_t)N * (big ? 6 : 3);
         err |= data > MAX_SIZE;
@@ -614,12 +627,15 @@ struct SpecEnc {
         return s;
     }
 
-    template <int F, class E>
-    static __device__ __forceinline__ void emit_values(const EncFields &f, E &em, Rec &x, decltype(em.pos) start) {
+    template <int F, class E, class Lists>
+    static __device__ __forceinline__ void emit_values(const EncFields &f, E &em, Rec &x, decltype(em.pos) start,
+                                                       uint64_t r, const Lists &lists) {
         if constexpr (F < N) {
             const uint64_t v = x.v[F][0];
             constexpr uint32_t k = Spec::kind[F];
-            if constexpr (k == K_BOOL) {
+            if constexpr (k == K_LIST) {
+                lists(em, (uint32_t)F, r);
+            } else if constexpr (k == K_BOOL) {
                 em.put1(v ? T_TRUE : T_FALSE);
             } else if constexpr (k == K_BYTE) {
                 em.put_n(v | (T_BYTE << 8), 2);
@@ -677,7 +693,7 @@ struct SpecEnc {
                 em.put1(k == K_STRING ? T_STRING : T_BYTES);
             }
             x.end[F] = (uint32_t)(em.pos - start);
-            emit_values<F + 1>(f, em, x, start);
+            emit_values<F + 1>(f, em, x, start, r, lists);
         }
     }
 
@@ -697,12 +713,15 @@ struct SpecEnc {
 
     // The record as one sequential byte run: values in write order, the table entries in
     // table order (their ends kept in registers), the trailer.
-    template <class Sink, class Pos>
-    static __device__ __forceinline__ void emit(const EncFields &f, const Sink &k, Pos start, uint64_t,
-                                                const Rec &rec, const RecSize &rs, const uint8_t *) {
+    // With a list field the emitter jumps over the list's items (written by other lanes), so it
+    // must never store below its position: no HEAD_ST4 then.
+    template <class Sink, class Pos, class Lists = NoListEmit>
+    static __device__ __forceinline__ void emit(const EncFields &f, const Sink &k, Pos start, uint64_t r,
+                                                const Rec &rec, const RecSize &rs, const uint8_t *,
+                                                const Lists &lists = Lists()) {
         Rec x = rec;
-        Emit<Sink, Pos, Sink::kHeadSt4> em(k, start);
-        emit_values<0>(f, em, x, start);
+        Emit<Sink, Pos, Sink::kHeadSt4 && !kHasList> em(k, start);
+        emit_values<0>(f, em, x, start, r, lists);
         emit_table<0>(em, x, rs.big);
         // trailer: rvarint(dataSize) | rvarint(tableSize) | type (internal/encode/msg.go:36-39)
         em.rvarint((uint32_t)rs.data);

@@ -1,0 +1,352 @@
+// encode_nested_core.hpp — device code of the list<message> encoder (BASELINE config 4), shared
+// by the precompiled kernels (encode_nested.hip: RuntimeEnc record policies) and the
+// schema-specialised ones (jit.cpp: SpecEnc<outer>, SpecEnc<item>).
+//
+// Per record, what a generated Write() does over the Writer:
+//   w.Field(tag).<Kind>(v) for the outer scalar fields, in write order
+//   l := w.Field(list_tag).List()           FieldWriter.List, internal/writer/msg.go:219-222
+//   for each item: m := l.Add()             MessageListWriter.Add, writer_list_msg.go:22-25
+//       m.Field(t).<Kind>(v)...; m.End()     -> endMessage + endElement (element offset =
+//                                              item end - list start), internal/writer/writer.go:299-337
+//   l.End()                                 -> endList: EncodeListTable (IsBigList: count > 255 or
+//                                              last offset > 65535), internal/writer/writer.go:339-372,
+//                                              internal/encode/list.go:15-75, internal/format/list.go:40-54
+//   w.Build()                               -> the outer table + trailer
+//
+// Layout of the work: one wave = 64 consecutive records (one per lane) and the items they own,
+// which are contiguous ([item_begin[first], item_begin[last + 1])).  Item sizes are computed
+// ITEM-parallel (item k of the wave on lane k % 64, coalesced item column loads) and
+// prefix-summed into LDS; a record's list size and every item's position follow from that
+// prefix.  Emission into the wave's LDS slab:
+//   A. lane per record: the outer fields, jumping over the list's items, then the list table
+//      (element ends from the prefix), list trailer, later fields, outer table, trailer;
+//   B. item per lane, chunks of 64 items from the LAST chunk to the first: each item as one
+//      straight run (HEAD_ST4 emitter: its first dword is stored whole, clobbering <= 3 bytes
+//      below the item, which belong to the previous item — written later, lockstep or a later
+//      chunk — or to the record's bytes before the list, restored in C);
+//   C. each record restores the dword under its list start from a copy taken after A.
+// The wave then copies the slab to HBM with 16-byte stores.  Waves with more than
+// NENC_ITEM_CAP items, invalid item ranges, or output that does not fit the slab take the
+// per-lane generic path straight to HBM (same bytes).
+#pragma once
+
+#include "encode_core.hpp"
+
+namespace spec {
+
+struct NestedEncodeArgs {
+    uint64_t n;
+    EncFields outer; // its K_LIST field is written from item_begin + item
+    EncFields item;
+    const uint32_t *item_begin; // [n + 1]
+    uint64_t nitems;            // item columns hold this many items
+    uint32_t check_heaps;
+    uint8_t *out;
+    uint64_t out_cap;
+    uint64_t *ends;
+    uint64_t *block_sums;
+    uint64_t nblocks;
+    uint64_t *total;
+};
+
+constexpr int NENC_BLOCK = 256;               // records per block (4 waves, one record per lane)
+constexpr int NENC_ITEM_CAP = 512;            // items per wave on the item-parallel path
+constexpr int NENC_PRE = (NENC_ITEM_CAP + 4) * 4; // per-wave item prefix (u32), 16-B multiple
+constexpr int NENC_SLAB = 17920;              // per-wave output staging
+constexpr int NENC_HEAD = 256;                // wsum[4] | inv_outer[64] | inv_item[64] | dummy | errs
+constexpr int NENC_WAVE_LDS = NENC_PRE + NENC_SLAB;
+constexpr size_t nenc_size_lds_bytes() { return NENC_HEAD + (size_t)(NENC_BLOCK / 64) * NENC_PRE; }
+constexpr size_t nenc_write_lds_bytes() { return NENC_HEAD + (size_t)(NENC_BLOCK / 64) * NENC_WAVE_LDS; }
+static_assert(NENC_PRE % 16 == 0 && NENC_WAVE_LDS % 16 == 0, "slab alignment");
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---- generic per-lane path (the whole list of a record on its lane) ------------------------
+
+struct ListSize {
+    uint64_t total, data;
+    uint32_t count;
+    bool big;
+};
+
+__device__ __forceinline__ ListSize list_size(const NestedEncodeArgs &a, uint64_t r, bool check, bool &err) {
+    ListSize ls = {0, 0, 0, false};
+    const uint32_t b = a.item_begin[r], e = a.item_begin[r + 1];
+    if (e < b || e > a.nitems) {
+        err = true;
+        return ls;
+    }
+    uint64_t data = 0;
+    for (uint32_t i = b; i < e; i++) data += record_size(a.item, i, check, err).total;
+    ls.count = e - b;
+    ls.data = data;
+    ls.big = ls.count > 255 || data > 65535; // IsBigList, internal/format/list.go:40-54
+    const uint64_t tsize = (uint64_t)ls.count * (ls.big ? 4 : 2);
+    if (data > MAX_SIZE || tsize > MAX_SIZE) err = true; // EncodeListTable: list too large
+    ls.total = data + tsize + vlen32((uint32_t)data) + vlen32((uint32_t)tsize) + 1;
+    return ls;
+}
+
+// Emits the list value of record r at the emitter's position (flushing it first) and moves
+// the emitter past it.
+template <class Sink, class Pos>
+struct ListEmitter {
+    const NestedEncodeArgs *a;
+    const Sink *k;
+    const uint8_t *item_inv;
+    template <class E>
+    __device__ __forceinline__ void operator()(E &em, uint32_t, uint64_t r) const {
+        em.finish();
+        bool err = false;
+        const ListSize ls = list_size(*a, r, false, err);
+        const Pos lstart = em.pos;
+        const Pos tstart = lstart + (Pos)ls.data;
+        const uint32_t esize = ls.big ? 4 : 2;
+        Pos p = lstart;
+        const uint32_t b = a->item_begin[r];
+        for (uint32_t j = 0; j < ls.count; j++) {
+            const RecSize irs = record_size(a->item, b + j, false, err);
+            p = emit_message(a->item, *k, p, (uint64_t)(b + j), irs, item_inv);
+            // element offset = item end - list start (writer.go:327-330), big-endian
+            const uint32_t off = (uint32_t)(p - lstart);
+            const Pos q = tstart + (Pos)(j * esize);
+            if (ls.big) {
+                k->st1(q, off >> 24);
+                k->st1(q + 1, (off >> 16) & 0xff);
+                k->st1(q + 2, (off >> 8) & 0xff);
+                k->st1(q + 3, off & 0xff);
+            } else {
+                k->st1(q, (off >> 8) & 0xff);
+                k->st1(q + 1, off & 0xff);
+            }
+        }
+        // trailer: rvarint(dataSize) | rvarint(tableSize) | type (internal/encode/list.go:36-43)
+        Emit<Sink, Pos> tr(*k, tstart + (Pos)((uint64_t)ls.count * esize));
+        tr.rvarint((uint32_t)ls.data);
+        tr.rvarint(ls.count * esize);
+        tr.put1(ls.big ? T_BIG_LIST : T_LIST);
+        tr.finish();
+        em.pos = tr.pos;
+        em.lo = tr.pos;
+        em.acc = 0;
+    }
+};
+
+// ---- item-parallel path ---------------------------------------------------------------
+
+// list size hook: the list's encoded size, known from the wave's item prefix
+struct KnownListSize {
+    uint64_t total;
+    __device__ __forceinline__ uint64_t operator()(uint32_t, uint64_t) const { return total; }
+};
+
+// list emit hook (phase A): skips the items, writes the list table and trailer, records where
+// the items start.
+struct WaveListEmit {
+    const uint32_t *pre; // wave item prefix at this record's first item
+    uint32_t count, data;
+    bool big;
+    mutable int lstart;
+    template <class E>
+    __device__ __forceinline__ void operator()(E &em, uint32_t, uint64_t) const {
+        em.finish();
+        lstart = (int)em.pos;
+        em.pos += data;
+        em.lo = em.pos;
+        em.acc = 0;
+        const uint32_t p0 = pre[0];
+        for (uint32_t j = 0; j < count; j++) {
+            const uint32_t end = pre[j + 1] - p0; // element offset = item end - list start
+            em.put_n(big ? bswap32(end) : (uint32_t)__builtin_bswap16((uint16_t)end), big ? 4 : 2);
+        }
+        em.rvarint(data);
+        em.rvarint(count * (big ? 4u : 2u));
+        em.put1(big ? T_BIG_LIST : T_LIST);
+    }
+};
+
+// Encoded sizes of the wave's items [I0, I0 + cnt) -> pre[k] = bytes of items I0..I0+k-1
+// (pre[0] = 0).  Returns false if the wave's item bytes do not fit 31 bits.
+template <class IP>
+__device__ __forceinline__ bool wave_item_prefix(const NestedEncodeArgs &a, uint32_t I0, uint32_t cnt,
+                                                 uint32_t *pre, int lane, bool check, bool &err) {
+    uint64_t carry = 0;
+    if (lane == 0) pre[0] = 0;
+    for (uint32_t c = 0; c < cnt; c += 64) {
+        const uint32_t k = c + lane;
+        const bool iv = k < cnt;
+        const uint64_t i = I0 + (iv ? k : 0);
+        const typename IP::Rec rec = IP::load(a.item, i);
+        bool e = false;
+        const uint64_t s = iv ? IP::size(a.item, rec, i, check, e).total : 0;
+        err |= iv & e;
+        uint64_t x = s;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (iv) pre[k + 1] = (uint32_t)(carry + x);
+        carry += __shfl(x, 63);
+    }
+    return carry <= MAX_SIZE;
+}
+
+// The lane's record and the wave's item range.
+struct LaneRecord {
+    uint64_t r;
+    bool valid;
+    uint32_t b, e; // items [b, e) (e = b for lanes past n)
+    uint32_t I0, cnt;
+    bool fast; // wave-uniform: item-parallel path
+};
+
+template <class IP>
+__device__ __forceinline__ LaneRecord lane_record(const NestedEncodeArgs &a, uint32_t *pre, int lane, bool check,
+                                                  bool &err) {
+    LaneRecord L;
+    L.r = (uint64_t)blockIdx.x * NENC_BLOCK + threadIdx.x;
+    L.valid = L.r < a.n;
+    L.b = a.item_begin[L.valid ? L.r : a.n];
+    L.e = L.valid ? a.item_begin[L.r + 1] : L.b;
+    const bool bad = L.valid && (L.e < L.b || (uint64_t)L.e > a.nitems);
+    L.I0 = __builtin_amdgcn_readfirstlane(L.b);
+    const uint32_t I1 = __builtin_amdgcn_readfirstlane(__shfl(L.e, 63));
+    L.cnt = I1 - L.I0;
+    L.fast = __ballot(bad) == 0 && L.cnt <= (uint32_t)NENC_ITEM_CAP;
+    if (L.fast) L.fast = wave_item_prefix<IP>(a, L.I0, L.cnt, pre, lane, check, err);
+    return L;
+}
+
+// Encoded size of the lane's record (valid lanes), list from the prefix or the generic path.
+template <class OP>
+__device__ __forceinline__ RecSize lane_record_size(const NestedEncodeArgs &a, const LaneRecord &L,
+                                                    const typename OP::Rec &orec, const uint32_t *pre, bool check,
+                                                    bool &err, ListSize &ls) {
+    if (L.fast) {
+        ls.count = L.e - L.b;
+        ls.data = L.valid ? pre[L.e - L.I0] - pre[L.b - L.I0] : 0;
+        ls.big = ls.count > 255 || ls.data > 65535; // IsBigList, internal/format/list.go:40-54
+        const uint32_t tsize = ls.count * (ls.big ? 4 : 2);
+        ls.total = ls.data + tsize + vlen32((uint32_t)ls.data) + vlen32(tsize) + 1;
+    } else {
+        ls = L.valid ? list_size(a, L.r, check, err) : ListSize{0, 0, 0, false};
+    }
+    return OP::size(a.outer, orec, L.r, check, err, KnownListSize{ls.total});
+}
+
+// Pass 1: per-block encoded bytes (all-ones on an encoder error).
+template <class OP, class IP>
+__device__ __forceinline__ void nested_enc_size_body(const NestedEncodeArgs &a, uint8_t *smem) {
+    uint64_t *part = (uint64_t *)smem;
+    int *errs = (int *)(smem + 164);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t *pre = (uint32_t *)(smem + NENC_HEAD + wave * NENC_PRE);
+    if (threadIdx.x == 0) *errs = 0;
+    __syncthreads();
+    bool err = false;
+    const LaneRecord L = lane_record<IP>(a, pre, lane, a.check_heaps, err);
+    const typename OP::Rec orec = OP::load(a.outer, L.valid ? L.r : a.n - 1);
+    ListSize ls;
+    const RecSize rs = lane_record_size<OP>(a, L, orec, pre, a.check_heaps, err, ls);
+    if (L.valid & err) *errs = 1;
+    uint64_t s = L.valid ? rs.total : 0;
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) part[wave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int w = 0; w < NENC_BLOCK / 64; w++) t += part[w];
+        a.block_sums[blockIdx.x] = *errs ? ~0ull : t;
+    }
+}
+
+// Pass 3: record offsets from the block scan, ends[], the records' bytes.
+template <class OP, class IP>
+__device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a, uint8_t *smem) {
+    uint64_t *wsum = (uint64_t *)smem;
+    uint8_t *inv_outer = smem + 32, *inv_item = smem + 96;
+    const uint64_t total = a.block_sums[a.nblocks];
+    if (total > a.out_cap) return; // capacity error or encoder error (total == ~0)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x < a.outer.nfields) inv_outer[a.outer.order[threadIdx.x]] = (uint8_t)threadIdx.x;
+    if (threadIdx.x < a.item.nfields) inv_item[a.item.order[threadIdx.x]] = (uint8_t)threadIdx.x;
+    uint32_t *pre = (uint32_t *)(smem + NENC_HEAD + wave * NENC_WAVE_LDS);
+    uint8_t *slab = (uint8_t *)pre + NENC_PRE;
+
+    bool err = false;
+    const LaneRecord L = lane_record<IP>(a, pre, lane, false, err);
+    const typename OP::Rec orec = OP::load(a.outer, L.valid ? L.r : a.n - 1);
+    ListSize ls;
+    RecSize rs = lane_record_size<OP>(a, L, orec, pre, false, err, ls);
+    if (!L.valid) rs.total = 0;
+    uint64_t x = rs.total; // block exclusive scan of sizes
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint64_t pre_b = a.block_sums[blockIdx.x];
+    for (int w = 0; w < wave; w++) pre_b += wsum[w];
+    const uint64_t start = pre_b + x - rs.total;
+    if (L.valid) a.ends[L.r] = start + rs.total;
+
+    const uint64_t wbase = (uint64_t)blockIdx.x * NENC_BLOCK + wave * 64;
+    if (wbase >= a.n) return;
+    const uint64_t S = __builtin_amdgcn_readfirstlane((uint32_t)start) |
+                       ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(start >> 32)) << 32);
+    const int last = (int)((a.n - wbase) < 64 ? a.n - wbase - 1 : 63);
+    const uint64_t Ev = __shfl(start + rs.total, last);
+    const uint64_t E = __builtin_amdgcn_readfirstlane((uint32_t)Ev) |
+                       ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(Ev >> 32)) << 32);
+    const uint64_t head = ((uint64_t)(a.out + S)) & 15; // slab pos of byte S keeps 16-B phase
+    if (!(L.fast && head + (E - S) + 16 <= (uint64_t)NENC_SLAB)) {
+        if (L.valid) {
+            GlobalSink k{a.out};
+            ListEmitter<GlobalSink, long long> le{&a, &k, inv_item};
+            emit_message(a.outer, k, (long long)start, L.r, rs, inv_outer, le);
+        }
+        return;
+    }
+    LdsSink k{slab, (int)(smem + 160 - slab)}; // dummy dword in the header
+    // A: outer records, the items skipped
+    WaveListEmit le{pre + (L.b - L.I0), ls.count, (uint32_t)ls.data, ls.big, 0};
+    if (L.valid) OP::emit(a.outer, k, (int)(head + (start - S)), L.r, orec, rs, inv_outer, le);
+    wave_sync();
+    const int lst = le.lstart;
+    const bool fix = L.valid && ls.count > 0 && (lst & 3);
+    const uint32_t saved = fix ? *(const uint32_t *)(slab + (lst & ~3)) : 0u;
+    wave_sync();
+    // B: items, last chunk first
+    const int lbase = lst - (int)pre[L.b - L.I0];
+    for (int c = ((int)L.cnt - 1) & ~63; c >= 0; c -= 64) {
+        const uint32_t kk = (uint32_t)c + lane;
+        const bool iv = kk < L.cnt;
+        const uint32_t i = L.I0 + (iv ? kk : 0u);
+        int o = 0; // owner lane: the last lane whose first item is <= i
+        for (int st = 32; st > 0; st >>= 1)
+            if (__shfl(L.b, o + st) <= i) o += st;
+        const int pos = __shfl(lbase, o) + (int)pre[iv ? kk : 0u];
+        if (iv) {
+            const typename IP::Rec rec = IP::load(a.item, i);
+            bool e2 = false;
+            const RecSize irs = IP::size(a.item, rec, i, false, e2);
+            IP::emit(a.item, k, pos, i, rec, irs, inv_item);
+        }
+        wave_sync();
+    }
+    // C: the bytes under the list start that the first item's head store overwrote
+    if (fix) {
+        uint32_t *d = (uint32_t *)(slab + (lst & ~3));
+        const uint32_t m = 0xffffffffu >> (32 - 8 * (lst & 3));
+        *d = (saved & m) | (*d & ~m);
+    }
+    wave_sync();
+    copy_slab_out(slab, a.out + S - head, head, head + (E - S), lane);
+}
+
+} // namespace spec

@@ -92,11 +92,11 @@ bool has_encoder(const spec_schema *s) {
     return true;
 }
 
-enum Prog { DECODE = 0, ENCODE = 1, NESTED = 2 };
+enum Prog { DECODE = 0, ENCODE = 1, NESTED = 2, NESTED_ENC = 3 };
 
 std::string key_of(const spec_schema *s, int device, Prog p) {
     std::ostringstream k;
-    k << (p == ENCODE ? "enc:" : "dec:") << device << ':' << (spec::persistent_decode() ? 'p' : 'o') << ':';
+    k << (p == ENCODE || p == NESTED_ENC ? "enc:" : "dec:") << device << ':' << (spec::persistent_decode() ? 'p' : 'o') << ':';
     for (uint32_t f = 0; f < s->nfields; f++) k << s->fields[f].tag << '/' << (int)s->fields[f].kind << ',';
     return k.str();
 }
@@ -145,14 +145,12 @@ std::string generate_nested(const spec_nested_schema *s) {
 
 // The generated Write() of internal/lang/generator/message.go:319-439 as constants: fields in
 // write order, the Writer's table order, IsBigMessage forced by a tag > 255.
-std::string generate_encode(const spec_schema *s) {
+void emit_enc_spec(std::ostringstream &o, const char *name, const spec_schema *s) {
     uint8_t order[SPEC_MAX_FIELDS];
     uint16_t sorted[SPEC_MAX_FIELDS];
     writer_order(s, order, sorted);
     bool big = false;
-    std::ostringstream o;
-    o << "#include \"encode_core.hpp\"\n"
-      << "struct GenEnc {\n  static constexpr int N = " << s->nfields << ";\n"
+    o << "struct " << name << " {\n  static constexpr int N = " << s->nfields << ";\n"
       << "  static constexpr uint32_t kind[N] = {";
     for (uint32_t f = 0; f < s->nfields; f++) o << (f ? "," : "") << (int)s->fields[f].kind;
     o << "};\n  static constexpr uint32_t tag[N] = {";
@@ -162,8 +160,38 @@ std::string generate_encode(const spec_schema *s) {
     }
     o << "};\n  static constexpr int order[N] = {";
     for (uint32_t k = 0; k < s->nfields; k++) o << (k ? "," : "") << (int)order[k];
-    o << "};\n  static constexpr bool big_forced = " << (big ? "true" : "false") << ";\n};\n"
-      << "using P = spec::SpecEnc<GenEnc>;\n"
+    o << "};\n  static constexpr bool big_forced = " << (big ? "true" : "false") << ";\n};\n";
+}
+
+// Nested encode: SpecEnc for the outer schema (its list field handled by the nested encoder's
+// hooks) and for the item schema, RuntimeEnc for a side without a specialised encoder.
+bool has_outer_encoder(const spec_schema *s) { return s->nfields > 0 && s->nfields <= ENC_MAX_FIELDS; }
+bool has_nested_encoder(const spec_nested_schema *s) {
+    return has_outer_encoder(&s->outer) || has_encoder(&s->item);
+}
+
+std::string generate_nested_encode(const spec_nested_schema *s) {
+    std::ostringstream o;
+    o << "#include \"encode_nested_core.hpp\"\n";
+    const bool fo = has_outer_encoder(&s->outer), fi = has_encoder(&s->item);
+    if (fo) emit_enc_spec(o, "GenOuter", &s->outer);
+    if (fi) emit_enc_spec(o, "GenItem", &s->item);
+    o << "using OP = " << (fo ? "spec::SpecEnc<GenOuter>" : "spec::RuntimeEnc") << ";\n"
+      << "using IP = " << (fi ? "spec::SpecEnc<GenItem>" : "spec::RuntimeEnc") << ";\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void spec_encode_nested_size_jit(spec::NestedEncodeArgs a) {\n"
+      << "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+      << "  spec::nested_enc_size_body<OP, IP>(a, smem);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void spec_encode_nested_write_jit(spec::NestedEncodeArgs a) {\n"
+      << "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+      << "  spec::nested_enc_write_body<OP, IP>(a, smem);\n}\n";
+    return o.str();
+}
+
+std::string generate_encode(const spec_schema *s) {
+    std::ostringstream o;
+    o << "#include \"encode_core.hpp\"\n";
+    emit_enc_spec(o, "GenEnc", s);
+    o << "using P = spec::SpecEnc<GenEnc>;\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void spec_encode_size_jit(spec::EncodeArgs a) {\n"
       << "  spec::encode_size_body<P>(a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void spec_encode_write_jit(spec::EncodeArgs a) {\n"
@@ -173,15 +201,20 @@ std::string generate_encode(const spec_schema *s) {
 }
 
 const char *prog_name(Prog p) {
-    return p == ENCODE ? "spec_encode_jit.hip" : p == NESTED ? "spec_decode_nested_jit.hip" : "spec_decode_flat_jit.hip";
+    return p == ENCODE       ? "spec_encode_jit.hip"
+           : p == NESTED     ? "spec_decode_nested_jit.hip"
+           : p == NESTED_ENC ? "spec_encode_nested_jit.hip"
+                             : "spec_decode_flat_jit.hip";
 }
 
 // hiprtc compile only; returns the code object (empty on failure)
 std::vector<char> compile_source(const std::string &src, Prog p) {
-    const char *hdr_src[4] = {kSpecDeviceHpp, kDecodeCoreHpp, kEncodeCoreHpp, kDecodeNestedCoreHpp};
-    const char *hdr_name[4] = {"spec_device.hpp", "decode_core.hpp", "encode_core.hpp", "decode_nested_core.hpp"};
+    const char *hdr_src[5] = {kSpecDeviceHpp, kDecodeCoreHpp, kEncodeCoreHpp, kDecodeNestedCoreHpp,
+                              kEncodeNestedCoreHpp};
+    const char *hdr_name[5] = {"spec_device.hpp", "decode_core.hpp", "encode_core.hpp", "decode_nested_core.hpp",
+                               "encode_nested_core.hpp"};
     hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), prog_name(p), 4, hdr_src, hdr_name) != HIPRTC_SUCCESS) return {};
+    if (hiprtcCreateProgram(&prog, src.c_str(), prog_name(p), 5, hdr_src, hdr_name) != HIPRTC_SUCCESS) return {};
     // SPEC_AMD_EXP=n: diagnostic variants of the kernel body (decode_core.hpp), timing only
     static std::string exp = [] {
         const char *e = getenv("SPEC_AMD_EXP");
@@ -224,7 +257,10 @@ std::vector<char> compile_source(const std::string &src, Prog p) {
     hiprtcDestroyProgram(&prog);
     // SPEC_AMD_JIT_DUMP=prefix: write the source and code object (ISA inspection)
     if (const char *d = getenv("SPEC_AMD_JIT_DUMP")) {
-        std::string base = std::string(d) + (p == ENCODE ? "encode" : p == NESTED ? "nested" : "decode");
+        std::string base = std::string(d) + (p == ENCODE       ? "encode"
+                                             : p == NESTED     ? "nested"
+                                             : p == NESTED_ENC ? "nested_encode"
+                                                               : "decode");
         if (FILE *f = fopen((base + ".hip").c_str(), "w")) {
             fwrite(src.data(), 1, src.size(), f);
             fclose(f);
@@ -247,9 +283,10 @@ Entry load(const std::vector<char> &code, Prog p) {
         e.failed = true;
         return e;
     }
-    const char *names[3][2] = {{"spec_decode_flat_jit", nullptr},
+    const char *names[4][2] = {{"spec_decode_flat_jit", nullptr},
                                {"spec_encode_size_jit", "spec_encode_write_jit"},
-                               {"spec_decode_nested_jit", "spec_decode_nested2_jit"}};
+                               {"spec_decode_nested_jit", "spec_decode_nested2_jit"},
+                               {"spec_encode_nested_size_jit", "spec_encode_nested_write_jit"}};
     bool ok = hipModuleLoadData(&e.mod, code.data()) == hipSuccess;
     for (int i = 0; ok && i < 2; i++)
         if (names[p][i]) ok = hipModuleGetFunction(&e.fn[i], e.mod, names[p][i]) == hipSuccess;
@@ -290,6 +327,14 @@ const Entry *lookup_nested(const spec_nested_schema *s) {
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     const std::string k = key_of(&s->outer, dev, NESTED) + "|" + key_of(&s->item, dev, NESTED);
     return lookup_key(k, NESTED, [&] { return compile_source(generate_nested(s), NESTED); });
+}
+
+const Entry *lookup_nested_encode(const spec_nested_schema *s) {
+    if (!enabled() || !has_nested_encoder(s)) return nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    const std::string k = key_of(&s->outer, dev, NESTED_ENC) + "|" + key_of(&s->item, dev, NESTED_ENC) + "|n";
+    return lookup_key(k, NESTED_ENC, [&] { return compile_source(generate_nested_encode(s), NESTED_ENC); });
 }
 
 } // namespace
@@ -355,6 +400,25 @@ int jit_launch_nested(const spec_nested_schema *schema, const NestedArgs &a, boo
     const unsigned groups = (unsigned)((a.n + 63) / 64);
     hipError_t rc = hipModuleLaunchKernel(e->fn[onepass ? 0 : 1], groups, 1, 1, 64, 1, 1, a.slab, stream, nullptr,
                                           extra);
+    return rc == hipSuccess ? 1 : -1;
+}
+
+long long jit_compile_only_nested_encode(const spec_nested_schema *schema) {
+    if (!has_nested_encoder(schema)) return 0;
+    return (long long)compile_source(generate_nested_encode(schema), NESTED_ENC).size();
+}
+
+int jit_launch_nested_encode(const spec_nested_schema *schema, const NestedEncodeArgs &a, bool write,
+                             hipStream_t stream) {
+    const Entry *e = lookup_nested_encode(schema);
+    if (!e) return 0;
+    NestedEncodeArgs args = a;
+    size_t size = sizeof(args);
+    void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
+                     HIP_LAUNCH_PARAM_END};
+    const unsigned lds = (unsigned)(write ? nenc_write_lds_bytes() : nenc_size_lds_bytes());
+    hipError_t rc = hipModuleLaunchKernel(e->fn[write ? 1 : 0], (unsigned)a.nblocks, 1, 1, NENC_BLOCK, 1, 1, lds,
+                                          stream, nullptr, extra);
     return rc == hipSuccess ? 1 : -1;
 }
 

@@ -8,26 +8,18 @@
 #include "../../include/spec_amd.h"
 #include "decode_core.hpp"
 #include "encode_core.hpp"
+#include "encode_nested_core.hpp"
 
 namespace spec {
 
 // encode_nested.hip
-struct NestedEncodeArgs {
-    uint64_t n;
-    EncFields outer; // its K_LIST field is written from item_begin + item
-    EncFields item;
-    const uint32_t *item_begin; // [n + 1]
-    uint64_t nitems;            // item columns hold this many items
-    uint32_t check_heaps;
-    uint8_t *out;
-    uint64_t out_cap;
-    uint64_t *ends;
-    uint64_t *block_sums;
-    uint64_t nblocks;
-    uint64_t *total;
-};
-
-int launch_nested_encode(const NestedEncodeArgs &a, bool write, hipStream_t stream);
+int launch_nested_encode(const spec_nested_schema *schema, const NestedEncodeArgs &a, bool write,
+                         hipStream_t stream);
+// jit.cpp: schema-specialised nested encode pass 1 (write=false) or 3; 1 launched, 0 use the
+// precompiled kernel, <0 HIP error.
+int jit_launch_nested_encode(const spec_nested_schema *schema, const NestedEncodeArgs &a, bool write,
+                             hipStream_t stream);
+long long jit_compile_only_nested_encode(const spec_nested_schema *schema);
 int launch_decode_flat(DecodeArgs a, double avg_record, hipStream_t stream);
 int device_cus(); // CUs of the current device (cached)
 bool persistent_decode(); // SPEC_AMD_PERSIST=1

@@ -86,3 +86,15 @@ def test_encode_jit_source_compiles_for_gfx950():
     assert L.spec_encode_flat_jit_compile(C.byref(odd.c)) > 1000
     many = spec_amd.Schema([(i + 1, spec_amd.Kind.INT64) for i in range(33)])
     assert L.spec_encode_flat_jit_compile(C.byref(many.c)) == 0
+
+
+def test_nested_encode_jit_source_compiles_for_gfx950():
+    """The schema-specialised nested encode kernels (jit.cpp over encode_nested_core.hpp:
+    SpecEnc<outer> with the list hooks, SpecEnc<item>) compile with hiprtc for gfx950."""
+    L = spec_amd.lib()
+    assert L.spec_encode_nested_jit_compile(C.byref(spec_amd.NESTED.c)) > 1000
+    # an item schema too wide for a specialised encoder: outer specialised, items generic
+    wide = spec_amd.NestedSchema(
+        [(1, spec_amd.Kind.INT64), (2, spec_amd.Kind.LIST)],
+        [(i + 1, spec_amd.Kind.INT32) for i in range(40)])
+    assert L.spec_encode_nested_jit_compile(C.byref(wide.c)) > 1000

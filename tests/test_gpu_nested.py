@@ -192,7 +192,7 @@ def nested_device_inputs(w, dev):
 
 
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 5000])
-def test_nested_encode_bitexact(dev, n):
+def test_nested_encode_bitexact(dev, kernel, n):
     import torch
 
     w = workload.nested(n, seed=n + 3)
@@ -204,7 +204,7 @@ def test_nested_encode_bitexact(dev, n):
     assert np.array_equal(out.cpu().numpy(), want)
 
 
-def test_nested_encode_big_lists_and_empty(dev):
+def test_nested_encode_big_lists_and_empty(dev, kernel):
     """Lists of 0 and > 255 items (IsBigList by count), long labels (big items / big lists by
     offset), in one batch."""
     import torch
@@ -256,3 +256,123 @@ def test_nested_roundtrip_full_size(dev):
         assert np.array_equal(got.items[1][:m].cpu().numpy().view(np.uint64).ravel(), w["value"].view(np.uint64))
         assert int(got.item_status[:m].sum()) == 0
         assert np.array_equal(got.outer[1].cpu().numpy().view(np.int64).ravel(), w["seq"])
+
+
+def test_nested_encode_many_items_per_wave(dev, kernel):
+    """Waves owning more than NENC_ITEM_CAP (512) items take the per-lane path; neighbours
+    with fewer items take the item-parallel path — one batch, both paths."""
+    import torch
+
+    n = 640
+    w = workload.nested(n, seed=21, count=(0, 6))
+    counts = np.diff(w["item_begin"]).astype(np.int64)
+    counts[128:192] = 12  # 768 items in the third wave
+    rng = np.random.default_rng(5)
+    m = int(counts.sum())
+    ib = np.zeros(n + 1, np.uint32)
+    np.cumsum(counts, out=ib[1:])
+    lens = rng.integers(0, 12, m).astype(np.uint32)
+    label = np.zeros((m, 2), np.uint32)
+    label[1:, 0] = np.cumsum(lens[:-1])
+    label[:, 1] = lens
+    w.update(item_begin=ib, key=rng.integers(-2**31, 2**31, m).astype(np.int32),
+             value=rng.standard_normal(m), label=label,
+             label_heap=rng.integers(32, 127, int(lens.sum()), dtype=np.uint8))
+    want, want_ends = O.encode_nested_batch(w)
+    oc, oh, ibd, ic, ih = nested_device_inputs(w, dev)
+    out, ends = spec_amd.encode_nested(NESTED, oc, oh, ibd, ic, ih, n)
+    torch.cuda.synchronize()
+    assert np.array_equal(ends.cpu().numpy().view(np.uint64), want_ends)
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+# A schema unlike NESTED: the list is the FIRST outer field (items start right at the record
+# start, so an item's head store lands in the previous record's bytes), item tags > 255 (big
+# item tables) and a repeated item tag (Writer tie order).
+GEN_OUTER = [(7, Kind.LIST), (2, Kind.BYTE), (9, Kind.STRING), (3, Kind.UINT32)]
+GEN_ITEM = [(4, Kind.BOOL), (1, Kind.UINT16), (300, Kind.BIN64), (2, Kind.BYTES), (1, Kind.INT16)]
+
+
+def _spans(rng, lens):
+    sp = np.zeros((len(lens), 2), np.uint32)
+    if len(lens):
+        sp[1:, 0] = np.cumsum(lens[:-1])
+    sp[:, 1] = lens
+    return sp, rng.integers(32, 127, int(np.sum(lens)), dtype=np.uint8)
+
+
+def _writer_encode_generic(c):
+    """The oracle Writer, record by record, for GEN_OUTER/GEN_ITEM (pure Python loop)."""
+    recs = []
+    ib = c["item_begin"]
+    for r in range(len(c["byte"])):
+        wr = O.Writer()
+        wr.message()
+        wr.field_list(7)
+        for i in range(int(ib[r]), int(ib[r + 1])):
+            wr.elem_message()
+            wr.field(4, "bool", int(c["bool"][i]))
+            wr.field(1, "uint16", int(c["u16"][i]))
+            wr.field(300, "bin64", c["bin"][i].tobytes())
+            o, ln = c["bytes"][i]
+            wr.field(2, "bytes", c["bytes_heap"][o:o + ln].tobytes())
+            wr.field(1, "int16", int(c["i16"][i]))
+            assert wr.end()[1] is None
+        assert wr.end()[1] is None
+        wr.field(2, "byte", int(c["byte"][r]))
+        o, ln = c["str"][r]
+        wr.field(9, "string", c["str_heap"][o:o + ln].tobytes())
+        wr.field(3, "uint32", int(c["u32"][r]))
+        b, err = wr.end()
+        assert err is None, err
+        recs.append(b)
+        wr.close()
+    return concat_records(recs)
+
+
+def test_nested_encode_generic_schema(dev, kernel):
+    import torch
+
+    schema = spec_amd.NestedSchema(GEN_OUTER, GEN_ITEM)
+    rng = np.random.default_rng(77)
+    n = 700
+    counts = rng.integers(0, 7, n)
+    counts[200:264] = 10        # a wave over the item cap (per-lane path)
+    counts[3] = 300             # a big list by count
+    slen = rng.integers(0, 30, n).astype(np.uint32)
+    slen[500] = 20000           # a wave whose output does not fit the LDS slab
+    ib = np.zeros(n + 1, np.uint32)
+    np.cumsum(counts, out=ib[1:])
+    m = int(ib[-1])
+    blen = rng.integers(0, 9, m).astype(np.uint32)
+    c = {"item_begin": ib, "byte": rng.integers(0, 256, n, dtype=np.uint8),
+         "u32": rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) >> rng.integers(0, 32, n).astype(np.uint32),
+         "bool": rng.integers(0, 2, m, dtype=np.uint8), "u16": rng.integers(0, 2**16, m).astype(np.uint16),
+         "bin": rng.integers(0, 256, (m, 8), dtype=np.uint8),
+         "i16": rng.integers(-2**15, 2**15, m).astype(np.int16)}
+    c["str"], c["str_heap"] = _spans(rng, slen)
+    c["bytes"], c["bytes_heap"] = _spans(rng, blen)
+    want, want_ends = _writer_encode_generic(c)
+    outer = [None, to_dev(c["byte"], dev), to_dev(c["str"], dev), to_dev(c["u32"], dev)]
+    items = [to_dev(c["bool"], dev), to_dev(c["u16"], dev), to_dev(c["bin"], dev), to_dev(c["bytes"], dev),
+             to_dev(c["i16"], dev)]
+    out, ends = spec_amd.encode_nested(schema, outer, {2: to_dev(c["str_heap"], dev)}, to_dev(ib.view(np.int32), dev),
+                                       items, {3: to_dev(c["bytes_heap"], dev)}, n)
+    torch.cuda.synchronize()
+    assert np.array_equal(ends.cpu().numpy().view(np.uint64), want_ends)
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+def test_nested_encode_errors(dev, kernel):
+    """An item string outside its heap or a non-monotonic item_begin is an encoder error."""
+    n = 300
+    w = workload.nested(n, seed=4)
+    oc, oh, ib, ic, ih = nested_device_inputs(w, dev)
+    bad = w["label"].copy()
+    bad[len(bad) // 2, 1] = 1 << 20
+    with pytest.raises(spec_amd.SpecError):
+        spec_amd.encode_nested(NESTED, oc, oh, ib, [ic[0], ic[1], to_dev(bad, dev)], ih, n)
+    ib2 = w["item_begin"].copy()
+    ib2[100] = ib2[102] + 1
+    with pytest.raises(spec_amd.SpecError):
+        spec_amd.encode_nested(NESTED, oc, oh, to_dev(ib2.view(np.int32), dev), ic, ih, n)
