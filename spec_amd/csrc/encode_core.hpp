@@ -311,6 +311,33 @@ struct Emit {
         acc = keep ? (last & (0xffffffffu >> (32 - 8 * keep))) : 0u;
         pos += n;
     }
+    // put_heap64 for n <= 4 * (M - 1) bytes (short strings): M output dwords from h[0..M].
+    template <int M, class H>
+    __device__ __forceinline__ void put_heap_short(const H &h, uint32_t off, uint32_t n) {
+        static_assert(HEAD_ST4 && M <= 8, "put_heap_short: whole-record emitters, <= 28 bytes");
+        const uint32_t ph = (uint32_t)(pos & 3);
+        const Pos d0 = pos & ~(Pos)3;
+        const uint32_t s = (off & 3) + 4 - ph;
+        const bool hi = s >= 4;
+        const uint32_t b = s & 3;
+        const uint32_t total = ph + n, full = total >> 2;
+        uint32_t v[M];
+#pragma unroll
+        for (int m = 0; m < M; m++) {
+            const uint32_t g0 = m == 0 ? 0u : h[m - 1], g1 = h[m], g2 = h[m + 1];
+            v[m] = hi ? __builtin_amdgcn_alignbyte(g2, g1, b) : __builtin_amdgcn_alignbyte(g1, g0, b);
+        }
+        v[0] = (v[0] & (0xffffffffu << (8 * ph))) | acc;
+        uint32_t last = v[0];
+#pragma unroll
+        for (int m = 0; m < M; m++) {
+            k.st4a_if((uint32_t)m < full, d0 + 4 * m, v[m]);
+            if (m) last = full == (uint32_t)m ? v[m] : last;
+        }
+        const uint32_t keep = total & 3;
+        acc = keep ? (last & (0xffffffffu >> (32 - 8 * keep))) : 0u;
+        pos += n;
+    }
     // reverse varint (oracle/compactint.c so_put_reverse_*): top group first, MSB clear;
     // following groups carry 0x80; the least-significant group is the last byte.  Up to 8
     // bytes (values < 2^56) are built in a register and appended at once.
@@ -563,13 +590,27 @@ struct SpecEnc {
             if constexpr (heap_kind<F>()) {
                 const __amdgpu_buffer_rsrc_t hr = heap_rsrc(f, F);
                 const uint32_t off = (uint32_t)x.v[F][0] & ~3u;
+                // the first 32 bytes always (short strings need no more), the rest only
+                // for lanes whose string runs past them
 #pragma unroll
-                for (int q = 0; q < 5; q++) {
+                for (int q = 0; q < 2; q++) {
                     const uint4 w = heap_ld128(hr, off + 16 * q, f.heap_lens[F]);
                     x.h[F][4 * q] = w.x;
                     x.h[F][4 * q + 1] = w.y;
                     x.h[F][4 * q + 2] = w.z;
                     x.h[F][4 * q + 3] = w.w;
+                }
+#pragma unroll
+                for (int q = 8; q < 20; q++) x.h[F][q] = 0;
+                if (((uint32_t)x.v[F][0] & 3u) + (uint32_t)(x.v[F][0] >> 32) > 32) {
+#pragma unroll
+                    for (int q = 2; q < 5; q++) {
+                        const uint4 w = heap_ld128(hr, off + 16 * q, f.heap_lens[F]);
+                        x.h[F][4 * q] = w.x;
+                        x.h[F][4 * q + 1] = w.y;
+                        x.h[F][4 * q + 2] = w.z;
+                        x.h[F][4 * q + 3] = w.w;
+                    }
                 }
             }
             load_heap<F + 1>(f, x);
@@ -675,7 +716,8 @@ struct SpecEnc {
                 const uint32_t off = (uint32_t)v, len = (uint32_t)(v >> 32), sh = off & 3;
                 const uint32_t n = len < 64 ? len : 64;
                 if constexpr (E::kHeadSt4) {
-                    em.put_heap64(x.h[F], off, n);
+                    if (__ballot(n > 16) == 0) em.template put_heap_short<5>(x.h[F], off, n); // wave-uniform
+                    else em.put_heap64(x.h[F], off, n);
                 } else {
 #pragma unroll
                     for (int j = 0; j < 16; j++) {

@@ -176,21 +176,30 @@ __device__ __forceinline__ bool wave_item_prefix(const NestedEncodeArgs &a, uint
                                                  uint32_t *pre, int lane, bool check, bool &err) {
     uint64_t carry = 0;
     if (lane == 0) pre[0] = 0;
-    for (uint32_t c = 0; c < cnt; c += 64) {
-        const uint32_t k = c + lane;
-        const bool iv = k < cnt;
-        const uint64_t i = I0 + (iv ? k : 0);
-        const typename IP::Rec rec = IP::load(a.item, i);
-        bool e = false;
-        const uint64_t s = iv ? IP::size(a.item, rec, i, check, e).total : 0;
-        err |= iv & e;
-        uint64_t x = s;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint64_t y = __shfl_up(x, o);
-            if (lane >= o) x += y;
+    // groups of 4 chunks (256 items): every load of the group in flight before the first
+    // size is needed; lanes past the end re-read the last item
+    for (uint32_t c0 = 0; c0 < cnt; c0 += 256) {
+        typename IP::Rec rec[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t k = c0 + 64 * j + lane;
+            rec[j] = IP::load(a.item, I0 + (k < cnt ? k : cnt - 1));
         }
-        if (iv) pre[k + 1] = (uint32_t)(carry + x);
-        carry += __shfl(x, 63);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t k = c0 + 64 * j + lane;
+            const bool iv = k < cnt;
+            bool e = false;
+            const uint64_t s = IP::size(a.item, rec[j], I0 + (iv ? k : cnt - 1), check, e).total;
+            err |= iv & e;
+            uint64_t x = iv ? s : 0;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint64_t y = __shfl_up(x, o);
+                if (lane >= o) x += y;
+            }
+            if (iv) pre[k + 1] = (uint32_t)(carry + x);
+            carry += __shfl(x, 63);
+        }
     }
     return carry <= MAX_SIZE;
 }
@@ -321,9 +330,17 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
     const bool fix = L.valid && ls.count > 0 && (lst & 3);
     const uint32_t saved = fix ? *(const uint32_t *)(slab + (lst & ~3)) : 0u;
     wave_sync();
-    // B: items, last chunk first
+    // B: items, last chunk first; the next chunk's loads issued before this chunk is emitted
     const int lbase = lst - (int)pre[L.b - L.I0];
-    for (int c = ((int)L.cnt - 1) & ~63; c >= 0; c -= 64) {
+    int c = ((int)L.cnt - 1) & ~63;
+    typename IP::Rec cur;
+    if (c >= 0) {
+        const uint32_t kk = (uint32_t)c + lane;
+        cur = IP::load(a.item, L.I0 + (kk < L.cnt ? kk : L.cnt - 1));
+    }
+    for (; c >= 0; c -= 64) {
+        typename IP::Rec nxt;
+        if (c >= 64) nxt = IP::load(a.item, L.I0 + (uint32_t)(c - 64) + lane);
         const uint32_t kk = (uint32_t)c + lane;
         const bool iv = kk < L.cnt;
         const uint32_t i = L.I0 + (iv ? kk : 0u);
@@ -332,12 +349,12 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
             if (__shfl(L.b, o + st) <= i) o += st;
         const int pos = __shfl(lbase, o) + (int)pre[iv ? kk : 0u];
         if (iv) {
-            const typename IP::Rec rec = IP::load(a.item, i);
             bool e2 = false;
-            const RecSize irs = IP::size(a.item, rec, i, false, e2);
-            IP::emit(a.item, k, pos, i, rec, irs, inv_item);
+            const RecSize irs = IP::size(a.item, cur, i, false, e2);
+            IP::emit(a.item, k, pos, i, cur, irs, inv_item);
         }
         wave_sync();
+        cur = nxt;
     }
     // C: the bytes under the list start that the first item's head store overwrote
     if (fix) {
