@@ -20,44 +20,43 @@ namespace {
 
 __global__ __launch_bounds__(256) void nested_count_kernel(NestedArgs a) { nested_count_body(a); }
 
-// Exclusive scan of the group totals + total items: one 1024-thread workgroup, tiles of
-// 16 consecutive totals per thread (thread sums -> wave scans -> wave totals in LDS).
+// Exclusive scan of the group totals + total items: one 1024-thread workgroup.  Tiles of
+// 16 rows of 1024 totals, every load of a tile issued at once and coalesced (row i, thread t
+// -> element i * 1024 + t); each row is one block scan (wave scans + wave totals in LDS).
 __global__ __launch_bounds__(1024) void nested_scan_kernel(NestedArgs a) {
-    constexpr int PER = 16;
-    __shared__ uint64_t wsum[1024 / 64];
+    constexpr int ROWS = 16;
+    __shared__ uint64_t wsum[2][1024 / 64];
     const uint64_t ngroups = (a.n + 63) / 64;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     uint64_t carry = 0;
-    for (uint64_t tile = 0; tile < ngroups; tile += 1024 * PER) {
-        const uint64_t b = tile + (uint64_t)t * PER;
-        uint64_t v[PER], sum = 0;
+    for (uint64_t tile = 0; tile < ngroups; tile += 1024 * ROWS) {
+        uint64_t v[ROWS];
 #pragma unroll
-        for (int i = 0; i < PER; i++) {
-            v[i] = b + i < ngroups ? a.group_base[b + i] : 0;
-            sum += v[i];
+        for (int i = 0; i < ROWS; i++) {
+            const uint64_t k = tile + (uint64_t)i * 1024 + t;
+            v[i] = k < ngroups ? a.group_base[k] : 0;
         }
-        uint64_t x = sum; // inclusive wave scan of the thread sums
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t y = __shfl_up(x, d);
-            if (lane >= d) x += y;
-        }
-        if (lane == 63) wsum[w] = x;
-        __syncthreads();
-        uint64_t before = 0, tile_total = 0;
+        for (int i = 0; i < ROWS; i++) {
+            uint64_t x = v[i]; // inclusive wave scan
 #pragma unroll
-        for (int k = 0; k < 1024 / 64; k++) {
-            before += k < w ? wsum[k] : 0;
-            tile_total += wsum[k];
-        }
-        uint64_t run = carry + before + x - sum;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint64_t y = __shfl_up(x, d);
+                if (lane >= d) x += y;
+            }
+            if (lane == 63) wsum[i & 1][w] = x;
+            __syncthreads(); // (double-buffered wave totals: one barrier per row)
+            uint64_t before = 0, row_total = 0;
 #pragma unroll
-        for (int i = 0; i < PER; i++) {
-            if (b + i < ngroups) a.group_base[b + i] = run;
-            run += v[i];
+            for (int k = 0; k < 1024 / 64; k++) {
+                const uint64_t s = wsum[i & 1][k];
+                before += k < w ? s : 0;
+                row_total += s;
+            }
+            const uint64_t k = tile + (uint64_t)i * 1024 + t;
+            if (k < ngroups) a.group_base[k] = carry + before + x - v[i];
+            carry += row_total;
         }
-        carry += tile_total;
-        __syncthreads();
     }
     if (t == 0) *a.total = carry;
 }

@@ -364,13 +364,17 @@ def test_decode_range_and_host_pipeline(dev):
     assert np.array_equal(st.cpu().numpy(), wst)
     for f in range(16):
         assert np.array_equal(out[f].cpu().numpy(), want[f]), f
-    hd = spec_amd.HostDecoder(FLAT16, n, stream.size, dev, chunks=5)
     h_stream = torch.from_numpy(stream).pin_memory()
     h_ends = torch.from_numpy(ends.view(np.int64)).pin_memory()
-    hcols, hst = hd.decode(h_stream, h_ends)
-    assert np.array_equal(hst.numpy()[:n], wst)
-    for f in range(16):
-        assert np.array_equal(hcols[f].numpy()[:n], want[f]), f
+    for chunks in (5, 16):
+        hd = spec_amd.HostDecoder(FLAT16, n, stream.size, dev, chunks=chunks)
+        hd.decode(h_stream, h_ends)
+        hcols, hst = hd.columns()
+        assert np.array_equal(hst.numpy(), wst), chunks
+        for f in range(16):
+            assert np.array_equal(hcols[f].numpy(), want[f]), (chunks, f)
+        r0, r1, c3, s3 = hd.chunk(3)
+        assert np.array_equal(c3[13].numpy(), want[13][r0:r1]) and np.array_equal(s3.numpy(), wst[r0:r1])
 
 
 def test_decode_frames_in_place(dev, kernel):
