@@ -256,7 +256,7 @@ def gather_leg(dec, dist, rank, world, n, steps):
             "note": "decode + RCCL gather of all columns to rank 0, per step"}
 
 
-def e2e_decode(stream_host, ends_host, dev, reps=5, chunks=16):
+def e2e_decode(stream_host, ends_host, dev, reps=5, chunks=8):
     """Pinned host -> H2D -> decode -> D2H of all columns + status, pipelined in record chunks
     over three streams (spec_amd.HostDecoder); whole-pipeline rate (Mmsg/s)."""
     n = ends_host.numel()

@@ -163,6 +163,26 @@ int spec_decode_frames(const spec_schema *schema, const uint8_t *frames, uint64_
                        const uint64_t *ends, uint64_t r0, uint64_t r1, uint64_t range_bytes, void *const *columns,
                        uint8_t *status, void *stream);
 
+/* ---- host pipeline (the path starts and ends in HOST memory: mpx connection buffers) ----
+ * spec_host_decoder decodes a batch held in pinned host memory (spec_host_alloc) into a pinned
+ * host output buffer, overlapping on three HIP streams the H2D copy of chunk k+1, the decode
+ * of chunk k (spec_decode_flat_range) and the D2H copy of chunk k-1 — the receive loop of
+ * mpx/conn_reader.go:179-194 followed by the per-record OpenMessageErr + getters, batched.
+ * Outputs are CHUNK-MAJOR: chunk k (records [r0, r1) = [n*k/chunks, n*(k+1)/chunks)) is one
+ * region of out_host — its records' column 0, column 1, ..., then their status bytes — so
+ * each chunk leaves the device in one copy; spec_host_decoder_chunk gives the offsets.
+ * Device buffers and streams are created once (n_cap records, stream_cap bytes);
+ * spec_host_decoder_run is synchronous (returns when out_host is complete). */
+typedef struct spec_host_decoder spec_host_decoder;
+int spec_host_decoder_create(const spec_schema *schema, uint64_t n_cap, uint64_t stream_cap, uint32_t chunks,
+                             spec_host_decoder **out);
+void spec_host_decoder_destroy(spec_host_decoder *d);
+uint64_t spec_host_decoder_out_bytes(const spec_host_decoder *d, uint64_t n);
+int spec_host_decoder_chunk(const spec_host_decoder *d, uint64_t n, uint32_t k, uint64_t *r0, uint64_t *r1,
+                            uint64_t *col_offsets, uint64_t *status_offset);
+int spec_host_decoder_run(spec_host_decoder *d, const uint8_t *stream_host, uint64_t stream_len,
+                          const uint64_t *ends_host, uint64_t n, uint8_t *out_host);
+
 /* ---- recursive validation ----
  * spec_parse_messages: for every record, spec.ParseMessage (msg.go:29-32 ->
  * internal/types/msg.go:58-82): the message table, then ParseValue on every non-empty field,

@@ -102,6 +102,14 @@ def _declare(L):
     L.spec_encode_flat.argtypes = [C.POINTER(SpecSchema), C.POINTER(vp), C.POINTER(vp),
                                    C.POINTER(C.c_uint64), C.c_uint64, vp, C.c_uint64, vp, vp,
                                    C.c_size_t, vp, vp]
+    L.spec_host_decoder_create.argtypes = [C.POINTER(SpecSchema), C.c_uint64, C.c_uint64, C.c_uint32, C.POINTER(vp)]
+    L.spec_host_decoder_destroy.argtypes = [vp]
+    L.spec_host_decoder_destroy.restype = None
+    L.spec_host_decoder_out_bytes.argtypes = [vp, C.c_uint64]
+    L.spec_host_decoder_out_bytes.restype = C.c_uint64
+    L.spec_host_decoder_chunk.argtypes = [vp, C.c_uint64, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                          C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    L.spec_host_decoder_run.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, vp]
 
 
 def strerror(rc: int) -> str:

@@ -96,6 +96,31 @@ int main(void) {
             return 3;
         }
 
+    /* the host pipeline (pinned host in, pinned host out, chunk-major outputs) */
+    spec_host_decoder *hd = NULL;
+    CHECK(spec_host_decoder_create(&s, n, total, 7, &hd));
+    void *h_out;
+    const uint64_t out_bytes = spec_host_decoder_out_bytes(hd, n);
+    CHECK(spec_host_alloc(out_bytes, &h_out));
+    CHECK(spec_host_decoder_run(hd, h_stream, total, h_ends, n, h_out));
+    for (uint32_t k = 0; k < 7; k++) {
+        uint64_t r0, r1, offs[5], soff;
+        CHECK(spec_host_decoder_chunk(hd, n, k, &r0, &r1, offs, &soff));
+        if (memcmp((uint8_t *)h_out + soff, wst + r0, r1 - r0)) {
+            fprintf(stderr, "host pipeline status mismatch (chunk %u)\n", k);
+            return 5;
+        }
+        for (int f = 0; f < 5; f++) {
+            const uint64_t w = (uint64_t)spec_kind_width(kinds[f]);
+            if (memcmp((uint8_t *)h_out + offs[f], want[f] + r0 * w, (r1 - r0) * w)) {
+                fprintf(stderr, "host pipeline column %d mismatch (chunk %u)\n", f, k);
+                return 5;
+            }
+        }
+    }
+    spec_host_decoder_destroy(hd);
+    CHECK(spec_host_free(h_out));
+
     /* encode on the device from the input columns: bytes must equal the oracle Writer's */
     void *d_in[5], *d_heap, *d_out, *d_ends2, *d_ws, *d_total;
     for (int f = 0; f < 5; f++) {

@@ -16,7 +16,7 @@ def main():
     _, _, _, _, stream, ends = bench.make_batch(n, 0x5EC0DE, dev)
     sh, eh = stream.cpu().pin_memory(), ends.cpu().pin_memory()
     res = {}
-    for chunks in (8, 16, 32, 64):
+    for chunks in (4, 6, 8, 12, 16):
         rate, dt, _ = bench.e2e_decode(sh, eh, dev, reps=5, chunks=chunks)
         res[chunks] = {"mmsg_s": round(rate, 1), "ms": round(dt * 1e3, 3)}
     print(json.dumps(res))
