@@ -21,42 +21,63 @@ namespace {
 __global__ __launch_bounds__(256) void nested_count_kernel(NestedArgs a) { nested_count_body(a); }
 
 // Exclusive scan of the group totals + total items: one 1024-thread workgroup.  Tiles of
-// 16 rows of 1024 totals, every load of a tile issued at once and coalesced (row i, thread t
-// -> element i * 1024 + t); each row is one block scan (wave scans + wave totals in LDS).
+// 16 x 1024 totals: loaded coalesced (all 16 loads in flight) into LDS as u32 (item counts of
+// 64 records), each thread then scans 16 CONSECUTIVE totals serially, one block scan of the
+// thread sums, results back through LDS, coalesced stores.  (A block scan per 1024 totals
+// costs ~1 us of barriers and shuffles on the one CU; this does one per tile.)
 __global__ __launch_bounds__(1024) void nested_scan_kernel(NestedArgs a) {
-    constexpr int ROWS = 16;
-    __shared__ uint64_t wsum[2][1024 / 64];
+    constexpr int PER = 16, TILE = 1024 * PER;
+    __shared__ uint32_t tv[TILE + TILE / 32]; // +1 pad word per 32: thread-contiguous reads spread banks
+    __shared__ uint64_t wsum[1024 / 64];
     const uint64_t ngroups = (a.n + 63) / 64;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    auto at = [](int k) { return k + (k >> 5); };
     uint64_t carry = 0;
-    for (uint64_t tile = 0; tile < ngroups; tile += 1024 * ROWS) {
-        uint64_t v[ROWS];
+    for (uint64_t tile = 0; tile < ngroups; tile += TILE) {
+        uint64_t v[PER];
 #pragma unroll
-        for (int i = 0; i < ROWS; i++) {
+        for (int i = 0; i < PER; i++) {
             const uint64_t k = tile + (uint64_t)i * 1024 + t;
             v[i] = k < ngroups ? a.group_base[k] : 0;
         }
 #pragma unroll
-        for (int i = 0; i < ROWS; i++) {
-            uint64_t x = v[i]; // inclusive wave scan
+        for (int i = 0; i < PER; i++) tv[at(i * 1024 + t)] = (uint32_t)v[i];
+        __syncthreads();
+        uint32_t mine[PER], sum = 0;
 #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint64_t y = __shfl_up(x, d);
-                if (lane >= d) x += y;
-            }
-            if (lane == 63) wsum[i & 1][w] = x;
-            __syncthreads(); // (double-buffered wave totals: one barrier per row)
-            uint64_t before = 0, row_total = 0;
-#pragma unroll
-            for (int k = 0; k < 1024 / 64; k++) {
-                const uint64_t s = wsum[i & 1][k];
-                before += k < w ? s : 0;
-                row_total += s;
-            }
-            const uint64_t k = tile + (uint64_t)i * 1024 + t;
-            if (k < ngroups) a.group_base[k] = carry + before + x - v[i];
-            carry += row_total;
+        for (int i = 0; i < PER; i++) {
+            mine[i] = tv[at(t * PER + i)];
+            sum += mine[i];
         }
+        uint64_t x = sum; // inclusive wave scan of the thread sums
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(x, d);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        uint64_t before = 0, tile_total = 0;
+#pragma unroll
+        for (int k = 0; k < 1024 / 64; k++) {
+            before += k < w ? wsum[k] : 0;
+            tile_total += wsum[k];
+        }
+        // exclusive offsets within the tile fit 32 bits (item_begin is uint32)
+        uint32_t run = (uint32_t)(before + x - sum);
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            tv[at(t * PER + i)] = run;
+            run += mine[i];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            const uint64_t k = tile + (uint64_t)i * 1024 + t;
+            if (k < ngroups) a.group_base[k] = carry + tv[at(i * 1024 + t)];
+        }
+        carry += tile_total;
+        __syncthreads();
     }
     if (t == 0) *a.total = carry;
 }

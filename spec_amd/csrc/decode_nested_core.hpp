@@ -184,30 +184,47 @@ __device__ __forceinline__ void decode_item(const Src &s, const ListInfo &li, ui
 }
 
 // The group's items, item-parallel: item j of the group (j = excl[owner] + i) on lane j % 64.
+// owner of group item j: the largest lane whose exclusive prefix is <= j (it has count > 0);
+// i = j's index in the owner's list
+__device__ __forceinline__ ListInfo item_owner(const ListInfo &li, uint32_t excl, uint32_t j, uint32_t &i) {
+    int l = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1) {
+        const uint32_t ex = __shfl(excl, l + step < 64 ? l + step : 63);
+        if (l + step < 64 && ex <= j) l += step;
+    }
+    ListInfo own;
+    i = j - __shfl(excl, l);
+    own.dstart = __shfl(li.dstart, l);
+    own.tstart = __shfl(li.tstart, l);
+    own.dsize = __shfl(li.dsize, l);
+    own.big = __shfl((int)li.big, l) != 0;
+    own.count = 0;
+    return own;
+}
+
+// The group's items, item-parallel: item j of the group (j = excl[owner] + i) on lane j % 64.
+// Two chunks of 64 items per iteration (NESTED_ITEM_U = 2): their owner searches and LDS
+// reads are independent, so each wave keeps twice the LDS traffic in flight.
+#ifndef NESTED_ITEM_U
+#define NESTED_ITEM_U 2
+#endif
 template <class ISpec, class Src>
 __device__ __forceinline__ void decode_group_items(const Src &s, const ListInfo &li, uint32_t excl, uint32_t total,
                                                    uint64_t item_base, int lane, long long to_stream,
                                                    const NestedArgs &a) {
-    for (uint32_t j0 = 0; j0 < total; j0 += 64) {
-        const uint32_t j = j0 + lane;
-        // owner: the largest lane whose exclusive prefix is <= j (it has count > 0)
-        int l = 0;
+    constexpr int U = NESTED_ITEM_U;
+    for (uint32_t j0 = 0; j0 < total; j0 += 64 * U) {
+        ListInfo own[U];
+        uint32_t idx[U];
 #pragma unroll
-        for (int step = 32; step >= 1; step >>= 1) {
-            const uint32_t ex = __shfl(excl, l + step < 64 ? l + step : 63);
-            if (l + step < 64 && ex <= j) l += step;
+        for (int u = 0; u < U; u++) own[u] = item_owner(li, excl, j0 + 64 * u + lane, idx[u]);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t j = j0 + 64 * u + lane;
+            const uint64_t out = item_base + j;
+            if (j < total && out < a.item_cap) decode_item<ISpec>(s, own[u], idx[u], out, to_stream, a);
         }
-        ListInfo own;
-        const uint32_t i = j - __shfl(excl, l);
-        own.dstart = __shfl(li.dstart, l);
-        own.tstart = __shfl(li.tstart, l);
-        own.dsize = __shfl(li.dsize, l);
-        own.big = __shfl((int)li.big, l) != 0;
-        own.count = 0;
-        if (j >= total) continue;
-        const uint64_t out = item_base + j;
-        if (out >= a.item_cap) continue;
-        decode_item<ISpec>(s, own, i, out, to_stream, a);
     }
 }
 
@@ -263,7 +280,11 @@ __device__ __forceinline__ void nested_group_body(const Src &s, long long rs, lo
                                                   uint64_t g, uint64_t item_base, int lane, long long to_stream,
                                                   const NestedArgs &a) {
     ListInfo li = {0, 0, 0, 0, false};
+#if defined(SPEC_EXP) && (SPEC_EXP == 8 || SPEC_EXP == 9) // diagnostic (timing only): lists, no outer columns
+    if (valid) li = list_open(s, rec_open(s, (typename Src::pos_t)rs, (typename Src::pos_t)re), a);
+#else
     if (valid) li = decode_outer<OSpec>(s, rs, re, r, to_stream, a);
+#endif
     const uint32_t incl = wave_incl_scan(li.count, lane);
     const uint32_t excl = incl - li.count;
     const uint32_t total = __shfl(incl, 63);
@@ -279,6 +300,9 @@ __device__ __forceinline__ void nested_group_body(const Src &s, long long rs, lo
         a.item_begin[r] = (uint32_t)(item_base + excl);
         if (r == a.n - 1) a.item_begin[a.n] = (uint32_t)(item_base + incl);
     }
+#if defined(SPEC_EXP) && (SPEC_EXP == 7 || SPEC_EXP == 9) // diagnostic (timing only): no items
+    return;
+#endif
     decode_group_items<ISpec>(s, li, excl, total, item_base, lane, to_stream, a);
 }
 
