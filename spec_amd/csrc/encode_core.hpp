@@ -311,10 +311,11 @@ struct Emit {
         acc = keep ? (last & (0xffffffffu >> (32 - 8 * keep))) : 0u;
         pos += n;
     }
-    // put_heap64 for n <= 4 * (M - 1) bytes (short strings): M output dwords from h[0..M].
+    // put_heap64 for n <= 4 * (M - 1) bytes (short strings, or a run of bytes built in
+    // registers with off = 0): M output dwords from h[0..M].
     template <int M, class H>
     __device__ __forceinline__ void put_heap_short(const H &h, uint32_t off, uint32_t n) {
-        static_assert(HEAD_ST4 && M <= 8, "put_heap_short: whole-record emitters, <= 28 bytes");
+        static_assert(HEAD_ST4 && M <= 18, "put_heap_short: whole-record emitters, <= 68 bytes");
         const uint32_t ph = (uint32_t)(pos & 3);
         const Pos d0 = pos & ~(Pos)3;
         const uint32_t s = (off & 3) + 4 - ph;
@@ -755,6 +756,41 @@ struct SpecEnc {
 
     // The record as one sequential byte run: values in write order, the table entries in
     // table order (their ends kept in registers), the trailer.
+    // Small table + trailer as ONE run of bytes built in registers (every entry's byte position
+    // is a compile-time constant), appended with one phase-shifted store per dword:
+    //   table {u8 tag, u16 BE end} x N | rvarint(dataSize) (<= 3 bytes: data <= 65535) |
+    //   rvarint(3N) (1 byte: 3N < 128) | TypeMessage          (internal/encode/msg.go:27-77)
+    static constexpr int TB = 3 * N;
+    static constexpr int RUN_M = (TB + 5 + 3) / 4 + 1; // output dwords covering the run at any phase
+    template <class E>
+    static __device__ __forceinline__ void emit_small_table_trailer(E &em, const Rec &x, uint32_t data) {
+        uint32_t w[RUN_M + 1];
+#pragma unroll
+        for (int i = 0; i <= RUN_M; i++) w[i] = 0;
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            const int f = Spec::order[j];
+            const uint32_t ent = Spec::tag[f] | ((uint32_t)__builtin_bswap16((uint16_t)x.end[f]) << 8);
+            const int b = 3 * j, d = b >> 2, s = 8 * (b & 3);
+            w[d] |= ent << s;
+            if (s > 8) w[d + 1] |= ent >> (32 - s);
+        }
+        // trailer bytes: the reverse varint of data (top group first, continuation bits on all
+        // but the first), then 3N, then the type
+        const uint32_t L = vlen32(data);
+        uint64_t v = data & 0x1fffff; // 3 groups of 7 bits -> bytes (inverse of rvarint_bf)
+        v = (v & 0x7f) | ((v & 0x3f80) << 1) | ((v & 0x1fc000) << 2);
+        const uint64_t be = (__builtin_bswap32((uint32_t)v) >> 8) >> (8 * (3 - L)); // byte i = group L-1-i
+        const uint64_t cont = (0x808080ull >> (8 * (3 - L))) & ~0xffull;
+        const uint64_t T = (be | cont) | ((uint64_t)TB << (8 * L)) | ((uint64_t)T_MESSAGE << (8 * (L + 1)));
+        {
+            constexpr int d = TB >> 2, s = 8 * (TB & 3);
+            w[d] |= (uint32_t)(T << s);
+            w[d + 1] |= (uint32_t)((T << s) >> 32);
+        }
+        em.template put_heap_short<RUN_M>(w, 0u, (uint32_t)TB + L + 2);
+    }
+
     // With a list field the emitter jumps over the list's items (written by other lanes), so it
     // must never store below its position: no HEAD_ST4 then.
     template <class Sink, class Pos, class Lists = NoListEmit>
@@ -764,6 +800,13 @@ struct SpecEnc {
         Rec x = rec;
         Emit<Sink, Pos, Sink::kHeadSt4 && !kHasList> em(k, start);
         emit_values<0>(f, em, x, start, r, lists);
+        if constexpr (Sink::kHeadSt4 && !kHasList && !Spec::big_forced && RUN_M <= 18) {
+            if (__ballot(rs.big) == 0) { // wave-uniform: every record of the wave has a small table
+                emit_small_table_trailer(em, x, (uint32_t)rs.data);
+                em.finish();
+                return;
+            }
+        }
         emit_table<0>(em, x, rs.big);
         // trailer: rvarint(dataSize) | rvarint(tableSize) | type (internal/encode/msg.go:36-39)
         em.rvarint((uint32_t)rs.data);
