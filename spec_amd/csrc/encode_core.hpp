@@ -125,43 +125,74 @@ __device__ __forceinline__ RecSize record_size(const EncFields &a, uint64_t r, b
 // ---- pass 2: exclusive scan of block sums (one workgroup), total ----------------------
 
 // One 1024-thread workgroup: block_sums[0..nblocks) -> exclusive offsets, block_sums[nblocks]
-// and *total = the total (all-ones if any block reported an encoder error).
+// and *total = the total (all-ones if any block reported an encoder error).  Tiles of 8 x 1024
+// sums: loaded coalesced (all loads in flight) into LDS, each thread scans 8 CONSECUTIVE sums
+// serially, one block scan of the thread sums per tile (a block scan costs ~1 us of barriers
+// and shuffles on the one CU), results back through LDS, coalesced stores.
 __device__ __forceinline__ void scan_block_sums(uint64_t *block_sums, uint64_t nblocks, uint64_t *total) {
+    constexpr int PER = 8, TILE = 1024 * PER;
+    __shared__ uint64_t tv[TILE + TILE / 16]; // +1 pad per 16: thread-contiguous reads spread banks
     __shared__ uint64_t wsum[16];
-    __shared__ uint64_t carry_s;
     __shared__ int err_s;
-    if (threadIdx.x == 0) {
-        carry_s = 0;
-        err_s = 0;
-    }
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    auto at = [](int k) { return k + (k >> 4); };
+    if (t == 0) err_s = 0;
     __syncthreads();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (uint64_t base = 0; base < nblocks; base += 1024) {
-        uint64_t i = base + threadIdx.x;
-        uint64_t v = i < nblocks ? block_sums[i] : 0;
-        if (v == ~0ull) {
-            err_s = 1;
-            v = 0;
+    uint64_t carry = 0;
+    for (uint64_t tile = 0; tile < nblocks; tile += TILE) {
+        uint64_t v[PER];
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            const uint64_t k = tile + (uint64_t)i * 1024 + t;
+            v[i] = k < nblocks ? block_sums[k] : 0;
         }
-        uint64_t x = v; // inclusive wave scan
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            if (v[i] == ~0ull) {
+                err_s = 1;
+                v[i] = 0;
+            }
+            tv[at(i * 1024 + t)] = v[i];
+        }
+        __syncthreads();
+        uint64_t mine[PER], sum = 0;
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            mine[i] = tv[at(t * PER + i)];
+            sum += mine[i];
+        }
+        uint64_t x = sum; // inclusive wave scan of the thread sums
         for (int o = 1; o < 64; o <<= 1) {
-            uint64_t y = __shfl_up(x, o);
+            const uint64_t y = __shfl_up(x, o);
             if (lane >= o) x += y;
         }
         if (lane == 63) wsum[wave] = x;
         __syncthreads();
-        uint64_t wpre = 0;
-        for (int w = 0; w < wave; w++) wpre += wsum[w];
-        uint64_t carry = carry_s;
-        if (i < nblocks) block_sums[i] = carry + wpre + x - v;
+        uint64_t before = 0, tile_total = 0;
+#pragma unroll
+        for (int w = 0; w < 16; w++) {
+            before += w < wave ? wsum[w] : 0;
+            tile_total += wsum[w];
+        }
+        uint64_t run = before + x - sum;
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            tv[at(t * PER + i)] = run;
+            run += mine[i];
+        }
         __syncthreads();
-        if (threadIdx.x == 1023) carry_s = carry + wpre + x;
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            const uint64_t k = tile + (uint64_t)i * 1024 + t;
+            if (k < nblocks) block_sums[k] = carry + tv[at(i * 1024 + t)];
+        }
+        carry += tile_total;
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
-        uint64_t t = err_s ? ~0ull : carry_s;
-        block_sums[nblocks] = t;
-        if (total) *total = t;
+    if (t == 0) {
+        const uint64_t tot = err_s ? ~0ull : carry;
+        block_sums[nblocks] = tot;
+        if (total) *total = tot;
     }
 }
 
@@ -359,6 +390,19 @@ struct Emit {
             uint32_t g = (uint32_t)(v >> (7 * (L - 1 - i))) & 0x7f;
             put1(g | (i ? 0x80 : 0));
         }
+    }
+    // [npre bytes of pre] | rvarint(v) | type as ONE append (v < 2^32: the varint is <= 5
+    // bytes, so the run is <= 8 bytes with npre <= 1): 32-bit ints, string/bytes lengths.
+    __device__ __forceinline__ void varint32_type(uint32_t v, uint32_t type, uint32_t pre = 0, uint32_t npre = 0) {
+        const uint32_t L = vlen32(v);
+        uint64_t x = v; // 7-bit groups -> bytes
+        x = (x & 0x000000000fffffffull) | ((x << 4) & 0x0000000f00000000ull);
+        x = (x & 0x00003fff00003fffull) | ((x << 2) & 0x3fff00003fff0000ull);
+        x = (x & 0x007f007f007f007full) | ((x << 1) & 0x7f007f007f007f00ull);
+        const uint32_t drop = 8 * (8 - L);
+        const uint64_t out = (__builtin_bswap64(x) >> drop) | ((0x8080808080808080ull >> drop) & ~0xffull);
+        const uint32_t sh = 8 * npre;
+        put_n((uint64_t)pre | (out << sh) | ((uint64_t)type << (sh + 8 * L)), npre + L + 1);
     }
     __device__ __forceinline__ void finish() {
         Pos d = pos & ~(Pos)3;
@@ -682,20 +726,19 @@ struct SpecEnc {
             } else if constexpr (k == K_BYTE) {
                 em.put_n(v | (T_BYTE << 8), 2);
             } else if constexpr (k == K_INT16) {
-                em.rvarint(zigzag32((int16_t)v));
-                em.put1(T_INT16);
+                em.varint32_type(zigzag32((int16_t)v), T_INT16);
             } else if constexpr (k == K_INT32) {
-                em.rvarint(zigzag32((int32_t)v));
-                em.put1(T_INT32);
+                em.varint32_type(zigzag32((int32_t)v), T_INT32);
             } else if constexpr (k == K_INT64) {
                 em.rvarint(zigzag64((int64_t)v));
                 em.put1(T_INT64);
-            } else if constexpr (k == K_UINT16 || k == K_UINT32 || k == K_UINT64) {
+            } else if constexpr (k == K_UINT16 || k == K_UINT32) {
+                em.varint32_type((uint32_t)v, k == K_UINT16 ? T_UINT16 : T_UINT32);
+            } else if constexpr (k == K_UINT64) {
                 em.rvarint(v);
-                em.put1(k == K_UINT16 ? T_UINT16 : (k == K_UINT32 ? T_UINT32 : T_UINT64));
+                em.put1(T_UINT64);
             } else if constexpr (k == K_FLOAT32) {
-                em.put4(bswap32((uint32_t)v));
-                em.put1(T_FLOAT32);
+                em.put_n(bswap32((uint32_t)v) | ((uint64_t)T_FLOAT32 << 32), 5);
             } else if constexpr (k == K_FLOAT64) {
                 em.put4(bswap32((uint32_t)(v >> 32)));
                 em.put4(bswap32((uint32_t)v));
@@ -731,9 +774,9 @@ struct SpecEnc {
                     }
                 }
                 if (len > 64) emit_heap(em, heap_rsrc(f, F), f.heap_lens[F], off + 64, len - 64);
-                if constexpr (k == K_STRING) em.put1(0);
-                em.rvarint(len);
-                em.put1(k == K_STRING ? T_STRING : T_BYTES);
+                // [NUL] | rvarint(len) | type in one append
+                if constexpr (k == K_STRING) em.varint32_type(len, T_STRING, 0u, 1u);
+                else em.varint32_type(len, T_BYTES);
             }
             x.end[F] = (uint32_t)(em.pos - start);
             emit_values<F + 1>(f, em, x, start, r, lists);
