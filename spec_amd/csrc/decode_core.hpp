@@ -611,10 +611,47 @@ struct FieldStore {
 // Fast path, part 1 (LdsSrc only): trailer, table check and every field's window read into
 // registers.  Returns false (nothing read into fr, nothing written) when the record needs
 // the generic path.  After it returns the record's LDS bytes are no longer needed.
+// Compact records (3N + 4 <= 16: list items, small messages): trailer AND table come from the
+// one 16-byte tail window — [table 3N][rvarint dataSize, 1-2 bytes][3N][TypeMessage] — so
+// the table needs no second round of LDS reads.  Accepts exactly what the general fast path
+// accepts, restricted to a 1-2 byte data size (anything else returns false: generic path).
+template <class Spec>
+__device__ __forceinline__ bool fast_prepare_compact(const LdsSrc &s, int rs, int re, FastRec<Spec> &fr) {
+    constexpr int N = Spec::N;
+    static_assert(3 * N + 4 <= 16, "compact records only");
+    const Tail t = load_tail(s, re);
+    const uint32_t type = (uint32_t)t.q0 & 0xff, tsz = (uint32_t)(t.q0 >> 8) & 0xff;
+    const uint32_t b3 = (uint32_t)(t.q0 >> 16) & 0xff, b4 = (uint32_t)(t.q0 >> 24) & 0xff;
+    const bool two = (b3 & 0x80) != 0; // data size: reverse varint ending at re-3
+    const uint32_t L = two ? 2u : 1u;
+    const uint32_t dsz = two ? ((b3 & 0x7f) | ((b4 & 0x7f) << 7)) : b3;
+    const int ts = re - 2 - (int)L - 3 * N, ds = ts - (int)dsz;
+    bool ok = (type == T_MESSAGE) & (tsz == 3u * N) & (!two | ((b4 & 0x80) == 0)) & (ds >= rs);
+    // table: shift the 128-bit tail (q1:q0, byte re-1 lowest) right past the trailer; entry
+    // N-1-k then sits in bits [24k, 24k + 24) as tag | end_hi | end_lo
+    const uint32_t sh = 8u * (2u + L);
+    const uint64_t lo = (t.q0 >> sh) | (t.q1 << (64 - sh)), hi = t.q1 >> sh;
+    uint32_t ends[N];
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        const int bo = 24 * (N - 1 - j);
+        const uint32_t ent =
+            (uint32_t)((bo >= 64 ? hi >> (bo - 64) : (lo >> bo) | (bo ? hi << (64 - bo) : 0ull)) & 0xffffff);
+        ok = ok & ((ent >> 16) == Spec::stag[j]);
+        ends[j] = ent & 0xffff;
+    }
+    if (!ok) return false;
+    FieldLoad<Spec, 0>::run(fr, s, ds, ends, dsz);
+    return FieldNat<Spec, 0>::ok(fr);
+}
+
 template <class Spec>
 __device__ __forceinline__ bool fast_prepare(const LdsSrc &s, int rs, int re, FastRec<Spec> &fr) {
     constexpr int N = Spec::N;
     if (re <= rs) return false;
+#if !defined(SPEC_NO_COMPACT)
+    if constexpr (3 * N + 4 <= 16) return fast_prepare_compact<Spec>(s, rs, re, fr);
+#endif
     Trailer tr = parse_trailer(s, rs, re);
     if ((tr.st != ST_OK) | tr.big | (tr.tsize != 3u * N)) return false;
     const int ts = (int)tr.tstart;

@@ -252,6 +252,57 @@ def test_fuzz_mutated_records(dev, kernel, seed):
     check_decode(dev, FLAT16, s2, e2, f"fuzz seed={seed}")
 
 
+COMPACT_SCHEMAS = [
+    [(1, Kind.INT32), (2, Kind.FLOAT64), (3, Kind.STRING)],              # the NESTED item schema
+    [(1, Kind.BOOL), (2, Kind.INT64), (3, Kind.STRING), (4, Kind.FLOAT64)],
+    [(7, Kind.UINT16)],
+    [(5, Kind.INT32), (9, Kind.BYTES)],
+]
+
+
+@pytest.mark.parametrize("si", range(len(COMPACT_SCHEMAS)))
+def test_fuzz_compact_records(dev, kernel, si):
+    """Schemas of <= 4 fields, whose trailer and table sit in one 16-byte tail window (the
+    decoder's compact fast path): data sizes with 1-, 2- and 3-byte varints, mutated
+    trailers/tables, truncations, garbage — against the oracle."""
+    rng = np.random.default_rng(77 + si)
+    fields = COMPACT_SCHEMAS[si]
+    n = 1500
+    lens = [0, 3, 100, 200, 20000]
+    recs = []
+    for i in range(n):
+        vals = []
+        for tag, kind in fields:
+            if kind == Kind.INT32:
+                v = int(rng.integers(-2**31, 2**31))
+            elif kind == Kind.INT64:
+                v = int(rng.integers(-2**63, 2**63, dtype=np.int64))
+            elif kind == Kind.UINT16:
+                v = int(rng.integers(0, 2**16))
+            elif kind == Kind.BOOL:
+                v = bool(rng.integers(0, 2))
+            elif kind == Kind.FLOAT64:
+                v = float(rng.standard_normal())
+            elif kind == Kind.STRING:
+                v = "s" * lens[int(rng.integers(0, len(lens) - (0 if i % 50 == 0 else 1)))]
+            else:
+                v = bytes(rng.integers(0, 256, lens[int(rng.integers(0, 4))], dtype=np.uint8))
+            vals.append((tag, kind, v))
+        b = bytearray(write_record(vals))
+        x = rng.integers(0, 6)
+        if x == 0:
+            b[len(b) - 1 - rng.integers(0, min(len(b), 16))] = rng.integers(0, 256)
+        elif x == 1:
+            b = b[:rng.integers(0, len(b))]
+        elif x == 2:
+            b = bytearray(rng.integers(0, 256, rng.integers(0, 40), dtype=np.uint8).tobytes())
+            if len(b) > 2:
+                b[-1], b[-2] = 80, 3 * len(fields)
+        recs.append(bytes(b))
+    stream, ends = concat_records(recs)
+    check_decode(dev, Schema(fields), stream, ends, f"compact schema {si}")
+
+
 def test_large_records_global_path(dev, kernel):
     """Records too large for a wave's LDS slab take the direct-HBM path; big messages
     (dataSize > 65535) use the 6-byte table."""
