@@ -404,6 +404,47 @@ struct Emit {
         const uint32_t sh = 8 * npre;
         put_n((uint64_t)pre | (out << sh) | ((uint64_t)type << (sh + 8 * L)), npre + L + 1);
     }
+    // rvarint(v) | type for any 64-bit v (<= 10 + 1 bytes) without a per-length branch: the 10
+    // reversed groups built in 128 bits, the leading (10 - L) bytes shifted out, continuation
+    // bits set, the type appended, the run stored as dwords (HEAD_ST4 emitters only).
+    __device__ __forceinline__ void varint64_type(uint64_t v, uint32_t type) {
+        const uint32_t L = vlen64(v);
+        uint64_t x = v & 0x00ffffffffffffffull; // groups 0..7 -> bytes 0..7
+        x = (x & 0x000000000fffffffull) | ((x << 4) & 0x0fffffff00000000ull);
+        x = (x & 0x00003fff00003fffull) | ((x << 2) & 0x3fff00003fff0000ull);
+        x = (x & 0x007f007f007f007full) | ((x << 1) & 0x7f007f007f007f00ull);
+        // memory order [g9 g8 g7 ... g0]: lo = first 8 bytes, hi = last 2 (little-endian u128)
+        const uint64_t g98 = ((v >> 63) & 1) | (((v >> 56) & 0x7f) << 8);
+        const uint64_t rev = __builtin_bswap64(x); // [g7 .. g0]
+        uint64_t lo = g98 | (rev << 16), hi = rev >> 48;
+        // drop the 10 - L leading bytes (shift right by 8 * (10 - L) in 128 bits)
+        const uint32_t d = 8 * (10 - L);
+        if (d >= 64) {
+            lo = hi >> (d - 64);
+            hi = 0;
+        } else if (d) {
+            lo = (lo >> d) | (hi << (64 - d));
+            hi >>= d;
+        }
+        // continuation bits on bytes 1..L-1, then the type at byte L
+        const uint64_t c = 0x8080808080808080ull;
+        lo |= L >= 8 ? (c & ~0xffull) : ((c & ((1ull << (8 * L)) - 1)) & ~0xffull);
+        hi |= L > 8 ? (c & ((1ull << (8 * (L - 8))) - 1)) : 0ull;
+        if (L >= 8) hi |= (uint64_t)type << (8 * (L - 8));
+        else lo |= (uint64_t)type << (8 * L);
+        const uint32_t w[5] = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32), 0u};
+        put_heap_short<4>(w, 0u, L + 1);
+    }
+    // NW payload dwords (memory order) then the type byte, as one run (HEAD_ST4 only)
+    template <int NW>
+    __device__ __forceinline__ void words_type(const uint32_t (&p)[NW], uint32_t type) {
+        uint32_t w[NW + 3];
+#pragma unroll
+        for (int i = 0; i < NW; i++) w[i] = p[i];
+        w[NW] = type;
+        w[NW + 1] = w[NW + 2] = 0;
+        put_heap_short<NW + 2>(w, 0u, 4 * NW + 1);
+    }
     __device__ __forceinline__ void finish() {
         Pos d = pos & ~(Pos)3;
         for (int i = 0; i < (int)(pos - d); i++)
@@ -729,16 +770,40 @@ struct SpecEnc {
                 em.varint32_type(zigzag32((int16_t)v), T_INT16);
             } else if constexpr (k == K_INT32) {
                 em.varint32_type(zigzag32((int32_t)v), T_INT32);
-            } else if constexpr (k == K_INT64) {
-                em.rvarint(zigzag64((int64_t)v));
-                em.put1(T_INT64);
+            } else if constexpr (k == K_INT64 || k == K_UINT64) {
+                const uint64_t u = k == K_INT64 ? zigzag64((int64_t)v) : v;
+                const uint32_t ty = k == K_INT64 ? T_INT64 : T_UINT64;
+                if constexpr (E::kHeadSt4) {
+                    em.varint64_type(u, ty);
+                } else {
+                    em.rvarint(u);
+                    em.put1(ty);
+                }
             } else if constexpr (k == K_UINT16 || k == K_UINT32) {
                 em.varint32_type((uint32_t)v, k == K_UINT16 ? T_UINT16 : T_UINT32);
-            } else if constexpr (k == K_UINT64) {
-                em.rvarint(v);
-                em.put1(T_UINT64);
             } else if constexpr (k == K_FLOAT32) {
                 em.put_n(bswap32((uint32_t)v) | ((uint64_t)T_FLOAT32 << 32), 5);
+            } else if constexpr (E::kHeadSt4 && (k == K_FLOAT64 || k == K_BIN64 || k == K_BIN128 || k == K_BIN256)) {
+                // fixed-width payload + type as one run of dwords
+                if constexpr (k == K_FLOAT64) {
+                    const uint32_t p[2] = {bswap32((uint32_t)(v >> 32)), bswap32((uint32_t)v)};
+                    em.words_type(p, T_FLOAT64);
+                } else if constexpr (k == K_BIN64) {
+                    const uint32_t p[2] = {(uint32_t)v, (uint32_t)(v >> 32)};
+                    em.words_type(p, T_BIN64);
+                } else if constexpr (k == K_BIN128) {
+                    const uint32_t p[4] = {(uint32_t)v, (uint32_t)(v >> 32), (uint32_t)x.v[F][1],
+                                           (uint32_t)(x.v[F][1] >> 32)};
+                    em.words_type(p, T_BIN128);
+                } else {
+                    uint32_t p[8];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        p[2 * q] = (uint32_t)x.v[F][q];
+                        p[2 * q + 1] = (uint32_t)(x.v[F][q] >> 32);
+                    }
+                    em.words_type(p, T_BIN256);
+                }
             } else if constexpr (k == K_FLOAT64) {
                 em.put4(bswap32((uint32_t)(v >> 32)));
                 em.put4(bswap32((uint32_t)v));
