@@ -899,16 +899,17 @@ struct SpecEnc {
         em.template put_heap_short<RUN_M>(w, 0u, (uint32_t)TB + L + 2);
     }
 
-    // With a list field the emitter jumps over the list's items (written by other lanes), so it
-    // must never store below its position: no HEAD_ST4 then.
+    // With a list field the emitter jumps over the list's items (written later by other lanes:
+    // encode_nested_core.hpp phase B).  HEAD_ST4 stays valid: the first store after the jump may
+    // clobber <= 3 bytes of the last item, which phase B then writes.
     template <class Sink, class Pos, class Lists = NoListEmit>
     static __device__ __forceinline__ void emit(const EncFields &f, const Sink &k, Pos start, uint64_t r,
                                                 const Rec &rec, const RecSize &rs, const uint8_t *,
                                                 const Lists &lists = Lists()) {
         Rec x = rec;
-        Emit<Sink, Pos, Sink::kHeadSt4 && !kHasList> em(k, start);
+        Emit<Sink, Pos, Sink::kHeadSt4> em(k, start);
         emit_values<0>(f, em, x, start, r, lists);
-        if constexpr (Sink::kHeadSt4 && !kHasList && !Spec::big_forced && RUN_M <= 18) {
+        if constexpr (Sink::kHeadSt4 && !Spec::big_forced && RUN_M <= 18) {
             if (__ballot(rs.big) == 0) { // wave-uniform: every record of the wave has a small table
                 emit_small_table_trailer(em, x, (uint32_t)rs.data);
                 em.finish();

@@ -145,7 +145,9 @@ struct KnownListSize {
 };
 
 // list emit hook (phase A): skips the items, writes the list table and trailer, records where
-// the items start.
+// the items start.  An empty list is no jump: the emitter keeps its pending bytes (a HEAD_ST4
+// emitter restarting at the same position would zero the bytes below it, and no item would
+// rewrite them).
 struct WaveListEmit {
     const uint32_t *pre; // wave item prefix at this record's first item
     uint32_t count, data;
@@ -153,11 +155,13 @@ struct WaveListEmit {
     mutable int lstart;
     template <class E>
     __device__ __forceinline__ void operator()(E &em, uint32_t, uint64_t) const {
-        em.finish();
         lstart = (int)em.pos;
-        em.pos += data;
-        em.lo = em.pos;
-        em.acc = 0;
+        if (data) {
+            em.finish();
+            em.pos += data;
+            em.lo = em.pos;
+            em.acc = 0;
+        }
         const uint32_t p0 = pre[0];
         for (uint32_t j = 0; j < count; j++) {
             const uint32_t end = pre[j + 1] - p0; // element offset = item end - list start
@@ -324,7 +328,11 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
     LdsSink k{slab, (int)(smem + 160 - slab)}; // dummy dword in the header
     // A: outer records, the items skipped
     WaveListEmit le{pre + (L.b - L.I0), ls.count, (uint32_t)ls.data, ls.big, 0};
+#if defined(NENC_EXP) && NENC_EXP == 1 // diagnostic (timing only): no outer emission
+    le.lstart = (int)(head + (start - S));
+#else
     if (L.valid) OP::emit(a.outer, k, (int)(head + (start - S)), L.r, orec, rs, inv_outer, le);
+#endif
     wave_sync();
     const int lst = le.lstart;
     const bool fix = L.valid && ls.count > 0 && (lst & 3);
@@ -348,11 +356,15 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
         for (int st = 32; st > 0; st >>= 1)
             if (__shfl(L.b, o + st) <= i) o += st;
         const int pos = __shfl(lbase, o) + (int)pre[iv ? kk : 0u];
+#if defined(NENC_EXP) && NENC_EXP == 2 // diagnostic (timing only): items loaded, not emitted
+        if (iv) k.st4a(pos & ~3, (uint32_t)cur.v[0][0]);
+#else
         if (iv) {
             bool e2 = false;
             const RecSize irs = IP::size(a.item, cur, i, false, e2);
             IP::emit(a.item, k, pos, i, cur, irs, inv_item);
         }
+#endif
         wave_sync();
         cur = nxt;
     }
@@ -363,7 +375,9 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
         *d = (saved & m) | (*d & ~m);
     }
     wave_sync();
+#if !(defined(NENC_EXP) && NENC_EXP == 3) // diagnostic (timing only): no copy-out
     copy_slab_out(slab, a.out + S - head, head, head + (E - S), lane);
+#endif
 }
 
 } // namespace spec

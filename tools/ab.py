@@ -2,7 +2,8 @@
 rounds to cancel box drift.
 Usage: python tools/ab.py 'NAME=ENV=VAL,ENV=VAL' ... [--rounds=R] [--tool=flat|nested]
   flat:   tools/bench_variants.py jit  (1M Flat16 decode, median per-launch ms)
-  nested: tools/bench_nested.py        (1M Nested one-pass decode, ms per launch)"""
+  nested: tools/bench_nested.py        (1M Nested one-pass decode, ms per launch)
+  encode / nested_encode: tools/bench_encode.py (flat / nested encode ms)"""
 import json
 import os
 import subprocess
@@ -17,7 +18,8 @@ for a in sys.argv[1:]:
     if a.startswith("--tool="):
         tool = a.split("=")[1]
 cmd, key = {"flat": (["bench_variants.py", "jit"], "jit"), "nested": (["bench_nested.py"], "nested"),
-            "encode": (["bench_encode.py"], "flat")}[tool]
+            "encode": (["bench_encode.py"], "flat"), "nested_encode": (["bench_encode.py", "nested"], "nested")}[tool]
+field = "encode_ms" if tool == "nested_encode" else "med"
 variants = []
 for a in args:
     name, _, envs = a.partition("=")
@@ -36,7 +38,7 @@ for _ in range(rounds):
             print(out.stderr[-2000:])
             sys.exit(1)
         d = json.loads(out.stdout.strip().splitlines()[-1])
-        res[name].append(d[key]["med"])
+        res[name].append(d[key][field])
         extra[name] = d[key]
 summary = {k: {"median_ms": sorted(v)[len(v) // 2], "all": v, "last": extra[k]} for k, v in res.items()}
 print(json.dumps(summary))
