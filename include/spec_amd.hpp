@@ -230,4 +230,63 @@ class MessageBatchWriter {
     std::vector<uint64_t> lens_;
 };
 
+// Pinned host memory (hipHostMalloc): what an mpx connection reads frames into.
+class PinnedBuffer {
+  public:
+    explicit PinnedBuffer(size_t bytes) : n_(bytes) { Check(spec_host_alloc(bytes ? bytes : 1, &p_), "spec_host_alloc"); }
+    ~PinnedBuffer() {
+        if (p_) spec_host_free(p_);
+    }
+    PinnedBuffer(const PinnedBuffer &) = delete;
+    PinnedBuffer &operator=(const PinnedBuffer &) = delete;
+    uint8_t *data() const { return (uint8_t *)p_; }
+    size_t size() const { return n_; }
+
+  private:
+    void *p_ = nullptr;
+    size_t n_ = 0;
+};
+
+// The receive side of an mpx connection, batched: records (stream + ends) in pinned host memory
+// in, decoded columns + status in pinned host memory out, H2D / decode / D2H overlapped in
+// chunks (spec_host_decoder_*).  Outputs are chunk-major: Chunk(k) locates chunk k's columns.
+class HostMessageReader {
+  public:
+    HostMessageReader(const Schema &schema, uint64_t max_records, uint64_t max_bytes, uint32_t chunks = 8)
+        : schema_(schema), chunks_(chunks) {
+        spec_schema c = schema.C();
+        Check(spec_host_decoder_create(&c, max_records, max_bytes, chunks, &d_), "spec_host_decoder_create");
+    }
+    ~HostMessageReader() { spec_host_decoder_destroy(d_); }
+    HostMessageReader(const HostMessageReader &) = delete;
+    HostMessageReader &operator=(const HostMessageReader &) = delete;
+
+    uint64_t OutBytes(uint64_t n) const { return spec_host_decoder_out_bytes(d_, n); }
+    // For every record i of stream[ends[i-1], ends[i]): OpenMessageErr + the getters (synchronous).
+    void Read(const PinnedBuffer &stream, uint64_t stream_len, const PinnedBuffer &ends, uint64_t n,
+              PinnedBuffer &out) {
+        if (out.size() < OutBytes(n) || ends.size() < n * 8) throw Error(SPEC_E_CAPACITY, "HostMessageReader::Read");
+        Check(spec_host_decoder_run(d_, stream.data(), stream_len, (const uint64_t *)ends.data(), n, out.data()),
+              "spec_host_decoder_run");
+    }
+    struct ChunkView {
+        uint64_t r0, r1;
+        std::vector<uint64_t> col_off; // byte offset of column f of records [r0, r1) in `out`
+        uint64_t status_off;
+    };
+    ChunkView Chunk(uint64_t n, uint32_t k) const {
+        ChunkView v;
+        v.col_off.resize(schema_.Len() ? schema_.Len() : 1);
+        Check(spec_host_decoder_chunk(d_, n, k, &v.r0, &v.r1, v.col_off.data(), &v.status_off),
+              "spec_host_decoder_chunk");
+        return v;
+    }
+    uint32_t Chunks() const { return chunks_; }
+
+  private:
+    Schema schema_;
+    uint32_t chunks_;
+    spec_host_decoder *d_ = nullptr;
+};
+
 } // namespace spec

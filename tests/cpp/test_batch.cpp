@@ -116,6 +116,37 @@ TEST(TestOpenMessageBatch__should_decode_written_records) {
     for (uint64_t i = 0; i < h.n; i++) REQUIRE(v[i] == h.i64[i]);
 }
 
+// the mpx receive loop batched: pinned host in, pinned host out (chunk-major), results as above
+TEST(TestHostMessageReader__should_decode_host_records) {
+    HostRecords h = test_records(20011);
+    const uint64_t n = h.n;
+    spec::PinnedBuffer stream(h.stream.size()), ends(n * 8);
+    std::memcpy(stream.data(), h.stream.data(), h.stream.size());
+    std::memcpy(ends.data(), h.ends.data(), n * 8);
+    spec::HostMessageReader reader(test_schema(), n, h.stream.size(), 6);
+    spec::PinnedBuffer out(reader.OutBytes(n));
+    reader.Read(stream, h.stream.size(), ends, n, out);
+    std::vector<std::vector<uint8_t>> want(5);
+    std::vector<void *> wp;
+    for (int f = 0; f < 5; f++) {
+        want[f].resize(n * spec_kind_width(kKinds[f]) + 1);
+        wp.push_back(want[f].data());
+    }
+    std::vector<uint8_t> wst(n + 1);
+    so_decode_flat_batch(5, kTags, kKinds, h.stream.data(), h.ends.data(), n, wp.data(), wst.data(), 1);
+    uint64_t covered = 0;
+    for (uint32_t k = 0; k < reader.Chunks(); k++) {
+        auto c = reader.Chunk(n, k);
+        covered += c.r1 - c.r0;
+        REQUIRE(std::memcmp(out.data() + c.status_off, wst.data() + c.r0, c.r1 - c.r0) == 0);
+        for (int f = 0; f < 5; f++) {
+            const uint64_t w = spec_kind_width(kKinds[f]);
+            REQUIRE(std::memcmp(out.data() + c.col_off[f], want[f].data() + c.r0 * w, (c.r1 - c.r0) * w) == 0);
+        }
+    }
+    REQUIRE(covered == n);
+}
+
 // internal/decode/msg_test.go:74-143 error classes, as records of one batch
 TEST(TestOpenMessageBatch__should_return_error_classes) {
     std::vector<std::vector<uint8_t>> recs = {
