@@ -231,6 +231,41 @@ def nested_leg(n, seed, dev):
             "encode_gb_s": round(enc_alg / (enc_ms * 1e-3) / 1e9, 1), "roundtrip_ok": bool(ok)}
 
 
+def frames_leg(stream, ends, dev):
+    """mpx frame index of the batch as frames ([u32 BE size][record], 1M frames): on the device
+    (spec_frames_index_device, all launches, HIP events) and on one host core (spec_frames_index,
+    the C walk), identical results."""
+    from spec_amd.frames import frames_index, frames_index_device, make_frames_device
+
+    import ctypes as C
+
+    n = ends.numel()
+    frames = make_frames_device(stream, ends)
+    fends, used, st = frames_index_device(frames, n)
+    L = spec_amd.lib()
+    wsb = L.spec_frames_index_device_workspace_size(frames.numel())
+    ws = torch.empty((wsb + 7) // 8, dtype=torch.int64, device=dev)
+    e2 = torch.empty(n, dtype=torch.int64, device=dev)
+    out = torch.zeros(3, dtype=torch.int64, device=dev)
+    p = C.c_void_p
+
+    def call():
+        L.spec_frames_index_device(p(frames.data_ptr()), frames.numel(), p(e2.data_ptr()), n, p(out.data_ptr()),
+                                   p(out.data_ptr() + 8), p(out.data_ptr() + 16), p(ws.data_ptr()), wsb,
+                                   p(torch.cuda.current_stream().cuda_stream))
+
+    ms, _ = kernel_time_events(call, 5, lead=2)
+    host = frames.cpu().numpy()
+    t0 = time.perf_counter()
+    hends, hused = frames_index(host, n)
+    host_ms = (time.perf_counter() - t0) * 1e3
+    ok = st == 0 and used == hused == frames.numel() and np.array_equal(fends.cpu().numpy().view(np.uint64), hends)
+    return {"frames": n, "bytes": int(frames.numel()), "device_ms": round(ms, 3),
+            "device_gb_s": round(frames.numel() / (ms * 1e-3) / 1e9, 1), "host_1core_ms": round(host_ms, 3),
+            "ok": bool(ok) and torch.equal(e2, fends),
+            "note": "device: 6 launches (segment exits, group composition, chain, entries, emit, finish)"}
+
+
 def gather_leg(dec, dist, rank, world, n, steps):
     """BASELINE config 5's collective: each rank decodes its shard, then every rank's columns
     (+ status) go to rank 0 over RCCL (xGMI).  Times decode + gather per step (max over ranks)."""
@@ -346,6 +381,10 @@ def main():
                     "pcie_bytes": int(sh.numel() + 8 * n + n * (COLUMN_BYTES + 1))}
             except Exception as e:
                 extras["e2e_pinned_decode"] = {"error": repr(e)[:300]}
+            try:
+                extras["frames_index"] = frames_leg(stream, ends, dev)
+            except Exception as e:
+                extras["frames_index"] = {"error": repr(e)[:300]}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -162,6 +162,17 @@ int spec_frames_index(const uint8_t *buf, uint64_t len, uint64_t *ends, uint64_t
 int spec_decode_frames(const spec_schema *schema, const uint8_t *frames, uint64_t frames_len,
                        const uint64_t *ends, uint64_t r0, uint64_t r1, uint64_t range_bytes, void *const *columns,
                        uint8_t *status, void *stream);
+/* spec_frames_index_device: spec_frames_index on a DEVICE buffer (4-byte aligned), with the same
+ * results: ends[0, min(frames, cap)), *count, *consumed (device uint64) and *status (device int32:
+ * SPEC_OK, or SPEC_E_CAPACITY when more than cap complete frames exist — then *count = cap).  The
+ * serial head chain is resolved in parallel: per 64 KiB segment the exit of every entry offset
+ * below 2048, composed over groups of segments; a frame straddling a segment boundary by 2048
+ * bytes or more (or > 4096 frames in a segment) falls back to a serial walk on the device.
+ * Workspace: spec_frames_index_device_workspace_size(len) bytes.  Asynchronous on `stream`. */
+size_t spec_frames_index_device_workspace_size(uint64_t len);
+int spec_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends, uint64_t cap, uint64_t *count,
+                             uint64_t *consumed, int32_t *status, void *workspace, size_t workspace_size,
+                             void *stream);
 
 /* ---- host pipeline (the path starts and ends in HOST memory: mpx connection buffers) ----
  * spec_host_decoder decodes a batch held in pinned host memory (spec_host_alloc) into a pinned

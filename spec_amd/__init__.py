@@ -7,13 +7,13 @@ decoded into SoA columns / encoded from them by hand-written gfx950 kernels
 """
 from ._lib import LIB_PATH, SpecError, header_symbols, lib, set_jit
 from .batch import Columns, Decoder, Encoder, alloc_columns, decode_flat, encode_flat, parse_messages
-from .frames import decode_frames, frames_index, make_frames
+from .frames import decode_frames, frames_index, frames_index_device, make_frames, make_frames_device
 from .pipeline import HostDecoder
 from .nested import NestedColumns, NestedDecoder, NestedEncoder, decode_nested, encode_nested
 from .schema import FLAT16, NESTED, Field, Kind, NestedSchema, Schema
 
 __all__ = [
-    "HostDecoder", "decode_frames", "frames_index", "make_frames", "LIB_PATH", "SpecError", "header_symbols", "lib", "set_jit", "Columns", "Decoder", "Encoder", "alloc_columns",
+    "HostDecoder", "decode_frames", "frames_index", "frames_index_device", "make_frames", "make_frames_device", "LIB_PATH", "SpecError", "header_symbols", "lib", "set_jit", "Columns", "Decoder", "Encoder", "alloc_columns",
     "decode_flat", "encode_flat", "parse_messages", "FLAT16", "Field", "Kind", "Schema",
     "NESTED", "NestedSchema", "NestedColumns", "NestedDecoder", "NestedEncoder", "decode_nested",
     "encode_nested",

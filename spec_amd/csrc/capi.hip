@@ -225,6 +225,20 @@ int spec_frames_index(const uint8_t *buf, uint64_t len, uint64_t *ends, uint64_t
     return SPEC_OK;
 }
 
+size_t spec_frames_index_device_workspace_size(uint64_t len) { return spec::frames_index_device_workspace(len); }
+
+int spec_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends, uint64_t cap, uint64_t *count,
+                             uint64_t *consumed, int32_t *status, void *workspace, size_t workspace_size,
+                             void *stream) {
+    if ((!buf && len) || ((uintptr_t)buf & 3) || !count || !consumed || !status || (cap && !ends) || !workspace)
+        return SPEC_E_INVALID_ARGUMENT;
+    if (len >= (1ull << 48)) return SPEC_E_TOO_LARGE;
+    if (workspace_size < spec::frames_index_device_workspace(len)) return SPEC_E_WORKSPACE;
+    if (spec::launch_frames_index_device(buf, len, ends, cap, count, consumed, status, workspace, (hipStream_t)stream))
+        return hip_rc(hipGetLastError());
+    return SPEC_OK;
+}
+
 int spec_parse_messages(const uint8_t *stream_bytes, uint64_t stream_len, const uint64_t *ends, uint64_t n,
                         uint32_t head, uint8_t *status, uint32_t *sizes, void *stream) {
     if (n == 0) return SPEC_OK;

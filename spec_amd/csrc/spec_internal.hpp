@@ -21,6 +21,10 @@ int jit_launch_nested_encode(const spec_nested_schema *schema, const NestedEncod
                              hipStream_t stream);
 long long jit_compile_only_nested_encode(const spec_nested_schema *schema);
 int launch_decode_flat(DecodeArgs a, double avg_record, hipStream_t stream);
+// frames_device.hip
+size_t frames_index_device_workspace(uint64_t len);
+int launch_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends, uint64_t cap, uint64_t *count,
+                               uint64_t *consumed, int32_t *status, void *ws, hipStream_t stream);
 int device_cus(); // CUs of the current device (cached)
 bool persistent_decode(); // SPEC_AMD_PERSIST=1
 unsigned decode_wpb();     // SPEC_AMD_WPB (waves per block, default 1)

@@ -31,6 +31,44 @@ def frames_index(buf: np.ndarray, cap: int | None = None):
     return ends[: cnt.value], used.value
 
 
+def frames_index_device(buf: torch.Tensor, cap: int | None = None, cuda_stream=None):
+    """spec_frames_index_device over a device buffer (4-byte aligned): -> (ends int64 device
+    tensor [count], consumed, status) — the host walk's results, computed on the GPU (reads the
+    three scalars back, so this wrapper synchronises; the C call itself does not)."""
+    _check_dev(buf, "buf", torch.uint8)
+    n = buf.numel()
+    cap = cap if cap is not None else max(1, n // 4)
+    dev = buf.device
+    ends = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+    out = torch.zeros(3, dtype=torch.int64, device=dev)  # count, consumed, status (int32 in slot 2)
+    L = _lib.lib()
+    ws_bytes = L.spec_frames_index_device_workspace_size(n)
+    ws = torch.empty((ws_bytes + 7) // 8, dtype=torch.int64, device=dev)
+    rc = L.spec_frames_index_device(_ptr(buf), n, _ptr(ends), cap, C.c_void_p(out.data_ptr()),
+                                    C.c_void_p(out.data_ptr() + 8), C.c_void_p(out.data_ptr() + 16), _ptr(ws),
+                                    ws_bytes, _stream_handle(cuda_stream))
+    _lib.check(rc, "spec_frames_index_device")
+    cnt, used, st = out.cpu().tolist()
+    st = st - (1 << 32) if st >= (1 << 31) else st  # int32 in the low half of the zeroed slot
+    return ends[:cnt], used, st
+
+
+def make_frames_device(stream: torch.Tensor, ends: torch.Tensor) -> torch.Tensor:
+    """make_frames on the device (benchmark input): a 4-byte BE head before every record."""
+    n = ends.numel()
+    out = torch.empty(stream.numel() + 4 * n, dtype=torch.uint8, device=stream.device)
+    if n == 0:
+        return out
+    starts = torch.cat([ends.new_zeros(1), ends[:-1]])
+    sizes = ends - starts
+    rec = torch.searchsorted(ends, torch.arange(stream.numel(), device=stream.device), right=True)
+    out[torch.arange(stream.numel(), device=stream.device) + 4 * (rec + 1)] = stream
+    hpos = starts + 4 * torch.arange(n, device=stream.device)
+    for b in range(4):
+        out[hpos + b] = ((sizes >> (8 * (3 - b))) & 0xff).to(torch.uint8)
+    return out
+
+
 def make_frames(stream: np.ndarray, ends: np.ndarray) -> np.ndarray:
     """Records (stream + ends) -> mpx frames [u32 BE size][record]..."""
     ends = np.asarray(ends, dtype=np.int64)
