@@ -218,6 +218,17 @@ def _declare(L):
     L.so_decode_nested_counts.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
     L.so_decode_nested_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64] + [C.c_void_p] * 9
     L.so_parse_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]
+    # lz4 (oracle/lz4.c)
+    L.so_xxh32.argtypes = [C.c_void_p, C.c_size_t, C.c_uint32]
+    L.so_xxh32.restype = C.c_uint32
+    for name in ("so_lz4_decompress_block", "so_lz4_compress_block"):
+        getattr(L, name).argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
+        getattr(L, name).restype = C.c_longlong
+    L.so_lz4_frame_write.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_int, C.c_int, C.c_int,
+                                     C.c_void_p, C.c_size_t]
+    L.so_lz4_frame_write.restype = C.c_longlong
+    L.so_lz4_frame_read.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t),
+                                    C.POINTER(C.c_size_t)]
 
 
 def _e(err):
@@ -605,3 +616,56 @@ def parse_batch(stream: np.ndarray, ends: np.ndarray, head: int = 0):
     sz = np.zeros(n, np.uint32)
     lib().so_parse_batch(_ptr(stream), _ptr(ends), n, head, _ptr(st), _ptr(sz))
     return st, sz
+
+
+# ---------------------------------------------------------------- lz4 (mpx compression)
+
+def _u8(b) -> np.ndarray:
+    return np.ascontiguousarray(np.frombuffer(bytes(b), dtype=np.uint8) if not isinstance(b, np.ndarray) else b,
+                                dtype=np.uint8)
+
+
+def xxh32(data, seed: int = 0) -> int:
+    a = _u8(data)
+    return int(lib().so_xxh32(_ptr(a) if a.size else None, a.size, seed))
+
+
+def lz4_compress_block(data) -> bytes:
+    a = _u8(data)
+    cap = a.size + a.size // 255 + 64
+    out = np.zeros(cap, np.uint8)
+    n = lib().so_lz4_compress_block(_ptr(a) if a.size else None, a.size, _ptr(out), cap)
+    if n < 0:
+        raise RuntimeError("lz4 compress")
+    return out[:n].tobytes()
+
+
+def lz4_decompress_block(data, cap: int):
+    """-> bytes, or None on a corrupt block (pierrec decodeBlock's error)."""
+    a = _u8(data)
+    out = np.zeros(max(cap, 1), np.uint8)
+    n = lib().so_lz4_decompress_block(_ptr(a) if a.size else None, a.size, _ptr(out), cap)
+    return None if n < 0 else out[:n].tobytes()
+
+
+def lz4_frame_write(data, flush_ends=None, block_max: int = 256 << 10, content_checksum=True, block_checksum=False,
+                    close=True) -> np.ndarray:
+    """One LZ4 frame as mpx's writer emits it (flush_ends: the Flush() points, default one at the end)."""
+    a = _u8(data)
+    fe = np.ascontiguousarray(flush_ends if flush_ends is not None else [a.size], dtype=np.uint64)
+    cap = a.size + a.size // 255 + 64 + 12 * (a.size // 1024 + len(fe) + 2)
+    out = np.zeros(cap, np.uint8)
+    n = lib().so_lz4_frame_write(_ptr(a) if a.size else None, _ptr(fe), fe.size, block_max, int(content_checksum),
+                                 int(block_checksum), int(close), _ptr(out), cap)
+    if n < 0:
+        raise RuntimeError("lz4 frame write")
+    return out[:n].copy()
+
+
+def lz4_frame_read(buf, cap: int):
+    """-> (rc, decompressed bytes as np.uint8, consumed)."""
+    a = _u8(buf)
+    out = np.zeros(max(cap, 1), np.uint8)
+    ol, used = C.c_size_t(0), C.c_size_t(0)
+    rc = lib().so_lz4_frame_read(_ptr(a) if a.size else None, a.size, _ptr(out), cap, C.byref(ol), C.byref(used))
+    return rc, out[:ol.value].copy(), used.value

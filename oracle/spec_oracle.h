@@ -327,6 +327,14 @@ int so_decode_nested_batch(const uint8_t *stream, const uint64_t *ends, uint64_t
 int so_parse_batch(const uint8_t *stream, const uint64_t *ends, uint64_t n, uint32_t head, uint8_t *status,
                    uint32_t *sizes);
 
+/* ---- LZ4 block + frame formats (oracle/lz4.c; mpx compression, pierrec/lz4/v4 restated) ---- */
+uint32_t so_xxh32(const void *data, size_t len, uint32_t seed);
+long long so_lz4_decompress_block(const uint8_t *src, size_t n, uint8_t *dst, size_t cap);
+long long so_lz4_compress_block(const uint8_t *src, size_t n, uint8_t *dst, size_t cap);
+long long so_lz4_frame_write(const uint8_t *data, const uint64_t *flush_ends, size_t nflush, uint32_t block_max,
+                             int content_checksum, int block_checksum, int close, uint8_t *out, size_t cap);
+int so_lz4_frame_read(const uint8_t *buf, size_t len, uint8_t *out, size_t cap, size_t *out_len, size_t *consumed);
+
 #ifdef __cplusplus
 }
 #endif
