@@ -80,6 +80,7 @@ typedef enum spec_rc {
     SPEC_E_TOO_LARGE = -3, /* stream_len >= 4 GiB or a record > format.MaxSize */
     SPEC_E_CAPACITY = -4,  /* output buffer smaller than the encoded batch */
     SPEC_E_WORKSPACE = -5, /* workspace smaller than *_workspace_size() */
+    SPEC_E_CORRUPT = -6,   /* corrupt LZ4 frame (magic, version, header/block checksum, block size) */
 } spec_rc;
 
 typedef struct spec_span {
@@ -173,6 +174,39 @@ size_t spec_frames_index_device_workspace_size(uint64_t len);
 int spec_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends, uint64_t cap, uint64_t *count,
                              uint64_t *consumed, int32_t *status, void *workspace, size_t workspace_size,
                              void *stream);
+
+/* ---- LZ4 (mpx connection compression: mpx/conn_writer.go:42-56, conn_reader.go:53-62) ----
+ * mpx wraps a connection in ONE LZ4 frame of independent blocks (pierrec/lz4/v4, 256 KiB blocks).
+ * spec_lz4_frame_blocks (HOST, CPU): walks the frame headers and block size words of buf[0, len)
+ * (one u32 per block; header checksums, and block checksums when the frame has them, verified)
+ * and lists every COMPLETE block; `state` carries an open frame across calls (zero it for a
+ * new connection): a later call continues with the frame's blocks.  *consumed = bytes the listed
+ * blocks (and finished frames) span.  SPEC_E_CORRUPT on a bad header, SPEC_E_CAPACITY when more
+ * than cap blocks are complete.  The content checksum (only written when a connection closes)
+ * is not verified.
+ * spec_lz4_decompress (DEVICE): block k (src[blocks[k].src_off, +src_len)) decompressed into
+ * slots + k * slot_bytes (slot_bytes >= the frame's block max size); sizes[k] = its size, or
+ * all-ones and status[k] = 1 for a corrupt block (pierrec decodeBlock's errors).
+ * spec_lz4_pack (DEVICE): the slots gathered into out back to back; *total (device) = bytes,
+ * all-ones if any block was corrupt; nothing written if *total > out_cap. */
+typedef struct spec_lz4_block {
+    uint64_t src_off; /* block data in the source buffer */
+    uint32_t src_len;
+    uint32_t stored;  /* 1: stored uncompressed (size word bit 31) */
+} spec_lz4_block;
+typedef struct spec_lz4_state {
+    uint32_t in_frame;  /* 1: the next bytes continue an open frame's blocks */
+    uint32_t block_max; /* that frame's block max size */
+    uint32_t flags;     /* bit 0 block checksums, bit 1 content checksum */
+    uint32_t reserved;
+} spec_lz4_state;
+int spec_lz4_frame_blocks(const uint8_t *buf, uint64_t len, spec_lz4_state *state, spec_lz4_block *blocks,
+                          uint64_t cap, uint64_t *nblocks, uint64_t *consumed, uint32_t *block_max);
+int spec_lz4_decompress(const uint8_t *src, uint64_t src_len, const spec_lz4_block *blocks, uint64_t nblocks,
+                        uint8_t *slots, uint64_t slot_bytes, uint32_t *sizes, uint8_t *status, void *stream);
+size_t spec_lz4_pack_workspace_size(uint64_t nblocks);
+int spec_lz4_pack(const uint8_t *slots, uint64_t slot_bytes, const uint32_t *sizes, uint64_t nblocks, uint8_t *out,
+                  uint64_t out_cap, uint64_t *total, void *workspace, size_t workspace_size, void *stream);
 
 /* ---- host pipeline (the path starts and ends in HOST memory: mpx connection buffers) ----
  * spec_host_decoder decodes a batch held in pinned host memory (spec_host_alloc) into a pinned

@@ -7,6 +7,7 @@ decoded into SoA columns / encoded from them by hand-written gfx950 kernels
 """
 from ._lib import LIB_PATH, SpecError, header_symbols, lib, set_jit
 from .batch import Columns, Decoder, Encoder, alloc_columns, decode_flat, encode_flat, parse_messages
+from . import lz4
 from .frames import decode_frames, frames_index, frames_index_device, make_frames, make_frames_device
 from .pipeline import HostDecoder
 from .nested import NestedColumns, NestedDecoder, NestedEncoder, decode_nested, encode_nested

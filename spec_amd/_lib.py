@@ -113,6 +113,12 @@ def _declare(L):
     L.spec_host_decoder_chunk.argtypes = [vp, C.c_uint64, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                           C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.spec_host_decoder_run.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, vp]
+    L.spec_lz4_frame_blocks.argtypes = [vp, C.c_uint64, vp, vp, C.c_uint64, C.POINTER(C.c_uint64),
+                                        C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]
+    L.spec_lz4_decompress.argtypes = [vp, C.c_uint64, vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp]
+    L.spec_lz4_pack_workspace_size.argtypes = [C.c_uint64]
+    L.spec_lz4_pack_workspace_size.restype = C.c_size_t
+    L.spec_lz4_pack.argtypes = [vp, C.c_uint64, vp, C.c_uint64, vp, C.c_uint64, vp, vp, C.c_size_t, vp]
 
 
 def strerror(rc: int) -> str:

@@ -124,6 +124,7 @@ const char *spec_strerror(int rc) {
     case SPEC_E_TOO_LARGE: return "batch too large (stream >= 4 GiB or record > format.MaxSize)";
     case SPEC_E_CAPACITY: return "output capacity too small";
     case SPEC_E_WORKSPACE: return "workspace too small";
+    case SPEC_E_CORRUPT: return "corrupt LZ4 frame";
     }
     return "unknown error";
 }

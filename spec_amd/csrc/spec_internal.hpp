@@ -21,6 +21,11 @@ int jit_launch_nested_encode(const spec_nested_schema *schema, const NestedEncod
                              hipStream_t stream);
 long long jit_compile_only_nested_encode(const spec_nested_schema *schema);
 int launch_decode_flat(DecodeArgs a, double avg_record, hipStream_t stream);
+// lz4_device.hip
+int launch_lz4_decompress(const uint8_t *src, uint64_t src_len, const spec_lz4_block *blocks, uint64_t nblocks,
+                          uint8_t *slots, uint64_t slot, uint32_t *sizes, uint8_t *status, hipStream_t stream);
+int launch_lz4_pack(const uint8_t *slots, uint64_t slot, const uint32_t *sizes, uint64_t nblocks, uint8_t *out,
+                    uint64_t out_cap, uint64_t *offsets, uint64_t *total, hipStream_t stream);
 // frames_device.hip
 size_t frames_index_device_workspace(uint64_t len);
 int launch_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends, uint64_t cap, uint64_t *count,
