@@ -266,6 +266,54 @@ def frames_leg(stream, ends, dev):
             "note": "device: 6 launches (segment exits, group composition, chain, entries, emit, finish)"}
 
 
+def lz4_leg(stream, ends, dev):
+    """mpx with compression (f#4): the batch as frames in one LZ4 frame of 256 KiB blocks (oracle
+    compressor, a Flush every 4096 frames), decompressed on the device (spec_lz4_decompress +
+    spec_lz4_pack, HIP events, device-resident input), next to the oracle's decompression of
+    the same frame on one host core."""
+    import ctypes as C
+
+    from oracle import oracle as O
+    from spec_amd.frames import make_frames_device
+    from spec_amd.lz4 import decompress, frame_blocks
+
+    n = ends.numel()
+    frames = make_frames_device(stream, ends).cpu().numpy()
+    fe = spec_amd.frames_index(frames, n)[0]
+    comp = O.lz4_frame_write(frames, list(fe[4095::4096]) + [frames.size], 256 << 10, close=False)
+    blocks, used, bmax, rc = frame_blocks(comp)
+    d = torch.from_numpy(comp).to(dev)
+    out, sizes, status = decompress(d, blocks, bmax)
+    ok = rc == 0 and out.numel() == frames.size and bool(torch.equal(out.cpu(), torch.from_numpy(frames)))
+    L = spec_amd.lib()
+    nb = len(blocks)
+    db = torch.from_numpy(blocks.view(np.uint8).copy()).to(dev)
+    slots = torch.empty(nb * bmax, dtype=torch.uint8, device=dev)
+    sz = torch.empty(nb, dtype=torch.int32, device=dev)
+    st = torch.empty(nb, dtype=torch.uint8, device=dev)
+    o2 = torch.empty(nb * bmax, dtype=torch.uint8, device=dev)
+    wsb = L.spec_lz4_pack_workspace_size(nb)
+    ws = torch.empty((wsb + 7) // 8, dtype=torch.int64, device=dev)
+    tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    p = C.c_void_p
+
+    def call():
+        s_ = p(torch.cuda.current_stream().cuda_stream)
+        L.spec_lz4_decompress(p(d.data_ptr()), d.numel(), p(db.data_ptr()), nb, p(slots.data_ptr()), bmax,
+                              p(sz.data_ptr()), p(st.data_ptr()), s_)
+        L.spec_lz4_pack(p(slots.data_ptr()), bmax, p(sz.data_ptr()), nb, p(o2.data_ptr()), o2.numel(),
+                        p(tot.data_ptr()), p(ws.data_ptr()), wsb, s_)
+
+    ms, _ = kernel_time_events(call, 5, lead=1)
+    t0 = time.perf_counter()
+    rc_h, host_out, _ = O.lz4_frame_read(comp, frames.size + 16)
+    host_ms = (time.perf_counter() - t0) * 1e3
+    return {"plain_bytes": int(frames.size), "compressed_bytes": int(comp.size), "blocks": nb,
+            "device_ms": round(ms, 3), "device_gb_s": round(frames.size / (ms * 1e-3) / 1e9, 1),
+            "host_oracle_1core_ms": round(host_ms, 1), "ok": bool(ok and rc_h == 0),
+            "note": "one wave per 256 KiB block: bound by the serial sequence chain, ~1 wave per SIMD"}
+
+
 def gather_leg(dec, dist, rank, world, n, steps):
     """BASELINE config 5's collective: each rank decodes its shard, then every rank's columns
     (+ status) go to rank 0 over RCCL (xGMI).  Times decode + gather per step (max over ranks)."""
@@ -385,6 +433,10 @@ def main():
                 extras["frames_index"] = frames_leg(stream, ends, dev)
             except Exception as e:
                 extras["frames_index"] = {"error": repr(e)[:300]}
+            try:
+                extras["lz4"] = lz4_leg(stream, ends, dev)
+            except Exception as e:
+                extras["lz4"] = {"error": repr(e)[:300]}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
