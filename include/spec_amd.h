@@ -185,7 +185,7 @@ int spec_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends, u
  * than cap blocks are complete.  The content checksum (only written when a connection closes)
  * is not verified.
  * spec_lz4_decompress (DEVICE): block k (src[blocks[k].src_off, +src_len)) decompressed into
- * slots + k * slot_bytes (slot_bytes >= the frame's block max size); sizes[k] = its size, or
+ * slots + k * slot_bytes (slot_bytes >= the block max size, a multiple of 16; slots 16-byte aligned); sizes[k] = its size, or
  * all-ones and status[k] = 1 for a corrupt block (pierrec decodeBlock's errors).
  * spec_lz4_pack (DEVICE): the slots gathered into out back to back; *total (device) = bytes,
  * all-ones if any block was corrupt; nothing written if *total > out_cap. */

@@ -67,6 +67,31 @@ __device__ __forceinline__ void win_advance(const Lz4Args &a, __amdgpu_buffer_rs
     W.w2 = src_dword(a, r, base + W.wb + 512 + 4 * (uint32_t)lane);
 }
 
+// ring[from, to) -> dst[from, to), 16 bytes per lane (from 16-aligned; up to 15 bytes past `to`
+// may be written: the slot is a multiple of 16 and bytes past the block's size are never read)
+__device__ __forceinline__ void ring_flush(const uint8_t *ring, uint8_t *dst, uint32_t from, uint32_t to, int lane) {
+    for (uint32_t p = from + 16 * (uint32_t)lane; p < to; p += 1024)
+        *(uint4 *)(dst + p) = *(const uint4 *)(ring + (p & RMASK));
+}
+
+__device__ __forceinline__ void wave_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Output goes to the LDS ring only; the ring is flushed to the slot 4 KiB at a time with
+// 16-byte stores (kept at most ~8 KiB behind), so the sequence loop issues no global stores —
+// on gfx9 stores count in vmcnt, and a store in flight would make every window read wait.
+__device__ __forceinline__ void ring_keep_up(const uint8_t *ring, uint8_t *dst, uint32_t upto, uint32_t &flushed,
+                                             int lane) {
+    if (upto - flushed >= 8192) {
+        wave_fence();
+        ring_flush(ring, dst, flushed, flushed + 4096, lane);
+        flushed += 4096;
+    }
+}
+
 __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t ring[];
     const uint64_t b = blockIdx.x;
@@ -95,7 +120,7 @@ __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
     W.w0 = src_dword(a, r, base + 4 * (uint32_t)lane);
     W.w1 = src_dword(a, r, base + 256 + 4 * (uint32_t)lane);
     W.w2 = src_dword(a, r, base + 512 + 4 * (uint32_t)lane);
-    uint32_t ip = 0, op = 0;
+    uint32_t ip = 0, op = 0, flushed = 0;
     while (!err && ip < n) {
         while (ip - W.wb >= 256) win_advance(a, r, base, W, lane);
         const uint32_t token = win_byte(W, ip++);
@@ -119,6 +144,7 @@ __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
                 break;
             }
             for (uint32_t c = 0; c < ll; c += 64) {
+                ring_keep_up(ring, dst, op + c, flushed, lane);
                 while (ip + c - W.wb >= 256) win_advance(a, r, base, W, lane);
                 const uint32_t rel = ip + c - W.wb + (uint32_t)lane; // < 320
                 const uint32_t addr = ((rel >> 2) & 63) * 4;
@@ -126,10 +152,7 @@ __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
                 const uint32_t v1 = __builtin_amdgcn_ds_bpermute(addr, W.w1);
                 const uint32_t v = (rel >> 8) ? v1 : v0;
                 const uint8_t byte = (uint8_t)(v >> (8 * (rel & 3)));
-                if (c + lane < ll) {
-                    ring[(op + c + lane) & RMASK] = byte;
-                    dst[op + c + lane] = byte;
-                }
+                if (c + lane < ll) ring[(op + c + lane) & RMASK] = byte;
             }
             ip += ll;
             op += ll;
@@ -165,13 +188,16 @@ __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
             err = true;
             break;
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_fence();
         const bool from_ring = off + ml <= RING;
         __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc((void *)dst, (short)0, (int)cap, 0x00020000);
-        if (!from_ring) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this wave's stores reach L2
+        if (!from_ring) { // the source is read back from the slot: everything before op stored first
+            ring_flush(ring, dst, flushed, op, lane);
+            flushed = op & ~15u;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         for (uint32_t c = 0; c < ml; c += 64) {
+            ring_keep_up(ring, dst, op + c, flushed, lane);
             const uint32_t i = c + lane;
             // out[op + i] = out[op - off + (i mod off)]: the source is always output before op
             const uint32_t s = op - off + (off >= ml ? i : i % off);
@@ -181,15 +207,14 @@ __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
                                  : (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(dr, s, 0, 16); // sc1: L2, not L1
             }
             __builtin_amdgcn_wave_barrier();
-            if (i < ml) {
-                ring[(op + i) & RMASK] = byte;
-                dst[op + i] = byte;
-            }
+            if (i < ml) ring[(op + i) & RMASK] = byte;
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_fence();
         op += ml;
+    }
+    if (!err) {
+        wave_fence();
+        ring_flush(ring, dst, flushed, op, lane);
     }
     if (lane == 0) {
         a.sizes[b] = err ? 0xffffffffu : op;

@@ -136,7 +136,8 @@ int spec_lz4_frame_blocks(const uint8_t *buf, uint64_t len, spec_lz4_state *stat
 int spec_lz4_decompress(const uint8_t *src, uint64_t src_len, const spec_lz4_block *blocks, uint64_t nblocks,
                         uint8_t *slots, uint64_t slot_bytes, uint32_t *sizes, uint8_t *status, void *stream) {
     if (nblocks == 0) return SPEC_OK;
-    if (!src || !blocks || !slots || !sizes || !status || slot_bytes == 0 || slot_bytes > (64u << 20))
+    if (!src || !blocks || !slots || !sizes || !status || slot_bytes == 0 || slot_bytes > (64u << 20) ||
+        (slot_bytes & 15) || ((uintptr_t)slots & 15))
         return SPEC_E_INVALID_ARGUMENT;
     if (src_len >= (1ull << 32)) return SPEC_E_TOO_LARGE;
     if (spec::launch_lz4_decompress(src, src_len, blocks, nblocks, slots, slot_bytes, sizes, status,
