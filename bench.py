@@ -420,10 +420,10 @@ def main():
                 eh = ends.cpu().pin_memory()
                 rate, dt, hd = e2e_decode(sh, eh, dev)
                 hcols, hst = hd.columns()
-                ok = bool(torch.equal(hst, status.cpu()) and torch.equal(hcols[13], out_cols[13].cpu())
-                          and torch.equal(hcols[0], out_cols[0].cpu()))
+                e2e_ok = bool(torch.equal(hst, status.cpu()) and torch.equal(hcols[13], out_cols[13].cpu())
+                              and torch.equal(hcols[0], out_cols[0].cpu()))
                 extras["e2e_pinned_decode"] = {
-                    "mmsg_s": round(rate, 1), "ms": round(dt * 1e3, 3), "ok": ok,
+                    "mmsg_s": round(rate, 1), "ms": round(dt * 1e3, 3), "ok": e2e_ok,
                     "note": f"pinned H2D stream+ends, decode, D2H columns+status; {hd.chunks} record chunks "
                             "pipelined over 3 streams, one D2H per chunk (chunk-major outputs)",
                     "pcie_bytes": int(sh.numel() + 8 * n + n * (COLUMN_BYTES + 1))}
