@@ -47,10 +47,28 @@ __device__ __forceinline__ uint32_t be32_lds(const uint8_t *l, uint32_t o) {
     return ((uint32_t)l[o] << 24) | ((uint32_t)l[o + 1] << 16) | ((uint32_t)l[o + 2] << 8) | l[o + 3];
 }
 
-// bytes [s0, s0 + SEG + 8) of buf into lds (zeros past len); buf is 4-byte aligned
+// bytes [s0, s0 + SEG + 16) of buf into lds (zeros past len); buf is 4-byte aligned
 __device__ __forceinline__ void stage_segment(const FiArgs &a, uint64_t s0, uint8_t *lds) {
+    constexpr uint32_t NQ = (FI_SEG + 16) / 16;
+    if (s0 + FI_SEG + 16 <= a.len) { // a whole segment: 16-byte loads, four in flight per thread
+        for (uint32_t i0 = 0; i0 < NQ; i0 += 4 * blockDim.x) {
+            uint4 v[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
+                if (i < NQ) v[j] = *(const uint4 *)(a.buf + s0 + 16ull * i);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
+                if (i < NQ) *(uint4 *)(lds + 16 * i) = v[j];
+            }
+        }
+        __syncthreads();
+        return;
+    }
     uint32_t *l32 = (uint32_t *)lds;
-    for (uint32_t i = threadIdx.x; i < (FI_SEG + 8) / 4; i += blockDim.x) {
+    for (uint32_t i = threadIdx.x; i < (FI_SEG + 16) / 4; i += blockDim.x) {
         const uint64_t p = s0 + 4ull * i;
         uint32_t w = 0;
         if (p + 4 <= a.len) {
@@ -265,7 +283,7 @@ int launch_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends,
     a.seg_entry = (uint32_t *)(w + L.off[6]);
     a.seg_base = (uint64_t *)(w + L.off[7]);
     a.misc = (uint64_t *)(w + L.off[8]);
-    const size_t lds = FI_SEG + 8;
+    const size_t lds = FI_SEG + 16;
     hipLaunchKernelGGL(fi_seg_kernel, dim3(L.nseg), dim3(1024), lds, stream, a);
     hipLaunchKernelGGL(fi_group_kernel, dim3(L.ngroups), dim3(1024), 0, stream, a);
     hipLaunchKernelGGL(fi_chain_kernel, dim3(1), dim3(64), 0, stream, a);
