@@ -309,3 +309,24 @@ int so_parse_batch(const uint8_t *stream, const uint64_t *ends, uint64_t n, uint
     }
     return 0;
 }
+
+/* mpx frame read loop (mpx/conn_reader.go:179-194, connReader.read): io.ReadFull of the 4-byte
+ * head, size = binary.BigEndian.Uint32(head), then io.ReadFull of size bytes — repeated over a
+ * received buffer.  A read that would run past len stops the loop (ReadFull would block for
+ * more bytes): ends[k] = offset just past frame k's message, *consumed = ends of the last
+ * complete frame.  Returns the frame count, or -1 when more than cap frames are complete
+ * (ends[0, cap) written). */
+long long so_frames_read(const uint8_t *buf, uint64_t len, uint64_t *ends, uint64_t cap, uint64_t *consumed) {
+    uint64_t p = 0, k = 0;
+    *consumed = 0;
+    while (p + 4 <= len) {
+        const uint64_t size = ((uint64_t)buf[p] << 24) | ((uint64_t)buf[p + 1] << 16) | ((uint64_t)buf[p + 2] << 8) |
+                              (uint64_t)buf[p + 3];
+        if (p + 4 + size > len) break; /* incomplete message: the next read continues it */
+        if (k == cap) return -1;
+        p += 4 + size;
+        ends[k++] = p;
+        *consumed = p;
+    }
+    return (long long)k;
+}

@@ -218,6 +218,8 @@ def _declare(L):
     L.so_decode_nested_counts.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
     L.so_decode_nested_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64] + [C.c_void_p] * 9
     L.so_parse_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]
+    L.so_frames_read.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
+    L.so_frames_read.restype = C.c_longlong
     # lz4 (oracle/lz4.c)
     L.so_xxh32.argtypes = [C.c_void_p, C.c_size_t, C.c_uint32]
     L.so_xxh32.restype = C.c_uint32
@@ -616,6 +618,18 @@ def parse_batch(stream: np.ndarray, ends: np.ndarray, head: int = 0):
     sz = np.zeros(n, np.uint32)
     lib().so_parse_batch(_ptr(stream), _ptr(ends), n, head, _ptr(st), _ptr(sz))
     return st, sz
+
+
+def frames_read(buf: np.ndarray, cap: int):
+    """mpx connReader.read loop over buf (mpx/conn_reader.go:179-194) -> (ends uint64[k] or None
+    when more than cap frames are complete, consumed)."""
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    ends = np.zeros(max(cap, 1), np.uint64)
+    used = C.c_uint64(0)
+    k = lib().so_frames_read(_ptr(buf) if buf.size else None, buf.size, _ptr(ends), cap, C.byref(used))
+    if k < 0:
+        return None, int(used.value)
+    return ends[:k].copy(), int(used.value)
 
 
 # ---------------------------------------------------------------- lz4 (mpx compression)

@@ -327,6 +327,10 @@ int so_decode_nested_batch(const uint8_t *stream, const uint64_t *ends, uint64_t
 int so_parse_batch(const uint8_t *stream, const uint64_t *ends, uint64_t n, uint32_t head, uint8_t *status,
                    uint32_t *sizes);
 
+/* mpx frame read loop over a received buffer (mpx/conn_reader.go:179-194): frame count and
+ * ends (offset past each complete frame's message), -1 if more than cap frames are complete. */
+long long so_frames_read(const uint8_t *buf, uint64_t len, uint64_t *ends, uint64_t cap, uint64_t *consumed);
+
 /* ---- LZ4 block + frame formats (oracle/lz4.c; mpx compression, pierrec/lz4/v4 restated) ---- */
 uint32_t so_xxh32(const void *data, size_t len, uint32_t seed);
 long long so_lz4_decompress_block(const uint8_t *src, size_t n, uint8_t *dst, size_t cap);

@@ -592,18 +592,14 @@ struct FieldNat {
 template <class Spec, int F>
 struct FieldStore {
     static __device__ __forceinline__ void run(const FastRec<Spec> &fr, long long to_stream, const FieldSet &fs,
-                                               uint64_t r, uint64_t &acc) {
+                                               uint64_t r) {
         if constexpr (F < Spec::N) {
             constexpr uint32_t K = Spec::kind[F];
             if constexpr (K != K_LIST) {
                 const Val v = decode_tail_k<K, true>(fr.w[F], fr.lo[F], fr.e[F], to_stream);
-#if defined(SPEC_EXP) && SPEC_EXP == 3 // diagnostic: decode, no column stores
-                acc ^= v.v0 ^ v.v1 ^ v.v2 ^ v.v3;
-#else
                 store_value_k<K>(fs.cols[F], r, v);
-#endif
             }
-            FieldStore<Spec, F + 1>::run(fr, to_stream, fs, r, acc);
+            FieldStore<Spec, F + 1>::run(fr, to_stream, fs, r);
         }
     }
 };
@@ -691,13 +687,8 @@ __device__ __forceinline__ bool fast_prepare(const LdsSrc &s, int rs, int re, Fa
 template <class Spec>
 __device__ __forceinline__ void fast_finish(const FastRec<Spec> &fr, uint64_t r, const FieldSet &fs,
                                             long long to_stream) {
-    uint64_t acc = 0;
-    FieldStore<Spec, 0>::run(fr, to_stream, fs, r, acc);
-#if defined(SPEC_EXP) && SPEC_EXP == 3
-    if (fs.status) fs.status[r] = (uint8_t)(acc ^ (acc >> 8) ^ (acc >> 16) ^ (acc >> 32));
-#else
+    FieldStore<Spec, 0>::run(fr, to_stream, fs, r);
     if (fs.status) fs.status[r] = ST_OK;
-#endif
 }
 
 // ---- kernel body -------------------------------------------------------------------------
@@ -875,10 +866,6 @@ __device__ __forceinline__ void decode_flat_once(const DecodeArgs &a) {
         const int rs = SLAB_GUARD + (int)(cur.rec_lo - cur.aligned_lo);
         const int re = SLAB_GUARD + (int)(cur.rec_hi - cur.aligned_lo);
         const long long to_stream = (long long)cur.aligned_lo - SLAB_GUARD;
-#if defined(SPEC_EXP) && SPEC_EXP == 1 // diagnostic: staging only
-        if (a.f.status) a.f.status[r] = slab[re - 1];
-        return;
-#endif
         if constexpr (Spec::N > 0) {
             FastRec<Spec> fr;
             if (fast_prepare<Spec>(s, rs, re, fr)) {

@@ -97,13 +97,7 @@ int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream) {
         (void)hipMemsetAsync(a.total, 0, sizeof(uint64_t), stream);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    // SPEC_AMD_COUNT_GLOBAL=1 (A/B): the count kernel reads each record's trailer and list
-    // trailer straight from HBM (no LDS staging of the whole group)
-    static const bool count_global = [] {
-        const char *e = getenv("SPEC_AMD_COUNT_GLOBAL");
-        return e && e[0] == '1';
-    }();
-    a.slab = count_global ? 0 : decode_slab_bytes(avg_record);
+    a.slab = decode_slab_bytes(avg_record);
     const uint64_t groups = (a.n + 63) / 64;
     dim3 grid((unsigned)((groups + DEC_WAVES - 1) / DEC_WAVES)), block(64 * DEC_WAVES);
     hipLaunchKernelGGL(nested_count_kernel, grid, block, (size_t)DEC_WAVES * a.slab, stream, a);

@@ -280,29 +280,18 @@ __device__ __forceinline__ void nested_group_body(const Src &s, long long rs, lo
                                                   uint64_t g, uint64_t item_base, int lane, long long to_stream,
                                                   const NestedArgs &a) {
     ListInfo li = {0, 0, 0, 0, false};
-#if defined(SPEC_EXP) && (SPEC_EXP == 8 || SPEC_EXP == 9) // diagnostic (timing only): lists, no outer columns
-    if (valid) li = list_open(s, rec_open(s, (typename Src::pos_t)rs, (typename Src::pos_t)re), a);
-#else
     if (valid) li = decode_outer<OSpec>(s, rs, re, r, to_stream, a);
-#endif
     const uint32_t incl = wave_incl_scan(li.count, lane);
     const uint32_t excl = incl - li.count;
     const uint32_t total = __shfl(incl, 63);
     if constexpr (ONEPASS) {
-#if defined(SPEC_EXP) && (SPEC_EXP == 5 || SPEC_EXP == 6) // diagnostic (timing only): no look-back
-        item_base = 0;
-#else
         item_base = uniform64(lookback(a.group_base, g, total, lane));
-#endif
         if (g == (a.n - 1) / 64 && lane == 0) *a.total = item_base + total;
     }
     if (valid) {
         a.item_begin[r] = (uint32_t)(item_base + excl);
         if (r == a.n - 1) a.item_begin[a.n] = (uint32_t)(item_base + incl);
     }
-#if defined(SPEC_EXP) && (SPEC_EXP == 7 || SPEC_EXP == 9) // diagnostic (timing only): no items
-    return;
-#endif
     decode_group_items<ISpec>(s, li, excl, total, item_base, lane, to_stream, a);
 }
 
@@ -316,13 +305,9 @@ __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
     const uint64_t ngroups = (a.n + 63) / 64;
     uint64_t g;
     if constexpr (ONEPASS) {
-#if defined(SPEC_EXP) && SPEC_EXP == 5 // diagnostic (timing only): no ticket
-        g = blockIdx.x;
-#else
         uint32_t t = 0;
         if (lane == 0) t = atomicAdd((unsigned int *)&a.group_base[ngroups], 1u);
         g = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
-#endif
     } else {
         g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
     }

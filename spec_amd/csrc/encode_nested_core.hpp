@@ -328,11 +328,7 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
     LdsSink k{slab, (int)(smem + 160 - slab)}; // dummy dword in the header
     // A: outer records, the items skipped
     WaveListEmit le{pre + (L.b - L.I0), ls.count, (uint32_t)ls.data, ls.big, 0};
-#if defined(NENC_EXP) && NENC_EXP == 1 // diagnostic (timing only): no outer emission
-    le.lstart = (int)(head + (start - S));
-#else
     if (L.valid) OP::emit(a.outer, k, (int)(head + (start - S)), L.r, orec, rs, inv_outer, le);
-#endif
     wave_sync();
     const int lst = le.lstart;
     const bool fix = L.valid && ls.count > 0 && (lst & 3);
@@ -356,15 +352,11 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
         for (int st = 32; st > 0; st >>= 1)
             if (__shfl(L.b, o + st) <= i) o += st;
         const int pos = __shfl(lbase, o) + (int)pre[iv ? kk : 0u];
-#if defined(NENC_EXP) && NENC_EXP == 2 // diagnostic (timing only): items loaded, not emitted
-        if (iv) k.st4a(pos & ~3, (uint32_t)cur.v[0][0]);
-#else
         if (iv) {
             bool e2 = false;
             const RecSize irs = IP::size(a.item, cur, i, false, e2);
             IP::emit(a.item, k, pos, i, cur, irs, inv_item);
         }
-#endif
         wave_sync();
         cur = nxt;
     }

@@ -50,7 +50,9 @@ __device__ __forceinline__ uint32_t be32_lds(const uint8_t *l, uint32_t o) {
 // bytes [s0, s0 + SEG + 16) of buf into lds (zeros past len); buf is 4-byte aligned
 __device__ __forceinline__ void stage_segment(const FiArgs &a, uint64_t s0, uint8_t *lds) {
     constexpr uint32_t NQ = (FI_SEG + 16) / 16;
-    if (s0 + FI_SEG + 16 <= a.len) { // a whole segment: 16-byte loads, four in flight per thread
+    // a whole segment from a 16-byte aligned buffer: 16-byte loads, four in flight per thread
+    // (the ABI only promises 4-byte alignment: other buffers take the dword loop)
+    if (s0 + FI_SEG + 16 <= a.len && ((uintptr_t)a.buf & 15) == 0) {
         for (uint32_t i0 = 0; i0 < NQ; i0 += 4 * blockDim.x) {
             uint4 v[4];
 #pragma unroll

@@ -19,6 +19,10 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <dlfcn.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <mutex>
 #include <sstream>
 #include <string>
@@ -208,34 +212,16 @@ const char *prog_name(Prog p) {
 }
 
 // hiprtc compile only; returns the code object (empty on failure)
-std::vector<char> compile_source(const std::string &src, Prog p) {
+std::vector<char> compile_uncached(const std::string &src, Prog p, const char *const *opts_in, int nopts) {
     const char *hdr_src[5] = {kSpecDeviceHpp, kDecodeCoreHpp, kEncodeCoreHpp, kDecodeNestedCoreHpp,
                               kEncodeNestedCoreHpp};
     const char *hdr_name[5] = {"spec_device.hpp", "decode_core.hpp", "encode_core.hpp", "decode_nested_core.hpp",
                                "encode_nested_core.hpp"};
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), prog_name(p), 5, hdr_src, hdr_name) != HIPRTC_SUCCESS) return {};
-    // SPEC_AMD_EXP=n: diagnostic variants of the kernel body (decode_core.hpp), timing only
-    static std::string exp = [] {
-        const char *e = getenv("SPEC_AMD_EXP");
-        return std::string(e && e[0] ? std::string("-DSPEC_EXP=") + e : std::string("-DSPEC_EXP=0"));
-    }();
-    // SPEC_AMD_JIT_DEFS="A=1,B": extra -D options (kernel variants for A/B timing)
-    static std::vector<std::string> defs = [] {
-        std::vector<std::string> v;
-        const char *e = getenv("SPEC_AMD_JIT_DEFS");
-        std::string s = e ? e : "";
-        size_t p = 0;
-        while (p < s.size()) {
-            size_t q = s.find(',', p);
-            if (q == std::string::npos) q = s.size();
-            if (q > p) v.push_back("-D" + s.substr(p, q - p));
-            p = q + 1;
-        }
-        return v;
-    }();
-    std::vector<const char *> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17", exp.c_str()};
-    for (const std::string &d : defs) opts.push_back(d.c_str());
+    // the product kernels are compiled with fixed options only: no environment variable can
+    // change what a kernel computes
+    std::vector<const char *> opts(opts_in, opts_in + nopts);
     hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
     if (rc != HIPRTC_SUCCESS || debug()) {
         size_t ls = 0;
@@ -247,6 +233,7 @@ std::vector<char> compile_source(const std::string &src, Prog p) {
         }
     }
     if (rc != HIPRTC_SUCCESS) {
+        fprintf(stderr, "spec_amd jit: hiprtc compile of %s failed; the generic kernel is used\n", prog_name(p));
         hiprtcDestroyProgram(&prog);
         return {};
     }
@@ -270,6 +257,75 @@ std::vector<char> compile_source(const std::string &src, Prog p) {
             fclose(f);
         }
     }
+    return code;
+}
+
+// ---- on-disk code-object cache -----------------------------------------------------------
+// A compile costs ~3 s per (schema, kernel set); its result depends only on the generated
+// source, the embedded headers and the options, so it is cached under <libdir>/jit_cache
+// (next to libspec_amd.so: build() fills it for the benchmark schemas, and it travels with the
+// library) or, where that is not writable, $XDG_CACHE_HOME/spec_amd or ~/.cache/spec_amd.
+uint64_t fnv1a(uint64_t h, const char *p, size_t n) {
+    for (size_t i = 0; i < n; i++) h = (h ^ (uint8_t)p[i]) * 0x100000001b3ull;
+    return h;
+}
+
+std::string lib_dir() {
+    Dl_info info;
+    if (dladdr((void *)&fnv1a, &info) && info.dli_fname) {
+        std::string f = info.dli_fname;
+        size_t k = f.rfind('/');
+        return k == std::string::npos ? std::string(".") : f.substr(0, k);
+    }
+    return ".";
+}
+
+std::vector<std::string> cache_dirs() {
+    std::vector<std::string> v = {lib_dir() + "/jit_cache"};
+    if (const char *x = getenv("XDG_CACHE_HOME")) v.push_back(std::string(x) + "/spec_amd");
+    else if (const char *h = getenv("HOME")) v.push_back(std::string(h) + "/.cache/spec_amd");
+    return v;
+}
+
+bool read_file(const std::string &path, std::vector<char> &out) {
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    fseek(f, 0, SEEK_END);
+    long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    out.resize(n > 0 ? (size_t)n : 0);
+    bool ok = n > 0 && fread(out.data(), 1, (size_t)n, f) == (size_t)n;
+    fclose(f);
+    return ok;
+}
+
+void write_cache(const std::string &name, const std::vector<char> &code) {
+    for (const std::string &d : cache_dirs()) {
+        mkdir(d.c_str(), 0755); // best effort; a missing parent makes the open below fail
+        const std::string tmp = d + "/." + name + "." + std::to_string(getpid());
+        FILE *f = fopen(tmp.c_str(), "wb");
+        if (!f) continue;
+        bool ok = fwrite(code.data(), 1, code.size(), f) == code.size();
+        ok = (fclose(f) == 0) && ok;
+        if (ok && rename(tmp.c_str(), (d + "/" + name).c_str()) == 0) return;
+        unlink(tmp.c_str());
+    }
+}
+
+std::vector<char> compile_source(const std::string &src, Prog p) {
+    static const char *const kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    uint64_t h = 0xcbf29ce484222325ull;
+    h = fnv1a(h, src.data(), src.size());
+    for (const char *hs : {kSpecDeviceHpp, kDecodeCoreHpp, kEncodeCoreHpp, kDecodeNestedCoreHpp, kEncodeNestedCoreHpp})
+        h = fnv1a(h, hs, strlen(hs) + 1);
+    for (const char *o : kOpts) h = fnv1a(h, o, strlen(o) + 1);
+    char name[64];
+    snprintf(name, sizeof name, "%016llx.co", (unsigned long long)h);
+    std::vector<char> cached;
+    for (const std::string &d : cache_dirs())
+        if (read_file(d + "/" + name, cached)) return cached;
+    std::vector<char> code = compile_uncached(src, p, kOpts, (int)(sizeof kOpts / sizeof kOpts[0]));
+    if (!code.empty()) write_cache(name, code);
     return code;
 }
 
@@ -305,7 +361,7 @@ const Entry *lookup_key(const std::string &k, Prog p, Make make) {
     auto it = g_cache.find(k);
     if (it == g_cache.end()) {
         Entry e = load(make(), p);
-        if (e.failed && debug()) fprintf(stderr, "spec_amd jit: compile/load failed, generic kernel in use\n");
+        if (e.failed) fprintf(stderr, "spec_amd jit: compile/load failed, generic kernel in use\n");
         it = g_cache.emplace(k, e).first;
     }
     return it->second.failed ? nullptr : &it->second;

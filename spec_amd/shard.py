@@ -5,13 +5,19 @@ per rank, with no data-path collective.  `shard_bounds` gives rank k's records;
 `shard_batch` cuts its bytes and rebases its `ends`; decoded string/bytes spans then point
 into the rank's shard (a span's global offset = shard byte base + off: a 16M-record batch is
 > 4 GiB, beyond 32-bit offsets, so spans stay shard-relative and the bases travel alongside).
-`gather_columns` is the one collective of config 5: every rank's columns to rank 0
-(torch.distributed, backend "nccl" = RCCL over xGMI on MI355X; "gloo" in the CPU tests).
+
+The one collective of config 5 gathers every rank's decoded columns to rank 0.  Each rank's
+columns and status live in ONE packed buffer (`PackedColumns`: column 0 of all records, then
+column 1, ..., then the status bytes), which the decode kernel writes directly, so the gather
+is a single `dist.gather` per rank — on backend "nccl" (RCCL over xGMI on MI355X) torch runs it
+as grouped ncclSend/ncclRecv; "gloo" (CPU tests) gets host copies.
 """
 from __future__ import annotations
 
 import numpy as np
 import torch
+
+from .schema import Schema
 
 
 def shard_bounds(n: int, world: int, rank: int):
@@ -30,24 +36,74 @@ def shard_batch(stream, ends, world: int, rank: int):
     return s, e, b0, (r0, r1)
 
 
-def gather_columns(cols, dist, dst: int = 0, group=None):
-    """Gather every rank's decoded columns (list of uint8 [n_k, w] tensors, equal n_k or not)
-    to rank `dst`.  Returns on dst a list (per column) of per-rank tensors, else None."""
-    world = dist.get_world_size(group)
+class PackedColumns:
+    """Decoded columns + status of n records in one contiguous uint8 buffer (record-major per
+    column): `cols[f]` is a [n, width_f] view, `status` a [n] view.  Pass `cols`/`status` to
+    spec_amd.Decoder so the decode writes the packed layout directly."""
+
+    def __init__(self, schema: Schema, n: int, device="cuda", buf: torch.Tensor | None = None):
+        self.schema, self.n = schema, n
+        self.nbytes = n * (schema.column_bytes + 1)
+        self.buf = buf if buf is not None else torch.empty(max(self.nbytes, 1), dtype=torch.uint8, device=device)
+        if self.buf.numel() < self.nbytes:
+            raise ValueError("packed buffer too small")
+        self.cols, off = [], 0
+        for w in schema.widths:
+            self.cols.append(self.buf[off: off + n * w].view(n, w))
+            off += n * w
+        self.status = self.buf[off: off + n]
+
+
+def _gather_sizes(nbytes: int, dist, group, device):
+    t = torch.tensor([nbytes], dtype=torch.int64, device=device)
+    sizes = [torch.zeros_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(sizes, t, group=group)
+    return [int(s.item()) for s in sizes]
+
+
+def gather_packed(buf: torch.Tensor, dist, dst: int = 0, group=None, sizes=None):
+    """Gather every rank's packed uint8 buffer to rank `dst` with ONE collective.  Buffers may
+    differ in size (padded to the largest for the collective, trimmed after); pass `sizes`
+    (bytes per rank) when known to skip the size exchange.  Returns the per-rank buffers on
+    dst (a list of 1-D uint8 tensors), None elsewhere."""
     rank = dist.get_rank(group)
-    n_local = torch.tensor([cols[0].shape[0] if cols else 0], dtype=torch.int64, device=cols[0].device)
-    sizes = [torch.zeros_like(n_local) for _ in range(world)]
-    dist.all_gather(sizes, n_local, group=group)
-    sizes = [int(s.item()) for s in sizes]
-    nmax = max(sizes)
-    out = [] if rank == dst else None
-    for c in cols:
-        pad = c
-        if c.shape[0] < nmax:  # collectives need equal shapes: pad, trim after
-            pad = torch.zeros((nmax, c.shape[1]), dtype=c.dtype, device=c.device)
-            pad[: c.shape[0]] = c
-        bufs = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
-        dist.gather(pad, gather_list=bufs, dst=dst, group=group)
-        if rank == dst:
-            out.append([b[: sizes[k]] for k, b in enumerate(bufs)])
+    world = dist.get_world_size(group)
+    on_host = dist.get_backend(group) == "gloo"
+    src = buf.reshape(-1)
+    if on_host and src.is_cuda:
+        src = src.cpu()
+    if sizes is None:
+        sizes = _gather_sizes(src.numel(), dist, group, src.device)
+    nmax = max(sizes) if sizes else 0
+    if src.numel() < nmax:  # collectives need equal shapes
+        pad = torch.zeros(nmax, dtype=torch.uint8, device=src.device)
+        pad[: src.numel()] = src
+        src = pad
+    bufs = [torch.empty(nmax, dtype=torch.uint8, device=src.device) for _ in range(world)] if rank == dst else None
+    dist.gather(src, gather_list=bufs, dst=dst, group=group)
+    if rank != dst:
+        return None
+    return [b[: sizes[k]] for k, b in enumerate(bufs)]
+
+
+def gather_columns(cols, dist, dst: int = 0, group=None):
+    """Gather every rank's decoded columns (list of uint8 [n_k, w] tensors) to rank `dst`,
+    packed into one buffer per rank (one collective).  Returns on dst a list (per column) of
+    per-rank [n_k, w] tensors, else None.  Every rank must pass the same column widths."""
+    if not cols:
+        return [] if dist.get_rank(group) == dst else None
+    widths = [int(c.shape[1]) for c in cols]
+    n_local = int(cols[0].shape[0])
+    packed = torch.cat([c.reshape(-1) for c in cols]) if n_local else cols[0].new_empty(0)
+    parts = gather_packed(packed, dist, dst, group)
+    if parts is None:
+        return None
+    row = sum(widths)
+    out = [[] for _ in cols]
+    for p in parts:
+        n_k = p.numel() // row if row else 0
+        off = 0
+        for f, w in enumerate(widths):
+            out[f].append(p[off: off + n_k * w].view(n_k, w))
+            off += n_k * w
     return out

@@ -29,6 +29,9 @@ def test_frames_index_matches_walk():
     got, used = spec_amd.frames_index(fr)
     want, wused = walk(fr)
     assert list(got) == want and used == wused == fr.size
+    o_ends, o_used = O.frames_read(fr, n)  # the oracle's mpx read loop
+    assert np.array_equal(o_ends, got) and o_used == used
+    assert np.array_equal(got, np.cumsum(np.diff(np.concatenate([[0], ends])) + 4))
     # records are recovered exactly
     starts = np.concatenate([[0], got[:-1]]).astype(np.int64) + 4
     for i in range(0, n, 37):

@@ -1,11 +1,14 @@
-"""GPU frame index (spec_frames_index_device) against the host walk (spec_frames_index): the
-same ends, count, consumed and capacity status, on mpx frame buffers of every shape the
-parallel algorithm distinguishes (segment boundaries, incomplete tails, frames longer than the
-entry window -> serial fallback, tiny frames -> step cap -> fallback, garbage)."""
+"""GPU frame index (spec_frames_index_device) against the oracle's restatement of the mpx read
+loop (oracle.frames_read, mpx/conn_reader.go:179-194) and, where the test builds the frames
+from known message sizes, against the cumulative sum of those sizes: the same ends, count,
+consumed and capacity status, on mpx frame buffers of every shape the parallel algorithm
+distinguishes (segment boundaries, incomplete tails, frames longer than the entry window ->
+serial fallback, tiny frames -> step cap -> fallback, garbage, buffers only 4-byte aligned)."""
 from __future__ import annotations
 
 import numpy as np
 import pytest
+import torch
 
 import spec_amd
 from oracle import oracle as O
@@ -25,25 +28,40 @@ def frames_of(sizes, rng, tail=b""):
     return np.frombuffer(bytes(out) + tail, dtype=np.uint8)
 
 
-def check(dev, buf, cap=None, label=""):
+def check(dev, buf, cap=None, label="", sizes=None, offset=0):
+    """Device index of buf (placed `offset` bytes into a 256-byte aligned allocation) vs the
+    oracle read loop; with `sizes`, also vs cumsum(4 + size) of the frames the test wrote."""
     buf = np.ascontiguousarray(buf, dtype=np.uint8)
     cap_h = cap if cap is not None else max(1, buf.size // 4)
-    want_ends, want_used = spec_amd.frames_index(buf, cap_h)
-    d = to_dev(buf if buf.size else np.zeros(4, np.uint8), dev)[: buf.size]
+    want_ends, want_used = O.frames_read(buf, cap_h)
+    over = want_ends is None
+    if over:  # more than cap complete frames: the first cap of them
+        want_ends, _ = O.frames_read(buf, buf.size // 4 + 1)
+        want_ends = want_ends[:cap_h]
+        want_used = int(want_ends[-1]) if cap_h else 0
+    if sizes is not None:
+        known = np.cumsum(np.asarray(sizes, np.uint64) + np.uint64(4))
+        k = want_ends.size
+        assert np.array_equal(known[:k], want_ends), f"{label}: oracle vs known sizes"
+    room = torch.zeros(offset + max(buf.size, 4), dtype=torch.uint8)
+    room[offset: offset + buf.size] = torch.from_numpy(buf)
+    d = room.to(dev)[offset: offset + buf.size]
     ends, used, st = spec_amd.frames_index_device(d, cap_h)
     got = ends.cpu().numpy().view(np.uint64)
     assert used == want_used, f"{label}: consumed {used} vs {want_used}"
     assert np.array_equal(got, want_ends), f"{label}: ends differ ({got.size} vs {want_ends.size} frames)"
-    # capacity status as the host call's return code
-    more = spec_amd.frames_index(buf, max(1, buf.size // 4 + 1))[0].size
-    assert st == (-4 if more > cap_h else 0), f"{label}: status {st}"
+    assert st == (-4 if over else 0), f"{label}: status {st}"
+    # the host indexer (product, CPU) agrees too
+    h_ends, h_used = spec_amd.frames_index(buf, cap_h)
+    assert np.array_equal(h_ends, want_ends) and h_used == want_used, f"{label}: host walk"
 
 
 @pytest.mark.parametrize("seed", range(3))
 def test_random_frames(dev, seed):
     rng = np.random.default_rng(seed)
     sizes = rng.integers(0, 600, 20000)
-    check(dev, frames_of(sizes, rng), label=f"random {seed}")
+    check(dev, frames_of(sizes, rng), label=f"random {seed}", sizes=sizes)
+    check(dev, frames_of(sizes, rng), label=f"random {seed} at +4", sizes=sizes, offset=4)
     # incomplete tails: a partial head, a partial frame
     check(dev, frames_of(sizes[:5000], rng, tail=b"\x00\x00"), label="partial head")
     check(dev, frames_of(sizes[:5000], rng, tail=b"\x00\x00\x01\x00" + b"x" * 100), label="partial frame")
@@ -55,16 +73,17 @@ def test_segment_boundaries(dev):
     rng = np.random.default_rng(9)
     for first in (SEG - 4, SEG - 5, SEG - 6, SEG - 7, SEG - 2048 - 4, SEG - 2049 - 4):
         sizes = [first] + list(rng.integers(0, 300, 500))
-        check(dev, frames_of(sizes, rng), label=f"first={first}")
+        check(dev, frames_of(sizes, rng), label=f"first={first}", sizes=sizes)
+        check(dev, frames_of(sizes, rng), label=f"first={first} at +12", sizes=sizes, offset=12)
     sizes = [SEG - 4] * 3
-    check(dev, frames_of(sizes, rng), label="exact segments")
+    check(dev, frames_of(sizes, rng), label="exact segments", sizes=sizes)
 
 
 def test_long_frames_fall_back(dev):
     """Frames longer than the 2048-byte entry window (and > 64 KiB) take the serial walk."""
     rng = np.random.default_rng(4)
     sizes = list(rng.integers(0, 300, 2000)) + [5000, 70000, 3] + list(rng.integers(0, 300, 2000))
-    check(dev, frames_of(sizes, rng), label="long frames")
+    check(dev, frames_of(sizes, rng), label="long frames", sizes=sizes)
 
 
 def test_tiny_frames_fall_back(dev):
@@ -77,6 +96,7 @@ def test_capacity_and_small(dev):
     buf = frames_of(rng.integers(0, 100, 3000), rng)
     for cap in (1, 10, 2999, 3000, 3001):
         check(dev, buf, cap=cap, label=f"cap {cap}")
+        check(dev, buf, cap=cap, label=f"cap {cap} at +4", offset=4)
     for n in (0, 1, 3, 4):
         check(dev, np.zeros(n, np.uint8) + 0, label=f"len {n}")
     check(dev, np.array([0, 0, 0, 1, 7], np.uint8), label="one byte frame")
@@ -92,8 +112,6 @@ def test_garbage(dev):
 
 def test_flat16_frames_then_decode(dev):
     """The receive path on the device: frames indexed on the GPU, decoded in place."""
-    import torch
-
     n = 100_000
     cols, heaps = workload.flat16(n, seed=6)
     stream, ends = O.encode_flat_batch(FLAT16.tags, FLAT16.kinds, cols, [heaps.get(f) for f in range(16)], n)

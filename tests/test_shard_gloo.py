@@ -1,7 +1,6 @@
-"""Multi-process (world_size 2, gloo, CPU) test of the record sharding and the column gather
-used by the multi-GPU path: each rank decodes its shard (with the oracle standing in for the
-GPU decode — this test covers the plumbing), rank 0 gathers and compares with a one-process
-decode of the whole batch."""
+"""Multi-process (world_size 2, gloo, CPU) tests of the record sharding and the packed column
+gather used by the multi-GPU path.  Here the oracle stands in for the decode (no GPU in this
+container); tests/test_gpu_shard.py runs the same flow with the HIP decode in every rank."""
 from __future__ import annotations
 
 import os
@@ -12,7 +11,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from spec_amd.shard import gather_columns, shard_batch, shard_bounds
+from spec_amd.shard import gather_columns, gather_packed, shard_batch, shard_bounds
 
 
 def _free_port():
@@ -21,6 +20,19 @@ def _free_port():
     p = s.getsockname()[1]
     s.close()
     return p
+
+
+def rebase_spans(parts, bases, kind_is_span):
+    """Concatenate per-rank column parts; shard-relative spans of non-empty values get their
+    shard's byte base added (what a consumer of config 5's gathered columns does)."""
+    if not kind_is_span:
+        return np.concatenate([p.numpy() if isinstance(p, torch.Tensor) else p for p in parts])
+    fixed = []
+    for k, p in enumerate(parts):
+        a = (p.numpy() if isinstance(p, torch.Tensor) else p).view(np.uint32).copy()
+        a[:, 0] += np.where(a[:, 1] > 0, np.uint32(int(bases[k])), np.uint32(0))
+        fixed.append(a.view(np.uint8))
+    return np.concatenate(fixed)
 
 
 def _worker(rank, world, port, q):
@@ -42,22 +54,20 @@ def _worker(rank, world, port, q):
         got = gather_columns([torch.from_numpy(c) for c in dec] + [torch.from_numpy(st).reshape(-1, 1)], dist)
         bases = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
         dist.all_gather(bases, torch.tensor([base], dtype=torch.int64))
+        # unequal sizes and an empty rank through the packed gather
+        mine = torch.arange(rank * 7, dtype=torch.int64).to(torch.uint8)
+        packed = gather_packed(mine, dist)
+        empty = gather_columns([], dist)
         if rank == 0:
             want, wst = O.decode_flat_batch(FLAT16.tags, FLAT16.kinds, stream, ends, FLAT16.widths)
             ok = True
             for f, fld in enumerate(FLAT16.fields):
-                parts = got[f]
-                if fld.kind.name in ("STRING", "BYTES"):  # shard-relative spans: add the shard base
-                    fixed = []
-                    for k, p in enumerate(parts):
-                        a = p.numpy().view(np.uint32).copy()
-                        a[:, 0] += np.where(a[:, 1] > 0, np.uint32(int(bases[k])), np.uint32(0))
-                        fixed.append(a.view(np.uint8))
-                    g = np.concatenate(fixed)
-                else:
-                    g = np.concatenate([p.numpy() for p in parts])
+                g = rebase_spans(got[f], bases, fld.kind.name in ("STRING", "BYTES"))
                 ok = ok and np.array_equal(g, want[f])
             ok = ok and np.array_equal(np.concatenate([p.numpy().ravel() for p in got[16]]), wst)
+            ok = ok and [p.numel() for p in packed] == [k * 7 for k in range(world)]
+            ok = ok and all(torch.equal(p, torch.arange(k * 7).to(torch.uint8)) for k, p in enumerate(packed))
+            ok = ok and empty == []
             q.put(ok)
     finally:
         dist.destroy_process_group()
