@@ -8,7 +8,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 echo "== pytest -m gpu"
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?; tail -n 3 $OUT/pytest_gpu.log; echo "pytest_rc=$rc"
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 echo "== smoke"
