@@ -1,6 +1,6 @@
-"""Nested (config 4) decode timing on one GPU: one-pass and two-pass, per launch (HIP events).
-Prints one JSON line; env variables (SPEC_AMD_JIT, SPEC_AMD_EXP, SPEC_AMD_JIT_DEFS) select
-kernel variants, so tools/ab.py-style interleaved runs compare them."""
+"""Nested (config 4) decode and encode timing on one GPU: one-pass and two-pass decode and the
+encode, per launch (HIP events).  Prints one JSON line.  Also the command profiled for the
+nested kernels' rocprofv3 stats and PMC passes (tools/gpu_round.sh)."""
 import json
 import os
 import sys
@@ -34,12 +34,17 @@ def main():
         d.decode()
 
     res = {}
+    enc = spec_amd.NestedEncoder(NESTED, n, dev)
+    out = torch.empty_like(stream)
+    e2 = torch.empty_like(ends)
+    enc_ms, _ = bench.kernel_time_events(lambda: enc.encode(outer, oh, ib, items, ih, m, out, e2), 10)
     two_ms, _ = bench.kernel_time_events(two, 20)
     one_ms, _ = bench.kernel_time_events(d.decode_onepass, 20)
     torch.cuda.synchronize()
     ok = int(d.total.item()) == m and torch.equal(d.items[0], items[0]) and torch.equal(d.item_begin, ib)
-    res["nested"] = {"onepass_ms": round(one_ms, 4), "twopass_ms": round(two_ms, 4), "ok": bool(ok),
-                     "med": round(one_ms, 4)}
+    ok = ok and torch.equal(out, stream)
+    res["nested"] = {"onepass_ms": round(one_ms, 4), "twopass_ms": round(two_ms, 4), "encode_ms": round(enc_ms, 4),
+                     "ok": bool(ok), "med": round(one_ms, 4)}
     print(json.dumps(res))
 
 
