@@ -54,8 +54,12 @@ typedef enum spec_kind {
     SPEC_KIND_BIN256 = 13, /* 32 opaque bytes  Message.Bin256   / FieldWriter.Bin256  */
     SPEC_KIND_STRING = 14, /* spec_span        Message.String   / FieldWriter.String  */
     SPEC_KIND_BYTES = 15,  /* spec_span        Message.Bytes    / FieldWriter.Bytes   */
-    SPEC_KIND_LIST = 16,   /* list<message>: only in spec_nested_schema.outer; its column is
-                              the item_begin CSR index   Message.List / FieldWriter.List */
+    SPEC_KIND_LIST = 16,   /* list<message> in spec_nested_schema.outer (its column is the item_begin CSR
+                              index); in a spec_tree, a list of any element kind.
+                                               Message.List / FieldWriter.List                    */
+    SPEC_KIND_STRUCT = 17, /* spec_tree only: a generated struct (OpenXxx(FieldRaw) / EncodeXxxTo)   */
+    SPEC_KIND_MESSAGE = 18,/* spec_tree only: a sub-message (Message(tag) / FieldWriter.Message)     */
+    SPEC_KIND_ANY = 19,    /* spec_tree only: spec_span of the raw value (Field(tag) / Field(tag).Any) */
 } spec_kind;
 
 /* Per-record status: the error class OpenMessageErr returns for the record
@@ -108,6 +112,107 @@ typedef struct spec_nested_schema {
     spec_schema outer;
     spec_schema item;
 } spec_nested_schema;
+
+/* ---- schema trees: every kind a generated reader/writer handles ----
+ * A spec_tree describes a record message as fields in PRE-ORDER: each field names its enclosing
+ * field (`parent`, an earlier index; -1 = the record).  Enclosing fields are
+ *   SPEC_KIND_MESSAGE            its children are the sub-message's fields (write order);
+ *   SPEC_KIND_STRUCT             its children are the struct's members (scalar kinds, declaration
+ *                                order; the struct is decoded members-last-first, as generated
+ *                                Decode does: internal/lang/generator/struct.go:75-113);
+ *   SPEC_KIND_LIST, elem MESSAGE its children are the item message's fields;
+ *   SPEC_KIND_LIST, elem STRUCT  its children are the struct's members.
+ * A list of scalars (elem = a scalar kind) has no children.  Enums are SPEC_KIND_INT32
+ * (internal/lang/generator/enum.go:69-92).  Recursive types (pkg1.spec Submessage.next) are
+ * unrolled to the depth the caller reads, exactly as a reader only opens what it accesses.
+ *
+ * Decoded output is a set of TABLES (spec_tree_layout): table 0 = the records; one table per
+ * MESSAGE field (a row per row of its owner table: the sub-message of that row) and one per
+ * LIST field (a row per list element, CSR-indexed by `begin` over its owner's rows).  Columns,
+ * table by table, in this order:
+ *   [BEGIN]  (LIST tables) uint32 [owner rows + 1]: row i's elements are [begin[i], begin[i+1])
+ *   per direct field, in field order:
+ *     scalar          VALUE  m.<Kind>(tag)                          (internal/types/msg.go:219-421)
+ *     STRUCT          VALUE per member: OpenXxx(m.FieldRaw(tag))    (msg.go:139-150)
+ *     ANY             VALUE spec_span of m.Field(tag) = OpenValue   (msg.go:108-124, value.go:18-31)
+ *     MESSAGE, LIST   PRESENT uint8 m.HasField(tag)                 (msg.go:101-106)
+ *   a list of scalars: VALUE = ValueList.Get(i) (list_value.go:87-92); a list of structs: a
+ *   VALUE per member;
+ *   STATUS uint8: records OpenMessageErr's class; sub-messages MessageErr's class (0 if absent);
+ *   list items OpenItemErr's class or SPEC_STATUS_PANIC (Go panics: element start > end);
+ *   list values / structs SPEC_STATUS_INVALID_VALUE when GetErr fails; any row whose struct or
+ *   any field would make Go panic (slice out of range) SPEC_STATUS_PANIC.
+ * Encode input uses the same columns (STATUS ignored): scalars and structs are always written,
+ * MESSAGE / LIST fields when PRESENT is non-zero (a present list may be empty), ANY when its span
+ * is non-empty (FieldWriter.Any copies the bytes: internal/writer/writer.go:438-456). */
+#define SPEC_TREE_MAX_FIELDS 256
+#define SPEC_TREE_MAX_TABLES 64
+#define SPEC_TREE_MAX_COLUMNS 512
+#define SPEC_TREE_MAX_DIRECT 64 /* direct fields of one message / members of one struct */
+
+typedef struct spec_tree_field {
+    uint16_t tag;    /* field tag (ignored for struct members) */
+    uint8_t kind;    /* spec_kind */
+    uint8_t elem;    /* SPEC_KIND_LIST: element kind (a scalar kind, STRUCT or MESSAGE) */
+    int16_t parent;  /* enclosing field, -1 = the record */
+    uint16_t reserved;
+} spec_tree_field;
+
+typedef struct spec_tree {
+    uint32_t nfields;
+    spec_tree_field fields[SPEC_TREE_MAX_FIELDS];
+} spec_tree;
+
+typedef enum spec_tree_rel { SPEC_REL_ROOT = 0, SPEC_REL_ONE = 1, SPEC_REL_MANY = 2 } spec_tree_rel;
+typedef enum spec_tree_shape { SPEC_SHAPE_MESSAGE = 0, SPEC_SHAPE_VALUE = 1, SPEC_SHAPE_STRUCT = 2 } spec_tree_shape;
+typedef enum spec_tree_role {
+    SPEC_COL_VALUE = 0, SPEC_COL_PRESENT = 1, SPEC_COL_BEGIN = 2, SPEC_COL_STATUS = 3
+} spec_tree_role;
+
+typedef struct spec_tree_table {
+    int16_t parent;  /* owner table (-1 for the records) */
+    int16_t field;   /* defining MESSAGE / LIST field (-1 for the records) */
+    uint8_t rel;     /* spec_tree_rel */
+    uint8_t shape;   /* spec_tree_shape */
+    uint16_t first_column, ncolumns;
+} spec_tree_table;
+
+typedef struct spec_tree_column {
+    uint16_t table;
+    int16_t field;   /* the field (a struct member for struct columns); the table's field for BEGIN/STATUS */
+    uint8_t role;    /* spec_tree_role */
+    uint8_t kind;    /* VALUE: scalar kind or SPEC_KIND_ANY */
+    uint16_t width;  /* bytes per row; a BEGIN column has owner rows + 1 entries */
+} spec_tree_column;
+
+/* Validate a tree and describe its tables and columns (arrays of SPEC_TREE_MAX_TABLES /
+ * SPEC_TREE_MAX_COLUMNS entries).  SPEC_E_INVALID_ARGUMENT on an invalid tree. */
+int spec_tree_layout(const spec_tree *tree, spec_tree_table *tables, uint32_t *ntables, spec_tree_column *columns,
+                     uint32_t *ncolumns);
+
+/* Decode: for every record, the generated reader's getters over the whole tree.  A decoder
+ * owns its device workspace (grown on demand, on its device).
+ *   spec_tree_decoder_index: the table row counts (host rows[ntables]); synchronises with the
+ *     stream once per LIST table (a list's row count sizes the tables below it);
+ *   spec_tree_decoder_decode: every column (columns[c] sized by spec_tree_layout and rows;
+ *     NULL skips a column), asynchronous on `stream`; the batch must be the one indexed. */
+typedef struct spec_tree_decoder spec_tree_decoder;
+int spec_tree_decoder_create(const spec_tree *tree, spec_tree_decoder **out);
+void spec_tree_decoder_destroy(spec_tree_decoder *d);
+int spec_tree_decoder_index(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len,
+                            const uint64_t *ends, uint64_t n, uint64_t *rows, void *stream);
+int spec_tree_decoder_decode(spec_tree_decoder *d, void *const *columns, void *stream);
+
+/* Encode: for every record, the generated Write() over the tree, Build() (writer.go:141-188),
+ * appended into out[] with ends[i] = record i's end.  rows[t] = rows of table t (host);
+ * heaps[c] / heap_lens[c] back string, bytes and any columns (NULL otherwise).  Writes *total
+ * (device); if it exceeds out_cap nothing is written; an encoder error (a span outside its heap,
+ * a value > format.MaxSize, a BEGIN column not monotonic) makes *total all-ones.  With
+ * out == NULL only *total is computed.  Workspace: spec_encode_tree_workspace_size(tree, rows). */
+size_t spec_encode_tree_workspace_size(const spec_tree *tree, const uint64_t *rows);
+int spec_encode_tree(const spec_tree *tree, const void *const *columns, const uint8_t *const *heaps,
+                     const uint64_t *heap_lens, const uint64_t *rows, uint8_t *out, uint64_t out_cap, uint64_t *ends,
+                     void *workspace, size_t workspace_size, uint64_t *total, void *stream);
 
 /* ---- introspection ---- */
 int spec_abi_version(void);

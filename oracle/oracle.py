@@ -218,6 +218,10 @@ def _declare(L):
     L.so_decode_nested_counts.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
     L.so_decode_nested_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64] + [C.c_void_p] * 9
     L.so_parse_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]
+    L.so_tree_layout.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_int), C.c_void_p, C.POINTER(C.c_int)]
+    L.so_decode_tree_batch.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+    L.so_encode_tree_batch.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                       C.c_void_p]
     L.so_frames_read.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
     L.so_frames_read.restype = C.c_longlong
     # lz4 (oracle/lz4.c)
@@ -618,6 +622,74 @@ def parse_batch(stream: np.ndarray, ends: np.ndarray, head: int = 0):
     sz = np.zeros(n, np.uint32)
     lib().so_parse_batch(_ptr(stream), _ptr(ends), n, head, _ptr(st), _ptr(sz))
     return st, sz
+
+
+# ---------------------------------------------------------------- schema trees (tree.c)
+
+TREE_FIELD = np.dtype([("tag", "<u2"), ("kind", "u1"), ("elem", "u1"), ("parent", "<i2"), ("reserved", "<u2")])
+TREE_TABLE = np.dtype([("parent", "<i2"), ("field", "<i2"), ("rel", "u1"), ("shape", "u1"), ("first_column", "<u2"),
+                       ("ncolumns", "<u2")])
+TREE_COLUMN = np.dtype([("table", "<u2"), ("field", "<i2"), ("role", "u1"), ("kind", "u1"), ("width", "<u2")])
+
+
+def tree_fields(fields) -> np.ndarray:
+    """[(tag, kind, elem, parent), ...] -> the so_tree_field array."""
+    a = np.zeros(len(fields), TREE_FIELD)
+    for i, (tag, kind, elem, parent) in enumerate(fields):
+        a[i] = (tag, kind, elem, parent, 0)
+    return a
+
+
+def tree_layout(fields: np.ndarray):
+    """so_tree_layout -> (tables, columns) structured arrays, or None for an invalid tree."""
+    t = np.zeros(64, TREE_TABLE)
+    c = np.zeros(512, TREE_COLUMN)
+    nt, nc = C.c_int(0), C.c_int(0)
+    rc = lib().so_tree_layout(_ptr(fields), len(fields), _ptr(t), C.byref(nt), _ptr(c), C.byref(nc))
+    if rc:
+        return None
+    return t[: nt.value].copy(), c[: nc.value].copy()
+
+
+def _entries(tables, col, rows):
+    return rows[tables[col["table"]]["parent"]] + 1 if col["role"] == 2 else rows[col["table"]]
+
+
+def decode_tree_batch(fields: np.ndarray, stream: np.ndarray, ends: np.ndarray):
+    """Generated reader over every record -> (rows per table, columns in layout order: uint8
+    [entries, width])."""
+    tables, cols = tree_layout(fields)
+    stream = np.ascontiguousarray(stream, dtype=np.uint8)
+    ends = np.ascontiguousarray(ends, dtype=np.uint64)
+    n = len(ends)
+    rows = np.zeros(len(tables), np.uint64)
+    sp = _ptr(stream) if stream.size else None
+    lib().so_decode_tree_batch(_ptr(fields), len(fields), sp, _ptr(ends) if n else None, n, None, _ptr(rows))
+    rows = [int(r) for r in rows]
+    out = [np.zeros((max(_entries(tables, c, rows), 1), int(c["width"])), np.uint8) for c in cols]
+    ptrs = (C.c_void_p * len(out))(*[o.ctypes.data for o in out])
+    rows2 = np.zeros(len(tables), np.uint64)
+    lib().so_decode_tree_batch(_ptr(fields), len(fields), sp, _ptr(ends) if n else None, n, ptrs, _ptr(rows2))
+    assert [int(r) for r in rows2] == rows
+    return rows, [o[: _entries(tables, c, rows)] for o, c in zip(out, cols)]
+
+
+def encode_tree_batch(fields: np.ndarray, columns, heaps, n: int, cap=None):
+    """Generated Write() per record -> (stream uint8[total], ends uint64[n]).  columns / heaps in
+    layout order (heaps None where unused)."""
+    cols = [np.ascontiguousarray(c) if c is not None else np.zeros((1, 1), np.uint8) for c in columns]
+    hs = [np.ascontiguousarray(h, dtype=np.uint8) if h is not None else None for h in heaps]
+    colptrs = (C.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
+    heapptrs = (C.c_void_p * len(hs))(*[h.ctypes.data if h is not None else 0 for h in hs])
+    if cap is None:
+        cap = 256 + sum(int(c.size) for c in cols) * 4 + sum(int(h.size) for h in hs if h is not None) * 2
+    out = np.zeros(cap, np.uint8)
+    ends = np.zeros(max(n, 1), np.uint64)
+    rc = lib().so_encode_tree_batch(_ptr(fields), len(fields), colptrs, heapptrs, n, _ptr(out), cap, _ptr(ends))
+    if rc != 0:
+        raise RuntimeError(f"so_encode_tree_batch rc={rc}")
+    total = int(ends[n - 1]) if n else 0
+    return out[:total].copy(), ends[:n].copy()
 
 
 def frames_read(buf: np.ndarray, cap: int):

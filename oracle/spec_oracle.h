@@ -254,6 +254,15 @@ so_err so_elem_begin_list(so_writer *w);    /* ListWriter.List() */
 so_err so_elem_begin_message(so_writer *w); /* ListWriter.Message() */
 int so_writer_list_len(so_writer *w);
 /* ValueWriter (writer/value.go) for root values */
+/* FieldWriter / ListWriter calls by column kind (v = column element; string/bytes = {u32 off,
+ * u32 len} into heap), and struct fields/elements (generated EncodeXxxTo: members then
+ * EncodeStruct, internal/lang/generator/struct.go:115-142) */
+so_err so_field_value(so_writer *w, uint16_t tag, int kind, const uint8_t *v, const uint8_t *heap);
+so_err so_elem_value(so_writer *w, int kind, const uint8_t *v, const uint8_t *heap);
+so_err so_field_struct(so_writer *w, uint16_t tag, int nm, const uint8_t *kinds, const uint8_t *const *vals,
+                       const uint8_t *const *heaps);
+so_err so_elem_struct(so_writer *w, int nm, const uint8_t *kinds, const uint8_t *const *vals,
+                      const uint8_t *const *heaps);
 so_err so_value_int64(so_writer *w, int64_t v);
 so_err so_value_string(so_writer *w, const char *v, size_t len);
 /* end(): MessageWriter.Build / ListWriter.Build / ValueWriter.Build (writer.go:141-188) */
@@ -326,6 +335,44 @@ int so_decode_nested_batch(const uint8_t *stream, const uint64_t *ends, uint64_t
  * head = bytes before each record (4 for mpx frames). */
 int so_parse_batch(const uint8_t *stream, const uint64_t *ends, uint64_t n, uint32_t head, uint8_t *status,
                    uint32_t *sizes);
+
+/* ---- schema trees (tree.c): structs, sub-messages, value lists, lists of structs/messages,
+ * any — the generated readers/writers of internal/lang/generator over a batch ----
+ * Field descriptors mirror include/spec_amd.h spec_tree_field (same layout and rules); the
+ * table/column layout is restated independently (tree.c) and compared with the engine's in
+ * the tests. */
+enum { SO_KIND_LIST = 16, SO_KIND_STRUCT = 17, SO_KIND_MESSAGE = 18, SO_KIND_ANY = 19 };
+typedef struct so_tree_field {
+    uint16_t tag;
+    uint8_t kind;
+    uint8_t elem;
+    int16_t parent;
+    uint16_t reserved;
+} so_tree_field;
+typedef struct so_tree_table {
+    int16_t parent, field;
+    uint8_t rel, shape;
+    uint16_t first_column, ncolumns;
+} so_tree_table;
+typedef struct so_tree_column {
+    uint16_t table;
+    int16_t field;
+    uint8_t role, kind;
+    uint16_t width;
+} so_tree_column;
+/* 0 ok, -1 invalid tree */
+int so_tree_layout(const so_tree_field *f, int nf, so_tree_table *tables, int *ntables, so_tree_column *cols,
+                   int *ncols);
+/* Per record: the generated reader's getters over the whole tree (OpenMessageErr, getters,
+ * HasField, Message(tag), List(tag) + Get(i), OpenStruct, Field(tag)).  rows[t] = rows of
+ * table t; columns (may be NULL: rows only) in layout order, sized by rows. */
+int so_decode_tree_batch(const so_tree_field *f, int nf, const uint8_t *stream, const uint64_t *ends, uint64_t n,
+                         void *const *columns, uint64_t *rows);
+/* Per record: the generated Write() over the tree (scalars always written; sub-messages and
+ * lists when their PRESENT byte is set; any when its span is non-empty), Build().
+ * heaps[c] backs string/bytes/any column c.  0 ok, -1 writer error, -2 out too small. */
+int so_encode_tree_batch(const so_tree_field *f, int nf, const void *const *columns, const uint8_t *const *heaps,
+                         uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *ends);
 
 /* mpx frame read loop over a received buffer (mpx/conn_reader.go:179-194): frame count and
  * ends (offset past each complete frame's message), -1 if more than cap frames are complete. */

@@ -461,3 +461,77 @@ so_err so_value_string(so_writer *w, const char *v, size_t len) {
     VALUE(so_encode_string(w->buf, v, len, &n_));
     return NULL;
 }
+
+/* ---- generic values by column kind (the generated writers' per-kind calls) ---- */
+
+/* One column element of `kind` appended through its encoder (internal/encode/...): v is the
+ * column element (so_kind_width(kind) bytes); string/bytes elements are {u32 off, u32 len}
+ * into heap. */
+static so_err encode_kind(so_buf *b, int kind, const uint8_t *v, const uint8_t *heap, int *n) {
+    switch (kind) {
+    case SO_KIND_BOOL: return so_encode_bool(b, v[0] != 0, n);
+    case SO_KIND_BYTE: return so_encode_byte(b, v[0], n);
+    case SO_KIND_INT16: { int16_t x; memcpy(&x, v, 2); return so_encode_int16(b, x, n); }
+    case SO_KIND_INT32: { int32_t x; memcpy(&x, v, 4); return so_encode_int32(b, x, n); }
+    case SO_KIND_INT64: { int64_t x; memcpy(&x, v, 8); return so_encode_int64(b, x, n); }
+    case SO_KIND_UINT16: { uint16_t x; memcpy(&x, v, 2); return so_encode_uint16(b, x, n); }
+    case SO_KIND_UINT32: { uint32_t x; memcpy(&x, v, 4); return so_encode_uint32(b, x, n); }
+    case SO_KIND_UINT64: { uint64_t x; memcpy(&x, v, 8); return so_encode_uint64(b, x, n); }
+    case SO_KIND_FLOAT32: { float x; memcpy(&x, v, 4); return so_encode_float32(b, x, n); }
+    case SO_KIND_FLOAT64: { double x; memcpy(&x, v, 8); return so_encode_float64(b, x, n); }
+    case SO_KIND_BIN64: return so_encode_bin64(b, v, n);
+    case SO_KIND_BIN128: return so_encode_bin128(b, v, n);
+    case SO_KIND_BIN256: return so_encode_bin256(b, v, n);
+    case SO_KIND_STRING:
+    case SO_KIND_BYTES: {
+        uint32_t span[2];
+        memcpy(span, v, 8);
+        const uint8_t *p = heap ? heap + span[0] : (const uint8_t *)"";
+        return kind == SO_KIND_STRING ? so_encode_string(b, (const char *)p, span[1], n)
+                                      : so_encode_bytes(b, p, span[1], n);
+    }
+    }
+    return "encode: unsupported kind";
+}
+
+/* The generated EncodeXxxTo of a struct (internal/lang/generator/struct.go:115-142): every
+ * member through its encoder in declaration order, then EncodeStruct(dataSize)
+ * (internal/encode/struct.go:14-21). */
+static so_err encode_struct(so_buf *b, int nm, const uint8_t *kinds, const uint8_t *const *vals,
+                            const uint8_t *const *heaps, int *n) {
+    int64_t data = 0;
+    for (int i = 0; i < nm; i++) {
+        int k = 0;
+        so_err e = encode_kind(b, kinds[i], vals[i], heaps ? heaps[i] : NULL, &k);
+        if (e) return e;
+        data += k;
+    }
+    int k = 0;
+    so_err e = so_encode_struct(b, data, &k);
+    if (e) return e;
+    *n = (int)(data + k);
+    return NULL;
+}
+
+/* FieldWriter.<Kind>(v) (internal/writer/msg.go:99-211) by column kind */
+so_err so_field_value(so_writer *w, uint16_t tag, int kind, const uint8_t *v, const uint8_t *heap) {
+    FIELD_OF(encode_kind(w->buf, kind, v, heap, &n_));
+}
+
+/* ListWriter.<Kind>(v) / ValueListWriter.Add (writer_list_value.go:26-29): value + element() */
+so_err so_elem_value(so_writer *w, int kind, const uint8_t *v, const uint8_t *heap) {
+    ELEM_OF(encode_kind(w->buf, kind, v, heap, &n_));
+}
+
+/* spec.WriteField(w.Field(tag), v, EncodeXxxTo) for a struct field (generator/message.go:402-408,
+ * internal/writer/msg.go:75-80): the struct through WriteValue, then field(tag) */
+so_err so_field_struct(so_writer *w, uint16_t tag, int nm, const uint8_t *kinds, const uint8_t *const *vals,
+                       const uint8_t *const *heaps) {
+    FIELD_OF(encode_struct(w->buf, nm, kinds, vals, heaps, &n_));
+}
+
+/* ValueListWriter[Struct].Add = WriteElement(list, v, EncodeXxxTo) (internal/writer/list.go:37-43) */
+so_err so_elem_struct(so_writer *w, int nm, const uint8_t *kinds, const uint8_t *const *vals,
+                      const uint8_t *const *heaps) {
+    ELEM_OF(encode_struct(w->buf, nm, kinds, vals, heaps, &n_));
+}

@@ -29,6 +29,30 @@ class SpecNestedSchema(C.Structure):
     _fields_ = [("outer", SpecSchema), ("item", SpecSchema)]
 
 
+SPEC_TREE_MAX_FIELDS = 256
+SPEC_TREE_MAX_TABLES = 64
+SPEC_TREE_MAX_COLUMNS = 512
+
+
+class SpecTreeField(C.Structure):
+    _fields_ = [("tag", C.c_uint16), ("kind", C.c_uint8), ("elem", C.c_uint8), ("parent", C.c_int16),
+                ("reserved", C.c_uint16)]
+
+
+class SpecTree(C.Structure):
+    _fields_ = [("nfields", C.c_uint32), ("fields", SpecTreeField * SPEC_TREE_MAX_FIELDS)]
+
+
+class SpecTreeTable(C.Structure):
+    _fields_ = [("parent", C.c_int16), ("field", C.c_int16), ("rel", C.c_uint8), ("shape", C.c_uint8),
+                ("first_column", C.c_uint16), ("ncolumns", C.c_uint16)]
+
+
+class SpecTreeColumn(C.Structure):
+    _fields_ = [("table", C.c_uint16), ("field", C.c_int16), ("role", C.c_uint8), ("kind", C.c_uint8),
+                ("width", C.c_uint16)]
+
+
 class SpecError(RuntimeError):
     def __init__(self, rc: int, what: str):
         self.rc = rc
@@ -119,6 +143,17 @@ def _declare(L):
     L.spec_lz4_pack_workspace_size.argtypes = [C.c_uint64]
     L.spec_lz4_pack_workspace_size.restype = C.c_size_t
     L.spec_lz4_pack.argtypes = [vp, C.c_uint64, vp, C.c_uint64, vp, C.c_uint64, vp, vp, C.c_size_t, vp]
+    L.spec_tree_layout.argtypes = [C.POINTER(SpecTree), C.POINTER(SpecTreeTable), C.POINTER(C.c_uint32),
+                                   C.POINTER(SpecTreeColumn), C.POINTER(C.c_uint32)]
+    L.spec_tree_decoder_create.argtypes = [C.POINTER(SpecTree), C.POINTER(vp)]
+    L.spec_tree_decoder_destroy.argtypes = [vp]
+    L.spec_tree_decoder_destroy.restype = None
+    L.spec_tree_decoder_index.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.POINTER(C.c_uint64), vp]
+    L.spec_tree_decoder_decode.argtypes = [vp, C.POINTER(vp), vp]
+    L.spec_encode_tree_workspace_size.argtypes = [C.POINTER(SpecTree), C.POINTER(C.c_uint64)]
+    L.spec_encode_tree_workspace_size.restype = C.c_size_t
+    L.spec_encode_tree.argtypes = [C.POINTER(SpecTree), C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_uint64),
+                                   C.POINTER(C.c_uint64), vp, C.c_uint64, vp, vp, C.c_size_t, vp, vp]
 
 
 def strerror(rc: int) -> str:

@@ -108,6 +108,12 @@ void fill_encode_args(spec::EncodeArgs &a, const spec_schema *schema, const void
 
 } // namespace
 
+namespace spec {
+void note_hip_error(hipError_t e) {
+    if (e != hipSuccess) g_last_hip_error = (int)e;
+}
+} // namespace spec
+
 extern "C" {
 
 int spec_abi_version(void) { return SPEC_AMD_ABI_VERSION; }

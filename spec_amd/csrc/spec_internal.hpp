@@ -31,6 +31,7 @@ size_t frames_index_device_workspace(uint64_t len);
 int launch_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends, uint64_t cap, uint64_t *count,
                                uint64_t *consumed, int32_t *status, void *ws, hipStream_t stream);
 int device_cus(); // CUs of the current device (cached)
+void note_hip_error(hipError_t e); // capi.hip: remembered for spec_last_hip_error()
 bool persistent_decode(); // SPEC_AMD_PERSIST=1
 unsigned decode_wpb();     // SPEC_AMD_WPB (waves per block, default 1)
 int launch_parse(DecodeArgs a, uint32_t *sizes, double avg_record, hipStream_t stream);

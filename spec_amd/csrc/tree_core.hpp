@@ -1,0 +1,502 @@
+// tree_core.hpp — device code of the schema-tree decoder and encoder (spec_decode_tree /
+// spec_encode_tree, include/spec_amd.h): every kind a generated reader/writer handles —
+// structs, sub-messages, value lists, lists of structs and of messages, any, enums (int32).
+//
+// The work is one lane per ROW of a table (a record, a sub-message, a list element), table by
+// table, so a row's bytes are whatever range its parent row found for it:
+//   decode  index   per row of a message table: OpenMessage, the range of every sub-message
+//                   field (rows 1:1) and the element count of every list field;
+//           scan    counts -> CSR begin (a list table's rows);
+//           expand  per owner row: the range of every list element (List.GetBytes);
+//           decode  per row: the table's columns (getters, Decode<Kind>, struct Decode, OpenValue);
+//   encode  size    per row, bottom-up: encoded size (values, structs, lists and sub-messages
+//                   from their already-sized rows), IsBigMessage / IsBigList;
+//           scan    record sizes -> record offsets, ends, total;
+//           write   per row, top-down: its bytes, and the start of every child row.
+// The reads go through range-checked buffer loads (GlobalSrc): this is the general path for
+// any schema; the benchmark schemas have the LDS-staged, schema-specialised kernels.
+#pragma once
+
+#include "decode_nested_core.hpp"
+#include "encode_core.hpp"
+
+namespace spec {
+
+constexpr int TREE_MAX_F = 256, TREE_MAX_T = 64, TREE_MAX_C = 512, TREE_MAX_D = 64;
+enum : uint32_t { K_STRUCT = 17, K_MESSAGE = 18, K_ANY = 19 };
+enum : uint32_t { REL_ROOT = 0, REL_ONE = 1, REL_MANY = 2 };
+enum : uint32_t { SHAPE_MESSAGE = 0, SHAPE_VALUE = 1, SHAPE_STRUCT = 2 };
+constexpr uint32_t RNG_PANIC = 0xffffffffu; // range (RNG_PANIC, 0): Go panics on this element
+
+struct TField {
+    uint16_t tag;
+    uint8_t kind, elem;
+    int16_t parent;
+    int16_t table;   // MESSAGE / LIST: the table it defines
+    int16_t col;     // VALUE column (scalar, any, struct member; a value list's element column)
+    int16_t present; // MESSAGE / LIST: PRESENT column
+    uint16_t rank;   // index of the tag in the writer's table of all direct fields (lookup probe)
+    uint16_t nmem, mem0; // STRUCT / LIST<STRUCT>: members[mem0 .. mem0 + nmem)
+};
+
+struct TTable {
+    int16_t parent, field;
+    uint8_t rel, shape, has_children, pad;
+    int16_t begin_col, status_col;
+    uint16_t nd, d0; // MESSAGE shape: direct[d0 .. d0 + nd) (write order), sorted[...] (table order)
+};
+
+struct TreeDesc {
+    uint32_t nfields, ntables, ncols, pad;
+    TField f[TREE_MAX_F];
+    TTable t[TREE_MAX_T];
+    uint16_t direct[TREE_MAX_F];
+    uint16_t sorted[TREE_MAX_F];
+    uint16_t members[TREE_MAX_F];
+    uint16_t width[TREE_MAX_C];
+};
+
+struct TreeBufs {
+    void *cols[TREE_MAX_C];
+    const uint8_t *heaps[TREE_MAX_C];
+    uint64_t heap_lens[TREE_MAX_C];
+    uint2 *rng[TREE_MAX_T];     // decode: row ranges (stream offsets lo, hi) of tables 1..
+    uint32_t *cnt[TREE_MAX_T];  // decode: LIST tables: counts per owner row, scanned into begin
+    uint32_t *size[TREE_MAX_T]; // encode: encoded bytes per row
+    uint64_t *pos[TREE_MAX_T];  // encode: start of each row in out (tables 1..)
+    uint64_t rows[TREE_MAX_T];
+    const uint8_t *stream;
+    uint64_t stream_len;
+    const uint64_t *ends;
+    uint64_t n;
+    uint8_t *out;
+    uint64_t out_cap;
+    uint64_t *ends_out;
+    uint64_t *offsets; // encode: record starts (exclusive scan of size[0])
+    uint64_t *total;
+    uint32_t *err;
+};
+
+__device__ __forceinline__ uint64_t grid_stride() { return (uint64_t)gridDim.x * blockDim.x; }
+__device__ __forceinline__ uint64_t grid_first() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+
+// ---- decode helpers ----------------------------------------------------------------------
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t stream_rsrc(const TreeBufs &B) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)B.stream, (short)0, (int)(uint32_t)B.stream_len, 0x00020000);
+}
+
+// The byte range of row `row` of table x (record, sub-message field slice, list element).
+__device__ __forceinline__ void row_range(const TreeBufs &B, uint32_t x, uint64_t row, long long &lo, long long &hi,
+                                          bool &panic) {
+    panic = false;
+    if (x == 0) {
+        lo = row ? (long long)B.ends[row - 1] : 0;
+        hi = (long long)B.ends[row];
+        if (hi < lo) hi = lo;
+        return;
+    }
+    const uint2 r = B.rng[x][row];
+    panic = r.x == RNG_PANIC && r.y == 0;
+    lo = panic ? 0 : r.x;
+    hi = panic ? 0 : r.y;
+}
+
+__device__ __forceinline__ void store_kind(void *colp, uint64_t r, uint32_t kind, const Val &v) {
+    uint8_t *c = (uint8_t *)colp;
+    if (!c) return;
+    switch (kind) {
+    case K_BOOL:
+    case K_BYTE: c[r] = (uint8_t)v.v0; break;
+    case K_INT16:
+    case K_UINT16: ((uint16_t *)c)[r] = (uint16_t)v.v0; break;
+    case K_INT32:
+    case K_UINT32:
+    case K_FLOAT32: ((uint32_t *)c)[r] = (uint32_t)v.v0; break;
+    case K_BIN128:
+        ((uint64_t *)c)[2 * r] = v.v0;
+        ((uint64_t *)c)[2 * r + 1] = v.v1;
+        break;
+    case K_BIN256:
+        ((uint64_t *)c)[4 * r] = v.v0;
+        ((uint64_t *)c)[4 * r + 1] = v.v1;
+        ((uint64_t *)c)[4 * r + 2] = v.v2;
+        ((uint64_t *)c)[4 * r + 3] = v.v3;
+        break;
+    default: ((uint64_t *)c)[r] = v.v0; break;
+    }
+}
+
+__device__ __forceinline__ void store_u8(void *colp, uint64_t r, uint32_t v) {
+    if (colp) ((uint8_t *)colp)[r] = (uint8_t)v;
+}
+
+// Decode<Kind>(b) of the value [lo, e) with Go's (value, n, err) (internal/decode/...; the
+// value rules are decode_tail_k's, n = bytes consumed from the end).  Returns !err.
+template <class Src>
+__device__ __forceinline__ bool decode_value_n(const Src &s, uint32_t kind, typename Src::pos_t lo,
+                                               typename Src::pos_t e, long long to_stream, Val &v, int &n) {
+    v = Val{0, 0, 0, 0};
+    n = 0;
+    const long long flen = (long long)(e - lo);
+    if (flen <= 0) return true; // empty input: zero value, n = 0, no error
+    const Tail t = load_tail(s, e);
+    const uint32_t type = (uint32_t)t.q0 & 0xff;
+    const uint64_t R = tail_r(t);
+    const uint32_t R2 = tail_r2(t);
+    const long long avail = flen - 1;
+    int m = 0;
+    bool ok = false;
+    switch (kind) {
+    case K_BOOL: n = 1; ok = true; break; // DecodeBool: any type, no error (byte.go:38-51)
+    case K_BYTE: ok = (type == T_BYTE) & (flen >= 2); n = 2; break;
+    case K_INT16:
+    case K_INT32:
+    case K_INT64: {
+        const bool w32 = (type == T_INT16) | (type == T_INT32);
+        if (!w32 && type != T_INT64) break;
+        const uint64_t u = rvarint_bf(R, R2, avail, w32 ? 5 : 10, m);
+        if (m < 0) break;
+        const long long x = w32 ? (long long)unzigzag32((uint32_t)u) : (long long)unzigzag64(u);
+        ok = kind == K_INT16 ? (x >= -32768) & (x <= 32767)
+             : kind == K_INT32 ? (w32 | ((x >= INT32_MIN) & (x <= INT32_MAX)))
+                               : true;
+        n = 1 + m;
+        break;
+    }
+    case K_UINT16:
+    case K_UINT32:
+    case K_UINT64: {
+        const bool w32 = (type == T_UINT16) | (type == T_UINT32);
+        if (!w32 && type != T_UINT64) break;
+        const uint64_t x = rvarint_bf(R, R2, avail, w32 ? 5 : 10, m);
+        if (m < 0) break;
+        ok = kind == K_UINT16 ? x <= 0xffffull : kind == K_UINT32 ? x <= 0xffffffffull : true;
+        n = 1 + m;
+        break;
+    }
+    case K_FLOAT32:
+    case K_FLOAT64: {
+        const bool f32 = (type == T_FLOAT32) & (flen >= 5), f64 = (type == T_FLOAT64) & (flen >= 9);
+        if (!f32 && !f64) break;
+        n = f32 ? 5 : 9;
+        ok = true;
+        if (kind == K_FLOAT32) { // +-MaxFloat32 range check (float.go:15-32); NaN passes
+            if (f32) {
+                const uint32_t b = (uint32_t)(R & 0xffffffffu);
+                ok = !((((b >> 23) & 0xff) == 0xff) & ((b & 0x7fffff) == 0));
+            } else {
+                const bool nan = (((R >> 52) & 0x7ff) == 0x7ff) & ((R & 0xfffffffffffffull) != 0);
+                ok = nan | ((R & 0x7fffffffffffffffull) <= 0x47EFFFFFE0000000ull);
+            }
+        }
+        break;
+    }
+    case K_BIN64: ok = (type == T_BIN64) & (flen >= 9); n = 9; break;
+    case K_BIN128: ok = (type == T_BIN128) & (flen >= 17); n = 17; break;
+    case K_BIN256: ok = (type == T_BIN256) & (flen >= 33); n = 33; break;
+    case K_STRING:
+    case K_BYTES: {
+        const bool str = kind == K_STRING;
+        if (type != (str ? T_STRING : T_BYTES)) break;
+        const uint32_t len = (uint32_t)rvarint_bf(R, R2, avail, 5, m);
+        if (m < 0) break;
+        const long long end = (long long)(e - 1) - m - (str ? 1 : 0);
+        const long long off = end - (long long)len;
+        ok = (end >= (long long)lo) & (off >= (long long)lo);
+        n = 1 + m + (str ? 1 : 0) + (int)len;
+        break;
+    }
+    }
+    if (!ok) {
+        n = 0;
+        return false;
+    }
+#define SPEC_CASE(K) \
+    case K: v = decode_tail_k<K>(load_win<K>(s, e), lo, e, to_stream); break;
+    switch (kind) {
+        SPEC_CASE(K_BOOL)
+        SPEC_CASE(K_BYTE)
+        SPEC_CASE(K_INT16)
+        SPEC_CASE(K_INT32)
+        SPEC_CASE(K_INT64)
+        SPEC_CASE(K_UINT16)
+        SPEC_CASE(K_UINT32)
+        SPEC_CASE(K_UINT64)
+        SPEC_CASE(K_FLOAT32)
+        SPEC_CASE(K_FLOAT64)
+        SPEC_CASE(K_BIN64)
+        SPEC_CASE(K_BIN128)
+        SPEC_CASE(K_BIN256)
+        SPEC_CASE(K_STRING)
+        SPEC_CASE(K_BYTES)
+    }
+#undef SPEC_CASE
+    return true;
+}
+
+// A generated struct's Decode (internal/lang/generator/struct.go:75-113) over [lo, e):
+// DecodeStruct, then the members from the LAST to the first over b[:off]; the first error
+// stops it and members decoded so far keep their values.  Returns ST_OK, ST_INVALID_VALUE, or
+// ST_PANIC where Go slices b[len(b)-size:] with size > len(b).
+template <class Src>
+__device__ __forceinline__ uint32_t tree_struct(const Src &s, const TreeDesc &D, const TreeBufs &B, uint32_t sf,
+                                                long long lo, long long e, uint64_t row, long long to_stream) {
+    const TField &F = D.f[sf];
+    const Val zero = {0, 0, 0, 0};
+    for (uint32_t k = 0; k < F.nmem; k++) {
+        const TField &M = D.f[D.members[F.mem0 + k]];
+        store_kind(B.cols[M.col], row, M.kind, zero);
+    }
+    if (e <= lo) return ST_OK;
+    if (s.u8(e - 1) != T_STRUCT) return ST_INVALID_VALUE; // DecodeStruct: invalid type
+    const Tail t = load_tail(s, (typename Src::pos_t)e);
+    int m;
+    const uint32_t ds = (uint32_t)rvarint_bf(tail_r(t), tail_r2(t), e - 1 - lo, 5, m);
+    if (m < 0) return ST_INVALID_VALUE;
+    const long long size = 1 + m + (long long)ds;
+    if (size > e - lo) return ST_PANIC;
+    const long long S = e - size;
+    long long off = S + ds;
+    for (int k = (int)F.nmem - 1; k >= 0; k--) {
+        const TField &M = D.f[D.members[F.mem0 + k]];
+        Val v;
+        int n;
+        const bool ok = decode_value_n(s, M.kind, (typename Src::pos_t)S, (typename Src::pos_t)off, to_stream, v, n);
+        store_kind(B.cols[M.col], row, M.kind, v);
+        if (!ok) return ST_INVALID_VALUE;
+        off -= n;
+    }
+    return ST_OK;
+}
+
+// compactint.ReverseSize (oracle/compactint.c so_reverse_size) over the bytes below e down to lo
+template <class Src>
+__device__ __forceinline__ int reverse_size(const Src &s, long long lo, long long e) {
+    for (int i = 0; i < 10; i++) {
+        if (e - 1 - i < lo) return -(i + 1);
+        if (s.u8((typename Src::pos_t)(e - 1 - i)) < 0x80) return i + 1;
+    }
+    return -11;
+}
+
+// decodeSize = ReverseUint32 of the bytes below e (>= lo): value, m (< 0 on error)
+template <class Src>
+__device__ __forceinline__ uint32_t rsize32(const Src &s, long long lo, long long e, int &m) {
+    if (e <= lo) {
+        m = -1;
+        return 0;
+    }
+    const Tail t = load_tail(s, (typename Src::pos_t)e + 1); // window ending just above e: R = bytes e-1..
+    return (uint32_t)rvarint_bf(tail_r(t), tail_r2(t), e - lo, 5, m);
+}
+
+// DecodeTypeSize (internal/decode/type.go:27-203) of the value ending at e over [lo, e):
+// returns false on an error; n may be negative (the struct case checks n, not m: the bug is
+// kept, type.go:185-191).
+template <class Src>
+__device__ __forceinline__ bool type_size(const Src &s, long long lo, long long e, long long &n) {
+    n = 0;
+    if (e <= lo) return true;
+    const uint32_t t = s.u8((typename Src::pos_t)(e - 1));
+    const long long len = e - lo, end = e - 1;
+    int m;
+    switch (t) {
+    case T_TRUE:
+    case T_FALSE: n = 1; return true;
+    case T_BYTE: n = 2; return end - lo >= 1;
+    case T_INT16: case T_INT32: case T_INT64:
+    case T_UINT16: case T_UINT32: case T_UINT64:
+        m = reverse_size(s, lo, end);
+        n = 1 + m;
+        return m > 0;
+    case T_FLOAT32: n = 5; return end - lo >= 4;
+    case T_FLOAT64: n = 9; return end - lo >= 8;
+    case T_BIN64: n = 9; return end - lo >= 8;
+    case T_BIN128: n = 17; return end - lo >= 16;
+    case T_BIN256: n = 33; return end - lo >= 32;
+    case T_BYTES:
+    case T_STRING: {
+        const uint32_t ds = rsize32(s, lo, end, m);
+        if (m < 0) return false;
+        n = 1 + m + (long long)ds + (t == T_STRING ? 1 : 0);
+        return len >= n;
+    }
+    case T_LIST: case T_BIG_LIST: case T_MESSAGE: case T_BIG_MESSAGE: {
+        const uint32_t ts = rsize32(s, lo, end, m);
+        if (m < 0) return false;
+        long long size = 1 + m + (long long)ts;
+        const long long end2 = end - m;
+        int m2;
+        const uint32_t ds = rsize32(s, lo, end2, m2);
+        if (m2 < 0) return false;
+        size += m2 + (long long)ds;
+        n = size;
+        return len >= size;
+    }
+    case T_STRUCT: {
+        const uint32_t ds = rsize32(s, lo, end, m);
+        const long long size = 1 + m + (long long)ds; // m unchecked (n is checked instead)
+        n = size;
+        return !(len < size);
+    }
+    }
+    return false;
+}
+
+// ---- encode helpers ----------------------------------------------------------------------
+
+__device__ __forceinline__ const uint8_t *cell(const TreeBufs &B, const TreeDesc &D, int c, uint64_t row) {
+    return (const uint8_t *)B.cols[c] + row * D.width[c];
+}
+
+// Encoded size of a column element of a scalar kind (encode_core.hpp field_size rules)
+__device__ __forceinline__ uint64_t value_size(const TreeBufs &B, const TreeDesc &D, int c, uint32_t kind,
+                                               uint64_t row, bool &err) {
+    const uint8_t *p = cell(B, D, c, row);
+    switch (kind) {
+    case K_BOOL: return 1;
+    case K_BYTE: return 2;
+    case K_INT16: return vlen32(zigzag32(*(const int16_t *)p)) + 1;
+    case K_INT32: return vlen32(zigzag32(*(const int32_t *)p)) + 1;
+    case K_INT64: return vlen64(zigzag64(*(const int64_t *)p)) + 1;
+    case K_UINT16: return vlen32(*(const uint16_t *)p) + 1;
+    case K_UINT32: return vlen32(*(const uint32_t *)p) + 1;
+    case K_UINT64: return vlen64(*(const uint64_t *)p) + 1;
+    case K_FLOAT32: return 5;
+    case K_FLOAT64: case K_BIN64: return 9;
+    case K_BIN128: return 17;
+    case K_BIN256: return 33;
+    case K_STRING:
+    case K_BYTES:
+    case K_ANY: {
+        const uint2 sp = *(const uint2 *)p;
+        if ((uint64_t)sp.y > MAX_SIZE || (uint64_t)sp.x + sp.y > B.heap_lens[c]) err = true;
+        if (kind == K_ANY) return sp.y;
+        return (uint64_t)sp.y + vlen32(sp.y) + 1 + (kind == K_STRING ? 1 : 0);
+    }
+    }
+    return 0;
+}
+
+__device__ __forceinline__ uint64_t struct_size(const TreeBufs &B, const TreeDesc &D, uint32_t sf, uint64_t row,
+                                                bool &err) {
+    const TField &F = D.f[sf];
+    uint64_t data = 0;
+    for (uint32_t k = 0; k < F.nmem; k++) {
+        const TField &M = D.f[D.members[F.mem0 + k]];
+        data += value_size(B, D, M.col, M.kind, row, err);
+    }
+    if (data > MAX_SIZE) err = true; // EncodeStruct: struct too large
+    return data + vlen64(data) + 1;
+}
+
+// [begin[row], begin[row + 1]) of list table y, from its BEGIN column (checked)
+__device__ __forceinline__ void list_span(const TreeBufs &B, const TreeDesc &D, uint32_t y, uint64_t row, uint32_t &j0,
+                                          uint32_t &j1, bool &err) {
+    const uint32_t *b = (const uint32_t *)B.cols[D.t[y].begin_col];
+    j0 = b[row];
+    j1 = b[row + 1];
+    if (j1 < j0 || (uint64_t)j1 > B.rows[y]) {
+        err = true;
+        j1 = j0;
+    }
+}
+
+struct TreeListSize {
+    uint64_t total, data;
+    uint32_t count;
+    bool big;
+};
+
+// EncodeListTable (internal/encode/list.go:15-75) over the elements' encoded sizes; IsBigList
+// (internal/format/list.go:40-54): count > 255 or the LAST end offset > 65535
+__device__ __forceinline__ TreeListSize list_size(const TreeBufs &B, const TreeDesc &D, uint32_t y, uint64_t row, bool &err) {
+    uint32_t j0, j1;
+    list_span(B, D, y, row, j0, j1, err);
+    TreeListSize L;
+    L.data = 0;
+    for (uint32_t j = j0; j < j1; j++) L.data += B.size[y][j];
+    L.count = j1 - j0;
+    L.big = L.count > 255 || (L.count > 0 && L.data > 65535);
+    const uint64_t tsize = (uint64_t)L.count * (L.big ? 4 : 2);
+    if (L.data > MAX_SIZE) err = true;
+    L.total = L.data + tsize + vlen64(L.data) + vlen64(tsize) + 1;
+    return L;
+}
+
+// Byte emitter over the output (one lane writes one row's own bytes; child rows are written by
+// later launches into the gaps this one skips).
+struct BEmit {
+    uint8_t *out;
+    uint64_t pos;
+    __device__ __forceinline__ void put1(uint32_t b) { out[pos++] = (uint8_t)b; }
+    __device__ __forceinline__ void rvarint(uint64_t v) { // oracle/compactint.c so_put_reverse_*
+        const uint32_t L = vlen64(v);
+        for (uint32_t i = 0; i < L; i++) put1(((uint32_t)(v >> (7 * (L - 1 - i))) & 0x7f) | (i ? 0x80 : 0));
+    }
+    __device__ __forceinline__ void be(uint64_t v, int nb) {
+        for (int i = nb - 1; i >= 0; i--) put1((uint32_t)(v >> (8 * i)) & 0xff);
+    }
+    __device__ __forceinline__ void le(uint64_t v, int nb) {
+        for (int i = 0; i < nb; i++) put1((uint32_t)(v >> (8 * i)) & 0xff);
+    }
+    __device__ __forceinline__ void heap(const uint8_t *h, uint32_t off, uint32_t len) {
+        for (uint32_t i = 0; i < len; i++) put1(h[off + i]);
+    }
+};
+
+// One column element through its encoder (internal/encode/...)
+__device__ __forceinline__ void emit_value(BEmit &em, const TreeBufs &B, const TreeDesc &D, int c, uint32_t kind,
+                                           uint64_t row) {
+    const uint8_t *p = cell(B, D, c, row);
+    switch (kind) {
+    case K_BOOL: em.put1(p[0] ? T_TRUE : T_FALSE); break;
+    case K_BYTE: em.put1(p[0]); em.put1(T_BYTE); break;
+    case K_INT16: em.rvarint(zigzag32(*(const int16_t *)p)); em.put1(T_INT16); break;
+    case K_INT32: em.rvarint(zigzag32(*(const int32_t *)p)); em.put1(T_INT32); break;
+    case K_INT64: em.rvarint(zigzag64(*(const int64_t *)p)); em.put1(T_INT64); break;
+    case K_UINT16: em.rvarint(*(const uint16_t *)p); em.put1(T_UINT16); break;
+    case K_UINT32: em.rvarint(*(const uint32_t *)p); em.put1(T_UINT32); break;
+    case K_UINT64: em.rvarint(*(const uint64_t *)p); em.put1(T_UINT64); break;
+    case K_FLOAT32: em.be(*(const uint32_t *)p, 4); em.put1(T_FLOAT32); break;
+    case K_FLOAT64: em.be(*(const uint64_t *)p, 8); em.put1(T_FLOAT64); break;
+    case K_BIN64: em.le(*(const uint64_t *)p, 8); em.put1(T_BIN64); break;
+    case K_BIN128:
+        em.le(((const uint64_t *)p)[0], 8);
+        em.le(((const uint64_t *)p)[1], 8);
+        em.put1(T_BIN128);
+        break;
+    case K_BIN256:
+        for (int i = 0; i < 4; i++) em.le(((const uint64_t *)p)[i], 8);
+        em.put1(T_BIN256);
+        break;
+    case K_STRING:
+    case K_BYTES: {
+        const uint2 sp = *(const uint2 *)p;
+        em.heap(B.heaps[c], sp.x, sp.y);
+        if (kind == K_STRING) em.put1(0);
+        em.rvarint(sp.y);
+        em.put1(kind == K_STRING ? T_STRING : T_BYTES);
+        break;
+    }
+    case K_ANY: {
+        const uint2 sp = *(const uint2 *)p;
+        em.heap(B.heaps[c], sp.x, sp.y);
+        break;
+    }
+    }
+}
+
+__device__ __forceinline__ void emit_struct(BEmit &em, const TreeBufs &B, const TreeDesc &D, uint32_t sf, uint64_t row) {
+    const TField &F = D.f[sf];
+    const uint64_t start = em.pos;
+    for (uint32_t k = 0; k < F.nmem; k++) {
+        const TField &M = D.f[D.members[F.mem0 + k]];
+        emit_value(em, B, D, M.col, M.kind, row);
+    }
+    em.rvarint(em.pos - start); // EncodeStruct: rvarint(dataSize) | TypeStruct
+    em.put1(T_STRUCT);
+}
+
+} // namespace spec

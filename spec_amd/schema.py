@@ -31,14 +31,17 @@ class Kind(enum.IntEnum):
     BIN256 = 13
     STRING = 14
     BYTES = 15
-    LIST = 16  # list<message> field of a NestedSchema's outer message (column = item_begin)
+    LIST = 16  # list<message> field of a NestedSchema's outer message (column = item_begin); tree lists
+    STRUCT = 17   # spec_tree only
+    MESSAGE = 18  # spec_tree only
+    ANY = 19      # spec_tree only: a span of the raw value
 
 
 WIDTH = {
     Kind.BOOL: 1, Kind.BYTE: 1, Kind.INT16: 2, Kind.INT32: 4, Kind.INT64: 8,
     Kind.UINT16: 2, Kind.UINT32: 4, Kind.UINT64: 8, Kind.FLOAT32: 4, Kind.FLOAT64: 8,
     Kind.BIN64: 8, Kind.BIN128: 16, Kind.BIN256: 32, Kind.STRING: 8, Kind.BYTES: 8,
-    Kind.LIST: 0,
+    Kind.LIST: 0, Kind.STRUCT: 0, Kind.MESSAGE: 0, Kind.ANY: 8,
 }
 
 # numpy view of one column element (bins stay raw bytes)
@@ -47,7 +50,7 @@ NP_DTYPE = {
     Kind.INT64: np.int64, Kind.UINT16: np.uint16, Kind.UINT32: np.uint32,
     Kind.UINT64: np.uint64, Kind.FLOAT32: np.uint32, Kind.FLOAT64: np.uint64,
     Kind.BIN64: np.uint8, Kind.BIN128: np.uint8, Kind.BIN256: np.uint8,
-    Kind.STRING: np.uint32, Kind.BYTES: np.uint32, Kind.LIST: np.uint32,
+    Kind.STRING: np.uint32, Kind.BYTES: np.uint32, Kind.LIST: np.uint32, Kind.ANY: np.uint32,
 }
 
 VARLEN = (Kind.STRING, Kind.BYTES)

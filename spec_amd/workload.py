@@ -135,3 +135,83 @@ def nested(n: int, seed: int = SEED, count=(0, 8), name_len=(8, 24), label_len=(
         "label": label,
         "label_heap": label_heap,
     }
+
+
+def _values(rng, kind, m, str_len):
+    """m random column elements of a scalar kind -> (uint8 [m, width], heap or None)."""
+    k = Kind(kind)
+    if k in (Kind.STRING, Kind.BYTES):
+        span, heap = _heap(rng, m, str_len[0], str_len[1], k == Kind.STRING)
+        return as_bytes(span, m), heap
+    sch = Schema([(1, k)])
+    cols, _ = gen_columns(sch, m, int(rng.integers(0, 2**63)))
+    return cols[0], None
+
+
+def _any_values(rng, m):
+    """Raw encoded values for `any` columns (no varints: the bytes are the same under any
+    reverse-varint layout): true/false, byte, float64, or empty (the field is not written)."""
+    choice = rng.integers(0, 4, size=m)
+    parts, spans, off = [], np.zeros((m, 2), np.uint32), 0
+    for i in range(m):
+        c = choice[i]
+        if c == 0:
+            b = bytes([1 if rng.integers(0, 2) else 2])
+        elif c == 1:
+            b = bytes([int(rng.integers(0, 256)), 3])
+        elif c == 2:
+            b = rng.integers(0, 256, 8, dtype=np.uint8).tobytes() + bytes([41])
+        else:
+            b = b""
+        spans[i] = (off if b else 0, len(b))
+        parts.append(b)
+        off += len(b)
+    heap = np.frombuffer(b"".join(parts) or b"\0", dtype=np.uint8).copy()
+    return as_bytes(spans, m), heap
+
+
+def tree_batch(tree, n: int, seed: int = SEED, count=(0, 4), present: float = 0.8, str_len=(0, 20)):
+    """Random columns for a spec_amd.Tree (canonical: a field under an absent sub-message or list
+    holds zeros, so decode(encode(x)) == x up to span offsets).  Returns (cols {name: uint8
+    [entries, width]}, heaps {name: uint8[]}, rows per table)."""
+    from .tree import REL_MANY, REL_ONE, ROLE_BEGIN, ROLE_PRESENT, ROLE_STATUS
+
+    rng = np.random.default_rng(seed)
+    T = tree.tables
+    rows = [0] * len(T)
+    rows[0] = n
+    alive = {0: np.ones(n, bool)}
+    cols, heaps = {}, {}
+    for t in T:
+        if t.index:
+            f = tree.fields[t.field]
+            pres = cols[f"{f.path}?"].reshape(-1).astype(bool)
+            if t.rel == REL_ONE:
+                rows[t.index] = rows[t.parent]
+                alive[t.index] = pres
+            else:
+                cnt = rng.integers(count[0], count[1] + 1, size=rows[t.parent]).astype(np.uint32) * pres
+                begin = np.zeros(rows[t.parent] + 1, np.uint32)
+                np.cumsum(cnt, out=begin[1:])
+                rows[t.index] = int(begin[-1])
+                alive[t.index] = np.ones(rows[t.index], bool)
+                cols[f"{f.path}#begin"] = begin.view(np.uint8).reshape(-1, 4)
+        R, live = rows[t.index], alive[t.index]
+        for c in t.columns:
+            if c.role in (ROLE_BEGIN,):
+                continue
+            if c.role == ROLE_STATUS:
+                cols[c.name] = np.zeros((R, 1), np.uint8)
+            elif c.role == ROLE_PRESENT:
+                cols[c.name] = ((rng.random(R) < present) & live).astype(np.uint8).reshape(R, 1)
+            elif c.kind == Kind.ANY:
+                a, h = _any_values(rng, R)
+                a.view(np.uint32)[~live] = 0
+                cols[c.name], heaps[c.name] = a, h
+            else:
+                a, h = _values(rng, c.kind, R, str_len)
+                a[~live] = 0
+                cols[c.name] = np.ascontiguousarray(a)
+                if h is not None:
+                    heaps[c.name] = h if h.size else np.zeros(1, np.uint8)
+    return cols, heaps, rows
