@@ -112,6 +112,23 @@ class Tree:
         self.c = c
         self._layout()
 
+    @classmethod
+    def from_fields(cls, fields):
+        """A tree from flattened fields [(path, tag, kind, elem, parent), ...] (pre-order)."""
+        t = cls.__new__(cls)
+        t.root = None
+        t.fields = [TreeField(p, tag, Kind(k), int(e), par) for p, tag, k, e, par in fields]
+        c = _lib.SpecTree()
+        c.nfields = len(t.fields)
+        for i, f in enumerate(t.fields):
+            c.fields[i].tag, c.fields[i].kind, c.fields[i].elem, c.fields[i].parent = f.tag, int(f.kind), f.elem, f.parent
+        t.c = c
+        t._layout()
+        return t
+
+    def to_fields(self):
+        return [(f.path, f.tag, int(f.kind), int(f.elem), f.parent) for f in self.fields]
+
     # -- flattening --
     def _add(self, path, tag, kind, elem=0, parent=-1):
         self.fields.append(TreeField(path, tag, Kind(kind), int(elem), parent))

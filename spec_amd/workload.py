@@ -67,7 +67,9 @@ def _heap(rng, n, lo, hi, ascii_only):
 
 
 def as_bytes(a: np.ndarray, n: int) -> np.ndarray:
-    return np.ascontiguousarray(a).view(np.uint8).reshape(n, -1)
+    a = np.ascontiguousarray(a)
+    width = a.dtype.itemsize * (int(np.prod(a.shape[1:])) if a.ndim > 1 else 1)
+    return a.view(np.uint8).reshape(n, width)
 
 
 def gen_columns(schema: Schema, n: int, seed: int = SEED, str_len=(30, 62)):

@@ -116,3 +116,16 @@ def test_encoder_error_span_outside_heap(dev):
     enc = spec_amd.TreeEncoder(tree, rows, dev)
     total = enc.encode(to_dev(cols, dev), to_dev(heaps, dev), None, None)
     assert int(total.item()) == -1
+
+
+@pytest.mark.parametrize("name", ["pkg1.Message", "pmpx.Message", "prpc.Message", "pmpx.ChannelOpen"])
+def test_reference_spec_trees(dev, name):
+    """Trees the .spec front end derives from the reference's own schemas (fixture made by
+    tests/golden/make_spec_trees.py from pkg1.spec, proto/pmpx/mpx.spec, proto/prpc/rpc.spec)."""
+    import json
+    import os
+
+    d = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "spec_trees.json")))
+    tree = spec_amd.Tree.from_fields(d[name])
+    cols, heaps, rows = workload.tree_batch(tree, 3000, 77, count=(0, 3))
+    check_encode_decode(tree, cols, heaps, rows, dev, 3000)

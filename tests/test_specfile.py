@@ -43,7 +43,7 @@ message WithStruct {
 }
 
 service Svc {
-    method(req Record) (resp Item);
+    method(req Record 1) (resp Item 1);
 }
 """
 
@@ -71,3 +71,104 @@ def test_unsupported_kinds():
         f.schema("WithStruct")
     s = f.schema("WithStruct", skip_unsupported=True)
     assert [(x.tag, x.kind) for x in s.fields] == [(2, Kind.INT64)]
+
+
+# ---- the full language (internal/lang/parser/grammar.y) and the reference's own schemas ----
+
+import glob  # noqa: E402
+import json  # noqa: E402
+import os  # noqa: E402
+
+from spec_amd import ListOf, Message, Struct  # noqa: E402
+from spec_amd.specfile import SpecFile, load_files  # noqa: E402
+
+REF = "/root/reference"
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "spec_trees.json")
+needs_ref = pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree absent (GPU box)")
+
+GRAMMAR = """
+import (
+    "pkg/a"
+    b "pkg/bee"
+)
+options ( go_package="x/y/z" opt2="v" )
+
+message Keywords {
+    any     any         1;
+    message message     2;
+    struct  a.Thing     3;
+    service []b.Item    4;
+    options int32       5
+}
+
+struct S { import int16; oneway bool; }
+
+service Svc {
+    sub(id bin128 1) Sub;
+    method();
+    m0(msg string 1) oneway;
+    m1(a int64 1, b float64 2, c bool 3) (a int64 1, b float64 2,);
+    m2(Req) Resp;
+    m3(a.Req) (<-In, Out->) Resp;
+    m4(Req) (In<-) Resp;
+    m5(Req) (->Out);
+    m6() (<-[]In);
+}
+
+subservice Sub { hello(msg string 1) (msg string 1); }
+"""
+
+
+def test_grammar_constructs():
+    f = SpecFile(GRAMMAR)
+    assert f.package == "z" and f.imports == {"a": "pkg/a", "b": "pkg/bee"} and f.options["opt2"] == "v"
+    assert f.messages["Keywords"] == [("any", "any", 1), ("message", "message", 2), ("struct", "a.Thing", 3),
+                                      ("service", "[]b.Item", 4), ("options", "int32", 5)]
+    assert f.structs["S"] == [("import", "int16"), ("oneway", "bool")]
+    methods = {m[0]: m for m in f.services["Svc"]}
+    assert methods["m0"][3] is True and methods["m2"][1:3] == ("Req", "Resp")
+    assert methods["m3"][4] == {"in": "In", "out": "Out"} and methods["m3"][1] == "a.Req"
+    assert methods["m4"][4] == {"in": "In"} and methods["m5"][4] == {"out": "Out"}
+    assert methods["m6"][4] == {"in": "[]In"} and methods["sub"][2] == "Sub"
+    assert methods["m1"][2] == [("a", "int64", 1), ("b", "float64", 2)]
+    assert f.services["Sub"][0][0] == "hello"
+
+
+@needs_ref
+def test_every_reference_spec_parses():
+    files = sorted(glob.glob(REF + "/**/*.spec", recursive=True))
+    assert len(files) >= 9
+    for p in files:
+        f = SpecFile(open(p).read())
+        assert f.messages or f.enums or f.structs or f.services, p
+    svc = SpecFile(open(REF + "/internal/tests/pkg4/service.spec").read())
+    assert len(svc.services["Service"]) == 13 and len(svc.services["Subservice"]) == 1
+
+
+@needs_ref
+def test_reference_trees_match_fixture():
+    """The committed fixture (tests/golden/make_spec_trees.py) is what the parser derives today."""
+    import sys
+
+    sys.path.insert(0, os.path.dirname(GOLDEN))
+    from make_spec_trees import trees
+
+    want = json.load(open(GOLDEN))
+    got = trees(REF)
+    assert {k: [list(x) for x in v] for k, v in got.items()} == want
+
+
+def test_fixture_trees_shapes():
+    d = json.load(open(GOLDEN))
+    pkg1 = {f[0]: f for f in d["pkg1.Message"]}
+    # struct1 Struct 61 -> STRUCT with int32 members; enum1 -> INT32; ints []int64 -> LIST<INT64>;
+    # submessages1 []pkg2.Submessage -> LIST<MESSAGE> with pkg3a.Value struct; any -> ANY
+    assert pkg1["struct1"][1:3] == [61, int(Kind.STRUCT)] and pkg1["struct1.key"][2] == int(Kind.INT32)
+    assert pkg1["enum1"][2] == int(Kind.INT32) and pkg1["ints"][2:4] == [int(Kind.LIST), int(Kind.INT64)]
+    assert pkg1["submessages1[].value.x"][2] == int(Kind.INT32) and pkg1["any"][2] == int(Kind.ANY)
+    assert pkg1["message1"][2] == int(Kind.ANY)  # `message` = any message (Field(tag).Message())
+    assert pkg1["submessage.next.value"][2] == int(Kind.STRING) and "submessage.next.next" not in pkg1
+    mpx = {f[0]: f for f in d["pmpx.Message"]}
+    assert mpx["code"][2] == int(Kind.INT32) and mpx["channel_open.id"][2] == int(Kind.BIN128)
+    assert mpx["batch.list"][2:4] == [int(Kind.LIST), int(Kind.MESSAGE)]
+    assert mpx["connect_request.versions"][2:4] == [int(Kind.LIST), int(Kind.INT32)]

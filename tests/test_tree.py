@@ -171,11 +171,11 @@ def test_oracle_test_object_roundtrip():
     assert roundtrip_mismatches(tree, cols, heaps, got, stream) == []
 
 
-@pytest.mark.parametrize("seed", [1, 2])
-def test_oracle_roundtrip_random_pkg1(seed):
+@pytest.mark.parametrize("seed,n", [(1, 300), (2, 300), (3, 1), (4, 2)])
+def test_oracle_roundtrip_random_pkg1(seed, n):
     tree = spec_amd.pkg1_tree()
-    cols, heaps, rows = workload.tree_batch(tree, 300, seed)
-    stream, ends = oracle_encode(tree, cols, heaps, 300)
+    cols, heaps, rows = workload.tree_batch(tree, n, seed)
+    stream, ends = oracle_encode(tree, cols, heaps, n)
     st, _ = O.parse_batch(stream, ends)
     assert not st.any()
     got_rows, got = oracle_decode(tree, stream, ends)
