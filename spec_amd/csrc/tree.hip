@@ -203,6 +203,7 @@ __global__ __launch_bounds__(TB) void tree_write_kernel(const TreeDesc *Dp, cons
     if (!B.out || *B.err || *B.total > B.out_cap) return;
     for (uint64_t row = grid_first(); row < rows; row += grid_stride()) {
         const uint64_t start = x == 0 ? B.offsets[row] : B.pos[x][row];
+        if (start == ~0ull) continue; // a row no written owner placed (absent message / list)
         if (x == 0 && B.ends_out) B.ends_out[row] = start + B.size[0][row];
         BEmit em{B.out, start};
         if (T.shape == SHAPE_VALUE) {
@@ -828,6 +829,9 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
     }
     // an encoder error: total = all-ones
     if (ok) hipLaunchKernelGGL(tree_err_kernel, dim3(1), dim3(1), 0, st, (const uint32_t *)B->err, total);
+    // child rows start unplaced: only rows their owner writes get a position
+    for (uint32_t x = 1; ok && out && x < L.nt; x++)
+        if (rows[x]) ok = hipMemsetAsync(B->pos[x], 0xff, rows[x] * sizeof(uint64_t), st) == hipSuccess;
     for (uint32_t x = 0; ok && out && x < L.nt; x++)
         if (rows[x]) hipLaunchKernelGGL(tree_write_kernel, dim3(row_grid(rows[x])), dim3(TB), 0, st, Dd, Bd, x, rows[x]);
     const hipError_t e = hipGetLastError();
