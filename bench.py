@@ -513,6 +513,62 @@ def verify_sample(cols, heaps, stream, ends, out_cols, status, m):
     return {"records": m, "encode_bytes_vs_oracle": bool(enc_ok), "decode_vs_oracle": bool(dec_ok)}
 
 
+def tree_leg(dev, n=1 << 18, seed=7):
+    """Schema trees (the generic any-shape path): pkg1.spec's Message — structs, enum, sub-messages,
+    recursive Submessage, value lists, struct lists, message lists, any — n records encoded with
+    spec_encode_tree and decoded with spec_tree_decoder_* (index + decode), wall time per call
+    (both synchronise with the host once per list table); encode bytes and every decoded column
+    checked against the oracle outside the timed region."""
+    from oracle import oracle as O  # noqa: F401  (checker only)
+    from tests.tree_helpers import mismatches, oracle_decode, oracle_encode
+
+    tree = spec_amd.pkg1_tree()
+    cols, heaps, rows = workload.tree_batch(tree, n, seed)
+    dc = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in cols.items()}
+    dh = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in heaps.items()}
+    enc = spec_amd.TreeEncoder(tree, rows, dev)
+    total = int(enc.encode(dc, dh, None, None).item())
+    out = torch.empty(total, dtype=torch.uint8, device=dev)
+    ends = torch.empty(n, dtype=torch.int64, device=dev)
+
+    def encode():
+        enc.encode(dc, dh, out, ends)
+
+    def decode():
+        d.index(out, ends)
+        return d.decode(cols=dcols)
+
+    encode()
+    torch.cuda.synchronize()
+    d = spec_amd.TreeDecoder(tree)
+    d.index(out, ends)
+    dcols = d.alloc(dev)
+    res = {}
+    for name, fn in (("encode", encode), ("decode", decode)):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        reps = 5
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        res[name] = (time.perf_counter() - t0) / reps
+    got = decode()
+    torch.cuda.synchronize()
+    want_stream, want_ends = oracle_encode(tree, cols, heaps, n)
+    ok = np.array_equal(out.cpu().numpy(), want_stream) and np.array_equal(ends.cpu().numpy().view(np.uint64), want_ends)
+    wrows, want = oracle_decode(tree, want_stream, want_ends)
+    ok = ok and wrows == got.rows and not mismatches(tree, [c.cpu().numpy() for c in got.cols], want)
+    col_bytes = sum(int(c.numel()) for c in got.cols)
+    return {"records": n, "tables": len(tree.tables), "columns": len(tree.columns), "rows": rows,
+            "mean_record_bytes": round(total / n, 1), "column_bytes": col_bytes,
+            "decode_ms": round(res["decode"] * 1e3, 3), "decode_mmsg_s": round(n / res["decode"] / 1e6, 1),
+            "decode_gb_s": round((total + col_bytes) / res["decode"] / 1e9, 1),
+            "encode_ms": round(res["encode"] * 1e3, 3), "encode_mmsg_s": round(n / res["encode"] / 1e6, 1),
+            "bit_exact_and_parity_vs_oracle": bool(ok),
+            "note": "generic row kernels (one lane per table row, table by table); wall time incl. host syncs"}
+
+
 def e2e_decode(stream_host, ends_host, dev, reps=5, chunks=8):
     """Pinned host -> H2D -> decode -> D2H of all columns + status, pipelined in record chunks
     over three streams (spec_amd.HostDecoder); whole-pipeline rate (Mmsg/s)."""
@@ -611,6 +667,11 @@ def run(args, env):
                 extras["nested"] = nested_leg(n, args.seed, dev)
             except Exception as e:
                 extras["nested"] = {"error": repr(e)[:300]}
+            try:
+                extras["tree_pkg1"] = tree_leg(dev)
+                checks["tree_parity"] = extras["tree_pkg1"]["bit_exact_and_parity_vs_oracle"]
+            except Exception as e:
+                extras["tree_pkg1"] = {"error": repr(e)[:300]}
         if rank == 0:
             try:
                 sh = stream.cpu().pin_memory()

@@ -247,6 +247,15 @@ int spec_decode_flat(const spec_schema *schema, const uint8_t *stream_bytes, uin
                      const uint64_t *ends, uint64_t n, void *const *columns, uint8_t *status,
                      void *stream);
 
+/* spec_decode_flat_errors: spec_decode_flat plus, per record, which getters' *Err variants
+ * return an error (internal/types/msg.go:233-459: Int32Err, StringErr, ...): errmask[i] bit f
+ * is set when field f is present and Decode<Kind> fails on it (an absent field is no error;
+ * the record-level OpenMessageErr class is in status).  Fields >= 64 are not reported.
+ * Runs the generic kernel (the schema-specialised one does not track field errors). */
+int spec_decode_flat_errors(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
+                            const uint64_t *ends, uint64_t n, void *const *columns, uint8_t *status, uint64_t *errmask,
+                            void *stream);
+
 /* spec_decode_flat_range: records [r0, r1) of a batch only — stream_bytes/stream_len/ends
  * describe the WHOLE batch (absolute offsets) and columns/status are indexed by record, so a
  * host pipeline can decode chunk k while chunk k+1 is still being copied in.  range_bytes =

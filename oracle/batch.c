@@ -330,3 +330,47 @@ long long so_frames_read(const uint8_t *buf, uint64_t len, uint64_t *ends, uint6
     }
     return (long long)k;
 }
+
+/* The *Err getters (internal/types/msg.go:233-459) of every field of every record:
+ * errmask[r] bit f = m.<Kind>Err(tag_f) returns an error (decode.Decode<Kind>(m.field(tag)):
+ * an absent field is nil and decodes without error).  Fields >= 64 are not reported. */
+int so_decode_flat_errors(int nfields, const uint16_t *tags, const uint8_t *kinds, const uint8_t *stream,
+                          const uint64_t *ends, uint64_t n, uint64_t *errmask) {
+    for (uint64_t r = 0; r < n; r++) {
+        const uint64_t s = rec_start(ends, r);
+        so_message m;
+        if (so_open_message_err(stream + s, (size_t)(ends[r] - s), &m)) memset(&m, 0, sizeof(m));
+        uint64_t bits = 0;
+        for (int f = 0; f < nfields && f < 64; f++) {
+            size_t len;
+            const uint8_t *b = so_message_field_raw(&m, tags[f], &len);
+            int k;
+            so_err e = NULL;
+            union {
+                int i; uint8_t u8; int16_t i16; int32_t i32; int64_t i64; uint16_t u16; uint32_t u32; uint64_t u64;
+                float f32; double f64; uint8_t bin[32];
+            } v;
+            size_t off, vlen;
+            switch (kinds[f]) {
+            case SO_KIND_BOOL: e = so_decode_bool(b, len, &v.i, &k); break;
+            case SO_KIND_BYTE: e = so_decode_byte(b, len, &v.u8, &k); break;
+            case SO_KIND_INT16: e = so_decode_int16(b, len, &v.i16, &k); break;
+            case SO_KIND_INT32: e = so_decode_int32(b, len, &v.i32, &k); break;
+            case SO_KIND_INT64: e = so_decode_int64(b, len, &v.i64, &k); break;
+            case SO_KIND_UINT16: e = so_decode_uint16(b, len, &v.u16, &k); break;
+            case SO_KIND_UINT32: e = so_decode_uint32(b, len, &v.u32, &k); break;
+            case SO_KIND_UINT64: e = so_decode_uint64(b, len, &v.u64, &k); break;
+            case SO_KIND_FLOAT32: e = so_decode_float32(b, len, &v.f32, &k); break;
+            case SO_KIND_FLOAT64: e = so_decode_float64(b, len, &v.f64, &k); break;
+            case SO_KIND_BIN64: e = so_decode_bin64(b, len, v.bin, &k); break;
+            case SO_KIND_BIN128: e = so_decode_bin128(b, len, v.bin, &k); break;
+            case SO_KIND_BIN256: e = so_decode_bin256(b, len, v.bin, &k); break;
+            case SO_KIND_STRING: e = so_decode_string(b, len, &off, &vlen, &k); break;
+            case SO_KIND_BYTES: e = so_decode_bytes(b, len, &off, &vlen, &k); break;
+            }
+            if (e) bits |= 1ull << f;
+        }
+        errmask[r] = bits;
+    }
+    return 0;
+}

@@ -218,6 +218,8 @@ def _declare(L):
     L.so_decode_nested_counts.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
     L.so_decode_nested_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64] + [C.c_void_p] * 9
     L.so_parse_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]
+    L.so_decode_flat_errors.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                        C.c_void_p]
     L.so_tree_layout.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_int), C.c_void_p, C.POINTER(C.c_int)]
     L.so_decode_tree_batch.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
     L.so_encode_tree_batch.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
@@ -547,6 +549,19 @@ def decode_flat_batch(tags, kinds, stream: np.ndarray, ends: np.ndarray, widths,
                                     _ptr(ends), n, colptrs, _ptr(status), nthreads)
     assert rc == 0
     return cols, status
+
+
+def decode_flat_errors(tags, kinds, stream: np.ndarray, ends: np.ndarray) -> np.ndarray:
+    """Per record the *Err getters' error bits (bit f = field f's getter errs) -> uint64 [n]."""
+    n = len(ends)
+    em = np.zeros(max(n, 1), np.uint64)
+    tags_a = np.asarray(tags, dtype=np.uint16)
+    kinds_a = np.asarray(kinds, dtype=np.uint8)
+    stream = np.ascontiguousarray(stream, dtype=np.uint8)
+    ends = np.ascontiguousarray(ends, dtype=np.uint64)
+    lib().so_decode_flat_errors(len(tags), _ptr(tags_a), _ptr(kinds_a), _ptr(stream) if stream.size else None,
+                                _ptr(ends) if n else None, n, _ptr(em))
+    return em[:n]
 
 
 def encode_flat_batch(tags, kinds, columns, heaps, n, cap=None):

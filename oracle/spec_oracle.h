@@ -305,6 +305,10 @@ int so_decode_flat_batch(int nfields, const uint16_t *tags, const uint8_t *kinds
                          const uint8_t *stream, const uint64_t *ends, uint64_t n,
                          void *const *columns, uint8_t *status, int nthreads);
 
+/* Per record, which *Err getters err (internal/types/msg.go:233-459): errmask bit f. */
+int so_decode_flat_errors(int nfields, const uint16_t *tags, const uint8_t *kinds, const uint8_t *stream,
+                          const uint64_t *ends, uint64_t n, uint64_t *errmask);
+
 /* Encode N flat records with the Writer (write_test.go:16-78 pattern:
  * NewMessageWriterBuffer + one FieldWriter call per field in schema order + Build).
  * string/bytes columns are {uint32 off, uint32 len} into heaps[i].

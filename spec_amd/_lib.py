@@ -85,6 +85,8 @@ def _declare(L):
     L.spec_decode_flat_range.argtypes = [C.POINTER(SpecSchema), vp, C.c_uint64, vp, C.c_uint64, C.c_uint64,
                                          C.c_uint64, C.POINTER(vp), vp, vp]
     L.spec_decode_frames.argtypes = L.spec_decode_flat_range.argtypes
+    L.spec_decode_flat_errors.argtypes = [C.POINTER(SpecSchema), vp, C.c_uint64, vp, C.c_uint64, C.POINTER(vp), vp, vp,
+                                          vp]
     L.spec_frames_index.argtypes = [vp, C.c_uint64, vp, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.spec_frames_index_device_workspace_size.argtypes = [C.c_uint64]
     L.spec_frames_index_device_workspace_size.restype = C.c_size_t

@@ -90,6 +90,22 @@ def decode_flat(schema: Schema, stream: torch.Tensor, ends: torch.Tensor, *, col
     return Columns(schema, cols, st)
 
 
+def decode_flat_errors(schema: Schema, stream: torch.Tensor, ends: torch.Tensor, cuda_stream=None):
+    """spec_decode_flat_errors: decode_flat plus the per-record field error mask (bit f: field f's
+    <Kind>Err getter errs, internal/types/msg.go:233-459) -> (Columns, errmask int64 [n])."""
+    _check_dev(stream, "stream", torch.uint8)
+    _check_dev(ends, "ends", torch.int64)
+    n = ends.numel()
+    cols = alloc_columns(schema, n, stream.device)
+    st = torch.empty(n, dtype=torch.uint8, device=stream.device)
+    em = torch.empty(max(n, 1), dtype=torch.int64, device=stream.device)
+    ptrs = (C.c_void_p * max(1, len(cols)))(*[c.data_ptr() for c in cols])
+    rc = _lib.lib().spec_decode_flat_errors(C.byref(schema.c), _ptr(stream), stream.numel(), _ptr(ends), n, ptrs,
+                                             _ptr(st), _ptr(em), _stream_handle(cuda_stream))
+    _lib.check(rc, "spec_decode_flat_errors")
+    return Columns(schema, cols, st), em[:n]
+
+
 class Decoder:
     """Pre-bound spec_decode_flat call (arguments marshalled once) for repeated launches."""
 

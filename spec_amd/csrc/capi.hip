@@ -76,6 +76,7 @@ int hip_rc(hipError_t e) {
 void fill_field_set(spec::FieldSet &fs, const spec_schema *schema, void *const *columns, uint8_t *status) {
     memset(&fs, 0, sizeof(fs));
     fs.status = status;
+    fs.errmask = nullptr;
     fs.nfields = schema->nfields;
     uint8_t order[SPEC_MAX_FIELDS];
     table_order(schema, order);
@@ -164,7 +165,7 @@ int spec_copy_d2d(void *dst, const void *src, size_t bytes, void *stream) {
 
 static int decode_flat_impl(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
                             const uint64_t *ends, uint64_t r0, uint64_t r1, uint64_t range_bytes, uint32_t head,
-                            void *const *columns, uint8_t *status, void *stream) {
+                            void *const *columns, uint8_t *status, void *stream, uint64_t *errmask = nullptr) {
     int rc = check_schema(schema);
     if (rc) return rc;
     if (r1 < r0) return SPEC_E_INVALID_ARGUMENT;
@@ -182,10 +183,12 @@ static int decode_flat_impl(const spec_schema *schema, const uint8_t *stream_byt
     a.r0 = r0;
     a.head = head;
     fill_field_set(a.f, schema, columns, status);
+    a.f.errmask = errmask;
     // LDS slab from the mean record size of the range (the caller knows the range's bytes;
     // for a whole batch it is stream_len / n)
     double avg = range_bytes ? (double)range_bytes / (double)(r1 - r0) : (double)stream_len / (double)r1;
-    int j = spec::jit_launch_decode_flat(schema, a, avg, (hipStream_t)stream);
+    // field error masks come from the generic path (the specialised kernels do not track them)
+    int j = errmask ? 0 : spec::jit_launch_decode_flat(schema, a, avg, (hipStream_t)stream);
     if (j < 0) return hip_rc(hipGetLastError());
     if (j == 0 && spec::launch_decode_flat(a, avg, (hipStream_t)stream)) return hip_rc(hipGetLastError());
     return SPEC_OK;
@@ -201,6 +204,13 @@ int spec_decode_flat(const spec_schema *schema, const uint8_t *stream_bytes, uin
                      const uint64_t *ends, uint64_t n, void *const *columns, uint8_t *status,
                      void *stream) {
     return decode_flat_impl(schema, stream_bytes, stream_len, ends, 0, n, 0, 0, columns, status, stream);
+}
+
+int spec_decode_flat_errors(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
+                            const uint64_t *ends, uint64_t n, void *const *columns, uint8_t *status, uint64_t *errmask,
+                            void *stream) {
+    if (!errmask && n) return SPEC_E_INVALID_ARGUMENT;
+    return decode_flat_impl(schema, stream_bytes, stream_len, ends, 0, n, 0, 0, columns, status, stream, errmask);
 }
 
 int spec_decode_frames(const spec_schema *schema, const uint8_t *frames, uint64_t frames_len,

@@ -38,6 +38,7 @@ namespace spec {
 // The fields a record decode produces: one column per schema field + the status column.
 struct FieldSet {
     uint8_t *status;
+    uint64_t *errmask; // optional: bit f = field f's <Kind>Err getter errs (generic path only)
     uint32_t nfields;
     uint16_t tags[SPEC_MAX_FIELDS];
     uint8_t kinds[SPEC_MAX_FIELDS];
@@ -212,10 +213,13 @@ __host__ __device__ constexpr uint32_t cross_kind_type(uint32_t k) {
 // NAT = true: the caller has checked that the value's type byte is cross_kind_type(KIND) (or
 // the field is empty), so the cross-width branches fold away; results are those of NAT = false
 // for such values.
+// okp (optional): set to false when the decoder returns an error (the getter's *Err variant,
+// internal/types/msg.go:233-459); a non-empty field only (callers handle flen <= 0).
 template <uint32_t KIND, bool NAT = false, class Pos>
-__device__ __forceinline__ Val decode_tail_k(const Win &w, Pos lo, Pos e, long long to_stream) {
+__device__ __forceinline__ Val decode_tail_k(const Win &w, Pos lo, Pos e, long long to_stream, bool *okp = nullptr) {
     const Tail &t = w.t;
     Val out = {0, 0, 0, 0};
+    bool okv = true;
     const long long flen = (long long)(e - lo);
     constexpr uint32_t NT = cross_kind_type(KIND);
     const uint32_t type = (NAT && NT) ? NT : (uint32_t)t.q0 & 0xff;
@@ -226,7 +230,8 @@ __device__ __forceinline__ Val decode_tail_k(const Win &w, Pos lo, Pos e, long l
     if constexpr (KIND == K_BOOL) { // DecodeBool, byte.go:38-51: true iff type == TypeTrue
         out.v0 = ((flen > 0) & (type == T_TRUE)) ? 1 : 0;
     } else if constexpr (KIND == K_BYTE) { // DecodeByte, byte.go:16-34
-        out.v0 = ((type == T_BYTE) & (flen >= 2)) ? (R & 0xff) : 0;
+        okv = (type == T_BYTE) & (flen >= 2);
+        out.v0 = okv ? (R & 0xff) : 0;
     } else if constexpr (KIND == K_INT16 | KIND == K_INT32 | KIND == K_INT64) {
         // DecodeInt16/32/64, int.go:16-135: 32-bit routine for Int16/Int32, 64-bit for Int64
         const bool w32 = (type == T_INT16) | (type == T_INT32);
@@ -235,6 +240,7 @@ __device__ __forceinline__ Val decode_tail_k(const Win &w, Pos lo, Pos e, long l
         bool ok = (flen > 0) & (w32 | (type == T_INT64)) & (m >= 0);
         if (KIND == K_INT16) ok = ok & (x >= -32768) & (x <= 32767);
         if (KIND == K_INT32) ok = ok & (w32 | ((x >= INT32_MIN) & (x <= INT32_MAX)));
+        okv = ok;
         out.v0 = ok ? (uint64_t)x : 0;
         if (KIND == K_INT16) out.v0 &= 0xffff;
         if (KIND == K_INT32) out.v0 &= 0xffffffffu;
@@ -245,6 +251,7 @@ __device__ __forceinline__ Val decode_tail_k(const Win &w, Pos lo, Pos e, long l
         bool ok = (flen > 0) & (w32 | (type == T_UINT64)) & (m >= 0);
         if (KIND == K_UINT16) ok = ok & (x <= 0xffffull);
         if (KIND == K_UINT32) ok = ok & (x <= 0xffffffffull);
+        okv = ok;
         out.v0 = ok ? x : 0;
     } else if constexpr (KIND == K_FLOAT32) { // DecodeFloat32, float.go:15-32 (via float64 + range check)
         uint32_t b = (uint32_t)(R & 0xffffffffu);
@@ -258,19 +265,24 @@ __device__ __forceinline__ Val decode_tail_k(const Win &w, Pos lo, Pos e, long l
         const bool over = !nan & ((d & 0x7fffffffffffffffull) > 0x47EFFFFFE0000000ull);
         const uint32_t from64 = f64_to_f32_bits_bf(d);
         const bool ok32 = (type == T_FLOAT32) & (flen >= 5) & !inf, ok64 = (type == T_FLOAT64) & (flen >= 9) & !over;
+        okv = ok32 | ok64;
         out.v0 = ok32 ? b : (ok64 ? from64 : 0u);
     } else if constexpr (KIND == K_FLOAT64) { // DecodeFloat64, float.go:34-78
         const uint64_t from32 = f32_to_f64_bits_bf((uint32_t)(R & 0xffffffffu));
         const bool ok32 = (type == T_FLOAT32) & (flen >= 5), ok64 = (type == T_FLOAT64) & (flen >= 9);
+        okv = ok32 | ok64;
         out.v0 = ok32 ? from32 : (ok64 ? R : 0ull);
     } else if constexpr (KIND == K_BIN64) { // DecodeBin64, bin.go:15-44: raw 8 bytes before the type byte
-        out.v0 = ((type == T_BIN64) & (flen >= 9)) ? __builtin_bswap64(R) : 0;
+        okv = (type == T_BIN64) & (flen >= 9);
+        out.v0 = okv ? __builtin_bswap64(R) : 0;
     } else if constexpr (KIND == K_BIN128) {
         const bool ok = (type == T_BIN128) & (flen >= 17);
+        okv = ok;
         out.v0 = ok ? w.x0 : 0;
         out.v1 = ok ? __builtin_bswap64(R) : 0;
     } else if constexpr (KIND == K_BIN256) {
         const bool ok = (type == T_BIN256) & (flen >= 33);
+        okv = ok;
         out.v0 = ok ? w.x0 : 0;
         out.v1 = ok ? w.x1 : 0;
         out.v2 = ok ? w.x2 : 0;
@@ -283,8 +295,10 @@ __device__ __forceinline__ Val decode_tail_k(const Win &w, Pos lo, Pos e, long l
         const long long off = end - (long long)len;
         const bool ok = (type == (str ? T_STRING : T_BYTES)) & (flen > 0) & (m >= 0) & (end >= (long long)lo) &
                         (off >= (long long)lo) & (len != 0);
+        okv = (type == (str ? T_STRING : T_BYTES)) & (m >= 0) & (end >= (long long)lo) & (off >= (long long)lo);
         out.v0 = ok ? ((uint64_t)(uint32_t)(off + to_stream) | ((uint64_t)len << 32)) : 0;
     }
+    if (okp) *okp = okv;
     return out;
 }
 
@@ -346,14 +360,16 @@ __device__ __forceinline__ void store_value_k(void *colp, uint64_t r, const Val 
 
 // run-time kind dispatch for the generic path (wave-uniform switches around ONE shared
 // tail-window load, so the generic kernel stays compact)
+// returns false when the field is present and its decoder errs (the *Err getter's error)
 template <class Src>
-__device__ __forceinline__ void decode_store(const Src &s, uint32_t kind, typename Src::pos_t lo, long long end,
+__device__ __forceinline__ bool decode_store(const Src &s, uint32_t kind, typename Src::pos_t lo, long long end,
                                              long long to_stream, void *col, uint64_t r) {
     Val v = {0, 0, 0, 0};
+    bool ok = true;
     if (end > 0) {
         const typename Src::pos_t e = lo + (typename Src::pos_t)end;
 #define SPEC_CASE(K) \
-    case K: v = decode_tail_k<K>(load_win<K>(s, e), lo, e, to_stream); break;
+    case K: v = decode_tail_k<K>(load_win<K>(s, e), lo, e, to_stream, &ok); break;
         switch (kind) {
             SPEC_CASE(K_BOOL)
             SPEC_CASE(K_BYTE)
@@ -386,6 +402,7 @@ __device__ __forceinline__ void decode_store(const Src &s, uint32_t kind, typena
     case K_BIN256: store_value_k<K_BIN256>(col, r, v); break;
     default: ((uint64_t *)c)[r] = v.v0; break;
     }
+    return ok;
 }
 
 // ---- record trailer: DecodeMessageTable, internal/decode/msg.go:14-99 -------------------
@@ -520,12 +537,15 @@ __device__ __forceinline__ void decode_record_generic(const Src &s, typename Src
     const RecInfo ri = rec_open(s, rs, re);
     if (fs.status) fs.status[r] = (uint8_t)ri.tr.st;
     const pos_t dstart = (pos_t)ri.tr.dstart;
+    uint64_t errs = 0;
     for (uint32_t f = 0; f < fs.nfields; f++) {
         const uint32_t kind = fs.kinds[f];
         if (kind == K_LIST) continue;
         const long long end = rec_field_end(s, ri, fs.tags[f], fs.rank[f]);
-        decode_store(s, kind, dstart, end, to_stream, fs.cols[f], r);
+        const bool ok = decode_store(s, kind, dstart, end, to_stream, fs.cols[f], r);
+        if (!ok && f < 64) errs |= 1ull << f;
     }
+    if (fs.errmask) fs.errmask[r] = errs;
 }
 
 // ---- fast path: compile-time schema ------------------------------------------------------

@@ -72,3 +72,23 @@ def concat_records(recs):
     ends = np.cumsum(lens, dtype=np.uint64) if len(recs) else np.zeros(0, np.uint64)
     stream = np.frombuffer(b"".join(recs), dtype=np.uint8).copy()
     return stream, ends
+
+
+def check_errors(dev, schema, stream: np.ndarray, ends: np.ndarray, label=""):
+    """spec_decode_flat_errors vs the oracle: columns, status and the *Err getters' bits."""
+    stream = np.ascontiguousarray(stream, dtype=np.uint8)
+    ends = np.ascontiguousarray(ends, dtype=np.uint64)
+    want_cols, want_status = O.decode_flat_batch(schema.tags, schema.kinds, stream, ends, schema.widths, nthreads=4)
+    want_mask = O.decode_flat_errors(schema.tags, schema.kinds, stream, ends)
+    d_stream = to_dev(stream if stream.size else np.zeros(1, np.uint8), dev)[: stream.size]
+    got, mask = spec_amd.decode_flat_errors(schema, d_stream, to_dev(ends.view(np.int64), dev))
+    torch.cuda.synchronize()
+    assert np.array_equal(got.status.cpu().numpy(), want_status), f"{label}: status"
+    for f in range(len(schema)):
+        assert np.array_equal(got.cols[f].cpu().numpy(), want_cols[f]), f"{label}: field {f}"
+    gm = mask.cpu().numpy().view(np.uint64)
+    if not np.array_equal(gm, want_mask):
+        i = int(np.nonzero(gm != want_mask)[0][0])
+        raise AssertionError(f"{label}: errmask[{i}] gpu={gm[i]:x} oracle={want_mask[i]:x} "
+                             f"record={_rec(stream, ends, i).tobytes().hex()}")
+    return gm

@@ -13,6 +13,7 @@ import struct
 
 import pytest
 
+import numpy as np
 from oracle import oracle as O
 
 T = dict(undefined=0, true=1, false=2, byte=3, int16=10, int32=11, int64=12, uint16=20, uint32=21,
@@ -317,3 +318,20 @@ def test_signed_zigzag():
         b = O.put_reverse_int64(v)
         got, n = O.reverse_int64(b)
         assert got == v and n == len(b)
+
+
+def test_err_getters_mask():
+    """*Err getters (internal/types/msg.go:233-459): an absent field is no error (field(tag) is
+    nil => Decode on empty input), a type mismatch is; bool never errs (byte.go:38-51)."""
+    w = O.Writer()
+    w.message()
+    assert w.field(1, "int64", 1 << 40) is None   # read as int32: overflow
+    assert w.field(2, "string", "x") is None      # read as int64: invalid type
+    assert w.field(3, "bool", True) is None       # read as bool: fine
+    assert w.field(4, "uint16", 7) is None        # read as uint64: cross-width fine
+    data, err = w.end()
+    w.close()
+    stream = np.frombuffer(data, np.uint8)
+    ends = np.array([len(data)], np.uint64)
+    mask = O.decode_flat_errors([1, 2, 3, 4, 5], [4, 5, 1, 8, 4], stream, ends)  # tag 5 absent
+    assert int(mask[0]) == 0b00011
