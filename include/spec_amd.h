@@ -408,6 +408,10 @@ int spec_decode_nested_onepass(const spec_nested_schema *schema, const uint8_t *
                                uint32_t *item_begin, void *const *item_columns, uint8_t *item_status,
                                uint64_t item_cap, void *workspace, size_t workspace_size, uint64_t *total_items,
                                void *stream);
+/* spec_set_nested_mode: the kernel of spec_decode_nested's decode pass (results never differ):
+ * 1 a wave per 64-record group, 2 persistent waves (one LDS slab each), 3 persistent waves with
+ * two slabs each, the next group's bytes staged while the current group decodes (default). */
+void spec_set_nested_mode(int mode);
 /* spec_decode_nested_jit_compile: compile (hiprtc, no GPU needed) the schema-specialised one-pass
  * kernel; code-object size, 0 if neither schema has a fast path. */
 long long spec_decode_nested_jit_compile(const spec_nested_schema *schema);

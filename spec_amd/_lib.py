@@ -108,6 +108,8 @@ def _declare(L):
     L.spec_decode_nested_onepass.argtypes = [C.POINTER(SpecNestedSchema), vp, C.c_uint64, vp, C.c_uint64,
                                              C.POINTER(vp), vp, vp, C.POINTER(vp), vp, C.c_uint64, vp, C.c_size_t,
                                              vp, vp]
+    L.spec_set_nested_mode.argtypes = [C.c_int]
+    L.spec_set_nested_mode.restype = None
     L.spec_decode_nested_jit_compile.argtypes = [C.POINTER(SpecNestedSchema)]
     L.spec_decode_nested_jit_compile.restype = C.c_longlong
     L.spec_encode_nested_jit_compile.argtypes = [C.POINTER(SpecNestedSchema)]

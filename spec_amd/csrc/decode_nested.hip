@@ -90,6 +90,16 @@ __global__ __launch_bounds__(64) void nested_onepass_kernel(NestedArgs a) {
     nested_decode_body<RuntimeSpec, RuntimeSpec, true>(a);
 }
 
+__global__ __launch_bounds__(64) void nested_persist1_kernel(NestedArgs a) {
+    nested_decode_persist_body<RuntimeSpec, RuntimeSpec, 1>(a);
+}
+
+__global__ __launch_bounds__(64) void nested_persist2_kernel(NestedArgs a) {
+    nested_decode_persist_body<RuntimeSpec, RuntimeSpec, 2>(a);
+}
+
+int g_nested_mode = NESTED_PERSIST2;
+
 } // namespace
 
 int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream) {
@@ -106,12 +116,26 @@ int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+int nested_decode_mode() { return g_nested_mode; }
+
+// The decode pass after the index kernels: a wave per group (NESTED_GROUPS) or persistent
+// waves looping over groups (NESTED_PERSIST1/2, spec_set_nested_mode).
 int launch_nested_decode(const spec_nested_schema *schema, NestedArgs a, double avg_record, hipStream_t stream) {
     if (a.n == 0) return 0;
     a.slab = decode_slab_bytes(avg_record);
-    const int j = jit_launch_nested(schema, a, false, stream);
+    const int mode = g_nested_mode;
+    const int j = jit_launch_nested(schema, a, mode, stream);
     if (j != 0) return j > 0 ? 0 : -1;
     const uint64_t groups = (a.n + 63) / 64;
+    if (mode >= NESTED_PERSIST1 && a.slab) {
+        const int nbuf = mode == NESTED_PERSIST2 ? 2 : 1;
+        const unsigned grid = nested_persist_grid(groups, a.slab, nbuf);
+        if (nbuf == 2)
+            hipLaunchKernelGGL(nested_persist2_kernel, dim3(grid), dim3(64), (size_t)2 * a.slab, stream, a);
+        else
+            hipLaunchKernelGGL(nested_persist1_kernel, dim3(grid), dim3(64), (size_t)a.slab, stream, a);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     dim3 grid((unsigned)((groups + DEC_WAVES - 1) / DEC_WAVES)), block(64 * DEC_WAVES);
     hipLaunchKernelGGL(nested_decode_kernel, grid, block, (size_t)DEC_WAVES * a.slab, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -142,10 +166,14 @@ int launch_nested_onepass(const spec_nested_schema *schema, NestedArgs a, double
     a.slab = decode_slab_bytes(avg_record);
     const uint64_t groups = (a.n + 63) / 64;
     if (hipMemsetAsync(a.group_base, 0, (groups + 1) * sizeof(uint64_t), stream) != hipSuccess) return -1;
-    const int j = jit_launch_nested(schema, a, true, stream);
+    const int j = jit_launch_nested(schema, a, NESTED_ONEPASS, stream);
     if (j < 0) return -1;
     if (j == 0) hipLaunchKernelGGL(nested_onepass_kernel, dim3((unsigned)groups), dim3(64), (size_t)a.slab, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 } // namespace spec
+
+extern "C" void spec_set_nested_mode(int mode) {
+    if (mode >= spec::NESTED_GROUPS && mode <= spec::NESTED_PERSIST2) spec::g_nested_mode = mode;
+}

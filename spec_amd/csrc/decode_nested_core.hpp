@@ -332,6 +332,91 @@ __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
     }
 }
 
+// Persistent kernel body of the two-pass decode (group offsets from the index kernels): wave w
+// of the W in the grid decodes groups w, w + W, w + 2W, ...  Each wave stays resident for the
+// whole batch — no per-group wave launch — and with NBUF = 2 owns two slabs: the next group's
+// DMA and its ends / item offset are issued before this group is decoded, so its stream bytes
+// arrive while the current group's outer records and items are being decoded.
+template <class OSpec, class ISpec, int NBUF>
+__device__ __forceinline__ void nested_decode_persist_body(const NestedArgs &a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wpb = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t ngroups = (a.n + 63) / 64;
+    const uint64_t W = (uint64_t)gridDim.x * wpb;
+    uint64_t g = (uint64_t)blockIdx.x * wpb + wave;
+    if (g >= ngroups) return;
+    uint8_t *slabs = smem + (size_t)wave * NBUF * a.slab;
+    __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
+    DecodeArgs d;
+    d.stream = a.stream;
+    d.stream_len = a.stream_len;
+    d.ends = a.ends;
+    d.n = a.n;
+    d.r0 = 0;
+    d.head = 0;
+    uint64_t lo, hi;
+    load_group_ends(d, g * 64, lane, lo, hi);
+    Group cur = make_group(d, g * 64, lane, lo, hi, a.slab);
+    uint64_t base_cur = a.group_base[g];
+    int b = 0;
+    if (cur.in_lds) issue_dma(rsrc, slabs, cur, lane);
+    uint64_t gn = g + W, nlo = 0, nhi = 0, base_nxt = 0;
+    if (gn < ngroups) {
+        load_group_ends(d, gn * 64, lane, nlo, nhi);
+        base_nxt = a.group_base[gn];
+    }
+    while (true) {
+        const bool has_next = gn < ngroups;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this group's DMA; the next group's ends
+        uint8_t *slab = slabs + b * a.slab;
+        if (cur.in_lds) fix_stream_tail(d, rsrc, slab, cur, lane);
+        const Group nxt = make_group(d, has_next ? gn * 64 : g * 64, lane, nlo, nhi, a.slab);
+        const uint64_t base_n = uniform64(base_nxt);
+        const uint64_t g2 = gn + W;
+        uint64_t lo2 = 0, hi2 = 0, base2 = 0;
+        if constexpr (NBUF == 2) {
+            if (has_next && nxt.in_lds) issue_dma(rsrc, slabs + (1 - b) * a.slab, nxt, lane);
+            if (g2 < ngroups) {
+                load_group_ends(d, g2 * 64, lane, lo2, hi2);
+                base2 = a.group_base[g2];
+            }
+        }
+        const uint64_t r = g * 64 + lane;
+        const bool valid = r < a.n;
+        const uint64_t item_base = uniform64(base_cur);
+        if (cur.in_lds) {
+            LdsSrc s{(lds_u8 *)slab};
+            nested_group_body<OSpec, ISpec, false>(s, SLAB_GUARD + (long long)(cur.rec_lo - cur.aligned_lo),
+                                                   SLAB_GUARD + (long long)(cur.rec_hi - cur.aligned_lo), valid, r, g,
+                                                   item_base, lane, (long long)cur.aligned_lo - SLAB_GUARD, a);
+        } else {
+            GlobalSrc s{rsrc, a.stream_len};
+            nested_group_body<OSpec, ISpec, false>(s, (long long)cur.rec_lo, (long long)cur.rec_hi, valid, r, g,
+                                                   item_base, lane, 0, a);
+        }
+        if (!has_next) break;
+        if constexpr (NBUF == 1) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // every LDS read of this group done
+            __builtin_amdgcn_wave_barrier();
+            if (nxt.in_lds) issue_dma(rsrc, slabs, nxt, lane);
+            if (g2 < ngroups) {
+                load_group_ends(d, g2 * 64, lane, lo2, hi2);
+                base2 = a.group_base[g2];
+            }
+        } else {
+            b = 1 - b;
+        }
+        g = gn;
+        gn = g2;
+        cur = nxt;
+        base_cur = base_n;
+        nlo = lo2;
+        nhi = hi2;
+        base_nxt = base2;
+    }
+}
+
 // Count kernel of the two-pass index: per group, the item total.
 __device__ __forceinline__ void nested_count_body(const NestedArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];

@@ -41,7 +41,7 @@ namespace {
 
 struct Entry {
     hipModule_t mod = nullptr;
-    hipFunction_t fn[2] = {nullptr, nullptr};
+    hipFunction_t fn[4] = {nullptr, nullptr, nullptr, nullptr};
     bool failed = false;
 };
 
@@ -143,7 +143,11 @@ std::string generate_nested(const spec_nested_schema *s) {
     o << "extern \"C\" __global__ __launch_bounds__(64) void spec_decode_nested_jit(spec::NestedArgs a) {\n"
       << "  spec::nested_decode_body<" << specs << ", true>(a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(64) void spec_decode_nested2_jit(spec::NestedArgs a) {\n"
-      << "  spec::nested_decode_body<" << specs << ", false>(a);\n}\n";
+      << "  spec::nested_decode_body<" << specs << ", false>(a);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(64) void spec_decode_nested_p1_jit(spec::NestedArgs a) {\n"
+      << "  spec::nested_decode_persist_body<" << specs << ", 1>(a);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(64) void spec_decode_nested_p2_jit(spec::NestedArgs a) {\n"
+      << "  spec::nested_decode_persist_body<" << specs << ", 2>(a);\n}\n";
     return o.str();
 }
 
@@ -339,17 +343,18 @@ Entry load(const std::vector<char> &code, Prog p) {
         e.failed = true;
         return e;
     }
-    const char *names[4][2] = {{"spec_decode_flat_jit", nullptr},
-                               {"spec_encode_size_jit", "spec_encode_write_jit"},
-                               {"spec_decode_nested_jit", "spec_decode_nested2_jit"},
-                               {"spec_encode_nested_size_jit", "spec_encode_nested_write_jit"}};
+    const char *names[4][4] = {{"spec_decode_flat_jit", nullptr, nullptr, nullptr},
+                               {"spec_encode_size_jit", "spec_encode_write_jit", nullptr, nullptr},
+                               {"spec_decode_nested_jit", "spec_decode_nested2_jit", "spec_decode_nested_p1_jit",
+                                "spec_decode_nested_p2_jit"},
+                               {"spec_encode_nested_size_jit", "spec_encode_nested_write_jit", nullptr, nullptr}};
     bool ok = hipModuleLoadData(&e.mod, code.data()) == hipSuccess;
-    for (int i = 0; ok && i < 2; i++)
+    for (int i = 0; ok && i < 4; i++)
         if (names[p][i]) ok = hipModuleGetFunction(&e.fn[i], e.mod, names[p][i]) == hipSuccess;
     if (!ok) {
         (void)hipGetLastError();
         e.failed = true;
-        e.fn[0] = e.fn[1] = nullptr;
+        for (hipFunction_t &f : e.fn) f = nullptr;
     }
     return e;
 }
@@ -445,7 +450,7 @@ long long jit_compile_only_nested(const spec_nested_schema *schema) {
     return (long long)compile_source(generate_nested(schema), NESTED).size();
 }
 
-int jit_launch_nested(const spec_nested_schema *schema, const NestedArgs &a, bool onepass, hipStream_t stream) {
+int jit_launch_nested(const spec_nested_schema *schema, const NestedArgs &a, int mode, hipStream_t stream) {
     if (a.slab == 0) return 0; // records too large for LDS: generic kernel
     const Entry *e = lookup_nested(schema);
     if (!e) return 0;
@@ -453,9 +458,15 @@ int jit_launch_nested(const spec_nested_schema *schema, const NestedArgs &a, boo
     size_t size = sizeof(args);
     void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                      HIP_LAUNCH_PARAM_END};
-    const unsigned groups = (unsigned)((a.n + 63) / 64);
-    hipError_t rc = hipModuleLaunchKernel(e->fn[onepass ? 0 : 1], groups, 1, 1, 64, 1, 1, a.slab, stream, nullptr,
-                                          extra);
+    const uint64_t groups = (a.n + 63) / 64;
+    unsigned grid = (unsigned)groups;
+    size_t lds = a.slab;
+    if (mode >= NESTED_PERSIST1) {
+        const int nbuf = mode == NESTED_PERSIST2 ? 2 : 1;
+        grid = nested_persist_grid(groups, a.slab, nbuf);
+        lds = (size_t)nbuf * a.slab;
+    }
+    hipError_t rc = hipModuleLaunchKernel(e->fn[mode], grid, 1, 1, 64, 1, 1, (unsigned)lds, stream, nullptr, extra);
     return rc == hipSuccess ? 1 : -1;
 }
 

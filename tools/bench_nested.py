@@ -39,6 +39,19 @@ def main():
     e2 = torch.empty_like(ends)
     enc_ms, _ = bench.kernel_time_events(lambda: enc.encode(outer, oh, ib, items, ih, m, out, e2), 10)
     two_ms, _ = bench.kernel_time_events(two, 20)
+    L = spec_amd.lib()
+    modes = {}
+    ref_items = [c.clone() for c in d.items]
+    for mode, name in ((1, "groups"), (2, "persist1"), (3, "persist2")):
+        L.spec_set_nested_mode(mode)
+        for c in d.items:
+            c.zero_()
+        dec_ms, _ = bench.kernel_time_events(d.decode, 20)
+        torch.cuda.synchronize()
+        same = all(torch.equal(a_, b_) for a_, b_ in zip(d.items, ref_items)) and int(d.status.sum()) == 0
+        modes[name] = {"decode_ms": round(dec_ms, 4), "same": bool(same)}
+    L.spec_set_nested_mode(3)
+    res["modes"] = modes
     one_ms, _ = bench.kernel_time_events(d.decode_onepass, 20)
     torch.cuda.synchronize()
     ok = int(d.total.item()) == m and torch.equal(d.items[0], items[0]) and torch.equal(d.item_begin, ib)
