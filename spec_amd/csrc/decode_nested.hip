@@ -90,15 +90,11 @@ __global__ __launch_bounds__(64) void nested_onepass_kernel(NestedArgs a) {
     nested_decode_body<RuntimeSpec, RuntimeSpec, true>(a);
 }
 
-__global__ __launch_bounds__(64) void nested_persist1_kernel(NestedArgs a) {
-    nested_decode_persist_body<RuntimeSpec, RuntimeSpec, 1>(a);
+__global__ __launch_bounds__(256) void nested_decode_ranges_kernel(NestedArgs a) {
+    nested_decode_body<RuntimeSpec, RuntimeSpec, false, true>(a);
 }
 
-__global__ __launch_bounds__(64) void nested_persist2_kernel(NestedArgs a) {
-    nested_decode_persist_body<RuntimeSpec, RuntimeSpec, 2>(a);
-}
-
-int g_nested_mode = NESTED_PERSIST2;
+int g_nested_mode = NESTED_RANGES;
 
 } // namespace
 
@@ -116,10 +112,8 @@ int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int nested_decode_mode() { return g_nested_mode; }
-
-// The decode pass after the index kernels: a wave per group (NESTED_GROUPS) or persistent
-// waves looping over groups (NESTED_PERSIST1/2, spec_set_nested_mode).
+// The decode pass after the index kernels: a wave per 64-record group; its items found by an
+// owner search (NESTED_GROUPS) or from ranges precomputed into LDS (NESTED_RANGES, default).
 int launch_nested_decode(const spec_nested_schema *schema, NestedArgs a, double avg_record, hipStream_t stream) {
     if (a.n == 0) return 0;
     a.slab = decode_slab_bytes(avg_record);
@@ -127,17 +121,12 @@ int launch_nested_decode(const spec_nested_schema *schema, NestedArgs a, double 
     const int j = jit_launch_nested(schema, a, mode, stream);
     if (j != 0) return j > 0 ? 0 : -1;
     const uint64_t groups = (a.n + 63) / 64;
-    if (mode >= NESTED_PERSIST1 && a.slab) {
-        const int nbuf = mode == NESTED_PERSIST2 ? 2 : 1;
-        const unsigned grid = nested_persist_grid(groups, a.slab, nbuf);
-        if (nbuf == 2)
-            hipLaunchKernelGGL(nested_persist2_kernel, dim3(grid), dim3(64), (size_t)2 * a.slab, stream, a);
-        else
-            hipLaunchKernelGGL(nested_persist1_kernel, dim3(grid), dim3(64), (size_t)a.slab, stream, a);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
     dim3 grid((unsigned)((groups + DEC_WAVES - 1) / DEC_WAVES)), block(64 * DEC_WAVES);
-    hipLaunchKernelGGL(nested_decode_kernel, grid, block, (size_t)DEC_WAVES * a.slab, stream, a);
+    if (mode == NESTED_RANGES)
+        hipLaunchKernelGGL(nested_decode_ranges_kernel, grid, block,
+                           (size_t)DEC_WAVES * (a.slab + NESTED_RANGE_BYTES), stream, a);
+    else
+        hipLaunchKernelGGL(nested_decode_kernel, grid, block, (size_t)DEC_WAVES * a.slab, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -175,5 +164,5 @@ int launch_nested_onepass(const spec_nested_schema *schema, NestedArgs a, double
 } // namespace spec
 
 extern "C" void spec_set_nested_mode(int mode) {
-    if (mode >= spec::NESTED_GROUPS && mode <= spec::NESTED_PERSIST2) spec::g_nested_mode = mode;
+    if (mode == spec::NESTED_GROUPS || mode == spec::NESTED_RANGES) spec::g_nested_mode = mode;
 }

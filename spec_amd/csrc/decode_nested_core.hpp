@@ -228,6 +228,82 @@ __device__ __forceinline__ void decode_group_items(const Src &s, const ListInfo 
     }
 }
 
+// The group's items from PRECOMPUTED ranges (LdsSrc only): each record's lane first writes the
+// slab range [lo, hi) of each of its items (its list table entries, List.GetBytes) into an LDS
+// array indexed by the group item, a window of NESTED_RANGE_ITEMS at a time; then item j of the
+// window reads its range with one LDS read — no owner search and no table reads on the item's
+// dependency chain.  Ranges pack two 16-bit slab positions (slabs are < 64 KiB); a nil item
+// (end > dataSize) is the empty range, a panicking one (start > end) RANGE_PANIC.
+constexpr uint32_t NESTED_RANGE_ITEMS = 256;
+constexpr uint32_t NESTED_RANGE_BYTES = NESTED_RANGE_ITEMS * 4;
+constexpr uint32_t RANGE_PANIC = 0xffffu;
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <class ISpec>
+__device__ __forceinline__ void decode_group_items_ranges(const LdsSrc &s, const ListInfo &li, uint32_t excl,
+                                                          uint32_t total, uint64_t item_base, int lane,
+                                                          long long to_stream, uint32_t *rng,
+                                                          const NestedArgs &a) {
+    constexpr int U = NESTED_ITEM_U;
+    for (uint32_t w0 = 0; w0 < total; w0 += NESTED_RANGE_ITEMS) {
+        const uint32_t w1 = total - w0 < NESTED_RANGE_ITEMS ? total : w0 + NESTED_RANGE_ITEMS;
+        // this record's items [excl, excl + count) within the window [w0, w1)
+        const uint32_t i0 = w0 > excl ? w0 - excl : 0u;
+        const uint32_t e1 = excl + li.count < w1 ? excl + li.count : w1;
+        const uint32_t i1 = e1 > excl ? e1 - excl : 0u;
+        for (uint32_t i = i0; i < i1; i++) {
+            uint32_t start, end;
+            if (li.big) {
+                end = be32_at(s, li.tstart + 4ll * i);
+                start = i ? be32_at(s, li.tstart + 4ll * (i - 1)) : 0;
+            } else {
+                end = be16_at(s, li.tstart + 2ll * i);
+                start = i ? be16_at(s, li.tstart + 2ll * (i - 1)) : 0;
+            }
+            uint32_t v;
+            if (end > li.dsize) v = 0u;              // nil: OpenItemErr(nil), an empty message
+            else if (start > end) v = RANGE_PANIC;   // Go panics on the slice
+            else v = (uint32_t)(li.dstart + start) | ((uint32_t)(li.dstart + end) << 16);
+            rng[excl + i - w0] = v;
+        }
+        wave_lds_sync();
+        for (uint32_t j0 = w0; j0 < w1; j0 += 64 * U) {
+            uint32_t v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t j = j0 + 64 * u + lane;
+                v[u] = j < w1 ? rng[j - w0] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t j = j0 + 64 * u + lane;
+                const uint64_t out = item_base + j;
+                if (j >= w1 || out >= a.item_cap) continue;
+                if (v[u] == RANGE_PANIC) {
+                    decode_record_generic(s, 0, 0, out, a.item, to_stream);
+                    if (a.item.status) a.item.status[out] = ST_PANIC;
+                    continue;
+                }
+                const int ib = (int)(v[u] & 0xffffu), ie = (int)(v[u] >> 16);
+                if constexpr (ISpec::N > 0) {
+                    FastRec<ISpec> fr;
+                    if (fast_prepare<ISpec>(s, ib, ie, fr)) {
+                        fast_finish<ISpec>(fr, out, a.item, to_stream);
+                        continue;
+                    }
+                }
+                decode_record_generic(s, ib, ie, out, a.item, to_stream);
+            }
+        }
+        wave_lds_sync(); // the next window's ranges overwrite this one's
+    }
+}
+
 // ---- decoupled look-back (one pass) ------------------------------------------------------
 
 constexpr uint64_t LB_AGG = 1ull << 62;       // word holds the group's own item count
@@ -278,7 +354,7 @@ __device__ __forceinline__ uint64_t lookback(uint64_t *state, uint64_t g, uint64
 template <class OSpec, class ISpec, bool ONEPASS, class Src>
 __device__ __forceinline__ void nested_group_body(const Src &s, long long rs, long long re, bool valid, uint64_t r,
                                                   uint64_t g, uint64_t item_base, int lane, long long to_stream,
-                                                  const NestedArgs &a) {
+                                                  const NestedArgs &a, uint32_t *rng = nullptr) {
     ListInfo li = {0, 0, 0, 0, false};
     if (valid) li = decode_outer<OSpec>(s, rs, re, r, to_stream, a);
     const uint32_t incl = wave_incl_scan(li.count, lane);
@@ -292,13 +368,19 @@ __device__ __forceinline__ void nested_group_body(const Src &s, long long rs, lo
         a.item_begin[r] = (uint32_t)(item_base + excl);
         if (r == a.n - 1) a.item_begin[a.n] = (uint32_t)(item_base + incl);
     }
+    if constexpr (__is_same(Src, LdsSrc)) {
+        if (rng) {
+            decode_group_items_ranges<ISpec>(s, li, excl, total, item_base, lane, to_stream, rng, a);
+            return;
+        }
+    }
     decode_group_items<ISpec>(s, li, excl, total, item_base, lane, to_stream, a);
 }
 
 // Kernel body for one group per wave.  ONEPASS: group = ticket order (a.group_base = state
 // words, ticket at state[ngroups], both zeroed by the launcher); else group = wave index and
 // a.group_base holds the exclusive item offsets from the index kernels.
-template <class OSpec, class ISpec, bool ONEPASS>
+template <class OSpec, class ISpec, bool ONEPASS, bool RANGES = false>
 __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -313,7 +395,8 @@ __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
     }
     const uint64_t base = g * 64;
     if (base >= a.n) return;
-    uint8_t *slab = smem + wave * a.slab;
+    // per wave: the slab, then (RANGES) the item range window
+    uint8_t *slab = smem + wave * (a.slab + (RANGES ? NESTED_RANGE_BYTES : 0u));
     __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
     const Group gr = nested_stage(a, rsrc, slab, base, lane);
@@ -324,96 +407,12 @@ __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
         LdsSrc s{(lds_u8 *)slab};
         nested_group_body<OSpec, ISpec, ONEPASS>(s, SLAB_GUARD + (long long)(gr.rec_lo - gr.aligned_lo),
                                                  SLAB_GUARD + (long long)(gr.rec_hi - gr.aligned_lo), valid, r, g,
-                                                 item_base, lane, (long long)gr.aligned_lo - SLAB_GUARD, a);
+                                                 item_base, lane, (long long)gr.aligned_lo - SLAB_GUARD, a,
+                                                 RANGES ? (uint32_t *)(slab + a.slab) : nullptr);
     } else {
         GlobalSrc s{rsrc, a.stream_len};
         nested_group_body<OSpec, ISpec, ONEPASS>(s, (long long)gr.rec_lo, (long long)gr.rec_hi, valid, r, g,
                                                  item_base, lane, 0, a);
-    }
-}
-
-// Persistent kernel body of the two-pass decode (group offsets from the index kernels): wave w
-// of the W in the grid decodes groups w, w + W, w + 2W, ...  Each wave stays resident for the
-// whole batch — no per-group wave launch — and with NBUF = 2 owns two slabs: the next group's
-// DMA and its ends / item offset are issued before this group is decoded, so its stream bytes
-// arrive while the current group's outer records and items are being decoded.
-template <class OSpec, class ISpec, int NBUF>
-__device__ __forceinline__ void nested_decode_persist_body(const NestedArgs &a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int wpb = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t ngroups = (a.n + 63) / 64;
-    const uint64_t W = (uint64_t)gridDim.x * wpb;
-    uint64_t g = (uint64_t)blockIdx.x * wpb + wave;
-    if (g >= ngroups) return;
-    uint8_t *slabs = smem + (size_t)wave * NBUF * a.slab;
-    __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
-    DecodeArgs d;
-    d.stream = a.stream;
-    d.stream_len = a.stream_len;
-    d.ends = a.ends;
-    d.n = a.n;
-    d.r0 = 0;
-    d.head = 0;
-    uint64_t lo, hi;
-    load_group_ends(d, g * 64, lane, lo, hi);
-    Group cur = make_group(d, g * 64, lane, lo, hi, a.slab);
-    uint64_t base_cur = a.group_base[g];
-    int b = 0;
-    if (cur.in_lds) issue_dma(rsrc, slabs, cur, lane);
-    uint64_t gn = g + W, nlo = 0, nhi = 0, base_nxt = 0;
-    if (gn < ngroups) {
-        load_group_ends(d, gn * 64, lane, nlo, nhi);
-        base_nxt = a.group_base[gn];
-    }
-    while (true) {
-        const bool has_next = gn < ngroups;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this group's DMA; the next group's ends
-        uint8_t *slab = slabs + b * a.slab;
-        if (cur.in_lds) fix_stream_tail(d, rsrc, slab, cur, lane);
-        const Group nxt = make_group(d, has_next ? gn * 64 : g * 64, lane, nlo, nhi, a.slab);
-        const uint64_t base_n = uniform64(base_nxt);
-        const uint64_t g2 = gn + W;
-        uint64_t lo2 = 0, hi2 = 0, base2 = 0;
-        if constexpr (NBUF == 2) {
-            if (has_next && nxt.in_lds) issue_dma(rsrc, slabs + (1 - b) * a.slab, nxt, lane);
-            if (g2 < ngroups) {
-                load_group_ends(d, g2 * 64, lane, lo2, hi2);
-                base2 = a.group_base[g2];
-            }
-        }
-        const uint64_t r = g * 64 + lane;
-        const bool valid = r < a.n;
-        const uint64_t item_base = uniform64(base_cur);
-        if (cur.in_lds) {
-            LdsSrc s{(lds_u8 *)slab};
-            nested_group_body<OSpec, ISpec, false>(s, SLAB_GUARD + (long long)(cur.rec_lo - cur.aligned_lo),
-                                                   SLAB_GUARD + (long long)(cur.rec_hi - cur.aligned_lo), valid, r, g,
-                                                   item_base, lane, (long long)cur.aligned_lo - SLAB_GUARD, a);
-        } else {
-            GlobalSrc s{rsrc, a.stream_len};
-            nested_group_body<OSpec, ISpec, false>(s, (long long)cur.rec_lo, (long long)cur.rec_hi, valid, r, g,
-                                                   item_base, lane, 0, a);
-        }
-        if (!has_next) break;
-        if constexpr (NBUF == 1) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // every LDS read of this group done
-            __builtin_amdgcn_wave_barrier();
-            if (nxt.in_lds) issue_dma(rsrc, slabs, nxt, lane);
-            if (g2 < ngroups) {
-                load_group_ends(d, g2 * 64, lane, lo2, hi2);
-                base2 = a.group_base[g2];
-            }
-        } else {
-            b = 1 - b;
-        }
-        g = gn;
-        gn = g2;
-        cur = nxt;
-        base_cur = base_n;
-        nlo = lo2;
-        nhi = hi2;
-        base_nxt = base2;
     }
 }
 

@@ -144,10 +144,8 @@ std::string generate_nested(const spec_nested_schema *s) {
       << "  spec::nested_decode_body<" << specs << ", true>(a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(64) void spec_decode_nested2_jit(spec::NestedArgs a) {\n"
       << "  spec::nested_decode_body<" << specs << ", false>(a);\n}\n"
-      << "extern \"C\" __global__ __launch_bounds__(64) void spec_decode_nested_p1_jit(spec::NestedArgs a) {\n"
-      << "  spec::nested_decode_persist_body<" << specs << ", 1>(a);\n}\n"
-      << "extern \"C\" __global__ __launch_bounds__(64) void spec_decode_nested_p2_jit(spec::NestedArgs a) {\n"
-      << "  spec::nested_decode_persist_body<" << specs << ", 2>(a);\n}\n";
+      << "extern \"C\" __global__ __launch_bounds__(64) void spec_decode_nested3_jit(spec::NestedArgs a) {\n"
+      << "  spec::nested_decode_body<" << specs << ", false, true>(a);\n}\n";
     return o.str();
 }
 
@@ -345,8 +343,7 @@ Entry load(const std::vector<char> &code, Prog p) {
     }
     const char *names[4][4] = {{"spec_decode_flat_jit", nullptr, nullptr, nullptr},
                                {"spec_encode_size_jit", "spec_encode_write_jit", nullptr, nullptr},
-                               {"spec_decode_nested_jit", "spec_decode_nested2_jit", "spec_decode_nested_p1_jit",
-                                "spec_decode_nested_p2_jit"},
+                               {"spec_decode_nested_jit", "spec_decode_nested2_jit", "spec_decode_nested3_jit", nullptr},
                                {"spec_encode_nested_size_jit", "spec_encode_nested_write_jit", nullptr, nullptr}};
     bool ok = hipModuleLoadData(&e.mod, code.data()) == hipSuccess;
     for (int i = 0; ok && i < 4; i++)
@@ -458,14 +455,8 @@ int jit_launch_nested(const spec_nested_schema *schema, const NestedArgs &a, int
     size_t size = sizeof(args);
     void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                      HIP_LAUNCH_PARAM_END};
-    const uint64_t groups = (a.n + 63) / 64;
-    unsigned grid = (unsigned)groups;
-    size_t lds = a.slab;
-    if (mode >= NESTED_PERSIST1) {
-        const int nbuf = mode == NESTED_PERSIST2 ? 2 : 1;
-        grid = nested_persist_grid(groups, a.slab, nbuf);
-        lds = (size_t)nbuf * a.slab;
-    }
+    const unsigned grid = (unsigned)((a.n + 63) / 64);
+    const size_t lds = a.slab + (mode == NESTED_RANGES ? NESTED_RANGE_BYTES : 0u);
     hipError_t rc = hipModuleLaunchKernel(e->fn[mode], grid, 1, 1, 64, 1, 1, (unsigned)lds, stream, nullptr, extra);
     return rc == hipSuccess ? 1 : -1;
 }

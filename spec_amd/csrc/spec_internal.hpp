@@ -9,6 +9,7 @@
 #include "decode_core.hpp"
 #include "encode_core.hpp"
 #include "encode_nested_core.hpp"
+#include "decode_nested_core.hpp"
 
 namespace spec {
 
@@ -42,18 +43,10 @@ int launch_nested_onepass(const spec_nested_schema *schema, NestedArgs a, double
 // else the decode pass after the index kernels); 1 launched, 0 use the precompiled kernel,
 // <0 HIP error.  a.slab must be set.
 // mode: NESTED_ONEPASS (look-back kernel), NESTED_GROUPS (a wave per group after the index
-// kernels), NESTED_PERSIST1 / NESTED_PERSIST2 (persistent waves after the index kernels, one /
-// two slabs per wave)
-enum { NESTED_ONEPASS = 0, NESTED_GROUPS = 1, NESTED_PERSIST1 = 2, NESTED_PERSIST2 = 3 };
+// kernels, items found by an owner search), NESTED_RANGES (same, items from ranges precomputed
+// into LDS by their records' lanes)
+enum { NESTED_ONEPASS = 0, NESTED_GROUPS = 1, NESTED_RANGES = 2 };
 int jit_launch_nested(const spec_nested_schema *schema, const NestedArgs &a, int mode, hipStream_t stream);
-int nested_decode_mode(); // the two-pass decode kernel in use (spec_set_nested_mode)
-// persistent grid: the waves the CUs hold with nbuf slabs each (one wave per block)
-inline unsigned nested_persist_grid(uint64_t groups, uint32_t slab, int nbuf) {
-    int per_cu = slab ? (int)((160 * 1024) / ((uint32_t)nbuf * slab)) : 8;
-    per_cu = per_cu < 1 ? 1 : (per_cu > 20 ? 20 : per_cu);
-    const uint64_t cap = (uint64_t)device_cus() * per_cu;
-    return (unsigned)(groups < cap ? groups : cap);
-}
 bool nested_lookback(); // SPEC_AMD_LOOKBACK=1: spec_decode_nested_onepass runs the look-back kernel
 long long jit_compile_only_nested(const spec_nested_schema *schema);
 // jit.cpp: schema-specialised decode kernel (hiprtc); returns 1 if launched, 0 if the caller

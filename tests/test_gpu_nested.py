@@ -25,19 +25,25 @@ def kernel(request):
     spec_amd.set_jit(True)
 
 
-def check_nested(dev, stream, ends, label="", modes=("twopass", "onepass", "onepass-small-cap")):
-    """Every decode mode against the oracle: index + decode, one pass with room for every
-    item, one pass that first runs out of item room (and decodes again with the total)."""
+def check_nested(dev, stream, ends, label="", modes=("twopass", "twopass-groups", "onepass", "onepass-small-cap")):
+    """Every decode mode against the oracle: index + decode (items from precomputed LDS ranges,
+    and items found by the owner search: spec_set_nested_mode 2 / 1), one pass with room for
+    every item, one pass that first runs out of item room (and decodes again with the total)."""
     stream = np.ascontiguousarray(stream, dtype=np.uint8)
     ends = np.ascontiguousarray(ends, dtype=np.uint64)
     want = O.decode_nested_batch(stream, ends)
     d_stream = to_dev(stream if stream.size else np.zeros(1, np.uint8), dev)[: stream.size]
     d_ends = to_dev(ends.view(np.int64), dev)
     got = None
+    L = spec_amd.lib()
     for mode in modes:
         cap = 1 if mode == "onepass-small-cap" else None
-        got = _check_nested_mode(dev, d_stream, d_ends, want, len(ends), f"{label} [{mode}]",
-                                 onepass=mode != "twopass", item_cap=cap)
+        L.spec_set_nested_mode(1 if mode == "twopass-groups" else 2)
+        try:
+            got = _check_nested_mode(dev, d_stream, d_ends, want, len(ends), f"{label} [{mode}]",
+                                     onepass=not mode.startswith("twopass"), item_cap=cap)
+        finally:
+            L.spec_set_nested_mode(2)
     return got, want
 
 

@@ -42,7 +42,7 @@ def main():
     L = spec_amd.lib()
     modes = {}
     ref_items = [c.clone() for c in d.items]
-    for mode, name in ((1, "groups"), (2, "persist1"), (3, "persist2")):
+    for mode, name in ((1, "groups"), (2, "ranges")):
         L.spec_set_nested_mode(mode)
         for c in d.items:
             c.zero_()
@@ -50,7 +50,7 @@ def main():
         torch.cuda.synchronize()
         same = all(torch.equal(a_, b_) for a_, b_ in zip(d.items, ref_items)) and int(d.status.sum()) == 0
         modes[name] = {"decode_ms": round(dec_ms, 4), "same": bool(same)}
-    L.spec_set_nested_mode(3)
+    L.spec_set_nested_mode(2)
     res["modes"] = modes
     one_ms, _ = bench.kernel_time_events(d.decode_onepass, 20)
     torch.cuda.synchronize()
