@@ -114,6 +114,38 @@ __device__ __forceinline__ Group nested_stage(const NestedArgs &a, __amdgpu_buff
     return gr;
 }
 
+// Lanes [l0, l1) of the group only (a group whose whole span exceeds the slab is staged and
+// decoded in two halves): the part's span, staged into the slab if it fits.
+__device__ __forceinline__ Group nested_stage_part(const NestedArgs &a, __amdgpu_buffer_rsrc_t rsrc, uint8_t *slab,
+                                                   uint64_t base, int lane, int l0, int l1) {
+    uint64_t lo, hi;
+    DecodeArgs d;
+    d.stream = a.stream;
+    d.stream_len = a.stream_len;
+    d.ends = a.ends;
+    d.n = a.n;
+    d.r0 = 0;
+    d.head = 0;
+    load_group_ends(d, base, lane, lo, hi);
+    Group gr;
+    gr.rec_lo = lo;
+    gr.rec_hi = hi < lo ? lo : hi;
+    const int nrec = (int)(a.n - base < 64 ? a.n - base : 64);
+    const int last = (l1 < nrec ? l1 : nrec) - 1;
+    const uint64_t span_lo = uniform64(__shfl(lo, l0));
+    const uint64_t span_hi = uniform64(__shfl(hi, last));
+    gr.aligned_lo = span_lo & ~15ull;
+    const uint64_t bytes = span_hi > gr.aligned_lo ? span_hi - gr.aligned_lo : 0;
+    gr.chunks = (uint32_t)((bytes + 1023) >> 10);
+    gr.in_lds = a.slab > 0 && l0 <= last && span_hi >= span_lo && SLAB_GUARD + (uint64_t)gr.chunks * 1024 + 16 <= a.slab;
+    if (gr.in_lds) {
+        issue_dma(rsrc, slab, gr, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        fix_stream_tail(d, rsrc, slab, gr, lane);
+    }
+    return gr;
+}
+
 // Item count of record [rs, re) (generic path).
 template <class Src>
 __device__ __forceinline__ uint32_t record_count(const Src &s, long long rs, long long re, const NestedArgs &a) {
@@ -352,9 +384,10 @@ __device__ __forceinline__ uint64_t lookback(uint64_t *state, uint64_t g, uint64
 // Decode a group: outer records (lane = record), then items (item-parallel).  item_base =
 // the group's first item; ONEPASS: item_base is found here by look-back (state = a.group_base).
 template <class OSpec, class ISpec, bool ONEPASS, class Src>
-__device__ __forceinline__ void nested_group_body(const Src &s, long long rs, long long re, bool valid, uint64_t r,
-                                                  uint64_t g, uint64_t item_base, int lane, long long to_stream,
-                                                  const NestedArgs &a, uint32_t *rng = nullptr) {
+__device__ __forceinline__ uint32_t nested_group_body(const Src &s, long long rs, long long re, bool valid,
+                                                      uint64_t r, uint64_t g, uint64_t item_base, int lane,
+                                                      long long to_stream, const NestedArgs &a,
+                                                      uint32_t *rng = nullptr) {
     ListInfo li = {0, 0, 0, 0, false};
     if (valid) li = decode_outer<OSpec>(s, rs, re, r, to_stream, a);
     const uint32_t incl = wave_incl_scan(li.count, lane);
@@ -371,10 +404,33 @@ __device__ __forceinline__ void nested_group_body(const Src &s, long long rs, lo
     if constexpr (__is_same(Src, LdsSrc)) {
         if (rng) {
             decode_group_items_ranges<ISpec>(s, li, excl, total, item_base, lane, to_stream, rng, a);
-            return;
+            return total;
         }
     }
     decode_group_items<ISpec>(s, li, excl, total, item_base, lane, to_stream, a);
+    return total;
+}
+
+// A part of a group (lanes [l0, l1)) from the slab when it fits, from HBM otherwise; the part's items
+// start at item_base.  Returns the part's item count.
+template <class OSpec, class ISpec, bool RANGES>
+__device__ __forceinline__ uint32_t nested_decode_part(const NestedArgs &a, __amdgpu_buffer_rsrc_t rsrc,
+                                                       uint8_t *slab, uint64_t g, uint64_t item_base, int lane,
+                                                       int l0, int l1) {
+    const uint64_t base = g * 64;
+    const Group gr = nested_stage_part(a, rsrc, slab, base, lane, l0, l1);
+    const uint64_t r = base + lane;
+    const bool valid = r < a.n && lane >= l0 && lane < l1;
+    if (gr.in_lds) {
+        LdsSrc s{(lds_u8 *)slab};
+        return nested_group_body<OSpec, ISpec, false>(s, SLAB_GUARD + (long long)(gr.rec_lo - gr.aligned_lo),
+                                                      SLAB_GUARD + (long long)(gr.rec_hi - gr.aligned_lo), valid, r,
+                                                      g, item_base, lane, (long long)gr.aligned_lo - SLAB_GUARD, a,
+                                                      RANGES ? (uint32_t *)(slab + a.slab) : nullptr);
+    }
+    GlobalSrc s{rsrc, a.stream_len};
+    return nested_group_body<OSpec, ISpec, false>(s, (long long)gr.rec_lo, (long long)gr.rec_hi, valid, r, g,
+                                                  item_base, lane, 0, a);
 }
 
 // Kernel body for one group per wave.  ONEPASS: group = ticket order (a.group_base = state
@@ -399,10 +455,31 @@ __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
     uint8_t *slab = smem + wave * (a.slab + (RANGES ? NESTED_RANGE_BYTES : 0u));
     __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
+    if constexpr (!ONEPASS) {
+        // the whole group in the slab; a group whose span exceeds it (a batch whose record sizes
+        // vary a lot) as two halves of 32 records, each staged on its own
+        const uint64_t item_base = uniform64(a.group_base[g]);
+        const Group whole = nested_stage_part(a, rsrc, slab, base, lane, 0, 64);
+        const uint64_t r = base + lane;
+        if (whole.in_lds) {
+            LdsSrc s{(lds_u8 *)slab};
+            nested_group_body<OSpec, ISpec, false>(s, SLAB_GUARD + (long long)(whole.rec_lo - whole.aligned_lo),
+                                                   SLAB_GUARD + (long long)(whole.rec_hi - whole.aligned_lo),
+                                                   r < a.n, r, g, item_base, lane,
+                                                   (long long)whole.aligned_lo - SLAB_GUARD, a,
+                                                   RANGES ? (uint32_t *)(slab + a.slab) : nullptr);
+            return;
+        }
+        const uint32_t first = nested_decode_part<OSpec, ISpec, RANGES>(a, rsrc, slab, g, item_base, lane, 0, 32);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the first half's LDS reads done
+        __builtin_amdgcn_wave_barrier();
+        nested_decode_part<OSpec, ISpec, RANGES>(a, rsrc, slab, g, item_base + first, lane, 32, 64);
+        return;
+    }
     const Group gr = nested_stage(a, rsrc, slab, base, lane);
     const uint64_t r = base + lane;
     const bool valid = r < a.n;
-    const uint64_t item_base = ONEPASS ? 0 : a.group_base[g];
+    const uint64_t item_base = 0;
     if (gr.in_lds) {
         LdsSrc s{(lds_u8 *)slab};
         nested_group_body<OSpec, ISpec, ONEPASS>(s, SLAB_GUARD + (long long)(gr.rec_lo - gr.aligned_lo),
@@ -426,18 +503,33 @@ __device__ __forceinline__ void nested_count_body(const NestedArgs &a) {
     uint8_t *slab = smem + wave * a.slab;
     __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
-    const Group gr = nested_stage(a, rsrc, slab, base, lane);
-    const bool valid = base + lane < a.n;
     uint32_t cnt = 0;
-    if (valid) {
-        if (gr.in_lds) {
-            LdsSrc s{(lds_u8 *)slab};
-            cnt = record_count(s, SLAB_GUARD + (long long)(gr.rec_lo - gr.aligned_lo),
-                               SLAB_GUARD + (long long)(gr.rec_hi - gr.aligned_lo), a);
-        } else {
-            GlobalSrc s{rsrc, a.stream_len};
-            cnt = record_count(s, (long long)gr.rec_lo, (long long)gr.rec_hi, a);
+    // the whole group, or (span larger than the slab) two halves of 32 records
+    for (int part = 0; part < 2; part++) {
+        const int l0 = part ? 32 : 0;
+        const int l1 = part ? 64 : 32;
+        const Group gr = nested_stage_part(a, rsrc, slab, base, lane, part ? l0 : 0, part ? l1 : 64);
+        const bool whole = part == 0 && gr.in_lds;
+        Group h = gr;
+        if (!whole && part == 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            h = nested_stage_part(a, rsrc, slab, base, lane, 0, 32);
         }
+        const int hl0 = whole ? 0 : l0, hl1 = whole ? 64 : l1;
+        const bool valid = base + lane < a.n && lane >= hl0 && lane < hl1;
+        if (valid) {
+            if (h.in_lds) {
+                LdsSrc s{(lds_u8 *)slab};
+                cnt = record_count(s, SLAB_GUARD + (long long)(h.rec_lo - h.aligned_lo),
+                                   SLAB_GUARD + (long long)(h.rec_hi - h.aligned_lo), a);
+            } else {
+                GlobalSrc s{rsrc, a.stream_len};
+                cnt = record_count(s, (long long)h.rec_lo, (long long)h.rec_hi, a);
+            }
+        }
+        if (whole) break;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // this half's LDS reads done
+        __builtin_amdgcn_wave_barrier();
     }
     const uint32_t sum = wave_sum(cnt);
     if (lane == 0) a.group_base[g] = sum;
