@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void nested_decode_ranges_kernel(NestedArgs a)
     nested_decode_body<RuntimeSpec, RuntimeSpec, false, true>(a);
 }
 
-int g_nested_mode = NESTED_RANGES;
+int g_nested_mode = NESTED_GROUPS;
 
 } // namespace
 
@@ -113,7 +113,7 @@ int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream) {
 }
 
 // The decode pass after the index kernels: a wave per 64-record group; its items found by an
-// owner search (NESTED_GROUPS) or from ranges precomputed into LDS (NESTED_RANGES, default).
+// owner search (NESTED_GROUPS, default) or from ranges precomputed into LDS (NESTED_RANGES).
 int launch_nested_decode(const spec_nested_schema *schema, NestedArgs a, double avg_record, hipStream_t stream) {
     if (a.n == 0) return 0;
     a.slab = decode_slab_bytes(avg_record);

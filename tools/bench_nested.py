@@ -50,7 +50,7 @@ def main():
         torch.cuda.synchronize()
         same = all(torch.equal(a_, b_) for a_, b_ in zip(d.items, ref_items)) and int(d.status.sum()) == 0
         modes[name] = {"decode_ms": round(dec_ms, 4), "same": bool(same)}
-    L.spec_set_nested_mode(2)
+    L.spec_set_nested_mode(1)
     res["modes"] = modes
     one_ms, _ = bench.kernel_time_events(d.decode_onepass, 20)
     torch.cuda.synchronize()
