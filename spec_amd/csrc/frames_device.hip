@@ -4,17 +4,18 @@
 //
 // The head chain is serial (frame k+1 starts where frame k ends), so the walk is split:
 //   1. segments of 64 KiB, staged in LDS; for EVERY entry offset e < W (2048) of a segment, the
-//      chain is walked to the segment end: exit offset into the next segment, frames completed
-//      (a false entry reads a random big size and leaves at once; the true one walks ~S/frame
-//      steps in LDS);
+//      chain is walked to the segment end: exit offset into the next segment, frames completed.
+//      Inside the segment the walk is itself split into 16 sub-segments of 4 KiB: every entry
+//      o < WS (1024) of sub-segments 1..15 is walked to the first position past its sub-segment
+//      that lies in some later sub-segment's window (or past the segment end), the results kept
+//      in LDS; a segment entry then walks sub-segment 0 and composes the tables (at most 15
+//      dependent LDS reads), so no thread walks more than ~4 KiB of frames (a false entry reads a
+//      random big size and leaves at once);
 //   2. groups of 64 segments compose their tables (every entry, 64 dependent table reads);
 //   3. one thread chains the groups from offset 0 (a few hundred dependent reads);
 //   4. each group resolves its segments' entries and frame bases;
-//   5. each segment walks its true chain again in LDS and writes ends[];
-// A frame that straddles a segment boundary by W bytes or more, or a segment with more than
-// 4096 frames, sets the overflow flag: a single-thread serial walk over HBM then produces the
-// same results (slow but exact).  One call, no host sync; count / consumed / status land in
-// device memory.
+//   5. each segment on the chain rebuilds its sub-segment tables, composes its true entry once,
+//      and 16 threads walk the 16 sub-segment pieces of the true chain writing ends[];
 #include <hip/hip_runtime.h>
 
 #include "spec_internal.hpp"
@@ -24,6 +25,12 @@ namespace spec {
 namespace {
 
 constexpr uint32_t FI_SEG = 65536, FI_W = 2048, FI_G = 64, FI_STEPCAP = 4096;
+constexpr uint32_t FI_BLOCK = 1024; // threads of the segment / group kernels (a constant: blockDim
+                                    // is a load from the dispatch packet)
+constexpr uint32_t FI_SUB = 4096, FI_NSUB = FI_SEG / FI_SUB, FI_WS = 1024;
+constexpr uint32_t FI_LDS_T = FI_SEG + 16, FI_LDS = FI_LDS_T + (FI_NSUB - 1) * FI_WS * 4;
+// a sub-segment walk result: [31] TERM, [30:17] frames, [16:0] segment-relative position
+constexpr uint32_t FI_T_TERM = 1u << 31, FI_T_OVF = 0xffffffffu, FI_T_POS = 0x1ffffu;
 constexpr uint32_t FI_OVF = 0xffffffffu, FI_TERM = 0x80000000u, FI_NONE = 0xffffffffu;
 constexpr uint64_t FI_G_TERM = 1ull << 63, FI_G_OVF = 1ull << 62;
 
@@ -43,34 +50,35 @@ struct FiArgs {
     uint64_t *misc;            // [0] overflow, [1] total frames, [2] consumed
 };
 
+// the big-endian u32 at byte o of the staged segment: two dword reads and a funnel shift
 __device__ __forceinline__ uint32_t be32_lds(const uint8_t *l, uint32_t o) {
-    return ((uint32_t)l[o] << 24) | ((uint32_t)l[o + 1] << 16) | ((uint32_t)l[o + 2] << 8) | l[o + 3];
+    const uint32_t *w = (const uint32_t *)l;
+    const uint64_t d = ((uint64_t)w[(o >> 2) + 1] << 32) | w[o >> 2];
+    return __builtin_bswap32((uint32_t)(d >> (8 * (o & 3))));
 }
 
 // bytes [s0, s0 + SEG + 16) of buf into lds (zeros past len); buf is 4-byte aligned
 __device__ __forceinline__ void stage_segment(const FiArgs &a, uint64_t s0, uint8_t *lds) {
-    constexpr uint32_t NQ = (FI_SEG + 16) / 16;
-    // a whole segment from a 16-byte aligned buffer: 16-byte loads, four in flight per thread
+    // a whole segment from a 16-byte aligned buffer: 16-byte loads, all of a thread's in flight
     // (the ABI only promises 4-byte alignment: other buffers take the dword loop)
     if (s0 + FI_SEG + 16 <= a.len && ((uintptr_t)a.buf & 15) == 0) {
-        for (uint32_t i0 = 0; i0 < NQ; i0 += 4 * blockDim.x) {
-            uint4 v[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
-                if (i < NQ) v[j] = *(const uint4 *)(a.buf + s0 + 16ull * i);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t i = i0 + threadIdx.x + j * blockDim.x;
-                if (i < NQ) *(uint4 *)(lds + 16 * i) = v[j];
-            }
+        const uint4 *src = (const uint4 *)(a.buf + s0);
+        uint4 *dst = (uint4 *)lds;
+        for (uint32_t i0 = 0; i0 < FI_SEG / 16; i0 += 4 * FI_BLOCK) {
+            const uint32_t i = i0 + threadIdx.x; // FI_SEG / 16 is a multiple of 4 * FI_BLOCK
+            const uint4 v0 = src[i], v1 = src[i + FI_BLOCK], v2 = src[i + 2 * FI_BLOCK],
+                        v3 = src[i + 3 * FI_BLOCK];
+            dst[i] = v0;
+            dst[i + FI_BLOCK] = v1;
+            dst[i + 2 * FI_BLOCK] = v2;
+            dst[i + 3 * FI_BLOCK] = v3;
         }
+        if (threadIdx.x == 0) dst[FI_SEG / 16] = src[FI_SEG / 16];
         __syncthreads();
         return;
     }
     uint32_t *l32 = (uint32_t *)lds;
-    for (uint32_t i = threadIdx.x; i < (FI_SEG + 16) / 4; i += blockDim.x) {
+    for (uint32_t i = threadIdx.x; i < (FI_SEG + 16) / 4; i += FI_BLOCK) {
         const uint64_t p = s0 + 4ull * i;
         uint32_t w = 0;
         if (p + 4 <= a.len) {
@@ -84,43 +92,100 @@ __device__ __forceinline__ void stage_segment(const FiArgs &a, uint64_t s0, uint
     __syncthreads();
 }
 
-__global__ __launch_bounds__(1024) void fi_seg_kernel(FiArgs a) {
+// Walk jobs i = threadIdx.x + m * FI_BLOCK < njobs: from start(i) -> (p, stop), the chain
+// until it stands on a position at or past `stop` that lies in the first WS bytes of a
+// sub-segment, or past the segment end (segend = s1 - s0, lenrel = len - s0); out[i] = code.  A
+// jump W or more past the segment end, or more than STEPCAP frames, is overflow (the serial
+// fallback).  One frame step per iteration, selects instead of branches, one predicated store:
+// a lane that finishes a walk starts its next at once, so a wave runs for its busiest lane's
+// steps, not for the sum over jobs of the longest walk.
+template <class Start>
+__device__ __forceinline__ void fi_walk_all(const uint8_t *lds, uint32_t njobs, uint32_t segend, uint64_t lenrel,
+                                            Start start, uint32_t *out) {
+    uint32_t i = threadIdx.x, p, stop, steps = 0;
+    if (i >= njobs) return;
+    start(i, p, stop);
+    const uint64_t far = (uint64_t)segend + FI_W;
+    while (true) {
+        const bool exit = p >= segend || (p >= stop && (p & (FI_SUB - 1)) < FI_WS);
+        const uint64_t q = (uint64_t)p + 4 + be32_lds(lds, p & 0xffffu); // in the staged bytes
+        const bool term = q > lenrel;
+        const bool fin = exit || term || q >= far || steps >= FI_STEPCAP;
+        const uint32_t code = exit ? (steps << 17) | p : term ? FI_T_TERM | (steps << 17) | p : FI_T_OVF;
+        if (fin) out[i] = code;
+        const uint32_t inext = fin ? i + FI_BLOCK : i;
+        if (inext >= njobs) break;
+        uint32_t p2, stop2;
+        start(inext, p2, stop2);
+        p = fin ? p2 : (uint32_t)q;
+        stop = fin ? stop2 : stop;
+        steps = fin ? 0 : steps + 1;
+        i = inext;
+    }
+}
+
+// stage the segment and walk every window entry of sub-segments 1..15 (tables after the data)
+__device__ __forceinline__ void fi_tables(const FiArgs &a, uint64_t s0, uint32_t segend, uint8_t *lds) {
+    stage_segment(a, s0, lds);
+    uint32_t *T = (uint32_t *)(lds + FI_LDS_T);
+    fi_walk_all(
+        lds, (FI_NSUB - 1) * FI_WS, segend, a.len - s0,
+        [](uint32_t i, uint32_t &p, uint32_t &stop) {
+            stop = (2 + i / FI_WS) * FI_SUB;
+            p = stop - FI_SUB + i % FI_WS;
+        },
+        T);
+    __syncthreads();
+}
+
+// a segment entry's result from its sub-segment 0 walk c: exit offset into the next segment
+// (< W), FI_TERM | position, or FI_OVF; frames in *steps.  With `ent`, the sub-segment pieces'
+// entries and frame counts before them (ent[j] = ~0u for sub-segments the chain jumps over).
+__device__ __forceinline__ uint32_t fi_compose(const uint32_t *T, uint32_t c, uint32_t segend, uint32_t *steps_out,
+                                               uint32_t *ent = nullptr, uint32_t *before = nullptr) {
+    uint32_t steps = 0;
+    while (true) {
+        if (c == FI_T_OVF) return FI_OVF;
+        steps += (c >> 17) & 0x3fffu;
+        if (steps > FI_STEPCAP) return FI_OVF;
+        const uint32_t p = c & FI_T_POS;
+        *steps_out = steps;
+        if (c & FI_T_TERM) return FI_TERM | p;
+        if (p >= segend) return p - segend < FI_W ? p - segend : FI_OVF;
+        if (ent) {
+            ent[p / FI_SUB] = p;
+            before[p / FI_SUB] = steps;
+        }
+        c = T[(p / FI_SUB - 1) * FI_WS + (p & (FI_SUB - 1))];
+    }
+}
+
+__global__ __launch_bounds__(FI_BLOCK) void fi_seg_kernel(FiArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t k = blockIdx.x;
     const uint64_t s0 = (uint64_t)k * FI_SEG, s1 = s0 + FI_SEG < a.len ? s0 + FI_SEG : a.len;
-    stage_segment(a, s0, lds);
-    for (uint32_t e = threadIdx.x; e < FI_W; e += blockDim.x) {
-        uint64_t p = s0 + e;
-        uint32_t steps = 0, code;
-        while (true) {
-            if (p >= s1) {
-                const uint64_t x = p - s1;
-                code = x < FI_W ? (uint32_t)x : FI_OVF;
-                break;
-            }
-            if (p + 4 > a.len) {
-                code = FI_TERM | (uint32_t)(p - s0);
-                break;
-            }
-            const uint64_t q = p + 4 + be32_lds(lds, (uint32_t)(p - s0));
-            if (q > a.len) {
-                code = FI_TERM | (uint32_t)(p - s0);
-                break;
-            }
-            p = q;
-            if (++steps > FI_STEPCAP) {
-                code = FI_OVF;
-                break;
-            }
-        }
+    const uint32_t segend = (uint32_t)(s1 - s0);
+    fi_tables(a, s0, segend, lds);
+    const uint32_t *T = (const uint32_t *)(lds + FI_LDS_T);
+    uint32_t *C = (uint32_t *)(lds + FI_LDS);
+    fi_walk_all(
+        lds, FI_W, segend, a.len - s0,
+        [](uint32_t e, uint32_t &p, uint32_t &stop) {
+            p = e;
+            stop = FI_SUB;
+        },
+        C);
+    for (uint32_t e = threadIdx.x; e < FI_W; e += FI_BLOCK) { // a lane composes its own walks
+        uint32_t steps = 0;
+        const uint32_t code = fi_compose(T, C[e], segend, &steps);
         a.exitT[(uint64_t)k * FI_W + e] = code;
         a.cntT[(uint64_t)k * FI_W + e] = steps;
     }
 }
 
-__global__ __launch_bounds__(1024) void fi_group_kernel(FiArgs a) {
+__global__ __launch_bounds__(FI_BLOCK) void fi_group_kernel(FiArgs a) {
     const uint32_t g = blockIdx.x, k0 = g * FI_G, k1 = k0 + FI_G < a.nseg ? k0 + FI_G : a.nseg;
-    for (uint32_t e = threadIdx.x; e < FI_W; e += blockDim.x) {
+    for (uint32_t e = threadIdx.x; e < FI_W; e += FI_BLOCK) {
         uint32_t x = e, cnt = 0;
         uint64_t code = 0;
         bool open = true;
@@ -187,23 +252,43 @@ __global__ void fi_segentry_kernel(FiArgs a) {
     }
 }
 
-// per segment: its true chain walked again in LDS, ends[] written
-__global__ __launch_bounds__(256) void fi_emit_kernel(FiArgs a) {
+// per segment on the chain: tables again, the true entry composed once, then one thread per
+// sub-segment piece of the true chain writes its ends[]
+__global__ __launch_bounds__(FI_BLOCK) void fi_emit_kernel(FiArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    __shared__ uint32_t ent[FI_NSUB], before[FI_NSUB];
     const uint32_t k = blockIdx.x;
     if (a.misc[0]) return;
     const uint32_t e = a.seg_entry[k];
     if (e == FI_NONE) return;
     const uint64_t s0 = (uint64_t)k * FI_SEG, s1 = s0 + FI_SEG < a.len ? s0 + FI_SEG : a.len;
-    stage_segment(a, s0, lds);
-    if (threadIdx.x != 0) return;
-    uint64_t p = s0 + e, i = a.seg_base[k];
-    while (p < s1 && p + 4 <= a.len) {
-        const uint64_t q = p + 4 + be32_lds(lds, (uint32_t)(p - s0));
-        if (q > a.len) break;
-        if (i < a.cap) a.ends[i] = q;
+    const uint32_t segend = (uint32_t)(s1 - s0);
+    const uint64_t lenrel = a.len - s0;
+    if (threadIdx.x < FI_NSUB) ent[threadIdx.x] = threadIdx.x ? ~0u : e, before[threadIdx.x] = 0;
+    fi_tables(a, s0, segend, lds);
+    if (threadIdx.x == 0) {
+        uint32_t steps;
+        uint32_t *C = (uint32_t *)(lds + FI_LDS);
+        fi_walk_all(
+            lds, 1, segend, lenrel,
+            [&](uint32_t, uint32_t &p, uint32_t &stop) {
+                p = e;
+                stop = FI_SUB;
+            },
+            C);
+        fi_compose((const uint32_t *)(lds + FI_LDS_T), C[0], segend, &steps, ent, before);
+    }
+    __syncthreads();
+    if (threadIdx.x >= FI_NSUB || ent[threadIdx.x] == ~0u) return;
+    const uint32_t stop = (threadIdx.x + 1) * FI_SUB;
+    uint32_t p = ent[threadIdx.x];
+    uint64_t i = a.seg_base[k] + before[threadIdx.x];
+    while (!(p >= segend || (p >= stop && (p & (FI_SUB - 1)) < FI_WS)) && (uint64_t)p + 4 <= lenrel) {
+        const uint64_t q = (uint64_t)p + 4 + be32_lds(lds, p);
+        if (q > lenrel) break;
+        if (i < a.cap) a.ends[i] = s0 + q;
         i++;
-        p = q;
+        p = (uint32_t)q;
     }
 }
 
@@ -285,12 +370,12 @@ int launch_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends,
     a.seg_entry = (uint32_t *)(w + L.off[6]);
     a.seg_base = (uint64_t *)(w + L.off[7]);
     a.misc = (uint64_t *)(w + L.off[8]);
-    const size_t lds = FI_SEG + 16;
-    hipLaunchKernelGGL(fi_seg_kernel, dim3(L.nseg), dim3(1024), lds, stream, a);
-    hipLaunchKernelGGL(fi_group_kernel, dim3(L.ngroups), dim3(1024), 0, stream, a);
+    const size_t lds = FI_LDS + FI_W * 4; // + the segment walks' sub-segment 0 codes
+    hipLaunchKernelGGL(fi_seg_kernel, dim3(L.nseg), dim3(FI_BLOCK), lds, stream, a);
+    hipLaunchKernelGGL(fi_group_kernel, dim3(L.ngroups), dim3(FI_BLOCK), 0, stream, a);
     hipLaunchKernelGGL(fi_chain_kernel, dim3(1), dim3(64), 0, stream, a);
     hipLaunchKernelGGL(fi_segentry_kernel, dim3((L.ngroups + 63) / 64), dim3(64), 0, stream, a);
-    hipLaunchKernelGGL(fi_emit_kernel, dim3(L.nseg), dim3(256), lds, stream, a);
+    hipLaunchKernelGGL(fi_emit_kernel, dim3(L.nseg), dim3(FI_BLOCK), lds, stream, a);
     hipLaunchKernelGGL(fi_finish_kernel, dim3(1), dim3(64), 0, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -79,6 +79,25 @@ def test_segment_boundaries(dev):
     check(dev, frames_of(sizes, rng), label="exact segments", sizes=sizes)
 
 
+def test_sub_segment_windows(dev):
+    """The 4 KiB sub-segment tables inside a segment: frames 1-2 KiB long (heads past a
+    sub-segment's 1024-byte window, so the walk runs on into the next sub-segment), 4 KiB frames
+    landing exactly on sub-segment starts, and heads at window offsets 1023 / 1024."""
+    rng = np.random.default_rng(11)
+    sub, ws = 4096, 1024
+    cases = {
+        "1-2 KiB": list(rng.integers(1000, 2000, 600)),
+        "3-4 KiB": list(rng.integers(3000, 4000, 300)),
+        "exact sub": [sub - 4] * 40,
+        "window 1023": [sub + ws - 1 - 4] + list(rng.integers(0, 300, 2000)),
+        "window 1024": [sub + ws - 4] + list(rng.integers(0, 300, 2000)),
+        "mixed": list(rng.choice([7, 60, 900, 1100, 1500, 2040, 4092], 3000)),
+    }
+    for label, sizes in cases.items():
+        check(dev, frames_of(sizes, rng), label=label, sizes=sizes)
+        check(dev, frames_of(sizes, rng), label=f"{label} at +20", sizes=sizes, offset=20)
+
+
 def test_long_frames_fall_back(dev):
     """Frames longer than the 2048-byte entry window (and > 64 KiB) take the serial walk."""
     rng = np.random.default_rng(4)

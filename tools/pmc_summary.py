@@ -12,7 +12,7 @@ for f in glob.glob(f"{out}/**/*counter_collection.csv", recursive=True):
         name = row["Kernel_Name"]
         if "spec" not in name:
             continue
-        short = name.split("(")[0][-60:]
+        short = name.replace("(anonymous namespace)", "anon").split("(")[0][-60:]
         acc[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
 res = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
 json.dump(res, open(f"{out}/summary.json", "w"), indent=1)
