@@ -3,19 +3,25 @@
 // the host walk spec_frames_index (capi.hip).
 //
 // The head chain is serial (frame k+1 starts where frame k ends), so the walk is split:
-//   1. segments of 64 KiB, staged in LDS; for EVERY entry offset e < W (2048) of a segment, the
+//   1. segments of 32 KiB, staged in LDS; for EVERY entry offset e < W (2048) of a segment, the
 //      chain is walked to the segment end: exit offset into the next segment, frames completed.
-//      Inside the segment the walk is itself split into 16 sub-segments of 4 KiB: every entry
-//      o < WS (1024) of sub-segments 1..15 is walked to the first position past its sub-segment
+//      Inside the segment the walk is itself split into 8 sub-segments of 4 KiB: every entry
+//      o < WS (1024) of sub-segments 1..7 is walked to the first position past its sub-segment
 //      that lies in some later sub-segment's window (or past the segment end), the results kept
-//      in LDS; a segment entry then walks sub-segment 0 and composes the tables (at most 15
+//      in LDS; a segment entry then walks sub-segment 0 and composes the tables (at most 7
 //      dependent LDS reads), so no thread walks more than ~4 KiB of frames (a false entry reads a
-//      random big size and leaves at once);
+//      random big size and leaves at once).  Entries that leave the segment (live: the true one
+//      and the others on the same chain, ~8 per segment) keep their pieces for step 5;
 //   2. groups of 64 segments compose their tables (every entry, 64 dependent table reads);
 //   3. one thread chains the groups from offset 0 (a few hundred dependent reads);
 //   4. each group resolves its segments' entries and frame bases;
-//   5. each segment on the chain rebuilds its sub-segment tables, composes its true entry once,
-//      and 16 threads walk the 16 sub-segment pieces of the true chain writing ends[];
+//   5. each segment on the chain: one lane per sub-segment piece of its true chain (from the
+//      live record of its entry) reads the heads from HBM and writes ends[]; a segment without a
+//      record (the chain ends in it) rebuilds its tables in LDS (a short work list).
+// A frame that straddles a segment boundary by W bytes or more, or a segment with more than
+// 4096 frames, sets the overflow flag: a single-thread serial walk over HBM then produces the
+// same results (slow but exact).  One call, no host sync; count / consumed / status land in
+// device memory.
 #include <hip/hip_runtime.h>
 
 #include "spec_internal.hpp"
@@ -24,12 +30,17 @@ namespace spec {
 
 namespace {
 
-constexpr uint32_t FI_SEG = 65536, FI_W = 2048, FI_G = 64, FI_STEPCAP = 4096;
+constexpr uint32_t FI_SEG = 32768, FI_W = 2048, FI_G = 64, FI_STEPCAP = 4096;
 constexpr uint32_t FI_BLOCK = 1024; // threads of the segment / group kernels (a constant: blockDim
                                     // is a load from the dispatch packet)
 constexpr uint32_t FI_SUB = 4096, FI_NSUB = FI_SEG / FI_SUB, FI_WS = 1024;
 constexpr uint32_t FI_LDS_T = FI_SEG + 16, FI_LDS = FI_LDS_T + (FI_NSUB - 1) * FI_WS * 4;
+// a segment table entry: exit x (< W) | frames << 16; FI_TERM | position | frames << 16; FI_OVF
+constexpr uint32_t FI_CNT_SHIFT = 16, FI_CNT_MASK = 0x1fffu, FI_POS_MASK = 0x7fffu;
 // a sub-segment walk result: [31] TERM, [30:17] frames, [16:0] segment-relative position
+// a segment's live entries (walks that leave it): entry, then per sub-segment piece of its chain
+// (position << 16 | frames before it, ~0u where the chain jumps over the sub-segment)
+constexpr uint32_t FI_LIVE = 32, FI_LREC = 1 + FI_NSUB;
 constexpr uint32_t FI_T_TERM = 1u << 31, FI_T_OVF = 0xffffffffu, FI_T_POS = 0x1ffffu;
 constexpr uint32_t FI_OVF = 0xffffffffu, FI_TERM = 0x80000000u, FI_NONE = 0xffffffffu;
 constexpr uint64_t FI_G_TERM = 1ull << 63, FI_G_OVF = 1ull << 62;
@@ -40,7 +51,7 @@ struct FiArgs {
     uint64_t *ends, *count, *consumed;
     int32_t *status;
     uint32_t nseg, ngroups;
-    uint32_t *exitT, *cntT;    // [nseg * W]
+    uint32_t *exitT;           // [nseg * W] packed: exit / TERM position, frames
     uint64_t *grpT;            // [ngroups * W]
     uint32_t *grpCnt;          // [ngroups * W]
     uint32_t *grp_entry;       // [ngroups]
@@ -48,6 +59,9 @@ struct FiArgs {
     uint32_t *seg_entry;       // [nseg]
     uint64_t *seg_base;        // [nseg]
     uint64_t *misc;            // [0] overflow, [1] total frames, [2] consumed
+    uint32_t *live_n;          // [nseg] live entries recorded (may exceed FI_LIVE)
+    uint32_t *live;            // [nseg * FI_LIVE * FI_LREC]
+    uint32_t *work;            // [1 + nseg] count, then segments the emit must rebuild
 };
 
 // the big-endian u32 at byte o of the staged segment: two dword reads and a funnel shift
@@ -64,15 +78,13 @@ __device__ __forceinline__ void stage_segment(const FiArgs &a, uint64_t s0, uint
     if (s0 + FI_SEG + 16 <= a.len && ((uintptr_t)a.buf & 15) == 0) {
         const uint4 *src = (const uint4 *)(a.buf + s0);
         uint4 *dst = (uint4 *)lds;
-        for (uint32_t i0 = 0; i0 < FI_SEG / 16; i0 += 4 * FI_BLOCK) {
-            const uint32_t i = i0 + threadIdx.x; // FI_SEG / 16 is a multiple of 4 * FI_BLOCK
-            const uint4 v0 = src[i], v1 = src[i + FI_BLOCK], v2 = src[i + 2 * FI_BLOCK],
-                        v3 = src[i + 3 * FI_BLOCK];
-            dst[i] = v0;
-            dst[i + FI_BLOCK] = v1;
-            dst[i + 2 * FI_BLOCK] = v2;
-            dst[i + 3 * FI_BLOCK] = v3;
-        }
+        constexpr uint32_t QPT = FI_SEG / 16 / FI_BLOCK; // quads per thread, all loads in flight
+        static_assert(QPT * 16 * FI_BLOCK == FI_SEG, "segment is a whole number of quads per thread");
+        uint4 v[QPT];
+#pragma unroll
+        for (uint32_t j = 0; j < QPT; j++) v[j] = src[threadIdx.x + j * FI_BLOCK];
+#pragma unroll
+        for (uint32_t j = 0; j < QPT; j++) dst[threadIdx.x + j * FI_BLOCK] = v[j];
         if (threadIdx.x == 0) dst[FI_SEG / 16] = src[FI_SEG / 16];
         __syncthreads();
         return;
@@ -108,7 +120,7 @@ __device__ __forceinline__ void fi_walk_all(const uint8_t *lds, uint32_t njobs, 
     const uint64_t far = (uint64_t)segend + FI_W;
     while (true) {
         const bool exit = p >= segend || (p >= stop && (p & (FI_SUB - 1)) < FI_WS);
-        const uint64_t q = (uint64_t)p + 4 + be32_lds(lds, p & 0xffffu); // in the staged bytes
+        const uint64_t q = (uint64_t)p + 4 + be32_lds(lds, p & (FI_SEG - 1)); // in the staged bytes
         const bool term = q > lenrel;
         const bool fin = exit || term || q >= far || steps >= FI_STEPCAP;
         const uint32_t code = exit ? (steps << 17) | p : term ? FI_T_TERM | (steps << 17) | p : FI_T_OVF;
@@ -139,10 +151,11 @@ __device__ __forceinline__ void fi_tables(const FiArgs &a, uint64_t s0, uint32_t
 }
 
 // a segment entry's result from its sub-segment 0 walk c: exit offset into the next segment
-// (< W), FI_TERM | position, or FI_OVF; frames in *steps.  With `ent`, the sub-segment pieces'
-// entries and frame counts before them (ent[j] = ~0u for sub-segments the chain jumps over).
+// (< W), FI_TERM | position, or FI_OVF; frames in *steps.  piece(j, p, before) for every later
+// sub-segment piece of the chain (entry position, frames before it).
+template <class Piece>
 __device__ __forceinline__ uint32_t fi_compose(const uint32_t *T, uint32_t c, uint32_t segend, uint32_t *steps_out,
-                                               uint32_t *ent = nullptr, uint32_t *before = nullptr) {
+                                               Piece piece) {
     uint32_t steps = 0;
     while (true) {
         if (c == FI_T_OVF) return FI_OVF;
@@ -152,19 +165,18 @@ __device__ __forceinline__ uint32_t fi_compose(const uint32_t *T, uint32_t c, ui
         *steps_out = steps;
         if (c & FI_T_TERM) return FI_TERM | p;
         if (p >= segend) return p - segend < FI_W ? p - segend : FI_OVF;
-        if (ent) {
-            ent[p / FI_SUB] = p;
-            before[p / FI_SUB] = steps;
-        }
+        piece(p / FI_SUB, p, steps);
         c = T[(p / FI_SUB - 1) * FI_WS + (p & (FI_SUB - 1))];
     }
 }
 
 __global__ __launch_bounds__(FI_BLOCK) void fi_seg_kernel(FiArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    __shared__ uint32_t nlive;
     const uint32_t k = blockIdx.x;
     const uint64_t s0 = (uint64_t)k * FI_SEG, s1 = s0 + FI_SEG < a.len ? s0 + FI_SEG : a.len;
     const uint32_t segend = (uint32_t)(s1 - s0);
+    if (threadIdx.x == 0) nlive = 0;
     fi_tables(a, s0, segend, lds);
     const uint32_t *T = (const uint32_t *)(lds + FI_LDS_T);
     uint32_t *C = (uint32_t *)(lds + FI_LDS);
@@ -175,12 +187,29 @@ __global__ __launch_bounds__(FI_BLOCK) void fi_seg_kernel(FiArgs a) {
             stop = FI_SUB;
         },
         C);
+    uint32_t *live = a.live + (uint64_t)k * FI_LIVE * FI_LREC;
     for (uint32_t e = threadIdx.x; e < FI_W; e += FI_BLOCK) { // a lane composes its own walks
+        // an entry that survives sub-segment 0 may be live: a record slot for its pieces
+        // (marked dead again if the chain ends in the segment after all)
+        const uint32_t c0 = C[e];
+        uint32_t *rec = nullptr;
+        if (c0 != FI_T_OVF && !(c0 & FI_T_TERM)) {
+            const uint32_t slot = atomicAdd(&nlive, 1u);
+            if (slot < FI_LIVE) {
+                rec = live + slot * FI_LREC;
+                rec[1] = e << 16;
+                for (uint32_t j = 1; j < FI_NSUB; j++) rec[1 + j] = ~0u;
+            }
+        }
         uint32_t steps = 0;
-        const uint32_t code = fi_compose(T, C[e], segend, &steps);
-        a.exitT[(uint64_t)k * FI_W + e] = code;
-        a.cntT[(uint64_t)k * FI_W + e] = steps;
+        const uint32_t code = fi_compose(T, c0, segend, &steps, [&](uint32_t j, uint32_t p, uint32_t before) {
+            if (rec) rec[1 + j] = (p << 16) | before;
+        });
+        if (rec) rec[0] = code < FI_W ? e : ~0u;
+        a.exitT[(uint64_t)k * FI_W + e] = code == FI_OVF ? FI_OVF : code | (steps << FI_CNT_SHIFT);
     }
+    __syncthreads();
+    if (threadIdx.x == 0) a.live_n[k] = nlive;
 }
 
 __global__ __launch_bounds__(FI_BLOCK) void fi_group_kernel(FiArgs a) {
@@ -191,15 +220,17 @@ __global__ __launch_bounds__(FI_BLOCK) void fi_group_kernel(FiArgs a) {
         bool open = true;
         for (uint32_t k = k0; k < k1 && open; k++) {
             const uint32_t c = a.exitT[(uint64_t)k * FI_W + x];
-            cnt += a.cntT[(uint64_t)k * FI_W + x];
-            if (c < FI_W) {
-                x = c;
-            } else if (c == FI_OVF) {
+            if (c == FI_OVF) {
                 code = FI_G_OVF;
                 open = false;
-            } else {
-                code = FI_G_TERM | ((uint64_t)k * FI_SEG + (c & 0xffffu));
+                break;
+            }
+            cnt += (c >> FI_CNT_SHIFT) & FI_CNT_MASK;
+            if (c & FI_TERM) {
+                code = FI_G_TERM | ((uint64_t)k * FI_SEG + (c & FI_POS_MASK));
                 open = false;
+            } else {
+                x = c & 0xffffu;
             }
         }
         if (open) code = x; // entry into segment k1
@@ -230,6 +261,7 @@ __global__ void fi_chain_kernel(FiArgs a) {
         x = c;
     }
     for (; g < a.ngroups; g++) a.grp_entry[g] = FI_NONE;
+    a.work[0] = 0;
     a.misc[0] = ovf;
     a.misc[1] = base;
     a.misc[2] = consumed;
@@ -247,48 +279,96 @@ __global__ void fi_segentry_kernel(FiArgs a) {
         a.seg_base[k] = base;
         if (x == FI_NONE) continue;
         const uint32_t c = a.exitT[(uint64_t)k * FI_W + x];
-        base += a.cntT[(uint64_t)k * FI_W + x];
-        x = c < FI_W ? c : FI_NONE;
+        if (c == FI_OVF) { // the chain kernel has raised the overflow flag
+            x = FI_NONE;
+            continue;
+        }
+        base += (c >> FI_CNT_SHIFT) & FI_CNT_MASK;
+        x = (c & FI_TERM) ? FI_NONE : c & 0xffffu;
     }
 }
 
-// per segment on the chain: tables again, the true entry composed once, then one thread per
-// sub-segment piece of the true chain writes its ends[]
-__global__ __launch_bounds__(FI_BLOCK) void fi_emit_kernel(FiArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    __shared__ uint32_t ent[FI_NSUB], before[FI_NSUB];
-    const uint32_t k = blockIdx.x;
-    if (a.misc[0]) return;
-    const uint32_t e = a.seg_entry[k];
-    if (e == FI_NONE) return;
-    const uint64_t s0 = (uint64_t)k * FI_SEG, s1 = s0 + FI_SEG < a.len ? s0 + FI_SEG : a.len;
-    const uint32_t segend = (uint32_t)(s1 - s0);
-    const uint64_t lenrel = a.len - s0;
-    if (threadIdx.x < FI_NSUB) ent[threadIdx.x] = threadIdx.x ? ~0u : e, before[threadIdx.x] = 0;
-    fi_tables(a, s0, segend, lds);
-    if (threadIdx.x == 0) {
-        uint32_t steps;
-        uint32_t *C = (uint32_t *)(lds + FI_LDS);
-        fi_walk_all(
-            lds, 1, segend, lenrel,
-            [&](uint32_t, uint32_t &p, uint32_t &stop) {
-                p = e;
-                stop = FI_SUB;
-            },
-            C);
-        fi_compose((const uint32_t *)(lds + FI_LDS_T), C[0], segend, &steps, ent, before);
+// the big-endian u32 at byte o of buf (zeros past len; buf is 4-byte aligned)
+__device__ __forceinline__ uint32_t be32_global(const uint8_t *buf, uint64_t len, uint64_t o) {
+    if (o + 8 <= len) {
+        const uint32_t *w = (const uint32_t *)(buf + (o & ~3ull));
+        const uint64_t d = ((uint64_t)w[1] << 32) | w[0];
+        return __builtin_bswap32((uint32_t)(d >> (8 * (o & 3))));
     }
-    __syncthreads();
-    if (threadIdx.x >= FI_NSUB || ent[threadIdx.x] == ~0u) return;
-    const uint32_t stop = (threadIdx.x + 1) * FI_SUB;
-    uint32_t p = ent[threadIdx.x];
-    uint64_t i = a.seg_base[k] + before[threadIdx.x];
+    uint32_t v = 0;
+    for (uint32_t b = 0; b < 4; b++) v = (v << 8) | (o + b < len ? buf[o + b] : 0u);
+    return v;
+}
+
+// One piece of a segment's true chain (from segment-relative p, frames before it in i): the
+// frames up to the next window position past `stop` (or the segment end), ends[] written.
+template <class Read>
+__device__ __forceinline__ void fi_emit_piece(const FiArgs &a, uint64_t s0, uint32_t segend, uint32_t stop,
+                                              uint32_t p, uint64_t i, Read be32) {
+    const uint64_t lenrel = a.len - s0;
     while (!(p >= segend || (p >= stop && (p & (FI_SUB - 1)) < FI_WS)) && (uint64_t)p + 4 <= lenrel) {
-        const uint64_t q = (uint64_t)p + 4 + be32_lds(lds, p);
+        const uint64_t q = (uint64_t)p + 4 + be32(p);
         if (q > lenrel) break;
         if (i < a.cap) a.ends[i] = s0 + q;
         i++;
         p = (uint32_t)q;
+    }
+}
+
+// per segment on the chain: its entry's pieces from the seg kernel's live records, one lane per
+// sub-segment piece reading the heads from HBM and writing ends[]; a segment whose entry has no
+// record (the chain ends in it, or more than FI_LIVE live entries) goes to the work list
+__global__ __launch_bounds__(64) void fi_emit_kernel(FiArgs a) {
+    const uint32_t k = blockIdx.x, lane = threadIdx.x;
+    if (a.misc[0]) return;
+    const uint32_t e = a.seg_entry[k];
+    if (e == FI_NONE) return;
+    const uint32_t n = a.live_n[k];
+    const uint32_t *live = a.live + (uint64_t)k * FI_LIVE * FI_LREC;
+    const uint64_t hit = __ballot(lane < n && lane < FI_LIVE && live[lane * FI_LREC] == e);
+    if (hit == 0) {
+        if (lane == 0) a.work[1 + atomicAdd(&a.work[0], 1u)] = k;
+        return;
+    }
+    if (lane >= FI_NSUB) return;
+    const uint32_t v = live[(__ffsll((unsigned long long)hit) - 1) * FI_LREC + 1 + lane];
+    if (v == ~0u) return;
+    const uint64_t s0 = (uint64_t)k * FI_SEG, s1 = s0 + FI_SEG < a.len ? s0 + FI_SEG : a.len;
+    fi_emit_piece(a, s0, (uint32_t)(s1 - s0), (lane + 1) * FI_SUB, v >> 16, a.seg_base[k] + (v & 0xffffu),
+                  [&](uint32_t p) { return be32_global(a.buf, a.len, s0 + p); });
+}
+
+// the work list's segments: tables again in LDS, the true entry composed once, one thread per
+// piece (a grid of at most 256 blocks striding the list; usually one segment, the chain's last)
+__global__ __launch_bounds__(FI_BLOCK) void fi_emit_slow_kernel(FiArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    __shared__ uint32_t ent[FI_NSUB], before[FI_NSUB];
+    const uint32_t nwork = a.work[0];
+    for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
+        const uint32_t k = a.work[1 + w], e = a.seg_entry[k];
+        const uint64_t s0 = (uint64_t)k * FI_SEG, s1 = s0 + FI_SEG < a.len ? s0 + FI_SEG : a.len;
+        const uint32_t segend = (uint32_t)(s1 - s0);
+        if (threadIdx.x < FI_NSUB) ent[threadIdx.x] = threadIdx.x ? ~0u : e, before[threadIdx.x] = 0;
+        fi_tables(a, s0, segend, lds);
+        if (threadIdx.x == 0) {
+            uint32_t steps, *C = (uint32_t *)(lds + FI_LDS);
+            fi_walk_all(
+                lds, 1, segend, a.len - s0,
+                [&](uint32_t, uint32_t &p, uint32_t &stop) {
+                    p = e;
+                    stop = FI_SUB;
+                },
+                C);
+            fi_compose((const uint32_t *)(lds + FI_LDS_T), C[0], segend, &steps, [&](uint32_t j, uint32_t p, uint32_t b) {
+                ent[j] = p;
+                before[j] = b;
+            });
+        }
+        __syncthreads();
+        if (threadIdx.x < FI_NSUB && ent[threadIdx.x] != ~0u)
+            fi_emit_piece(a, s0, segend, (threadIdx.x + 1) * FI_SUB, ent[threadIdx.x],
+                          a.seg_base[k] + before[threadIdx.x], [&](uint32_t p) { return be32_lds(lds, p); });
+        __syncthreads();
     }
 }
 
@@ -323,7 +403,7 @@ __global__ void fi_finish_kernel(FiArgs a) {
 
 struct FiLayout {
     uint32_t nseg, ngroups;
-    size_t off[9], bytes;
+    size_t off[12], bytes;
 };
 
 FiLayout fi_layout(uint64_t len) {
@@ -331,11 +411,12 @@ FiLayout fi_layout(uint64_t len) {
     L.nseg = (uint32_t)((len + FI_SEG - 1) / FI_SEG);
     if (L.nseg == 0) L.nseg = 1;
     L.ngroups = (L.nseg + FI_G - 1) / FI_G;
-    const size_t sz[9] = {(size_t)L.nseg * FI_W * 4, (size_t)L.nseg * FI_W * 4, (size_t)L.ngroups * FI_W * 8,
+    const size_t sz[12] = {(size_t)L.nseg * FI_W * 4, 0, (size_t)L.ngroups * FI_W * 8,
                           (size_t)L.ngroups * FI_W * 4, (size_t)L.ngroups * 4, (size_t)L.ngroups * 8,
-                          (size_t)L.nseg * 4, (size_t)L.nseg * 8, 64};
+                          (size_t)L.nseg * 4, (size_t)L.nseg * 8, 64, (size_t)L.nseg * 4,
+                          (size_t)L.nseg * FI_LIVE * FI_LREC * 4, ((size_t)L.nseg + 1) * 4};
     size_t o = 0;
-    for (int i = 0; i < 9; i++) {
+    for (int i = 0; i < 12; i++) {
         L.off[i] = o;
         o += (sz[i] + 255) / 256 * 256;
     }
@@ -362,7 +443,6 @@ int launch_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends,
     a.nseg = L.nseg;
     a.ngroups = L.ngroups;
     a.exitT = (uint32_t *)(w + L.off[0]);
-    a.cntT = (uint32_t *)(w + L.off[1]);
     a.grpT = (uint64_t *)(w + L.off[2]);
     a.grpCnt = (uint32_t *)(w + L.off[3]);
     a.grp_entry = (uint32_t *)(w + L.off[4]);
@@ -370,12 +450,16 @@ int launch_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends,
     a.seg_entry = (uint32_t *)(w + L.off[6]);
     a.seg_base = (uint64_t *)(w + L.off[7]);
     a.misc = (uint64_t *)(w + L.off[8]);
+    a.live_n = (uint32_t *)(w + L.off[9]);
+    a.live = (uint32_t *)(w + L.off[10]);
+    a.work = (uint32_t *)(w + L.off[11]);
     const size_t lds = FI_LDS + FI_W * 4; // + the segment walks' sub-segment 0 codes
     hipLaunchKernelGGL(fi_seg_kernel, dim3(L.nseg), dim3(FI_BLOCK), lds, stream, a);
     hipLaunchKernelGGL(fi_group_kernel, dim3(L.ngroups), dim3(FI_BLOCK), 0, stream, a);
     hipLaunchKernelGGL(fi_chain_kernel, dim3(1), dim3(64), 0, stream, a);
     hipLaunchKernelGGL(fi_segentry_kernel, dim3((L.ngroups + 63) / 64), dim3(64), 0, stream, a);
-    hipLaunchKernelGGL(fi_emit_kernel, dim3(L.nseg), dim3(FI_BLOCK), lds, stream, a);
+    hipLaunchKernelGGL(fi_emit_kernel, dim3(L.nseg), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(fi_emit_slow_kernel, dim3(L.nseg < 256 ? L.nseg : 256), dim3(FI_BLOCK), lds, stream, a);
     hipLaunchKernelGGL(fi_finish_kernel, dim3(1), dim3(64), 0, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

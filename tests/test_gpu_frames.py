@@ -17,7 +17,7 @@ from tests.gpu_helpers import to_dev
 
 pytestmark = pytest.mark.gpu
 
-SEG = 65536
+SEG = 32768  # frames_device.hip FI_SEG
 
 
 def frames_of(sizes, rng, tail=b""):
@@ -68,7 +68,7 @@ def test_random_frames(dev, seed):
 
 
 def test_segment_boundaries(dev):
-    """Frames ending exactly on 64 KiB boundaries, heads straddling them, a stream that ends
+    """Frames ending exactly on 32 KiB segment boundaries, heads straddling them, a stream that ends
     exactly at a boundary."""
     rng = np.random.default_rng(9)
     for first in (SEG - 4, SEG - 5, SEG - 6, SEG - 7, SEG - 2048 - 4, SEG - 2049 - 4):
@@ -82,7 +82,8 @@ def test_segment_boundaries(dev):
 def test_sub_segment_windows(dev):
     """The 4 KiB sub-segment tables inside a segment: frames 1-2 KiB long (heads past a
     sub-segment's 1024-byte window, so the walk runs on into the next sub-segment), 4 KiB frames
-    landing exactly on sub-segment starts, and heads at window offsets 1023 / 1024."""
+    landing exactly on sub-segment starts, heads at window offsets 1023 / 1024, and frames so
+    small that a segment has more live entries than the emit's records."""
     rng = np.random.default_rng(11)
     sub, ws = 4096, 1024
     cases = {
@@ -92,6 +93,9 @@ def test_sub_segment_windows(dev):
         "window 1023": [sub + ws - 1 - 4] + list(rng.integers(0, 300, 2000)),
         "window 1024": [sub + ws - 4] + list(rng.integers(0, 300, 2000)),
         "mixed": list(rng.choice([7, 60, 900, 1100, 1500, 2040, 4092], 3000)),
+        # ~70 true heads in a segment's 2048-byte entry window: more live entries than the 32
+        # records kept, so some segments' emits rebuild their tables (the work list)
+        "small": list(rng.integers(6, 36, 30000)),
     }
     for label, sizes in cases.items():
         check(dev, frames_of(sizes, rng), label=label, sizes=sizes)
