@@ -12,9 +12,10 @@
 //      dependent LDS reads), so no thread walks more than ~4 KiB of frames (a false entry reads a
 //      random big size and leaves at once).  Entries that leave the segment (live: the true one
 //      and the others on the same chain, ~8 per segment) keep their pieces for step 5;
-//   2. groups of 64 segments compose their tables (every entry, 64 dependent table reads);
-//   3. one thread chains the groups from offset 0 (a few hundred dependent reads);
-//   4. each group resolves its segments' entries and frame bases;
+//   2. groups of 16 segments compose their tables (every entry, 16 dependent table reads), and
+//      super-groups of 16 groups compose those (every entry, 16 reads);
+//   3. one thread chains the super-groups from offset 0 (nseg / 256 dependent reads);
+//   4. each super-group resolves its groups' entries and frame bases, each group its segments';
 //   5. each segment on the chain: one lane per sub-segment piece of its true chain (from the
 //      live record of its entry) reads the heads from HBM and writes ends[]; a segment without a
 //      record (the chain ends in it) rebuilds its tables in LDS (a short work list).
@@ -30,7 +31,8 @@ namespace spec {
 
 namespace {
 
-constexpr uint32_t FI_SEG = 32768, FI_W = 2048, FI_G = 64, FI_STEPCAP = 4096;
+constexpr uint32_t FI_SEG = 32768, FI_W = 2048, FI_STEPCAP = 4096;
+constexpr uint32_t FI_G1 = 16, FI_G2 = 16; // segments per group, groups per super-group
 constexpr uint32_t FI_BLOCK = 1024; // threads of the segment / group kernels (a constant: blockDim
                                     // is a load from the dispatch packet)
 constexpr uint32_t FI_SUB = 4096, FI_NSUB = FI_SEG / FI_SUB, FI_WS = 1024;
@@ -50,12 +52,14 @@ struct FiArgs {
     uint64_t len, cap;
     uint64_t *ends, *count, *consumed;
     int32_t *status;
-    uint32_t nseg, ngroups;
+    uint32_t nseg, ng1, ng2;
     uint32_t *exitT;           // [nseg * W] packed: exit / TERM position, frames
-    uint64_t *grpT;            // [ngroups * W]
-    uint32_t *grpCnt;          // [ngroups * W]
-    uint32_t *grp_entry;       // [ngroups]
-    uint64_t *grp_base;        // [ngroups]
+    uint64_t *g1T, *g2T;       // [ng1 * W], [ng2 * W]: entry into the next, FI_G_TERM | position, FI_G_OVF
+    uint32_t *g1Cnt, *g2Cnt;   // frames
+    uint32_t *g1_entry;        // [ng1]
+    uint64_t *g1_base;         // [ng1]
+    uint32_t *g2_entry;        // [ng2]
+    uint64_t *g2_base;         // [ng2]
     uint32_t *seg_entry;       // [nseg]
     uint64_t *seg_base;        // [nseg]
     uint64_t *misc;            // [0] overflow, [1] total frames, [2] consumed
@@ -71,20 +75,23 @@ __device__ __forceinline__ uint32_t be32_lds(const uint8_t *l, uint32_t o) {
     return __builtin_bswap32((uint32_t)(d >> (8 * (o & 3))));
 }
 
-// bytes [s0, s0 + SEG + 16) of buf into lds (zeros past len); buf is 4-byte aligned
+constexpr uint32_t FI_QPT = FI_SEG / 16 / FI_BLOCK; // 16-byte quads of a segment per thread
+static_assert(FI_QPT == 2 && FI_QPT * 16 * FI_BLOCK == FI_SEG, "two 16-byte quads of a segment per thread");
+
+// a segment the quad path stages: whole (with its 16 halo bytes) from a 16-byte aligned buffer
+// (the ABI only promises 4-byte alignment: other buffers, and the tail, take the dword loop)
+__device__ __forceinline__ bool quad_segment(const FiArgs &a, uint64_t s0) {
+    return s0 + FI_SEG + 16 <= a.len && ((uintptr_t)a.buf & 15) == 0;
+}
+
+// bytes [s0, s0 + SEG + 16) of buf into lds (zeros past len; buf is 4-byte aligned), then a barrier
 __device__ __forceinline__ void stage_segment(const FiArgs &a, uint64_t s0, uint8_t *lds) {
-    // a whole segment from a 16-byte aligned buffer: 16-byte loads, all of a thread's in flight
-    // (the ABI only promises 4-byte alignment: other buffers take the dword loop)
-    if (s0 + FI_SEG + 16 <= a.len && ((uintptr_t)a.buf & 15) == 0) {
+    if (quad_segment(a, s0)) {
         const uint4 *src = (const uint4 *)(a.buf + s0);
         uint4 *dst = (uint4 *)lds;
-        constexpr uint32_t QPT = FI_SEG / 16 / FI_BLOCK; // quads per thread, all loads in flight
-        static_assert(QPT * 16 * FI_BLOCK == FI_SEG, "segment is a whole number of quads per thread");
-        uint4 v[QPT];
-#pragma unroll
-        for (uint32_t j = 0; j < QPT; j++) v[j] = src[threadIdx.x + j * FI_BLOCK];
-#pragma unroll
-        for (uint32_t j = 0; j < QPT; j++) dst[threadIdx.x + j * FI_BLOCK] = v[j];
+        const uint4 v0 = src[threadIdx.x], v1 = src[threadIdx.x + FI_BLOCK];
+        dst[threadIdx.x] = v0;
+        dst[threadIdx.x + FI_BLOCK] = v1;
         if (threadIdx.x == 0) dst[FI_SEG / 16] = src[FI_SEG / 16];
         __syncthreads();
         return;
@@ -104,49 +111,43 @@ __device__ __forceinline__ void stage_segment(const FiArgs &a, uint64_t s0, uint
     __syncthreads();
 }
 
-// Walk jobs i = threadIdx.x + m * FI_BLOCK < njobs: from start(i) -> (p, stop), the chain
-// until it stands on a position at or past `stop` that lies in the first WS bytes of a
-// sub-segment, or past the segment end (segend = s1 - s0, lenrel = len - s0); out[i] = code.  A
-// jump W or more past the segment end, or more than STEPCAP frames, is overflow (the serial
-// fallback).  One frame step per iteration, selects instead of branches, one predicated store:
-// a lane that finishes a walk starts its next at once, so a wave runs for its busiest lane's
-// steps, not for the sum over jobs of the longest walk.
-template <class Start>
-__device__ __forceinline__ void fi_walk_all(const uint8_t *lds, uint32_t njobs, uint32_t segend, uint64_t lenrel,
-                                            Start start, uint32_t *out) {
-    uint32_t i = threadIdx.x, p, stop, steps = 0;
-    if (i >= njobs) return;
-    start(i, p, stop);
-    const uint64_t far = (uint64_t)segend + FI_W;
-    while (true) {
-        const bool exit = p >= segend || (p >= stop && (p & (FI_SUB - 1)) < FI_WS);
-        const uint64_t q = (uint64_t)p + 4 + be32_lds(lds, p & (FI_SEG - 1)); // in the staged bytes
-        const bool term = q > lenrel;
-        const bool fin = exit || term || q >= far || steps >= FI_STEPCAP;
-        const uint32_t code = exit ? (steps << 17) | p : term ? FI_T_TERM | (steps << 17) | p : FI_T_OVF;
-        if (fin) out[i] = code;
-        const uint32_t inext = fin ? i + FI_BLOCK : i;
-        if (inext >= njobs) break;
-        uint32_t p2, stop2;
-        start(inext, p2, stop2);
-        p = fin ? p2 : (uint32_t)q;
-        stop = fin ? stop2 : stop;
+// The walks of a staged segment, job m of this lane (m = 0 .. NSUB-2: entry threadIdx.x of the
+// window of sub-segment m + 1, into T; then, with `entries`, W / BLOCK segment entries
+// (m - NSUB + 1) * BLOCK + threadIdx.x of sub-segment 0, into C right after T): the chain until
+// it stands on a position at or past its stop (the next sub-segment) that lies in the first WS
+// bytes of a sub-segment, or past the segment end (segend = s1 - s0, lenrel = len - s0).  A jump
+// W or more past the segment end, or more than STEPCAP frames, is overflow (the serial
+// fallback).  One frame step per iteration with 32-bit arithmetic (the size saturates; the exact
+// TERM test runs once per walk): a lane that finishes a walk starts its next at once, so a wave
+// runs for its busiest lane's steps, not for the sum over jobs of the longest walk.  Then a
+// barrier.
+__device__ __forceinline__ void fi_tables(const FiArgs &a, uint64_t s0, uint32_t segend, uint8_t *lds,
+                                          bool entries) {
+    constexpr uint32_t NT = FI_NSUB - 1, NE = FI_W / FI_BLOCK;
+    static_assert(FI_LDS == FI_LDS_T + NT * FI_WS * 4 && FI_WS == FI_BLOCK, "T: a window entry per lane; C follows");
+    static_assert(FI_SUB - FI_WS == 0xc00u, "window test by mask");
+    uint32_t *out = (uint32_t *)(lds + FI_LDS_T) + threadIdx.x;
+    const uint64_t lenrel = a.len - s0;
+    const uint32_t far = (uint32_t)((uint64_t)segend + FI_W < lenrel + 1 ? (uint64_t)segend + FI_W : lenrel + 1);
+    const uint32_t njobs = entries ? NT + NE : NT;
+    uint32_t m = 0, p = FI_SUB + threadIdx.x, stop = 2 * FI_SUB, steps = 0;
+    while (true) { // flat: selects and one predicated store (a branch would nest a loop per job)
+        const uint32_t v = be32_lds(lds, p & (FI_SEG - 1)); // in the staged bytes
+        const uint32_t q = p + 4 + (v < 0x7fffffffu ? v : 0x7fffffffu);
+        const bool exit = (p >= segend) | ((p >= stop) & ((p & 0xc00u) == 0));
+        const bool fin = exit | (q >= far) | (steps >= FI_STEPCAP);
+        const bool term = (uint64_t)p + 4 + v > lenrel;
+        if (fin) out[m * FI_BLOCK] = exit ? (steps << 17) | p : term ? FI_T_TERM | (steps << 17) | p : FI_T_OVF;
+        uint32_t mn = m + (fin ? 1u : 0u);
+        if (mn >= njobs) break;
+        asm volatile("" : "+v"(mn)); // opaque: no per-job copies of the loop
+        const uint32_t pn = mn < NT ? (mn + 1) * FI_SUB + threadIdx.x : (mn - NT) * FI_BLOCK + threadIdx.x;
+        const uint32_t stopn = mn < NT ? (mn + 2) * FI_SUB : FI_SUB;
+        p = fin ? pn : q;
+        stop = fin ? stopn : stop;
         steps = fin ? 0 : steps + 1;
-        i = inext;
+        m = mn;
     }
-}
-
-// stage the segment and walk every window entry of sub-segments 1..15 (tables after the data)
-__device__ __forceinline__ void fi_tables(const FiArgs &a, uint64_t s0, uint32_t segend, uint8_t *lds) {
-    stage_segment(a, s0, lds);
-    uint32_t *T = (uint32_t *)(lds + FI_LDS_T);
-    fi_walk_all(
-        lds, (FI_NSUB - 1) * FI_WS, segend, a.len - s0,
-        [](uint32_t i, uint32_t &p, uint32_t &stop) {
-            stop = (2 + i / FI_WS) * FI_SUB;
-            p = stop - FI_SUB + i % FI_WS;
-        },
-        T);
     __syncthreads();
 }
 
@@ -170,50 +171,71 @@ __device__ __forceinline__ uint32_t fi_compose(const uint32_t *T, uint32_t c, ui
     }
 }
 
+// Persistent: a block strides over the segments; the next segment's bytes are loaded into
+// registers while this one is walked, so HBM latency hides behind the walks.
 __global__ __launch_bounds__(FI_BLOCK) void fi_seg_kernel(FiArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     __shared__ uint32_t nlive;
-    const uint32_t k = blockIdx.x;
-    const uint64_t s0 = (uint64_t)k * FI_SEG, s1 = s0 + FI_SEG < a.len ? s0 + FI_SEG : a.len;
-    const uint32_t segend = (uint32_t)(s1 - s0);
-    if (threadIdx.x == 0) nlive = 0;
-    fi_tables(a, s0, segend, lds);
-    const uint32_t *T = (const uint32_t *)(lds + FI_LDS_T);
-    uint32_t *C = (uint32_t *)(lds + FI_LDS);
-    fi_walk_all(
-        lds, FI_W, segend, a.len - s0,
-        [](uint32_t e, uint32_t &p, uint32_t &stop) {
-            p = e;
-            stop = FI_SUB;
-        },
-        C);
-    uint32_t *live = a.live + (uint64_t)k * FI_LIVE * FI_LREC;
-    for (uint32_t e = threadIdx.x; e < FI_W; e += FI_BLOCK) { // a lane composes its own walks
-        // an entry that survives sub-segment 0 may be live: a record slot for its pieces
-        // (marked dead again if the chain ends in the segment after all)
-        const uint32_t c0 = C[e];
-        uint32_t *rec = nullptr;
-        if (c0 != FI_T_OVF && !(c0 & FI_T_TERM)) {
-            const uint32_t slot = atomicAdd(&nlive, 1u);
-            if (slot < FI_LIVE) {
-                rec = live + slot * FI_LREC;
-                rec[1] = e << 16;
-                for (uint32_t j = 1; j < FI_NSUB; j++) rec[1 + j] = ~0u;
-            }
-        }
-        uint32_t steps = 0;
-        const uint32_t code = fi_compose(T, c0, segend, &steps, [&](uint32_t j, uint32_t p, uint32_t before) {
-            if (rec) rec[1 + j] = (p << 16) | before;
-        });
-        if (rec) rec[0] = code < FI_W ? e : ~0u;
-        a.exitT[(uint64_t)k * FI_W + e] = code == FI_OVF ? FI_OVF : code | (steps << FI_CNT_SHIFT);
+    const uint32_t stride = gridDim.x;
+    const uint4 *src = (const uint4 *)a.buf; // quad_segment: 16-byte aligned
+    uint4 v0 = {}, v1 = {}, halo = {};
+    uint32_t k = blockIdx.x;
+    if (k < a.nseg && quad_segment(a, (uint64_t)k * FI_SEG)) {
+        const uint64_t q0 = (uint64_t)k * (FI_SEG / 16);
+        v0 = src[q0 + threadIdx.x];
+        v1 = src[q0 + threadIdx.x + FI_BLOCK];
+        if (threadIdx.x == 0) halo = src[q0 + FI_SEG / 16];
     }
-    __syncthreads();
-    if (threadIdx.x == 0) a.live_n[k] = nlive;
+    for (; k < a.nseg; k += stride) {
+        const uint64_t s0 = (uint64_t)k * FI_SEG, s1 = s0 + FI_SEG < a.len ? s0 + FI_SEG : a.len;
+        const uint32_t segend = (uint32_t)(s1 - s0);
+        if (threadIdx.x == 0) nlive = 0;
+        if (quad_segment(a, s0)) {
+            uint4 *dst = (uint4 *)lds;
+            dst[threadIdx.x] = v0;
+            dst[threadIdx.x + FI_BLOCK] = v1;
+            if (threadIdx.x == 0) dst[FI_SEG / 16] = halo;
+            __syncthreads();
+        } else {
+            stage_segment(a, s0, lds);
+        }
+        if (k + stride < a.nseg && quad_segment(a, (uint64_t)(k + stride) * FI_SEG)) { // the next, in flight
+            const uint64_t q0 = (uint64_t)(k + stride) * (FI_SEG / 16);
+            v0 = src[q0 + threadIdx.x];
+            v1 = src[q0 + threadIdx.x + FI_BLOCK];
+            if (threadIdx.x == 0) halo = src[q0 + FI_SEG / 16];
+        }
+        fi_tables(a, s0, segend, lds, true);
+        const uint32_t *T = (const uint32_t *)(lds + FI_LDS_T), *C = (const uint32_t *)(lds + FI_LDS);
+        uint32_t *live = a.live + (uint64_t)k * FI_LIVE * FI_LREC;
+        for (uint32_t e = threadIdx.x; e < FI_W; e += FI_BLOCK) { // a lane composes its own walks
+            // an entry that survives sub-segment 0 may be live: a record slot for its pieces
+            // (marked dead again if the chain ends in the segment after all)
+            const uint32_t c0 = C[e];
+            uint32_t *rec = nullptr;
+            if (c0 != FI_T_OVF && !(c0 & FI_T_TERM)) {
+                const uint32_t slot = atomicAdd(&nlive, 1u);
+                if (slot < FI_LIVE) {
+                    rec = live + slot * FI_LREC;
+                    rec[1] = e << 16;
+                    for (uint32_t j = 1; j < FI_NSUB; j++) rec[1 + j] = ~0u;
+                }
+            }
+            uint32_t steps = 0;
+            const uint32_t code = fi_compose(T, c0, segend, &steps, [&](uint32_t j, uint32_t p, uint32_t before) {
+                if (rec) rec[1 + j] = (p << 16) | before;
+            });
+            if (rec) rec[0] = code < FI_W ? e : ~0u;
+            a.exitT[(uint64_t)k * FI_W + e] = code == FI_OVF ? FI_OVF : code | (steps << FI_CNT_SHIFT);
+        }
+        __syncthreads(); // nlive final; the LDS free for the next segment
+        if (threadIdx.x == 0) a.live_n[k] = nlive;
+    }
 }
 
-__global__ __launch_bounds__(FI_BLOCK) void fi_group_kernel(FiArgs a) {
-    const uint32_t g = blockIdx.x, k0 = g * FI_G, k1 = k0 + FI_G < a.nseg ? k0 + FI_G : a.nseg;
+// groups of G1 segments: every entry's exit composed over the group's tables (G1 dependent reads)
+__global__ __launch_bounds__(FI_BLOCK) void fi_group1_kernel(FiArgs a) {
+    const uint32_t g = blockIdx.x, k0 = g * FI_G1, k1 = k0 + FI_G1 < a.nseg ? k0 + FI_G1 : a.nseg;
     for (uint32_t e = threadIdx.x; e < FI_W; e += FI_BLOCK) {
         uint32_t x = e, cnt = 0;
         uint64_t code = 0;
@@ -234,21 +256,38 @@ __global__ __launch_bounds__(FI_BLOCK) void fi_group_kernel(FiArgs a) {
             }
         }
         if (open) code = x; // entry into segment k1
-        a.grpT[(uint64_t)g * FI_W + e] = code;
-        a.grpCnt[(uint64_t)g * FI_W + e] = cnt;
+        a.g1T[(uint64_t)g * FI_W + e] = code;
+        a.g1Cnt[(uint64_t)g * FI_W + e] = cnt;
     }
 }
 
-// one thread: the groups chained from offset 0
+// super-groups of G2 groups: the same over the group tables
+__global__ __launch_bounds__(FI_BLOCK) void fi_group2_kernel(FiArgs a) {
+    const uint32_t g = blockIdx.x, j0 = g * FI_G2, j1 = j0 + FI_G2 < a.ng1 ? j0 + FI_G2 : a.ng1;
+    for (uint32_t e = threadIdx.x; e < FI_W; e += FI_BLOCK) {
+        uint64_t code = e;
+        uint32_t cnt = 0;
+        for (uint32_t j = j0; j < j1; j++) {
+            const uint64_t c = a.g1T[(uint64_t)j * FI_W + code];
+            cnt += a.g1Cnt[(uint64_t)j * FI_W + code];
+            code = c;
+            if (c & (FI_G_TERM | FI_G_OVF)) break;
+        }
+        a.g2T[(uint64_t)g * FI_W + e] = code;
+        a.g2Cnt[(uint64_t)g * FI_W + e] = cnt;
+    }
+}
+
+// one thread: the super-groups chained from offset 0
 __global__ void fi_chain_kernel(FiArgs a) {
     if (threadIdx.x != 0) return;
     uint64_t x = 0, base = 0, consumed = a.len, ovf = 0;
     uint32_t g = 0;
-    for (; g < a.ngroups; g++) {
-        a.grp_entry[g] = (uint32_t)x;
-        a.grp_base[g] = base;
-        const uint64_t c = a.grpT[(uint64_t)g * FI_W + x];
-        base += a.grpCnt[(uint64_t)g * FI_W + x];
+    for (; g < a.ng2; g++) {
+        a.g2_entry[g] = (uint32_t)x;
+        a.g2_base[g] = base;
+        const uint64_t c = a.g2T[(uint64_t)g * FI_W + x];
+        base += a.g2Cnt[(uint64_t)g * FI_W + x];
         if (c & FI_G_OVF) {
             ovf = 1;
             break;
@@ -260,20 +299,37 @@ __global__ void fi_chain_kernel(FiArgs a) {
         }
         x = c;
     }
-    for (; g < a.ngroups; g++) a.grp_entry[g] = FI_NONE;
+    for (; g < a.ng2; g++) a.g2_entry[g] = FI_NONE;
     a.work[0] = 0;
     a.misc[0] = ovf;
     a.misc[1] = base;
     a.misc[2] = consumed;
 }
 
+// per super-group (one thread): its groups' entries and frame bases
+__global__ void fi_resolve2_kernel(FiArgs a) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= a.ng2 || a.misc[0]) return;
+    const uint32_t j0 = g * FI_G2, j1 = j0 + FI_G2 < a.ng1 ? j0 + FI_G2 : a.ng1;
+    uint32_t x = a.g2_entry[g];
+    uint64_t base = a.g2_base[g];
+    for (uint32_t j = j0; j < j1; j++) {
+        a.g1_entry[j] = x;
+        a.g1_base[j] = base;
+        if (x == FI_NONE) continue;
+        const uint64_t c = a.g1T[(uint64_t)j * FI_W + x];
+        base += a.g1Cnt[(uint64_t)j * FI_W + x];
+        x = (c & (FI_G_TERM | FI_G_OVF)) ? FI_NONE : (uint32_t)c;
+    }
+}
+
 // per group (one thread): its segments' entries and frame bases
 __global__ void fi_segentry_kernel(FiArgs a) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= a.ngroups || a.misc[0]) return;
-    const uint32_t k0 = g * FI_G, k1 = k0 + FI_G < a.nseg ? k0 + FI_G : a.nseg;
-    uint32_t x = a.grp_entry[g];
-    uint64_t base = a.grp_base[g];
+    if (g >= a.ng1 || a.misc[0]) return;
+    const uint32_t k0 = g * FI_G1, k1 = k0 + FI_G1 < a.nseg ? k0 + FI_G1 : a.nseg;
+    uint32_t x = a.g1_entry[g];
+    uint64_t base = a.g1_base[g];
     for (uint32_t k = k0; k < k1; k++) {
         a.seg_entry[k] = x;
         a.seg_base[k] = base;
@@ -349,17 +405,12 @@ __global__ __launch_bounds__(FI_BLOCK) void fi_emit_slow_kernel(FiArgs a) {
         const uint64_t s0 = (uint64_t)k * FI_SEG, s1 = s0 + FI_SEG < a.len ? s0 + FI_SEG : a.len;
         const uint32_t segend = (uint32_t)(s1 - s0);
         if (threadIdx.x < FI_NSUB) ent[threadIdx.x] = threadIdx.x ? ~0u : e, before[threadIdx.x] = 0;
-        fi_tables(a, s0, segend, lds);
+        stage_segment(a, s0, lds);
+        fi_tables(a, s0, segend, lds, true);
         if (threadIdx.x == 0) {
-            uint32_t steps, *C = (uint32_t *)(lds + FI_LDS);
-            fi_walk_all(
-                lds, 1, segend, a.len - s0,
-                [&](uint32_t, uint32_t &p, uint32_t &stop) {
-                    p = e;
-                    stop = FI_SUB;
-                },
-                C);
-            fi_compose((const uint32_t *)(lds + FI_LDS_T), C[0], segend, &steps, [&](uint32_t j, uint32_t p, uint32_t b) {
+            uint32_t steps;
+            const uint32_t *C = (const uint32_t *)(lds + FI_LDS);
+            fi_compose((const uint32_t *)(lds + FI_LDS_T), C[e], segend, &steps, [&](uint32_t j, uint32_t p, uint32_t b) {
                 ent[j] = p;
                 before[j] = b;
             });
@@ -402,21 +453,23 @@ __global__ void fi_finish_kernel(FiArgs a) {
 }
 
 struct FiLayout {
-    uint32_t nseg, ngroups;
-    size_t off[12], bytes;
+    uint32_t nseg, ng1, ng2;
+    size_t off[15], bytes;
 };
 
 FiLayout fi_layout(uint64_t len) {
     FiLayout L;
     L.nseg = (uint32_t)((len + FI_SEG - 1) / FI_SEG);
     if (L.nseg == 0) L.nseg = 1;
-    L.ngroups = (L.nseg + FI_G - 1) / FI_G;
-    const size_t sz[12] = {(size_t)L.nseg * FI_W * 4, 0, (size_t)L.ngroups * FI_W * 8,
-                          (size_t)L.ngroups * FI_W * 4, (size_t)L.ngroups * 4, (size_t)L.ngroups * 8,
-                          (size_t)L.nseg * 4, (size_t)L.nseg * 8, 64, (size_t)L.nseg * 4,
-                          (size_t)L.nseg * FI_LIVE * FI_LREC * 4, ((size_t)L.nseg + 1) * 4};
+    L.ng1 = (L.nseg + FI_G1 - 1) / FI_G1;
+    L.ng2 = (L.ng1 + FI_G2 - 1) / FI_G2;
+    const size_t W = FI_W;
+    const size_t sz[15] = {L.nseg * W * 4,  L.ng1 * W * 8, L.ng1 * W * 4, L.ng2 * W * 8,
+                           L.ng2 * W * 4,   (size_t)L.ng1 * 4, (size_t)L.ng1 * 8, (size_t)L.ng2 * 4,
+                           (size_t)L.ng2 * 8, (size_t)L.nseg * 4, (size_t)L.nseg * 8, 64,
+                           (size_t)L.nseg * 4, (size_t)L.nseg * FI_LIVE * FI_LREC * 4, ((size_t)L.nseg + 1) * 4};
     size_t o = 0;
-    for (int i = 0; i < 12; i++) {
+    for (int i = 0; i < 15; i++) {
         L.off[i] = o;
         o += (sz[i] + 255) / 256 * 256;
     }
@@ -441,23 +494,31 @@ int launch_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends,
     a.consumed = consumed;
     a.status = status;
     a.nseg = L.nseg;
-    a.ngroups = L.ngroups;
+    a.ng1 = L.ng1;
+    a.ng2 = L.ng2;
     a.exitT = (uint32_t *)(w + L.off[0]);
-    a.grpT = (uint64_t *)(w + L.off[2]);
-    a.grpCnt = (uint32_t *)(w + L.off[3]);
-    a.grp_entry = (uint32_t *)(w + L.off[4]);
-    a.grp_base = (uint64_t *)(w + L.off[5]);
-    a.seg_entry = (uint32_t *)(w + L.off[6]);
-    a.seg_base = (uint64_t *)(w + L.off[7]);
-    a.misc = (uint64_t *)(w + L.off[8]);
-    a.live_n = (uint32_t *)(w + L.off[9]);
-    a.live = (uint32_t *)(w + L.off[10]);
-    a.work = (uint32_t *)(w + L.off[11]);
+    a.g1T = (uint64_t *)(w + L.off[1]);
+    a.g1Cnt = (uint32_t *)(w + L.off[2]);
+    a.g2T = (uint64_t *)(w + L.off[3]);
+    a.g2Cnt = (uint32_t *)(w + L.off[4]);
+    a.g1_entry = (uint32_t *)(w + L.off[5]);
+    a.g1_base = (uint64_t *)(w + L.off[6]);
+    a.g2_entry = (uint32_t *)(w + L.off[7]);
+    a.g2_base = (uint64_t *)(w + L.off[8]);
+    a.seg_entry = (uint32_t *)(w + L.off[9]);
+    a.seg_base = (uint64_t *)(w + L.off[10]);
+    a.misc = (uint64_t *)(w + L.off[11]);
+    a.live_n = (uint32_t *)(w + L.off[12]);
+    a.live = (uint32_t *)(w + L.off[13]);
+    a.work = (uint32_t *)(w + L.off[14]);
     const size_t lds = FI_LDS + FI_W * 4; // + the segment walks' sub-segment 0 codes
-    hipLaunchKernelGGL(fi_seg_kernel, dim3(L.nseg), dim3(FI_BLOCK), lds, stream, a);
-    hipLaunchKernelGGL(fi_group_kernel, dim3(L.ngroups), dim3(FI_BLOCK), 0, stream, a);
+    const uint32_t seg_blocks = 2u * (uint32_t)device_cus(); // two 70 KiB-LDS blocks per CU, persistent
+    hipLaunchKernelGGL(fi_seg_kernel, dim3(L.nseg < seg_blocks ? L.nseg : seg_blocks), dim3(FI_BLOCK), lds, stream, a);
+    hipLaunchKernelGGL(fi_group1_kernel, dim3(L.ng1), dim3(FI_BLOCK), 0, stream, a);
+    hipLaunchKernelGGL(fi_group2_kernel, dim3(L.ng2), dim3(FI_BLOCK), 0, stream, a);
     hipLaunchKernelGGL(fi_chain_kernel, dim3(1), dim3(64), 0, stream, a);
-    hipLaunchKernelGGL(fi_segentry_kernel, dim3((L.ngroups + 63) / 64), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(fi_resolve2_kernel, dim3((L.ng2 + 63) / 64), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(fi_segentry_kernel, dim3((L.ng1 + 63) / 64), dim3(64), 0, stream, a);
     hipLaunchKernelGGL(fi_emit_kernel, dim3(L.nseg), dim3(64), 0, stream, a);
     hipLaunchKernelGGL(fi_emit_slow_kernel, dim3(L.nseg < 256 ? L.nseg : 256), dim3(FI_BLOCK), lds, stream, a);
     hipLaunchKernelGGL(fi_finish_kernel, dim3(1), dim3(64), 0, stream, a);
