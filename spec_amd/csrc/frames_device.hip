@@ -35,7 +35,7 @@ constexpr uint32_t FI_SEG = 32768, FI_W = 2048, FI_STEPCAP = 4096;
 constexpr uint32_t FI_G1 = 16, FI_G2 = 16; // segments per group, groups per super-group
 constexpr uint32_t FI_BLOCK = 1024; // threads of the segment / group kernels (a constant: blockDim
                                     // is a load from the dispatch packet)
-constexpr uint32_t FI_SUB = 4096, FI_NSUB = FI_SEG / FI_SUB, FI_WS = 1024;
+constexpr uint32_t FI_SUB = 4096, FI_NSUB = FI_SEG / FI_SUB, FI_WS = 512;
 constexpr uint32_t FI_LDS_T = FI_SEG + 16, FI_LDS = FI_LDS_T + (FI_NSUB - 1) * FI_WS * 4;
 // a segment table entry: exit x (< W) | frames << 16; FI_TERM | position | frames << 16; FI_OVF
 constexpr uint32_t FI_CNT_SHIFT = 16, FI_CNT_MASK = 0x1fffu, FI_POS_MASK = 0x7fffu;
@@ -67,6 +67,11 @@ struct FiArgs {
     uint32_t *live;            // [nseg * FI_LIVE * FI_LREC]
     uint32_t *work;            // [1 + nseg] count, then segments the emit must rebuild
 };
+
+// A workgroup barrier for LDS data only: __syncthreads also waits for every global load and
+// store in flight (vmcnt), which would stall on the next segment's prefetch and on this
+// segment's table stores.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // the big-endian u32 at byte o of the staged segment: two dword reads and a funnel shift
 __device__ __forceinline__ uint32_t be32_lds(const uint8_t *l, uint32_t o) {
@@ -111,44 +116,56 @@ __device__ __forceinline__ void stage_segment(const FiArgs &a, uint64_t s0, uint
     __syncthreads();
 }
 
-// The walks of a staged segment, job m of this lane (m = 0 .. NSUB-2: entry threadIdx.x of the
-// window of sub-segment m + 1, into T; then, with `entries`, W / BLOCK segment entries
-// (m - NSUB + 1) * BLOCK + threadIdx.x of sub-segment 0, into C right after T): the chain until
-// it stands on a position at or past its stop (the next sub-segment) that lies in the first WS
-// bytes of a sub-segment, or past the segment end (segend = s1 - s0, lenrel = len - s0).  A jump
-// W or more past the segment end, or more than STEPCAP frames, is overflow (the serial
-// fallback).  One frame step per iteration with 32-bit arithmetic (the size saturates; the exact
-// TERM test runs once per walk): a lane that finishes a walk starts its next at once, so a wave
-// runs for its busiest lane's steps, not for the sum over jobs of the longest walk.  Then a
-// barrier.
+// The walks of a staged segment.  Jobs j < NT = (NSUB-1) * WS: entry j % WS of the window of
+// sub-segment 1 + j / WS, into T[j]; then, with `entries`, the W segment entries e = j - NT of
+// sub-segment 0, into C[e] right after T.  A walk follows the chain until it stands on a
+// position at or past its stop (the next sub-segment) that lies in the first WS bytes of a
+// sub-segment, or past the segment end (segend = s1 - s0, lenrel = len - s0).  A jump W or more
+// past the segment end, or more than STEPCAP frames, is overflow (the serial fallback).
+// Each wave owns a contiguous share of the jobs and hands the next ones to whichever lanes just
+// finished (ballot + mbcnt), one frame step per iteration with 32-bit arithmetic (the size
+// saturates; the exact TERM test only decides a finished walk's code): the wave runs for about
+// its share's total steps / 64 plus one long walk, not for its lanes' longest job sequence.
+// Then a barrier.
 __device__ __forceinline__ void fi_tables(const FiArgs &a, uint64_t s0, uint32_t segend, uint8_t *lds,
                                           bool entries) {
-    constexpr uint32_t NT = FI_NSUB - 1, NE = FI_W / FI_BLOCK;
-    static_assert(FI_LDS == FI_LDS_T + NT * FI_WS * 4 && FI_WS == FI_BLOCK, "T: a window entry per lane; C follows");
-    static_assert(FI_SUB - FI_WS == 0xc00u, "window test by mask");
-    uint32_t *out = (uint32_t *)(lds + FI_LDS_T) + threadIdx.x;
+    constexpr uint32_t NT = (FI_NSUB - 1) * FI_WS, NWAVES = FI_BLOCK / 64;
+    static_assert(FI_LDS == FI_LDS_T + NT * 4, "C follows T");
+    static_assert((FI_SUB - FI_WS) == 0xe00u, "window test by mask");
+    uint32_t *out = (uint32_t *)(lds + FI_LDS_T);
     const uint64_t lenrel = a.len - s0;
     const uint32_t far = (uint32_t)((uint64_t)segend + FI_W < lenrel + 1 ? (uint64_t)segend + FI_W : lenrel + 1);
-    const uint32_t njobs = entries ? NT + NE : NT;
-    uint32_t m = 0, p = FI_SUB + threadIdx.x, stop = 2 * FI_SUB, steps = 0;
-    while (true) { // flat: selects and one predicated store (a branch would nest a loop per job)
+    const uint32_t njobs = entries ? NT + FI_W : NT, share = (njobs + NWAVES - 1) / NWAVES;
+    const uint32_t lane = threadIdx.x & 63, j0 = (threadIdx.x >> 6) * share;
+    const uint32_t j1 = j0 + share < njobs ? j0 + share : njobs;
+    auto start = [](uint32_t j, uint32_t &p, uint32_t &stop) {
+        const bool win = j < NT;
+        const uint32_t sub = 1 + j / FI_WS;
+        p = win ? sub * FI_SUB + j % FI_WS : j - NT;
+        stop = win ? (sub + 1) * FI_SUB : FI_SUB;
+    };
+    uint32_t j = j0 + lane, next = j0 + 64, p, stop, steps = 0;
+    start(j, p, stop);
+    bool active = j < j1;
+    while (__ballot(active)) {
         const uint32_t v = be32_lds(lds, p & (FI_SEG - 1)); // in the staged bytes
         const uint32_t q = p + 4 + (v < 0x7fffffffu ? v : 0x7fffffffu);
-        const bool exit = (p >= segend) | ((p >= stop) & ((p & 0xc00u) == 0));
-        const bool fin = exit | (q >= far) | (steps >= FI_STEPCAP);
+        const bool exit = (p >= segend) | ((p >= stop) & ((p & 0xe00u) == 0));
+        const bool fin = active & (exit | (q >= far) | (steps >= FI_STEPCAP));
         const bool term = (uint64_t)p + 4 + v > lenrel;
-        if (fin) out[m * FI_BLOCK] = exit ? (steps << 17) | p : term ? FI_T_TERM | (steps << 17) | p : FI_T_OVF;
-        uint32_t mn = m + (fin ? 1u : 0u);
-        if (mn >= njobs) break;
-        asm volatile("" : "+v"(mn)); // opaque: no per-job copies of the loop
-        const uint32_t pn = mn < NT ? (mn + 1) * FI_SUB + threadIdx.x : (mn - NT) * FI_BLOCK + threadIdx.x;
-        const uint32_t stopn = mn < NT ? (mn + 2) * FI_SUB : FI_SUB;
+        if (fin) out[j] = exit ? (steps << 17) | p : term ? FI_T_TERM | (steps << 17) | p : FI_T_OVF;
+        const uint64_t fm = __ballot(fin);
+        const uint32_t jn = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+        next += (uint32_t)__popcll(fm);
+        uint32_t pn, stopn;
+        start(jn, pn, stopn);
+        j = fin ? jn : j;
+        active = fin ? jn < j1 : active;
         p = fin ? pn : q;
         stop = fin ? stopn : stop;
         steps = fin ? 0 : steps + 1;
-        m = mn;
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 // a segment entry's result from its sub-segment 0 walk c: exit offset into the next segment
@@ -195,7 +212,7 @@ __global__ __launch_bounds__(FI_BLOCK) void fi_seg_kernel(FiArgs a) {
             dst[threadIdx.x] = v0;
             dst[threadIdx.x + FI_BLOCK] = v1;
             if (threadIdx.x == 0) dst[FI_SEG / 16] = halo;
-            __syncthreads();
+            lds_barrier();
         } else {
             stage_segment(a, s0, lds);
         }
@@ -228,7 +245,7 @@ __global__ __launch_bounds__(FI_BLOCK) void fi_seg_kernel(FiArgs a) {
             if (rec) rec[0] = code < FI_W ? e : ~0u;
             a.exitT[(uint64_t)k * FI_W + e] = code == FI_OVF ? FI_OVF : code | (steps << FI_CNT_SHIFT);
         }
-        __syncthreads(); // nlive final; the LDS free for the next segment
+        lds_barrier(); // nlive final; the LDS free for the next segment
         if (threadIdx.x == 0) a.live_n[k] = nlive;
     }
 }

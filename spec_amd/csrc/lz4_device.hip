@@ -3,16 +3,20 @@
 //
 // mpx wraps the connection in one LZ4 frame of independent 256 KiB blocks (mpx/conn_writer.go:
 // 42-56, pierrec/lz4/v4).  The host walks the frame's block headers (spec_lz4_frame_blocks:
-// one u32 per block) and hands the block table over; here ONE WAVE DECODES ONE BLOCK:
-//   * the sequence chain (token, literal length, offset, match length) is serial, so it is
-//     parsed by the scalar unit: the compressed bytes sit in a 768-byte register window (3
-//     VGPRs x 64 lanes, refilled 256 bytes at a time) read with v_readlane at uniform indices;
-//   * literal and match bytes are moved by all 64 lanes (64 bytes per instruction): literals
-//     by ds_bpermute out of the window, matches out of a 64 KiB LDS ring holding the block's
-//     last 64 KiB of output (every LZ4 offset is < 64 KiB) — a match whose source would be
-//     overwritten in the ring during the copy (offset + length > 64 KiB) reads the output back
-//     from HBM instead, with L1-bypassing loads after its own stores have drained;
-//   * output bytes go to the block's slot in HBM.
+// one u32 per block) and hands the block table over; here ONE WAVE DECODES ONE BLOCK, in
+// batches of up to 64 sequences:
+//   * PARSE (serial, uniform): the compressed bytes stream through a 16 KiB LDS ring (2 KiB
+//     chunks loaded 4 KiB ahead); a sequence's token and, for literal runs up to 5 bytes, its
+//     offset come from one 8-byte LDS read.  Each sequence is checked exactly as the reference
+//     decoder checks it and recorded in the registers of lane k (k-th sequence of the batch):
+//     literal source, literal length, output position, offset, match length;
+//   * EXECUTE (the batch's output, at most 8 KiB, is assembled in an LDS window): every lane
+//     copies its own short literal, long literals go wave-wide; matches read out[mop - off +
+//     (i mod off)] — always bytes before mop — so a match whose source ends before the batch
+//     (far) is read back from HBM by its own lane, all far matches at once; matches whose source
+//     lies in the window (near; the few that straddle the window start read that part from HBM)
+//     run in order, 64 bytes per instruction; then the window is stored to the block's slot;
+//   * a sequence longer than 4 KiB (literal + match) runs alone, HBM to HBM.
 // Errors are those of pierrec's decodeBlock (oracle/lz4.c so_lz4_decompress_block): the block's
 // status is 1 and its size all-ones.  spec_lz4_pack then gathers the slots into one contiguous
 // stream (exclusive scan of the sizes + a copy).
@@ -24,7 +28,8 @@ namespace spec {
 
 namespace {
 
-constexpr uint32_t RING = 65536, RMASK = RING - 1;
+constexpr uint32_t CR = 16384, CRW = CR / 4, CHUNK = 2048, LOOK = 4096; // compressed ring
+constexpr uint32_t WIN = 8192, SOLO = 4096, BATCH = 64;                 // output window
 
 struct Lz4Args {
     const uint8_t *src;
@@ -46,56 +51,25 @@ __device__ __forceinline__ uint32_t src_dword(const Lz4Args &a, __amdgpu_buffer_
     return w;
 }
 
-struct Window {
-    uint32_t w0, w1, w2; // bytes [wb, wb + 256), [wb + 256, +512), [wb + 512, +768) of the block
-    uint32_t wb;
-};
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-__device__ __forceinline__ uint32_t win_byte(const Window &W, uint32_t p) { // p uniform, wb <= p < wb + 768
-    const uint32_t rel = p - W.wb, l = (rel >> 2) & 63, sh = 8 * (rel & 3);
-    const uint32_t sel = rel >> 8;
-    const uint32_t w = sel == 0 ? __builtin_amdgcn_readlane(W.w0, l)
-                                : (sel == 1 ? __builtin_amdgcn_readlane(W.w1, l) : __builtin_amdgcn_readlane(W.w2, l));
-    return (w >> sh) & 0xff;
+// a byte of the block's output already stored by this wave (L2: sc1 bypasses the L1)
+__device__ __forceinline__ uint8_t out_byte(__amdgpu_buffer_rsrc_t dr, uint32_t o) {
+    return (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(dr, o, 0, 16);
 }
 
-__device__ __forceinline__ void win_advance(const Lz4Args &a, __amdgpu_buffer_rsrc_t r, uint64_t base, Window &W,
-                                            int lane) {
-    W.w0 = W.w1;
-    W.w1 = W.w2;
-    W.wb += 256;
-    W.w2 = src_dword(a, r, base + W.wb + 512 + 4 * (uint32_t)lane);
-}
-
-// ring[from, to) -> dst[from, to), 16 bytes per lane (from 16-aligned; up to 15 bytes past `to`
-// may be written: the slot is a multiple of 16 and bytes past the block's size are never read)
-__device__ __forceinline__ void ring_flush(const uint8_t *ring, uint8_t *dst, uint32_t from, uint32_t to, int lane) {
-    for (uint32_t p = from + 16 * (uint32_t)lane; p < to; p += 1024)
-        *(uint4 *)(dst + p) = *(const uint4 *)(ring + (p & RMASK));
-}
-
-__device__ __forceinline__ void wave_fence() {
+__device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Output goes to the LDS ring only; the ring is flushed to the slot 4 KiB at a time with
-// 16-byte stores (kept at most ~8 KiB behind), so the sequence loop issues no global stores —
-// on gfx9 stores count in vmcnt, and a store in flight would make every window read wait.
-__device__ __forceinline__ void ring_keep_up(const uint8_t *ring, uint8_t *dst, uint32_t upto, uint32_t &flushed,
-                                             int lane) {
-    if (upto - flushed >= 8192) {
-        wave_fence();
-        ring_flush(ring, dst, flushed, flushed + 4096, lane);
-        flushed += 4096;
-    }
-}
-
 __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t ring[];
+    __shared__ __attribute__((aligned(16))) uint32_t ringw[CRW];
+    __shared__ __attribute__((aligned(16))) uint8_t win[WIN + 16];
+    const uint8_t *ring = (const uint8_t *)ringw;
     const uint64_t b = blockIdx.x;
-    const int lane = threadIdx.x;
+    const uint32_t lane = threadIdx.x;
     const spec_lz4_block blk = a.blocks[b];
     const uint64_t base = blk.src_off;
     const uint32_t n = blk.src_len;
@@ -103,6 +77,7 @@ __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
     const uint32_t cap = (uint32_t)a.slot;
     __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
         (void *)a.src, (short)0, (int)(uint32_t)(a.src_len > 0xffffffffull ? 0xffffffffull : a.src_len), 0x00020000);
+    __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc((void *)dst, (short)0, (int)cap, 0x00020000);
     bool err = base + n > a.src_len;
     if (!err && blk.stored) { // a block the writer stored uncompressed
         err = n > cap;
@@ -115,107 +90,236 @@ __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
         return;
     }
     err |= n == 0;
-    Window W;
-    W.wb = 0;
-    W.w0 = src_dword(a, r, base + 4 * (uint32_t)lane);
-    W.w1 = src_dword(a, r, base + 256 + 4 * (uint32_t)lane);
-    W.w2 = src_dword(a, r, base + 512 + 4 * (uint32_t)lane);
-    uint32_t ip = 0, op = 0, flushed = 0;
-    while (!err && ip < n) {
-        while (ip - W.wb >= 256) win_advance(a, r, base, W, lane);
-        const uint32_t token = win_byte(W, ip++);
+
+    // ---- ring: compressed bytes [max(vlo, filled - CR), filled) are in ring[x mod CR]; a chunk
+    // is only loaded while it leaves the batch's literals (>= bs) in place
+    uint32_t filled = 0, vlo = 0, bs = 0;
+    auto load_chunk = [&]() __attribute__((always_inline)) {
+        uint32_t v[CHUNK / 256];
+#pragma unroll
+        for (uint32_t j = 0; j < CHUNK / 256; j++) v[j] = src_dword(a, r, base + filled + 4 * (lane + 64 * j));
+#pragma unroll
+        for (uint32_t j = 0; j < CHUNK / 256; j++) ringw[((filled >> 2) + lane + 64 * j) & (CRW - 1)] = v[j];
+        filled += CHUNK;
+    };
+    // 8 bytes at x (uniform; must be loaded)
+    auto rd8 = [&](uint32_t x) __attribute__((always_inline)) -> uint64_t {
+        const uint32_t d = x >> 2, sh = 8 * (x & 3);
+        const uint32_t w0 = ringw[d & (CRW - 1)], w1 = ringw[(d + 1) & (CRW - 1)], w2 = ringw[(d + 2) & (CRW - 1)];
+        const uint64_t lo = (((uint64_t)w1 << 32) | w0) >> sh;
+        const uint64_t v = sh ? lo | ((uint64_t)w2 << (64 - sh)) : lo;
+        return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+    };
+
+    // ---- the batch: lane k holds sequence k
+    uint32_t nb = 0, first_op = 0, wb = 0;
+    uint32_t r_lit = 0, r_ll = 0, r_op = 0, r_off = 0, r_ml = 0;
+    bool r_ring = false;
+
+    auto flush = [&]() __attribute__((always_inline)) {
+        if (nb == 0) return;
+        const bool mine = lane < nb;
+        const uint32_t mop = r_op + r_ll, msrc = mop - r_off, mspan = r_off < r_ml ? r_off : r_ml;
+        wave_lds_fence();
+        // (1) literals: each lane its first 16 ring bytes; the rest (and HBM literals) wave-wide
+#pragma unroll
+        for (uint32_t t = 0; t < 16; t++)
+            if (mine && r_ring && t < r_ll) win[r_op + t - wb] = ring[(r_lit + t) & (CR - 1)];
+        uint64_t longlit = __ballot(mine && (r_ll > 16 || (!r_ring && r_ll > 0)));
+        while (longlit) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(longlit);
+            longlit &= longlit - 1;
+            const uint32_t lit = uni(__builtin_amdgcn_readlane(r_lit, k)), ll = uni(__builtin_amdgcn_readlane(r_ll, k));
+            const uint32_t o = uni(__builtin_amdgcn_readlane(r_op, k));
+            const bool inring = __builtin_amdgcn_readlane((uint32_t)r_ring, k) != 0;
+            for (uint32_t c = inring ? 16 : 0; c < ll; c += 64) {
+                const uint32_t i = c + lane;
+                if (i < ll)
+                    win[o + i - wb] = inring ? ring[(lit + i) & (CR - 1)]
+                                             : (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, (uint32_t)(base + lit + i), 0, 0);
+            }
+        }
+        // (2) far matches (source before the window): each lane reads its own from HBM
+        const bool far = mine && r_ml > 0 && msrc + mspan <= first_op;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // earlier batches' stores have landed
+        uint32_t farmax = 0;
+        {
+            uint32_t m = far ? r_ml : 0;
+            for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
+            farmax = uni(m);
+        }
+        for (uint32_t c = 0; c < farmax; c += 16) {
+            uint8_t v[16];
+#pragma unroll
+            for (uint32_t t = 0; t < 16; t++) {
+                const uint32_t i = c + t;
+                v[t] = (far && i < r_ml) ? out_byte(dr, msrc + (r_off >= r_ml ? i : i % r_off)) : 0;
+            }
+#pragma unroll
+            for (uint32_t t = 0; t < 16; t++)
+                if (far && c + t < r_ml) win[mop + c + t - wb] = v[t];
+        }
+        // (3) near (and straddling) matches, in order, 64 bytes per instruction
+        uint64_t near = __ballot(mine && r_ml > 0 && !far);
+        while (near) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(near);
+            near &= near - 1;
+            const uint32_t o = uni(__builtin_amdgcn_readlane(mop, k)), off = uni(__builtin_amdgcn_readlane(r_off, k));
+            const uint32_t ml = uni(__builtin_amdgcn_readlane(r_ml, k));
+            wave_lds_fence();
+            for (uint32_t c = 0; c < ml; c += 64) {
+                const uint32_t i = c + lane;
+                const uint32_t sidx = o - off + (off >= ml ? i : i % off);
+                uint8_t v = 0;
+                if (i < ml) v = sidx >= first_op ? win[sidx - wb] : out_byte(dr, sidx);
+                __builtin_amdgcn_wave_barrier();
+                if (i < ml) win[o + i - wb] = v;
+            }
+        }
+        wave_lds_fence();
+        // (4) the window [first_op, end) to the slot: dwords where whole, bytes at the edges
+        const uint32_t end = uni(__builtin_amdgcn_readlane(r_op + r_ll + r_ml, nb - 1));
+        for (uint32_t u = first_op & ~3u; u < end; u += 256) {
+            const uint32_t ad = u + 4 * lane;
+            if (ad >= first_op && ad + 4 <= end) {
+                *(uint32_t *)(dst + ad) = *(const uint32_t *)(win + (ad - wb));
+            } else {
+                for (uint32_t t = 0; t < 4; t++)
+                    if (ad + t >= first_op && ad + t < end) dst[ad + t] = win[ad + t - wb];
+            }
+        }
+        nb = 0;
+    };
+
+    // make [x, x + 8) readable (or everything up to n); may execute the batch first when the
+    // ring cannot reach x without overwriting the batch's literals
+    auto need = [&](uint32_t x) __attribute__((always_inline)) {
+        if (x + 8 <= filled || filled >= n) return;
+        if (x + 8 + CHUNK > bs + CR) {
+            flush();
+            bs = x;
+        }
+        if (filled + CR < x || filled < (x & ~3u)) { // skip what nobody reads from the ring
+            filled = x & ~3u;
+            vlo = filled;
+        }
+        const uint32_t want = x + LOOK;
+        while (filled < want && filled < n && filled + CHUNK <= bs + CR) load_chunk();
+        wave_lds_fence();
+    };
+    // one byte of a length extension at ip
+    auto ext_byte = [&](uint32_t x) __attribute__((always_inline)) -> uint32_t {
+        need(x);
+        return (uint32_t)(rd8(x) & 0xff);
+    };
+
+    uint32_t ip = 0, op = 0;
+    need(0);
+    while (!err) {
+        if (ip >= n) break; // the last sequence ended exactly at the block end
+        need(ip);
+        const uint64_t w8 = rd8(ip);
+        const uint32_t token = (uint32_t)(w8 & 0xff);
+        ip++;
         uint32_t ll = token >> 4;
+        bool simple = true;
         if (ll == 15) {
+            simple = false;
             for (;;) {
                 if (ip >= n) {
                     err = true;
                     break;
                 }
-                while (ip - W.wb >= 256) win_advance(a, r, base, W, lane);
-                const uint32_t x = win_byte(W, ip++);
+                const uint32_t x = ext_byte(ip++);
                 ll += x;
                 if (x != 255) break;
             }
             if (err) break;
         }
-        if (ll) {
-            if (ll > n - ip || ll > cap - op) {
+        const uint32_t lit = ip;
+        if (ll > n - ip || ll > cap - op) {
+            err = true;
+            break;
+        }
+        ip += ll;
+        uint32_t ml = token & 15, off = 0;
+        const bool last = ip == n && ml == 0;
+        if (!last) {
+            if (ip + 2 > n) {
                 err = true;
                 break;
             }
-            for (uint32_t c = 0; c < ll; c += 64) {
-                ring_keep_up(ring, dst, op + c, flushed, lane);
-                while (ip + c - W.wb >= 256) win_advance(a, r, base, W, lane);
-                const uint32_t rel = ip + c - W.wb + (uint32_t)lane; // < 320
-                const uint32_t addr = ((rel >> 2) & 63) * 4;
-                const uint32_t v0 = __builtin_amdgcn_ds_bpermute(addr, W.w0);
-                const uint32_t v1 = __builtin_amdgcn_ds_bpermute(addr, W.w1);
-                const uint32_t v = (rel >> 8) ? v1 : v0;
-                const uint8_t byte = (uint8_t)(v >> (8 * (rel & 3)));
-                if (c + lane < ll) ring[(op + c + lane) & RMASK] = byte;
+            if (simple && ll <= 5) {
+                off = (uint32_t)(w8 >> (8 * (1 + ll))) & 0xffff;
+            } else {
+                need(ip);
+                off = (uint32_t)(rd8(ip) & 0xffff);
             }
-            ip += ll;
-            op += ll;
-        }
-        uint32_t ml = token & 15;
-        if (ip == n && ml == 0) break;
-        if (ip + 2 > n) {
-            err = true;
-            break;
-        }
-        while (ip - W.wb >= 256) win_advance(a, r, base, W, lane);
-        const uint32_t off = win_byte(W, ip) | (win_byte(W, ip + 1) << 8);
-        ip += 2;
-        if (off == 0) {
-            err = true;
-            break;
-        }
-        ml += 4;
-        if (ml == 19) {
-            for (;;) {
-                if (ip >= n) {
-                    err = true;
-                    break;
+            ip += 2;
+            if (off == 0) {
+                err = true;
+                break;
+            }
+            ml += 4;
+            if (ml == 19) {
+                for (;;) {
+                    if (ip >= n) {
+                        err = true;
+                        break;
+                    }
+                    const uint32_t x = ext_byte(ip++);
+                    ml += x;
+                    if (x != 255) break;
                 }
-                while (ip - W.wb >= 256) win_advance(a, r, base, W, lane);
-                const uint32_t x = win_byte(W, ip++);
-                ml += x;
-                if (x != 255) break;
+                if (err) break;
             }
-            if (err) break;
+            if (off > op + ll || ml > cap - op - ll) {
+                err = true;
+                break;
+            }
+        } else {
+            ml = 0;
         }
-        if (off > op || ml > cap - op) {
-            err = true;
-            break;
-        }
-        wave_fence();
-        const bool from_ring = off + ml <= RING;
-        __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc((void *)dst, (short)0, (int)cap, 0x00020000);
-        if (!from_ring) { // the source is read back from the slot: everything before op stored first
-            ring_flush(ring, dst, flushed, op, lane);
-            flushed = op & ~15u;
+        const uint32_t total = ll + ml;
+        if (total > SOLO) { // alone, HBM to HBM
+            flush();
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        for (uint32_t c = 0; c < ml; c += 64) {
-            ring_keep_up(ring, dst, op + c, flushed, lane);
-            const uint32_t i = c + lane;
-            // out[op + i] = out[op - off + (i mod off)]: the source is always output before op
-            const uint32_t s = op - off + (off >= ml ? i : i % off);
-            uint8_t byte = 0;
-            if (i < ml) {
-                byte = from_ring ? ring[s & RMASK]
-                                 : (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(dr, s, 0, 16); // sc1: L2, not L1
+            for (uint32_t c = 0; c < ll; c += 64)
+                if (c + lane < ll)
+                    dst[op + c + lane] = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, (uint32_t)(base + lit + c + lane), 0, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint32_t mop = op + ll;
+            for (uint32_t c = 0; c < ml; c += 64) {
+                const uint32_t i = c + lane;
+                if (i < ml) dst[mop + i] = out_byte(dr, mop - off + (off >= ml ? i : i % off));
             }
-            __builtin_amdgcn_wave_barrier();
-            if (i < ml) ring[(op + i) & RMASK] = byte;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            op += total;
+            bs = ip;
+        } else {
+            if (nb == BATCH || (nb > 0 && op + total - wb > WIN)) { // the batch is full: run it
+                flush();
+                bs = lit;
+            }
+            if (nb == 0) {
+                first_op = op;
+                wb = op & ~15u;
+            }
+            const bool inring = lit >= vlo && lit + CR >= filled && lit + ll <= filled && lit >= bs;
+            if (lane == nb) {
+                r_lit = lit;
+                r_ll = ll;
+                r_op = op;
+                r_off = off;
+                r_ml = ml;
+                r_ring = inring;
+            }
+            nb++;
+            op += total;
         }
-        wave_fence();
-        op += ml;
+        if (last) break;
     }
-    if (!err) {
-        wave_fence();
-        ring_flush(ring, dst, flushed, op, lane);
-    }
+    if (!err) flush();
     if (lane == 0) {
         a.sizes[b] = err ? 0xffffffffu : op;
         a.status[b] = err ? 1 : 0;
@@ -293,7 +397,7 @@ int launch_lz4_decompress(const uint8_t *src, uint64_t src_len, const spec_lz4_b
                           uint8_t *slots, uint64_t slot, uint32_t *sizes, uint8_t *status, hipStream_t stream) {
     if (nblocks == 0) return 0;
     Lz4Args a = {src, src_len, blocks, nblocks, slots, slot, sizes, status};
-    hipLaunchKernelGGL(lz4_block_kernel, dim3((unsigned)nblocks), dim3(64), RING, stream, a);
+    hipLaunchKernelGGL(lz4_block_kernel, dim3((unsigned)nblocks), dim3(64), 0, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

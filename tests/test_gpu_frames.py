@@ -82,10 +82,10 @@ def test_segment_boundaries(dev):
 def test_sub_segment_windows(dev):
     """The 4 KiB sub-segment tables inside a segment: frames 1-2 KiB long (heads past a
     sub-segment's 1024-byte window, so the walk runs on into the next sub-segment), 4 KiB frames
-    landing exactly on sub-segment starts, heads at window offsets 1023 / 1024, and frames so
+    landing exactly on sub-segment starts, heads at window offsets WS - 1 / WS, and frames so
     small that a segment has more live entries than the emit's records."""
     rng = np.random.default_rng(11)
-    sub, ws = 4096, 1024
+    sub, ws = 4096, 512  # frames_device.hip FI_SUB, FI_WS
     cases = {
         "1-2 KiB": list(rng.integers(1000, 2000, 600)),
         "3-4 KiB": list(rng.integers(3000, 4000, 300)),

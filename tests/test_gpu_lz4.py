@@ -1,7 +1,7 @@
 """GPU LZ4 decompression (spec_lz4_decompress + spec_lz4_pack) against the oracle (oracle/lz4.c):
 every block of oracle-written frames decompressed on the device equals the content; corrupt
-blocks get the oracle's verdict; long matches (offset + length > the 64 KiB LDS ring) take the
-HBM read-back path; and the whole compressed receive path (LZ4 frame -> blocks -> device
+blocks get the oracle's verdict; short and long literals, near / far / overlapping matches and
+sequences too long for the batch window are all exercised; and the whole compressed receive path (LZ4 frame -> blocks -> device
 decompress -> device frame index -> in-place decode) equals the oracle decode."""
 from __future__ import annotations
 
@@ -24,7 +24,18 @@ def gpu_content(dev, f):
     return out.cpu().numpy(), status.cpu().numpy()
 
 
-@pytest.mark.parametrize("kind", ["text", "random", "mixed", "zeros", "period3", "period200"])
+def _chunks(rng, n, lit, rep):
+    """random runs of `lit` bytes, each followed by `rep` bytes copied from earlier output"""
+    out = bytearray()
+    while len(out) < n:
+        out += rng.integers(0, 256, lit, dtype=np.uint8).tobytes()
+        src = int(rng.integers(0, max(1, len(out) - rep)))
+        out += out[src:src + rep]
+    return np.frombuffer(bytes(out[:n]), np.uint8)
+
+
+@pytest.mark.parametrize("kind", ["text", "random", "mixed", "zeros", "period3", "period200", "records", "chunks",
+                                  "longlit"])
 def test_frames_round_trip(dev, kind):
     rng = np.random.default_rng(hash(kind) % 1000)
     n = 700000
@@ -36,6 +47,11 @@ def test_frames_round_trip(dev, kind):
         "zeros": np.zeros(n, np.uint8),          # one match per block far longer than the ring
         "period3": np.frombuffer((b"abc" * n)[:n], np.uint8),
         "period200": np.tile(rng.integers(0, 256, 200, dtype=np.uint8), n // 200 + 1)[:n],
+        # many short sequences, near and far matches, batch windows filling up
+        "records": np.tile(np.frombuffer(b"".join(bytes([7, i % 13, 0, 0]) + rng.integers(0, 256, 9, dtype=np.uint8)
+                                                  .tobytes() for i in range(64)), np.uint8), n // 832 + 1)[:n],
+        "chunks": _chunks(rng, n, 300, 700),  # literals > 16 bytes, matches reaching back up to a block
+        "longlit": _chunks(rng, n, 9000, 3000),  # literals longer than the ring look-ahead: alone, HBM to HBM
     }[kind]
     for flushes in ([n], [1, 4000, 300001, n]):
         f = O.lz4_frame_write(data, flushes, 256 << 10)
