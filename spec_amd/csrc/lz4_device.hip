@@ -114,30 +114,24 @@ __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
     // ---- the batch: lane k holds sequence k
     uint32_t nb = 0, first_op = 0, wb = 0;
     uint32_t r_lit = 0, r_ll = 0, r_op = 0, r_off = 0, r_ml = 0;
-    bool r_ring = false;
 
     auto flush = [&]() __attribute__((always_inline)) {
         if (nb == 0) return;
         const bool mine = lane < nb;
         const uint32_t mop = r_op + r_ll, msrc = mop - r_off, mspan = r_off < r_ml ? r_off : r_ml;
         wave_lds_fence();
-        // (1) literals: each lane its first 16 ring bytes; the rest (and HBM literals) wave-wide
+        // (1) literals (all in the ring): each lane its first 16 bytes, longer ones wave-wide
 #pragma unroll
         for (uint32_t t = 0; t < 16; t++)
-            if (mine && r_ring && t < r_ll) win[r_op + t - wb] = ring[(r_lit + t) & (CR - 1)];
-        uint64_t longlit = __ballot(mine && (r_ll > 16 || (!r_ring && r_ll > 0)));
+            if (mine && t < r_ll) win[r_op + t - wb] = ring[(r_lit + t) & (CR - 1)];
+        uint64_t longlit = __ballot(mine && r_ll > 16);
         while (longlit) {
             const uint32_t k = (uint32_t)__builtin_ctzll(longlit);
             longlit &= longlit - 1;
             const uint32_t lit = uni(__builtin_amdgcn_readlane(r_lit, k)), ll = uni(__builtin_amdgcn_readlane(r_ll, k));
             const uint32_t o = uni(__builtin_amdgcn_readlane(r_op, k));
-            const bool inring = __builtin_amdgcn_readlane((uint32_t)r_ring, k) != 0;
-            for (uint32_t c = inring ? 16 : 0; c < ll; c += 64) {
-                const uint32_t i = c + lane;
-                if (i < ll)
-                    win[o + i - wb] = inring ? ring[(lit + i) & (CR - 1)]
-                                             : (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, (uint32_t)(base + lit + i), 0, 0);
-            }
+            for (uint32_t c = 16; c < ll; c += 64)
+                if (c + lane < ll) win[o + c + lane - wb] = ring[(lit + c + lane) & (CR - 1)];
         }
         // (2) far matches (source before the window): each lane reads its own from HBM
         const bool far = mine && r_ml > 0 && msrc + mspan <= first_op;
@@ -191,135 +185,233 @@ __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
         nb = 0;
     };
 
-    // make [x, x + 8) readable (or everything up to n); may execute the batch first when the
-    // ring cannot reach x without overwriting the batch's literals
-    auto need = [&](uint32_t x) __attribute__((always_inline)) {
-        if (x + 8 <= filled || filled >= n) return;
-        if (x + 8 + CHUNK > bs + CR) {
-            flush();
-            bs = x;
-        }
-        if (filled + CR < x || filled < (x & ~3u)) { // skip what nobody reads from the ring
-            filled = x & ~3u;
-            vlo = filled;
-        }
-        const uint32_t want = x + LOOK;
-        while (filled < want && filled < n && filled + CHUNK <= bs + CR) load_chunk();
-        wave_lds_fence();
+    // 8 bytes at x: from the ring when loaded, else (the headers of sequences too long for the
+    // ring's look-ahead) straight from HBM
+    auto rd = [&](uint32_t x) __attribute__((always_inline)) -> uint64_t {
+        if (x + 8 <= filled && x + CR >= filled + 8 && x >= vlo) return rd8(x);
+        uint64_t v = 0;
+        for (uint32_t t = 0; t < 8; t++)
+            v |= (uint64_t)(x + t < n ? __builtin_amdgcn_raw_buffer_load_b8(r, (uint32_t)(base + x + t), 0, 0) : 0u) << (8 * t);
+        return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
     };
-    // one byte of a length extension at ip
-    auto ext_byte = [&](uint32_t x) __attribute__((always_inline)) -> uint32_t {
-        need(x);
-        return (uint32_t)(rd8(x) & 0xff);
+    // a length extension starting at x: adds bytes until one is not 255; false past the block
+    auto ext = [&](uint32_t &x, uint32_t &len) __attribute__((always_inline)) -> bool {
+        for (;;) {
+            if (x >= n) return false;
+            const uint32_t v = (uint32_t)(rd(x++) & 0xff);
+            len += v;
+            if (v != 255) return true;
+        }
     };
 
-    uint32_t ip = 0, op = 0;
-    need(0);
-    while (!err) {
-        if (ip >= n) break; // the last sequence ended exactly at the block end
-        need(ip);
-        const uint64_t w8 = rd8(ip);
-        const uint32_t token = (uint32_t)(w8 & 0xff);
-        ip++;
-        uint32_t ll = token >> 4;
-        bool simple = true;
-        if (ll == 15) {
-            simple = false;
-            for (;;) {
-                if (ip >= n) {
-                    err = true;
-                    break;
-                }
-                const uint32_t x = ext_byte(ip++);
-                ll += x;
-                if (x != 255) break;
-            }
-            if (err) break;
-        }
-        const uint32_t lit = ip;
-        if (ll > n - ip || ll > cap - op) {
+    uint32_t ip = 0, op = 0, guard = 0;
+    bool end = false;
+    // every pass of either loop below consumes input or runs a batch; the guard only turns a
+    // logic slip into a failed block instead of a wave that never finishes
+    const uint32_t guard_max = 4 * n + 4096;
+    while (!err && !end) {
+        if (++guard > guard_max) {
             err = true;
             break;
         }
-        ip += ll;
-        uint32_t ml = token & 15, off = 0;
-        const bool last = ip == n && ml == 0;
-        if (!last) {
-            if (ip + 2 > n) {
-                err = true;
-                break;
+        // ---- top up the ring to LOOK bytes past ip (the previous batch has run: bs = ip)
+        bs = ip;
+        if (filled < n && ip + LOOK > filled) {
+            if (filled + CR < ip || filled < (ip & ~3u)) { // skip what nobody reads from the ring
+                filled = ip & ~3u;
+                vlo = filled;
             }
-            if (simple && ll <= 5) {
-                off = (uint32_t)(w8 >> (8 * (1 + ll))) & 0xffff;
-            } else {
-                need(ip);
-                off = (uint32_t)(rd8(ip) & 0xffff);
-            }
-            ip += 2;
-            if (off == 0) {
-                err = true;
-                break;
-            }
-            ml += 4;
-            if (ml == 19) {
-                for (;;) {
-                    if (ip >= n) {
-                        err = true;
-                        break;
-                    }
-                    const uint32_t x = ext_byte(ip++);
-                    ml += x;
-                    if (x != 255) break;
-                }
-                if (err) break;
-            }
-            if (off > op + ll || ml > cap - op - ll) {
-                err = true;
-                break;
-            }
-        } else {
-            ml = 0;
+            while (filled < ip + LOOK && filled < n && filled + CHUNK <= bs + CR) load_chunk();
+            wave_lds_fence();
         }
-        const uint32_t total = ll + ml;
-        if (total > SOLO) { // alone, HBM to HBM
-            flush();
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            for (uint32_t c = 0; c < ll; c += 64)
-                if (c + lane < ll)
-                    dst[op + c + lane] = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, (uint32_t)(base + lit + c + lane), 0, 0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const uint32_t mop = op + ll;
-            for (uint32_t c = 0; c < ml; c += 64) {
-                const uint32_t i = c + lane;
-                if (i < ml) dst[mop + i] = out_byte(dr, mop - off + (off >= ml ? i : i % off));
+        const uint32_t lim = filled >= n ? 0xffffffffu : filled;
+        // ---- the chain: up to 64 sequences (lengths only; lane k records sequence k) whose
+        // bytes are all in the ring and whose output fits the window
+        first_op = op;
+        wb = op & ~15u;
+        uint32_t o = op, c_pos = 0, c_op = 0;
+        bool solo = false;
+        uint32_t s_lit = 0, s_ll = 0, s_ml = 0, s_q = 0;
+        // Speculative next-pointers: for each of the 256 positions x of a window, as if a token
+        // sat at x, (next token - x) | (literal + match length) << 16 — or ~0 when that
+        // sequence needs the careful path (a length extension of 255s, bytes past the ring or
+        // the block, an error).  The chain then costs one readlane per sequence.
+        auto spec_next = [&](uint32_t x) __attribute__((always_inline)) -> uint32_t {
+            if (x + 4 > lim || x >= n) return ~0u;
+            const uint32_t t = ring[x & (CR - 1)], b1 = ring[(x + 1) & (CR - 1)];
+            uint32_t ll = t >> 4, lit = x + 1;
+            if (ll == 15) {
+                if (b1 == 255) return ~0u;
+                ll += b1;
+                lit++;
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            op += total;
-            bs = ip;
-        } else {
-            if (nb == BATCH || (nb > 0 && op + total - wb > WIN)) { // the batch is full: run it
-                flush();
-                bs = lit;
+            if (lit > n || ll > n - lit) return ~0u;
+            const uint32_t q = lit + ll, mlnib = t & 15;
+            if (q == n && mlnib == 0) return (n - x) | (ll << 16);
+            if (q + 2 > n || q + 3 > lim) return ~0u;
+            uint32_t ml = mlnib + 4, nx = q + 2;
+            if (mlnib == 15) {
+                if (nx >= n) return ~0u;
+                const uint32_t b2 = ring[nx & (CR - 1)];
+                if (b2 == 255) return ~0u;
+                ml += b2;
+                nx++;
             }
-            if (nb == 0) {
-                first_op = op;
-                wb = op & ~15u;
+            if (nx + 8 > lim) return ~0u;
+            return (nx - x) | ((ll + ml) << 16);
+        };
+        uint32_t swb = 0, sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0;
+        bool sval = false; // the window [swb, swb + 256) is computed
+        while (nb < BATCH) {
+            if (ip >= n) { // the last sequence ended exactly at the block end
+                end = true;
+                break;
             }
-            const bool inring = lit >= vlo && lit + CR >= filled && lit + ll <= filled && lit >= bs;
+            if (ip + 8 > lim || ++guard > guard_max) break;
+            if (!sval || ip - swb >= 256) {
+                sval = true;
+                swb = ip;
+                sp0 = spec_next(swb + lane);
+                sp1 = spec_next(swb + 64 + lane);
+                sp2 = spec_next(swb + 128 + lane);
+                sp3 = spec_next(swb + 192 + lane);
+            }
+            {
+                const uint32_t rel = ip - swb, l = rel & 63, kq = rel >> 6;
+                const uint32_t v = uni(kq == 0   ? __builtin_amdgcn_readlane(sp0, l)
+                                       : kq == 1 ? __builtin_amdgcn_readlane(sp1, l)
+                                       : kq == 2 ? __builtin_amdgcn_readlane(sp2, l)
+                                                 : __builtin_amdgcn_readlane(sp3, l));
+                if (v != ~0u && (v & 0xffff) != 0) {
+                    const uint32_t total = v >> 16;
+                    if (o + total - wb > WIN) break; // the batch is full: run it, top up
+                    if (lane == nb) {
+                        c_pos = ip;
+                        c_op = o;
+                    }
+                    nb++;
+                    o += total;
+                    ip += v & 0xffff;
+                    continue;
+                }
+            }
+            // ---- the careful path: this sequence parsed and checked serially
+            const uint32_t token = (uint32_t)(rd8(ip) & 0xff);
+            uint32_t ll = token >> 4, x = ip + 1;
+            if (ll == 15 && !ext(x, ll)) {
+                err = true;
+                break;
+            }
+            const uint32_t lit = x;
+            if (ll > n - lit || ll > cap - o) { // the reference: si + ll > n || di + ll > cap
+                err = true;
+                break;
+            }
+            const uint32_t q = lit + ll;
+            uint32_t ml = token & 15, nxt;
+            const bool last = q == n && ml == 0;
+            if (last) {
+                nxt = n;
+            } else {
+                if (q + 2 > n) {
+                    err = true;
+                    break;
+                }
+                ml += 4;
+                nxt = q + 2;
+                if (ml == 19 && !ext(nxt, ml)) {
+                    err = true;
+                    break;
+                }
+            }
+            const uint32_t total = ll + ml;
+            const bool fits = nxt + 8 <= lim || lim == 0xffffffffu;
+            if (total > SOLO || (!fits && nb == 0)) { // alone, after the batch
+                if (nb > 0) break;
+                solo = true;
+                s_lit = lit;
+                s_ll = ll;
+                s_ml = ml;
+                s_q = last ? ~0u : q;
+                ip = nxt;
+                end = last;
+                break;
+            }
+            if (!fits || o + total - wb > WIN) break; // the batch is full: run it, top up
             if (lane == nb) {
-                r_lit = lit;
-                r_ll = ll;
-                r_op = op;
-                r_off = off;
-                r_ml = ml;
-                r_ring = inring;
+                c_pos = ip;
+                c_op = o;
             }
             nb++;
-            op += total;
+            o += total;
+            ip = nxt;
         }
-        if (last) break;
+        if (err) break;
+        // ---- every lane parses its own sequence again (all its bytes are in the ring) and makes
+        // the reference's remaining checks
+        if (nb > 0) {
+            const bool mine = lane < nb;
+            uint32_t ll = 0, ml = 0, off = 0, lit = 0;
+            bool bad = false;
+            if (mine) {
+                const uint32_t t = ring[c_pos & (CR - 1)];
+                uint32_t x = c_pos + 1;
+                ll = t >> 4;
+                if (ll == 15)
+                    for (uint32_t v = 255, i = 0; v == 255 && i < 32; i++) { // <= SOLO: < 17 bytes
+                        v = ring[(x++) & (CR - 1)];
+                        ll += v;
+                    }
+                lit = x;
+                const uint32_t q = lit + ll, mlnib = t & 15;
+                if (!(q == n && mlnib == 0)) {
+                    off = (uint32_t)ring[q & (CR - 1)] | ((uint32_t)ring[(q + 1) & (CR - 1)] << 8);
+                    ml = mlnib + 4;
+                    if (mlnib == 15)
+                        for (uint32_t v = 255, y = q + 2, i = 0; v == 255 && i < 32; i++) {
+                            v = ring[(y++) & (CR - 1)];
+                            ml += v;
+                        }
+                    const uint32_t di = c_op + ll;
+                    bad = off == 0 || off > di || ml > cap - di;
+                }
+                bad |= ll > cap - c_op;
+            }
+            if (__ballot(bad)) {
+                err = true;
+                break;
+            }
+            r_lit = lit;
+            r_ll = ll;
+            r_op = c_op;
+            r_off = off;
+            r_ml = ml;
+            op = o;
+            flush();
+        }
+        if (solo) { // HBM to HBM
+            uint32_t off = 0;
+            if (s_q != ~0u) {
+                off = (uint32_t)(rd(s_q) & 0xffff);
+                if (off == 0 || off > op + s_ll || s_ml > cap - op - s_ll) {
+                    err = true;
+                    break;
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint32_t mop = op + s_ll;
+            for (uint32_t c = 0; c < s_ll; c += 64)
+                if (c + lane < s_ll)
+                    dst[op + c + lane] = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, (uint32_t)(base + s_lit + c + lane), 0, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            for (uint32_t c = 0; c < s_ml; c += 64) {
+                const uint32_t i = c + lane;
+                if (i < s_ml) dst[mop + i] = out_byte(dr, mop - off + (off >= s_ml ? i : i % off));
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            op = mop + s_ml;
+        }
     }
-    if (!err) flush();
     if (lane == 0) {
         a.sizes[b] = err ? 0xffffffffu : op;
         a.status[b] = err ? 1 : 0;
