@@ -64,12 +64,22 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
+__global__ __launch_bounds__(128) void lz4_block_kernel(Lz4Args a) {
     __shared__ __attribute__((aligned(16))) uint32_t ringw[CRW];
     __shared__ __attribute__((aligned(16))) uint8_t win[WIN + 16];
+    // the batch queue: two slots of per-lane records (literal source, literal length, output
+    // position, offset, match length) and their batch's size / window / ring start
+    __shared__ uint32_t q_desc[2][5][64], q_meta[2][3];
+    __shared__ uint32_t q_posted, q_taken, q_done; // q_done: 1 parser finished, 2 failed
     const uint8_t *ring = (const uint8_t *)ringw;
     const uint64_t b = blockIdx.x;
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) {
+        q_posted = 0;
+        q_taken = 0;
+        q_done = 0;
+    }
+    __syncthreads();
     const spec_lz4_block blk = a.blocks[b];
     const uint64_t base = blk.src_off;
     const uint32_t n = blk.src_len;
@@ -80,6 +90,7 @@ __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
     __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc((void *)dst, (short)0, (int)cap, 0x00020000);
     bool err = base + n > a.src_len;
     if (!err && blk.stored) { // a block the writer stored uncompressed
+        if (wave != 0) return;
         err = n > cap;
         if (!err)
             for (uint32_t i = lane; i < n; i += 64) dst[i] = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, (uint32_t)(base + i), 0, 0);
@@ -90,14 +101,110 @@ __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
         return;
     }
     err |= n == 0;
+    if (err && wave != 0) return;
+    if (wave == 1) { // ---- the copier: runs the parser's batches in order
+        uint32_t taken = 0;
+        for (;;) {
+            for (;;) {
+                if (__hip_atomic_load(&q_posted, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > taken) break;
+                const uint32_t d = __hip_atomic_load(&q_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (d == 2) return;
+                if (d == 1 && __hip_atomic_load(&q_posted, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= taken)
+                    return;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            const uint32_t slot = taken & 1;
+            const uint32_t nb = q_meta[slot][0], first_op = q_meta[slot][1], wb = q_meta[slot][2];
+            const uint32_t r_lit = q_desc[slot][0][lane], r_ll = q_desc[slot][1][lane], r_op = q_desc[slot][2][lane];
+            const uint32_t r_off = q_desc[slot][3][lane], r_ml = q_desc[slot][4][lane];
+            const bool mine = lane < nb;
+            const uint32_t mop = r_op + r_ll, msrc = mop - r_off, mspan = r_off < r_ml ? r_off : r_ml;
+            wave_lds_fence();
+            // (1) literals (all in the ring): each lane its first 16 bytes, longer ones wave-wide
+#pragma unroll
+            for (uint32_t t = 0; t < 16; t++)
+                if (mine && t < r_ll) win[r_op + t - wb] = ring[(r_lit + t) & (CR - 1)];
+            uint64_t longlit = __ballot(mine && r_ll > 16);
+            while (longlit) {
+                const uint32_t k = (uint32_t)__builtin_ctzll(longlit);
+                longlit &= longlit - 1;
+                const uint32_t lit = uni(__builtin_amdgcn_readlane(r_lit, k)), ll = uni(__builtin_amdgcn_readlane(r_ll, k));
+                const uint32_t o = uni(__builtin_amdgcn_readlane(r_op, k));
+                for (uint32_t c = 16; c < ll; c += 64)
+                    if (c + lane < ll) win[o + c + lane - wb] = ring[(lit + c + lane) & (CR - 1)];
+            }
+            // (2) far matches (source before the window): each lane reads its own from HBM
+            const bool far = mine && r_ml > 0 && msrc + mspan <= first_op;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // earlier batches' stores have landed
+            uint32_t farmax = 0;
+            {
+                uint32_t m = far ? r_ml : 0;
+                for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
+                farmax = uni(m);
+            }
+            for (uint32_t c = 0; c < farmax; c += 16) {
+                uint8_t v[16];
+#pragma unroll
+                for (uint32_t t = 0; t < 16; t++) {
+                    const uint32_t i = c + t;
+                    v[t] = (far && i < r_ml) ? out_byte(dr, msrc + (r_off >= r_ml ? i : i % r_off)) : 0;
+                }
+#pragma unroll
+                for (uint32_t t = 0; t < 16; t++)
+                    if (far && c + t < r_ml) win[mop + c + t - wb] = v[t];
+            }
+            // (3) near (and straddling) matches, in order, 64 bytes per instruction
+            uint64_t near = __ballot(mine && r_ml > 0 && !far);
+            while (near) {
+                const uint32_t k = (uint32_t)__builtin_ctzll(near);
+                near &= near - 1;
+                const uint32_t o = uni(__builtin_amdgcn_readlane(mop, k)), off = uni(__builtin_amdgcn_readlane(r_off, k));
+                const uint32_t ml = uni(__builtin_amdgcn_readlane(r_ml, k));
+                wave_lds_fence();
+                for (uint32_t c = 0; c < ml; c += 64) {
+                    const uint32_t i = c + lane;
+                    const uint32_t sidx = o - off + (off >= ml ? i : i % off);
+                    uint8_t v = 0;
+                    if (i < ml) v = sidx >= first_op ? win[sidx - wb] : out_byte(dr, sidx);
+                    __builtin_amdgcn_wave_barrier();
+                    if (i < ml) win[o + i - wb] = v;
+                }
+            }
+            wave_lds_fence();
+            // (4) the window [first_op, end) to the slot: dwords where whole, bytes at the edges
+            const uint32_t end = uni(__builtin_amdgcn_readlane(r_op + r_ll + r_ml, nb - 1));
+            for (uint32_t u = first_op & ~3u; u < end; u += 256) {
+                const uint32_t ad = u + 4 * lane;
+                if (ad >= first_op && ad + 4 <= end) {
+                    *(uint32_t *)(dst + ad) = *(const uint32_t *)(win + (ad - wb));
+                } else {
+                    for (uint32_t t = 0; t < 4; t++)
+                        if (ad + t >= first_op && ad + t < end) dst[ad + t] = win[ad + t - wb];
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // landed: the parser's alone-sequences read them
+            taken++;
+            __hip_atomic_store(&q_taken, taken, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
 
     // ---- ring: compressed bytes [max(vlo, filled - CR), filled) are in ring[x mod CR]; a chunk
     // is only loaded while it leaves the batch's literals (>= bs) in place
     uint32_t filled = 0, vlo = 0, bs = 0;
+    // one chunk is kept in flight in registers (pf, for the bytes at pf_at) while the batch runs
+    uint32_t pf[CHUNK / 256], pf_at = ~0u;
+    auto fetch = [&](uint32_t at, uint32_t *v) __attribute__((always_inline)) {
+#pragma unroll
+        for (uint32_t j = 0; j < CHUNK / 256; j++) v[j] = src_dword(a, r, base + at + 4 * (lane + 64 * j));
+    };
     auto load_chunk = [&]() __attribute__((always_inline)) {
         uint32_t v[CHUNK / 256];
+        if (pf_at == filled) {
 #pragma unroll
-        for (uint32_t j = 0; j < CHUNK / 256; j++) v[j] = src_dword(a, r, base + filled + 4 * (lane + 64 * j));
+            for (uint32_t j = 0; j < CHUNK / 256; j++) v[j] = pf[j];
+        } else {
+            fetch(filled, v);
+        }
 #pragma unroll
         for (uint32_t j = 0; j < CHUNK / 256; j++) ringw[((filled >> 2) + lane + 64 * j) & (CRW - 1)] = v[j];
         filled += CHUNK;
@@ -111,78 +218,36 @@ __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
         return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
     };
 
-    // ---- the batch: lane k holds sequence k
-    uint32_t nb = 0, first_op = 0, wb = 0;
+    // ---- the parser: lane k holds sequence k of the batch being assembled
+    uint32_t nb = 0, first_op = 0, wb = 0, posted = 0, bs_of[2] = {0, 0};
     uint32_t r_lit = 0, r_ll = 0, r_op = 0, r_off = 0, r_ml = 0;
-
-    auto flush = [&]() __attribute__((always_inline)) {
-        if (nb == 0) return;
-        const bool mine = lane < nb;
-        const uint32_t mop = r_op + r_ll, msrc = mop - r_off, mspan = r_off < r_ml ? r_off : r_ml;
-        wave_lds_fence();
-        // (1) literals (all in the ring): each lane its first 16 bytes, longer ones wave-wide
-#pragma unroll
-        for (uint32_t t = 0; t < 16; t++)
-            if (mine && t < r_ll) win[r_op + t - wb] = ring[(r_lit + t) & (CR - 1)];
-        uint64_t longlit = __ballot(mine && r_ll > 16);
-        while (longlit) {
-            const uint32_t k = (uint32_t)__builtin_ctzll(longlit);
-            longlit &= longlit - 1;
-            const uint32_t lit = uni(__builtin_amdgcn_readlane(r_lit, k)), ll = uni(__builtin_amdgcn_readlane(r_ll, k));
-            const uint32_t o = uni(__builtin_amdgcn_readlane(r_op, k));
-            for (uint32_t c = 16; c < ll; c += 64)
-                if (c + lane < ll) win[o + c + lane - wb] = ring[(lit + c + lane) & (CR - 1)];
+    auto taken_now = [&]() __attribute__((always_inline)) -> uint32_t {
+        return uni(__hip_atomic_load(&q_taken, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+    };
+    // hand the batch to the copier (waiting for a free slot)
+    auto post = [&]() __attribute__((always_inline)) {
+        while (posted - taken_now() >= 2) __builtin_amdgcn_s_sleep(1);
+        const uint32_t slot = posted & 1;
+        q_desc[slot][0][lane] = r_lit;
+        q_desc[slot][1][lane] = r_ll;
+        q_desc[slot][2][lane] = r_op;
+        q_desc[slot][3][lane] = r_off;
+        q_desc[slot][4][lane] = r_ml;
+        if (lane == 0) {
+            q_meta[slot][0] = nb;
+            q_meta[slot][1] = first_op;
+            q_meta[slot][2] = wb;
         }
-        // (2) far matches (source before the window): each lane reads its own from HBM
-        const bool far = mine && r_ml > 0 && msrc + mspan <= first_op;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // earlier batches' stores have landed
-        uint32_t farmax = 0;
-        {
-            uint32_t m = far ? r_ml : 0;
-            for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
-            farmax = uni(m);
-        }
-        for (uint32_t c = 0; c < farmax; c += 16) {
-            uint8_t v[16];
-#pragma unroll
-            for (uint32_t t = 0; t < 16; t++) {
-                const uint32_t i = c + t;
-                v[t] = (far && i < r_ml) ? out_byte(dr, msrc + (r_off >= r_ml ? i : i % r_off)) : 0;
-            }
-#pragma unroll
-            for (uint32_t t = 0; t < 16; t++)
-                if (far && c + t < r_ml) win[mop + c + t - wb] = v[t];
-        }
-        // (3) near (and straddling) matches, in order, 64 bytes per instruction
-        uint64_t near = __ballot(mine && r_ml > 0 && !far);
-        while (near) {
-            const uint32_t k = (uint32_t)__builtin_ctzll(near);
-            near &= near - 1;
-            const uint32_t o = uni(__builtin_amdgcn_readlane(mop, k)), off = uni(__builtin_amdgcn_readlane(r_off, k));
-            const uint32_t ml = uni(__builtin_amdgcn_readlane(r_ml, k));
-            wave_lds_fence();
-            for (uint32_t c = 0; c < ml; c += 64) {
-                const uint32_t i = c + lane;
-                const uint32_t sidx = o - off + (off >= ml ? i : i % off);
-                uint8_t v = 0;
-                if (i < ml) v = sidx >= first_op ? win[sidx - wb] : out_byte(dr, sidx);
-                __builtin_amdgcn_wave_barrier();
-                if (i < ml) win[o + i - wb] = v;
-            }
-        }
-        wave_lds_fence();
-        // (4) the window [first_op, end) to the slot: dwords where whole, bytes at the edges
-        const uint32_t end = uni(__builtin_amdgcn_readlane(r_op + r_ll + r_ml, nb - 1));
-        for (uint32_t u = first_op & ~3u; u < end; u += 256) {
-            const uint32_t ad = u + 4 * lane;
-            if (ad >= first_op && ad + 4 <= end) {
-                *(uint32_t *)(dst + ad) = *(const uint32_t *)(win + (ad - wb));
-            } else {
-                for (uint32_t t = 0; t < 4; t++)
-                    if (ad + t >= first_op && ad + t < end) dst[ad + t] = win[ad + t - wb];
-            }
-        }
+        bs_of[slot] = bs;
+        posted++;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&q_posted, posted, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         nb = 0;
+    };
+    // the ring start that unconsumed batches still need (their literals)
+    auto oldest = [&](uint32_t cur) __attribute__((always_inline)) -> uint32_t {
+        const uint32_t t = taken_now();
+        return t < posted ? (bs_of[t & 1] < cur ? bs_of[t & 1] : cur) : cur;
     };
 
     // 8 bytes at x: from the ring when loaded, else (the headers of sequences too long for the
@@ -214,8 +279,8 @@ __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
             err = true;
             break;
         }
-        // ---- top up the ring to LOOK bytes past ip (the previous batch has run: bs = ip)
-        bs = ip;
+        // ---- top up the ring to LOOK bytes past ip, keeping what unconsumed batches need
+        bs = oldest(ip);
         if (filled < n && ip + LOOK > filled) {
             if (filled + CR < ip || filled < (ip & ~3u)) { // skip what nobody reads from the ring
                 filled = ip & ~3u;
@@ -224,7 +289,22 @@ __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
             while (filled < ip + LOOK && filled < n && filled + CHUNK <= bs + CR) load_chunk();
             wave_lds_fence();
         }
+        if (filled < n && pf_at != filled) { // the next chunk, in flight while this batch runs
+            fetch(filled, pf);
+            pf_at = filled;
+        }
+        if (filled < n && ip + 8 > filled) { // the ring is full of unconsumed batches: wait for the copier
+            const uint32_t t = taken_now();
+            if (t >= posted) { // nothing to wait for: cannot happen
+                err = true;
+                break;
+            }
+            while (taken_now() == t) __builtin_amdgcn_s_sleep(1);
+            guard--;
+            continue;
+        }
         const uint32_t lim = filled >= n ? 0xffffffffu : filled;
+        bs = ip; // this batch's literals start here
         // ---- the chain: up to 64 sequences (lengths only; lane k records sequence k) whose
         // bytes are all in the ring and whose output fits the window
         first_op = op;
@@ -237,64 +317,58 @@ __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
         // sequence needs the careful path (a length extension of 255s, bytes past the ring or
         // the block, an error).  The chain then costs one readlane per sequence.
         auto spec_next = [&](uint32_t x) __attribute__((always_inline)) -> uint32_t {
-            if (x + 4 > lim || x >= n) return ~0u;
+            // straight-line: every byte read (masked into the ring), the verdict by selects
             const uint32_t t = ring[x & (CR - 1)], b1 = ring[(x + 1) & (CR - 1)];
-            uint32_t ll = t >> 4, lit = x + 1;
-            if (ll == 15) {
-                if (b1 == 255) return ~0u;
-                ll += b1;
-                lit++;
-            }
-            if (lit > n || ll > n - lit) return ~0u;
-            const uint32_t q = lit + ll, mlnib = t & 15;
-            if (q == n && mlnib == 0) return (n - x) | (ll << 16);
-            if (q + 2 > n || q + 3 > lim) return ~0u;
-            uint32_t ml = mlnib + 4, nx = q + 2;
-            if (mlnib == 15) {
-                if (nx >= n) return ~0u;
-                const uint32_t b2 = ring[nx & (CR - 1)];
-                if (b2 == 255) return ~0u;
-                ml += b2;
-                nx++;
-            }
-            if (nx + 8 > lim) return ~0u;
-            return (nx - x) | ((ll + ml) << 16);
+            const uint32_t llnib = t >> 4, mlnib = t & 15;
+            const bool e1 = llnib == 15, e2 = mlnib == 15;
+            const uint32_t ll = llnib + (e1 ? b1 : 0u), lit = x + 1 + (e1 ? 1u : 0u), q = lit + ll;
+            const uint32_t b2 = ring[(q + 2) & (CR - 1)];
+            const uint32_t ml = mlnib + 4 + (e2 ? b2 : 0u), nx = q + 2 + (e2 ? 1u : 0u);
+            const bool last = q == n && mlnib == 0;
+            const bool bad = (x + 4 > lim) | (x >= n) | (e1 & (b1 == 255)) | (lit > n) | (ll > n - lit) |
+                             (!last & ((q + 2 > n) | (q + 3 > lim) | (e2 & ((q + 2 >= n) | (b2 == 255))) |
+                                       (nx + 8 > lim)));
+            const uint32_t res = last ? (n - x) | (ll << 16) : (nx - x) | ((ll + ml) << 16);
+            return bad ? ~0u : res;
         };
         uint32_t swb = 0, sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0;
-        bool sval = false; // the window [swb, swb + 256) is computed
+        bool sval = false, full = false; // sval: the window [swb, swb + 256) is computed
         while (nb < BATCH) {
+            // the fast chain: one readlane per sequence while the window knows the next token
+            for (;;) {
+                if (ip >= n || ip + 8 > lim || nb >= BATCH) break;
+                if (!sval || ip - swb >= 256) {
+                    sval = true;
+                    swb = ip;
+                    sp0 = spec_next(swb + lane);
+                    sp1 = spec_next(swb + 64 + lane);
+                    sp2 = spec_next(swb + 128 + lane);
+                    sp3 = spec_next(swb + 192 + lane);
+                }
+                const uint32_t rel = ip - swb, l = rel & 63, kq = rel >> 6;
+                const uint32_t v0 = __builtin_amdgcn_readlane(sp0, l), v1 = __builtin_amdgcn_readlane(sp1, l);
+                const uint32_t v2 = __builtin_amdgcn_readlane(sp2, l), v3 = __builtin_amdgcn_readlane(sp3, l);
+                const uint32_t v = kq == 0 ? v0 : kq == 1 ? v1 : kq == 2 ? v2 : v3;
+                if (v == ~0u || (v & 0xffff) == 0) break; // the careful path
+                const uint32_t total = v >> 16;
+                if (o + total - wb > WIN) { // the batch is full: run it, top up
+                    full = true;
+                    break;
+                }
+                if (lane == nb) {
+                    c_pos = ip;
+                    c_op = o;
+                }
+                nb++;
+                o += total;
+                ip += v & 0xffff;
+            }
+            if (full || nb >= BATCH) break;
             if (ip >= n) { // the last sequence ended exactly at the block end
                 end = true;
                 break;
             }
             if (ip + 8 > lim || ++guard > guard_max) break;
-            if (!sval || ip - swb >= 256) {
-                sval = true;
-                swb = ip;
-                sp0 = spec_next(swb + lane);
-                sp1 = spec_next(swb + 64 + lane);
-                sp2 = spec_next(swb + 128 + lane);
-                sp3 = spec_next(swb + 192 + lane);
-            }
-            {
-                const uint32_t rel = ip - swb, l = rel & 63, kq = rel >> 6;
-                const uint32_t v = uni(kq == 0   ? __builtin_amdgcn_readlane(sp0, l)
-                                       : kq == 1 ? __builtin_amdgcn_readlane(sp1, l)
-                                       : kq == 2 ? __builtin_amdgcn_readlane(sp2, l)
-                                                 : __builtin_amdgcn_readlane(sp3, l));
-                if (v != ~0u && (v & 0xffff) != 0) {
-                    const uint32_t total = v >> 16;
-                    if (o + total - wb > WIN) break; // the batch is full: run it, top up
-                    if (lane == nb) {
-                        c_pos = ip;
-                        c_op = o;
-                    }
-                    nb++;
-                    o += total;
-                    ip += v & 0xffff;
-                    continue;
-                }
-            }
             // ---- the careful path: this sequence parsed and checked serially
             const uint32_t token = (uint32_t)(rd8(ip) & 0xff);
             uint32_t ll = token >> 4, x = ip + 1;
@@ -387,9 +461,10 @@ __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
             r_off = off;
             r_ml = ml;
             op = o;
-            flush();
+            post();
         }
-        if (solo) { // HBM to HBM
+        if (solo) { // HBM to HBM, once the copier has stored every batch before it
+            while (taken_now() < posted) __builtin_amdgcn_s_sleep(1);
             uint32_t off = 0;
             if (s_q != ~0u) {
                 off = (uint32_t)(rd(s_q) & 0xffff);
@@ -412,6 +487,9 @@ __global__ __launch_bounds__(64) void lz4_block_kernel(Lz4Args a) {
             op = mop + s_ml;
         }
     }
+    if (lane == 0) __hip_atomic_store(&q_done, err ? 2u : 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (!err)
+        while (taken_now() < posted) __builtin_amdgcn_s_sleep(1);
     if (lane == 0) {
         a.sizes[b] = err ? 0xffffffffu : op;
         a.status[b] = err ? 1 : 0;
@@ -489,7 +567,7 @@ int launch_lz4_decompress(const uint8_t *src, uint64_t src_len, const spec_lz4_b
                           uint8_t *slots, uint64_t slot, uint32_t *sizes, uint8_t *status, hipStream_t stream) {
     if (nblocks == 0) return 0;
     Lz4Args a = {src, src_len, blocks, nblocks, slots, slot, sizes, status};
-    hipLaunchKernelGGL(lz4_block_kernel, dim3((unsigned)nblocks), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(lz4_block_kernel, dim3((unsigned)nblocks), dim3(128), 0, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
