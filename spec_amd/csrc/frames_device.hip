@@ -36,7 +36,9 @@ constexpr uint32_t FI_G1 = 16, FI_G2 = 16; // segments per group, groups per sup
 constexpr uint32_t FI_BLOCK = 1024; // threads of the segment / group kernels (a constant: blockDim
                                     // is a load from the dispatch packet)
 constexpr uint32_t FI_SUB = 4096, FI_NSUB = FI_SEG / FI_SUB, FI_WS = 512;
+// LDS: the segment (+16 halo), T (window walks), C (segment-entry walks), the survivor list
 constexpr uint32_t FI_LDS_T = FI_SEG + 16, FI_LDS = FI_LDS_T + (FI_NSUB - 1) * FI_WS * 4;
+constexpr uint32_t FI_LDS_L = FI_LDS + FI_W * 4, FI_LDS_END = FI_LDS_L + ((FI_NSUB - 1) * FI_WS + FI_W) * 4;
 // a segment table entry: exit x (< W) | frames << 16; FI_TERM | position | frames << 16; FI_OVF
 constexpr uint32_t FI_CNT_SHIFT = 16, FI_CNT_MASK = 0x1fffu, FI_POS_MASK = 0x7fffu;
 // a sub-segment walk result: [31] TERM, [30:17] frames, [16:0] segment-relative position
@@ -122,50 +124,77 @@ __device__ __forceinline__ void stage_segment(const FiArgs &a, uint64_t s0, uint
 // position at or past its stop (the next sub-segment) that lies in the first WS bytes of a
 // sub-segment, or past the segment end (segend = s1 - s0, lenrel = len - s0).  A jump W or more
 // past the segment end, or more than STEPCAP frames, is overflow (the serial fallback).
-// Each wave owns a contiguous share of the jobs and hands the next ones to whichever lanes just
-// finished (ballot + mbcnt), one frame step per iteration with 32-bit arithmetic (the size
-// saturates; the exact TERM test only decides a finished walk's code): the wave runs for about
-// its share's total steps / 64 plus one long walk, not for its lanes' longest job sequence.
-// Then a barrier.
-__device__ __forceinline__ void fi_tables(const FiArgs &a, uint64_t s0, uint32_t segend, uint8_t *lds,
-                                          bool entries) {
+//  1. every job takes its first step at once (one LDS read per job, no loop): nearly all of
+//     them (a false entry reads a random big size) finish there; the survivors (job, position
+//     after the first step) are appended to a list in LDS;
+//  2. the survivors are walked, one frame step per iteration with 32-bit arithmetic (the size
+//     saturates; the exact TERM test only decides a finished walk's code), shared out to the
+//     waves 64 at a time — the others skip the loop — and handed to whichever lanes just
+//     finished (ballot + mbcnt).
+// Then a barrier.  *nsurv (LDS) must be 0 on entry; it is 0 again on return.
+__device__ __forceinline__ void fi_tables(const FiArgs &a, uint64_t s0, uint32_t segend, uint8_t *lds, bool entries,
+                                          uint32_t *nsurv) {
     constexpr uint32_t NT = (FI_NSUB - 1) * FI_WS, NWAVES = FI_BLOCK / 64;
     static_assert(FI_LDS == FI_LDS_T + NT * 4, "C follows T");
     static_assert((FI_SUB - FI_WS) == 0xe00u, "window test by mask");
-    uint32_t *out = (uint32_t *)(lds + FI_LDS_T);
+    static_assert(NT + FI_W <= (1u << 13) && FI_SEG + FI_W <= (1u << 19), "a survivor packs job | position << 13");
+    uint32_t *out = (uint32_t *)(lds + FI_LDS_T), *list = (uint32_t *)(lds + FI_LDS_L);
     const uint64_t lenrel = a.len - s0;
     const uint32_t far = (uint32_t)((uint64_t)segend + FI_W < lenrel + 1 ? (uint64_t)segend + FI_W : lenrel + 1);
-    const uint32_t njobs = entries ? NT + FI_W : NT, share = (njobs + NWAVES - 1) / NWAVES;
-    const uint32_t lane = threadIdx.x & 63, j0 = (threadIdx.x >> 6) * share;
-    const uint32_t j1 = j0 + share < njobs ? j0 + share : njobs;
-    auto start = [](uint32_t j, uint32_t &p, uint32_t &stop) {
-        const bool win = j < NT;
-        const uint32_t sub = 1 + j / FI_WS;
-        p = win ? sub * FI_SUB + j % FI_WS : j - NT;
-        stop = win ? (sub + 1) * FI_SUB : FI_SUB;
-    };
-    uint32_t j = j0 + lane, next = j0 + 64, p, stop, steps = 0;
-    start(j, p, stop);
-    bool active = j < j1;
+    const uint32_t njobs = entries ? NT + FI_W : NT;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    auto stop_of = [](uint32_t j) -> uint32_t { return j < NT ? (2 + j / FI_WS) * FI_SUB : FI_SUB; };
+    // 1. first steps
+    for (uint32_t j = threadIdx.x; j < (NT + FI_W + FI_BLOCK - 1) / FI_BLOCK * FI_BLOCK; j += FI_BLOCK) {
+        const bool valid = j < njobs;
+        const uint32_t p = j < NT ? (1 + j / FI_WS) * FI_SUB + j % FI_WS : j - NT;
+        const uint32_t v = be32_lds(lds, p & (FI_SEG - 1));
+        const uint32_t q = p + 4 + (v < 0x7fffffffu ? v : 0x7fffffffu);
+        const bool exit = p >= segend, fin = exit | (q >= far);
+        if (valid & fin) out[j] = exit ? p : (uint64_t)p + 4 + v > lenrel ? FI_T_TERM | p : FI_T_OVF;
+        const bool alive = valid & !fin;
+        const uint64_t m = __ballot(alive);
+        if (m) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(nsurv, (uint32_t)__popcll(m));
+            base = __builtin_amdgcn_readlane(base, 0);
+            if (alive)
+                list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+                    j | (q << 13);
+        }
+    }
+    lds_barrier();
+    // 2. the survivors, 64 per wave at a time
+    const uint32_t S = *nsurv, share = (S + NWAVES * 64 - 1) / (NWAVES * 64) * 64;
+    const uint32_t j0 = wave * share, j1 = j0 + share < S ? j0 + share : S;
+    uint32_t i = j0 + lane, next = j0 + 64, job = 0, p = 0, stop = 0, steps = 1;
+    bool active = i < j1;
+    if (active) {
+        const uint32_t e = list[i];
+        job = e & 0x1fffu;
+        p = e >> 13;
+        stop = stop_of(job);
+    }
     while (__ballot(active)) {
         const uint32_t v = be32_lds(lds, p & (FI_SEG - 1)); // in the staged bytes
         const uint32_t q = p + 4 + (v < 0x7fffffffu ? v : 0x7fffffffu);
         const bool exit = (p >= segend) | ((p >= stop) & ((p & 0xe00u) == 0));
         const bool fin = active & (exit | (q >= far) | (steps >= FI_STEPCAP));
-        const bool term = (uint64_t)p + 4 + v > lenrel;
-        if (fin) out[j] = exit ? (steps << 17) | p : term ? FI_T_TERM | (steps << 17) | p : FI_T_OVF;
+        if (fin)
+            out[job] = exit ? (steps << 17) | p
+                            : (uint64_t)p + 4 + v > lenrel ? FI_T_TERM | (steps << 17) | p : FI_T_OVF;
         const uint64_t fm = __ballot(fin);
-        const uint32_t jn = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+        const uint32_t in = next + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
         next += (uint32_t)__popcll(fm);
-        uint32_t pn, stopn;
-        start(jn, pn, stopn);
-        j = fin ? jn : j;
-        active = fin ? jn < j1 : active;
-        p = fin ? pn : q;
-        stop = fin ? stopn : stop;
-        steps = fin ? 0 : steps + 1;
+        const uint32_t e = list[in < j1 ? in : j0]; // (a real entry either way)
+        active = fin ? in < j1 : active;
+        job = fin ? e & 0x1fffu : job;
+        p = fin ? e >> 13 : q;
+        stop = fin ? stop_of(e & 0x1fffu) : stop;
+        steps = fin ? 1 : steps + 1;
     }
     lds_barrier();
+    if (threadIdx.x == 0) *nsurv = 0;
 }
 
 // a segment entry's result from its sub-segment 0 walk c: exit offset into the next segment
@@ -192,8 +221,9 @@ __device__ __forceinline__ uint32_t fi_compose(const uint32_t *T, uint32_t c, ui
 // registers while this one is walked, so HBM latency hides behind the walks.
 __global__ __launch_bounds__(FI_BLOCK) void fi_seg_kernel(FiArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    __shared__ uint32_t nlive;
+    __shared__ uint32_t nlive, nsurv;
     const uint32_t stride = gridDim.x;
+    if (threadIdx.x == 0) nsurv = 0; // (fi_tables leaves it 0; the first barrier is the staging's)
     const uint4 *src = (const uint4 *)a.buf; // quad_segment: 16-byte aligned
     uint4 v0 = {}, v1 = {}, halo = {};
     uint32_t k = blockIdx.x;
@@ -222,7 +252,7 @@ __global__ __launch_bounds__(FI_BLOCK) void fi_seg_kernel(FiArgs a) {
             v1 = src[q0 + threadIdx.x + FI_BLOCK];
             if (threadIdx.x == 0) halo = src[q0 + FI_SEG / 16];
         }
-        fi_tables(a, s0, segend, lds, true);
+        fi_tables(a, s0, segend, lds, true, &nsurv);
         const uint32_t *T = (const uint32_t *)(lds + FI_LDS_T), *C = (const uint32_t *)(lds + FI_LDS);
         uint32_t *live = a.live + (uint64_t)k * FI_LIVE * FI_LREC;
         for (uint32_t e = threadIdx.x; e < FI_W; e += FI_BLOCK) { // a lane composes its own walks
@@ -415,7 +445,8 @@ __global__ __launch_bounds__(64) void fi_emit_kernel(FiArgs a) {
 // piece (a grid of at most 256 blocks striding the list; usually one segment, the chain's last)
 __global__ __launch_bounds__(FI_BLOCK) void fi_emit_slow_kernel(FiArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    __shared__ uint32_t ent[FI_NSUB], before[FI_NSUB];
+    __shared__ uint32_t ent[FI_NSUB], before[FI_NSUB], nsurv;
+    if (threadIdx.x == 0) nsurv = 0;
     const uint32_t nwork = a.work[0];
     for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
         const uint32_t k = a.work[1 + w], e = a.seg_entry[k];
@@ -423,7 +454,7 @@ __global__ __launch_bounds__(FI_BLOCK) void fi_emit_slow_kernel(FiArgs a) {
         const uint32_t segend = (uint32_t)(s1 - s0);
         if (threadIdx.x < FI_NSUB) ent[threadIdx.x] = threadIdx.x ? ~0u : e, before[threadIdx.x] = 0;
         stage_segment(a, s0, lds);
-        fi_tables(a, s0, segend, lds, true);
+        fi_tables(a, s0, segend, lds, true, &nsurv);
         if (threadIdx.x == 0) {
             uint32_t steps;
             const uint32_t *C = (const uint32_t *)(lds + FI_LDS);
@@ -528,7 +559,7 @@ int launch_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends,
     a.live_n = (uint32_t *)(w + L.off[12]);
     a.live = (uint32_t *)(w + L.off[13]);
     a.work = (uint32_t *)(w + L.off[14]);
-    const size_t lds = FI_LDS + FI_W * 4; // + the segment walks' sub-segment 0 codes
+    const size_t lds = FI_LDS_END;
     const uint32_t seg_blocks = 2u * (uint32_t)device_cus(); // two 70 KiB-LDS blocks per CU, persistent
     hipLaunchKernelGGL(fi_seg_kernel, dim3(L.nseg < seg_blocks ? L.nseg : seg_blocks), dim3(FI_BLOCK), lds, stream, a);
     hipLaunchKernelGGL(fi_group1_kernel, dim3(L.ng1), dim3(FI_BLOCK), 0, stream, a);
