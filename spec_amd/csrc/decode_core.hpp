@@ -80,15 +80,18 @@ constexpr int DEC_WAVES = 4; // waves per block of the nested kernels
 constexpr int SLAB_GUARD = 48; // >= the deepest read below a value end (bin256: 33 + 7)
 
 // LDS slab per wave: guard + the 1 KiB DMA chunks a 64-record span needs + pad.  Sized at
-// launch from the batch's mean record size with a 4 % margin; a wave whose span does not
-// fit parses from HBM instead (GlobalSrc), so the margin only affects speed.
+// launch from the batch's mean record size with a margin (4 % for flat records; 16 % for
+// nested ones, whose item counts vary: on config 4, 4 % left 17.8 % of the groups over the
+// slab, 16 % leaves 0.05 %); a wave whose span does not fit is staged in halves or parses
+// from HBM, so the margin only affects speed.
 constexpr int SLAB_MAX_CHUNKS = 40;
-__host__ __device__ inline uint32_t decode_slab_bytes(double avg_record) {
-    const double span = avg_record * 64 * 1.04;
+__host__ __device__ inline uint32_t decode_slab_bytes(double avg_record, double margin = 1.04) {
+    const double span = avg_record * 64 * margin;
     int chunks = (int)(span / 1024.0) + 1;
     if (chunks > SLAB_MAX_CHUNKS) return 0;
     return (uint32_t)(SLAB_GUARD + chunks * 1024 + 32);
 }
+__host__ __device__ inline uint32_t nested_slab_bytes(double avg_record) { return decode_slab_bytes(avg_record, 1.16); }
 
 // ---- message table lookup --------------------------------------------------------------
 

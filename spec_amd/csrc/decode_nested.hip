@@ -103,7 +103,7 @@ int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream) {
         (void)hipMemsetAsync(a.total, 0, sizeof(uint64_t), stream);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    a.slab = decode_slab_bytes(avg_record);
+    a.slab = nested_slab_bytes(avg_record);
     const uint64_t groups = (a.n + 63) / 64;
     dim3 grid((unsigned)((groups + DEC_WAVES - 1) / DEC_WAVES)), block(64 * DEC_WAVES);
     hipLaunchKernelGGL(nested_count_kernel, grid, block, (size_t)DEC_WAVES * a.slab, stream, a);
@@ -116,7 +116,7 @@ int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream) {
 // owner search (NESTED_GROUPS, default) or from ranges precomputed into LDS (NESTED_RANGES).
 int launch_nested_decode(const spec_nested_schema *schema, NestedArgs a, double avg_record, hipStream_t stream) {
     if (a.n == 0) return 0;
-    a.slab = decode_slab_bytes(avg_record);
+    a.slab = nested_slab_bytes(avg_record);
     const int mode = g_nested_mode;
     const int j = jit_launch_nested(schema, a, mode, stream);
     if (j != 0) return j > 0 ? 0 : -1;
@@ -152,7 +152,7 @@ int launch_nested_onepass(const spec_nested_schema *schema, NestedArgs a, double
         if (launch_nested_index(a, avg_record, stream)) return -1;
         return launch_nested_decode(schema, a, avg_record, stream);
     }
-    a.slab = decode_slab_bytes(avg_record);
+    a.slab = nested_slab_bytes(avg_record);
     const uint64_t groups = (a.n + 63) / 64;
     if (hipMemsetAsync(a.group_base, 0, (groups + 1) * sizeof(uint64_t), stream) != hipSuccess) return -1;
     const int j = jit_launch_nested(schema, a, NESTED_ONEPASS, stream);

@@ -357,25 +357,45 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 
 // Publish group g's item count `agg`, return the items of groups [0, g).  Every group < g
 // holds a ticket taken before g's, so its wave is resident and will publish: the wait ends.
+// The window looks back 256 groups per round (4 per lane, nearest first): all resident groups
+// start together, so the inclusive prefixes move forward a window per round.
 __device__ __forceinline__ uint64_t lookback(uint64_t *state, uint64_t g, uint64_t agg, int lane) {
+    constexpr int K = 4;
     if (lane == 0) lb_store(&state[g], (g == 0 ? LB_PRE : LB_AGG) | agg);
     if (g == 0) return 0;
     uint64_t excl = 0;
-    long long hi = (long long)g - 1; // window: groups hi, hi-1, ..., hi-63 on lanes 0..63
+    long long hi = (long long)g - 1; // window: group hi - (lane + 64 k) on lane `lane`, slot k
     while (true) {
-        const long long j = hi - lane;
-        const uint64_t v = j >= 0 ? lb_load(&state[j]) : LB_PRE; // before group 0: prefix 0
-        const uint64_t pre = __ballot((v >> 62) == 2);
-        const uint64_t none = __ballot((v >> 62) == 0);
-        const int first = pre ? __builtin_ctzll(pre) : 64; // nearest inclusive prefix
-        const uint64_t upto = first >= 63 ? ~0ull : ((2ull << first) - 1); // lanes 0..first
-        if (none & upto) { // a nearer group has not published yet
+        uint64_t v[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const long long j = hi - lane - 64 * k;
+            v[k] = j >= 0 ? lb_load(&state[j]) : LB_PRE; // before group 0: prefix 0
+        }
+        int first = 64 * K; // distance of the nearest inclusive prefix
+        bool wait = false;
+#pragma unroll
+        for (int k = K - 1; k >= 0; k--) {
+            const uint64_t pre = __ballot((v[k] >> 62) == 2);
+            if (pre) first = 64 * k + __builtin_ctzll(pre);
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const uint64_t none = __ballot((v[k] >> 62) == 0);
+            const int lim = first - 64 * k; // lanes of slot k nearer than `first`, or at it
+            if (lim >= 0 && none & (lim >= 63 ? ~0ull : ((2ull << lim) - 1))) wait = true;
+        }
+        if (wait) { // a nearer group has not published yet
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
-        excl += wave_sum64((upto >> lane) & 1 ? (v & LB_VAL) : 0);
-        if (first < 64) break;
-        hi -= 64;
+        uint64_t part = 0;
+#pragma unroll
+        for (int k = 0; k < K; k++)
+            if (lane + 64 * k <= first) part += v[k] & LB_VAL;
+        excl += wave_sum64(part);
+        if (first < 64 * K) break;
+        hi -= 64 * K;
     }
     if (lane == 0) lb_store(&state[g], LB_PRE | (excl + agg));
     return excl;
