@@ -367,9 +367,7 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
         *d = (saved & m) | (*d & ~m);
     }
     wave_sync();
-#if !(defined(NENC_EXP) && NENC_EXP == 3) // diagnostic (timing only): no copy-out
     copy_slab_out(slab, a.out + S - head, head, head + (E - S), lane);
-#endif
 }
 
 } // namespace spec

@@ -591,7 +591,7 @@ int spec_tree_decoder_create(const spec_tree *tree, spec_tree_decoder **out) {
     }
     memset(&d->B, 0, sizeof(d->B));
     if (hipGetDevice(&d->device) != hipSuccess || d->desc.reserve(sizeof(TreeDesc)) ||
-        d->bufs.reserve(sizeof(TreeBufs)) || d->total.reserve(sizeof(uint64_t)) ||
+        d->bufs.reserve(sizeof(TreeBufs)) || d->total.reserve(sizeof(uint64_t) * TREE_MAX_T) ||
         hipMemcpy(d->desc.p, &d->L.desc, sizeof(TreeDesc), hipMemcpyHostToDevice) != hipSuccess) {
         note_hip_error(hipGetLastError());
         delete d;
@@ -639,22 +639,35 @@ int spec_tree_decoder_index(spec_tree_decoder *d, const uint8_t *stream_bytes, u
         }
         if (!upload()) return SPEC_E_HIP;
         if (R) hipLaunchKernelGGL(tree_index_kernel, dim3(row_grid(R)), dim3(TB), 0, st, Dd, Bd, x, R);
+        // every list child: counts -> begin (in place), its total into totals[y]; then ONE copy of
+        // the totals to the host and one sync for all of this table's lists
+        bool lists = false;
         for (uint32_t y = x + 1; y < L.nt; y++) {
             if (L.desc.t[y].parent != (int)x || L.desc.t[y].rel != REL_MANY) continue;
-            // counts -> begin (in place), total -> host: the list table's rows
+            lists = true;
             if (d->scan_ws.reserve(scan_ws_bytes(R))) return SPEC_E_HIP;
-            if (R == 0) (void)hipMemsetAsync(B.cnt[y], 0, sizeof(uint32_t), st);
-            if (R && launch_scan(B.cnt[y], R, B.cnt[y], nullptr, nullptr, (uint64_t *)d->scan_ws.p,
-                                 (uint64_t *)d->total.p, st))
+            uint64_t *tot_y = (uint64_t *)d->total.p + y;
+            if (R == 0) {
+                (void)hipMemsetAsync(B.cnt[y], 0, sizeof(uint32_t), st);
+                (void)hipMemsetAsync(tot_y, 0, sizeof(uint64_t), st);
+            } else if (launch_scan(B.cnt[y], R, B.cnt[y], nullptr, nullptr, (uint64_t *)d->scan_ws.p, tot_y, st)) {
                 return SPEC_E_HIP;
-            uint64_t tot = 0;
-            if (R && (hipMemcpyAsync(&tot, d->total.p, sizeof(uint64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-                      hipStreamSynchronize(st) != hipSuccess))
-                return SPEC_E_HIP;
-            B.rows[y] = tot;
-            if (d->rng[y].reserve(std::max<uint64_t>(tot, 1) * sizeof(uint2))) return SPEC_E_HIP;
+            }
+        }
+        if (!lists) continue;
+        uint64_t tot[TREE_MAX_T];
+        if (hipMemcpyAsync(tot, d->total.p, sizeof(uint64_t) * L.nt, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return SPEC_E_HIP;
+        for (uint32_t y = x + 1; y < L.nt; y++) {
+            if (L.desc.t[y].parent != (int)x || L.desc.t[y].rel != REL_MANY) continue;
+            B.rows[y] = tot[y];
+            if (d->rng[y].reserve(std::max<uint64_t>(tot[y], 1) * sizeof(uint2))) return SPEC_E_HIP;
             B.rng[y] = (uint2 *)d->rng[y].p;
-            if (!upload()) return SPEC_E_HIP;
+        }
+        if (!upload()) return SPEC_E_HIP;
+        for (uint32_t y = x + 1; y < L.nt; y++) {
+            if (L.desc.t[y].parent != (int)x || L.desc.t[y].rel != REL_MANY) continue;
             if (R) hipLaunchKernelGGL(tree_expand_kernel, dim3(row_grid(R)), dim3(TB), 0, st, Dd, Bd, x, y, R);
         }
     }
