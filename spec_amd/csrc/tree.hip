@@ -24,6 +24,84 @@ unsigned row_grid(uint64_t rows) {
 }
 
 // ---- decode kernels ------------------------------------------------------------------------
+//
+// A wave takes 64 consecutive rows of a table; the rows' bytes usually lie close together in
+// the stream (consecutive records, their sub-messages, the elements of neighbouring lists), so
+// the span [min lo, max hi) of the wave's rows is staged in an LDS slab with 16-byte loads and
+// parsed from there (SlabSrc); reads outside the staged bytes, and waves whose span does not fit,
+// go to HBM (GlobalSrc) — the same bytes either way.
+
+constexpr int TSLAB = 16384 + 128; // per wave
+constexpr int TREE_LDS = (TB / 64) * TSLAB;
+
+struct SlabSrc {
+    using pos_t = long long;
+    lds_u8 *lds;    // stream bytes [base, end)
+    long long base, end;
+    GlobalSrc g;
+    __device__ __forceinline__ bool in(long long p, int n) const { return p >= base && p + n <= end; }
+    __device__ __forceinline__ uint32_t u8(long long p) const { return in(p, 1) ? lds[p - base] : g.u8(p); }
+    __device__ __forceinline__ uint64_t d64(long long p) const {
+        return in(p, 8) ? *(lds_u64 *)(lds + (p - base)) : g.d64(p);
+    }
+    __device__ __forceinline__ uint32_t d32(long long p) const {
+        return in(p, 4) ? *(lds_u32 *)(lds + (p - base)) : g.d32(p);
+    }
+};
+
+__device__ __forceinline__ void tree_wave_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Every wave of the grid over the rows of table x, 64 at a time: body(src, row, lo, hi, panic)
+// for its valid rows, src = the staged slab when the wave's span fits, else HBM.
+template <class Body>
+__device__ __forceinline__ void tree_rows(const TreeBufs &B, uint32_t x, uint64_t rows, Body body) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint8_t *slab = smem + wave * TSLAB;
+    const GlobalSrc gs{stream_rsrc(B), B.stream_len};
+    const uint64_t wstride = (uint64_t)gridDim.x * (TB / 64) * 64;
+    for (uint64_t base = ((uint64_t)blockIdx.x * (TB / 64) + wave) * 64; base < rows; base += wstride) {
+        const uint64_t row = base + lane;
+        const bool valid = row < rows;
+        long long lo = 0, hi = 0;
+        bool panic = false;
+        if (valid) row_range(B, x, row, lo, hi, panic);
+        const bool some = valid && hi > lo;
+        long long slo = some ? lo : (long long)B.stream_len, shi = some ? hi : 0;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const long long a = __shfl_xor(slo, d), b2 = __shfl_xor(shi, d);
+            slo = a < slo ? a : slo;
+            shi = b2 > shi ? b2 : shi;
+        }
+        slo = (long long)uniform64((uint64_t)slo);
+        shi = (long long)uniform64((uint64_t)shi);
+        const long long sb = (slo > 64 ? slo - 64 : 0) & ~15ll, se = (shi + 16 + 15) & ~15ll;
+        if (slo < shi && se - sb <= TSLAB) {
+            for (long long off = 16ll * lane; off < se - sb; off += 1024) {
+                const long long p = sb + off;
+                uint4 v;
+                if ((uint64_t)p + 16 <= B.stream_len) {
+                    const auto q = __builtin_amdgcn_raw_buffer_load_b128(gs.rsrc, (uint32_t)p, 0, 0);
+                    v = make_uint4(q[0], q[1], q[2], q[3]);
+                } else {
+                    v = make_uint4(gs.d32(p), gs.d32(p + 4), gs.d32(p + 8), gs.d32(p + 12));
+                }
+                *(uint4 *)(slab + off) = v;
+            }
+            tree_wave_fence();
+            const SlabSrc ss{(lds_u8 *)slab, sb, se, gs};
+            if (valid) body(ss, row, lo, hi, panic);
+        } else if (valid) {
+            body(gs, row, lo, hi, panic);
+        }
+        tree_wave_fence(); // the slab is read before the next rows overwrite it
+    }
+}
 
 // Per row of message table x: the range of every sub-message field (its child row) and the
 // element count of every list field (m.field(tag), internal/types/msg.go:466-475; OpenList,
@@ -33,11 +111,7 @@ __global__ __launch_bounds__(TB) void tree_index_kernel(const TreeDesc *Dp, cons
     const TreeDesc &D = *Dp;
     const TreeBufs &B = *Bp;
     const TTable &T = D.t[x];
-    GlobalSrc s{stream_rsrc(B), B.stream_len};
-    for (uint64_t row = grid_first(); row < rows; row += grid_stride()) {
-        long long lo, hi;
-        bool panic;
-        row_range(B, x, row, lo, hi, panic);
+    tree_rows(B, x, rows, [&](const auto &s, uint64_t row, long long lo, long long hi, bool) {
         const RecInfo ri = rec_open(s, lo, hi);
         const long long ds = ri.tr.dstart;
         for (uint32_t k = 0; k < T.nd; k++) {
@@ -51,7 +125,7 @@ __global__ __launch_bounds__(TB) void tree_index_kernel(const TreeDesc *Dp, cons
                 B.cnt[F.table][row] = li.count;
             }
         }
-    }
+    });
 }
 
 // Per owner row: the range of every element of list table y (List.GetBytes,
@@ -61,11 +135,7 @@ __global__ __launch_bounds__(TB) void tree_expand_kernel(const TreeDesc *Dp, con
     const TreeDesc &D = *Dp;
     const TreeBufs &B = *Bp;
     const TField &F = D.f[D.t[y].field];
-    GlobalSrc s{stream_rsrc(B), B.stream_len};
-    for (uint64_t row = grid_first(); row < rows; row += grid_stride()) {
-        long long lo, hi;
-        bool panic;
-        row_range(B, x, row, lo, hi, panic);
+    tree_rows(B, x, rows, [&](const auto &s, uint64_t row, long long lo, long long hi, bool) {
         const RecInfo ri = rec_open(s, lo, hi);
         const long long ds = ri.tr.dstart;
         const long long end = rec_field_end(s, ri, F.tag, F.rank);
@@ -86,7 +156,7 @@ __global__ __launch_bounds__(TB) void tree_expand_kernel(const TreeDesc *Dp, con
             else r = make_uint2((uint32_t)(li.dstart + a), (uint32_t)(li.dstart + b));
             out[j] = r;
         }
-    }
+    });
 }
 
 // Every column of table x.
@@ -95,11 +165,7 @@ __global__ __launch_bounds__(TB) void tree_decode_kernel(const TreeDesc *Dp, con
     const TreeDesc &D = *Dp;
     const TreeBufs &B = *Bp;
     const TTable &T = D.t[x];
-    GlobalSrc s{stream_rsrc(B), B.stream_len};
-    for (uint64_t row = grid_first(); row < rows; row += grid_stride()) {
-        long long lo, hi;
-        bool panic;
-        row_range(B, x, row, lo, hi, panic);
+    tree_rows(B, x, rows, [&](const auto &s, uint64_t row, long long lo, long long hi, bool panic) {
         uint32_t st = ST_OK;
         if (T.shape == SHAPE_VALUE) {
             const TField &F = D.f[T.field];
@@ -144,7 +210,7 @@ __global__ __launch_bounds__(TB) void tree_decode_kernel(const TreeDesc *Dp, con
             if (panic) st = ST_PANIC;
         }
         store_u8(B.cols[T.status_col], row, st);
-    }
+    });
 }
 
 // ---- encode kernels ------------------------------------------------------------------------
@@ -638,7 +704,7 @@ int spec_tree_decoder_index(spec_tree_decoder *d, const uint8_t *stream_bytes, u
             }
         }
         if (!upload()) return SPEC_E_HIP;
-        if (R) hipLaunchKernelGGL(tree_index_kernel, dim3(row_grid(R)), dim3(TB), 0, st, Dd, Bd, x, R);
+        if (R) hipLaunchKernelGGL(tree_index_kernel, dim3(row_grid(R)), dim3(TB), TREE_LDS, st, Dd, Bd, x, R);
         // every list child: counts -> begin (in place), its total into totals[y]; then ONE copy of
         // the totals to the host and one sync for all of this table's lists
         bool lists = false;
@@ -668,7 +734,7 @@ int spec_tree_decoder_index(spec_tree_decoder *d, const uint8_t *stream_bytes, u
         if (!upload()) return SPEC_E_HIP;
         for (uint32_t y = x + 1; y < L.nt; y++) {
             if (L.desc.t[y].parent != (int)x || L.desc.t[y].rel != REL_MANY) continue;
-            if (R) hipLaunchKernelGGL(tree_expand_kernel, dim3(row_grid(R)), dim3(TB), 0, st, Dd, Bd, x, y, R);
+            if (R) hipLaunchKernelGGL(tree_expand_kernel, dim3(row_grid(R)), dim3(TB), TREE_LDS, st, Dd, Bd, x, y, R);
         }
     }
     // tables whose owner has no rows to index (empty batch / no message children) keep 0 rows
@@ -715,7 +781,7 @@ int spec_tree_decoder_decode(spec_tree_decoder *d, void *const *columns, void *s
                 return SPEC_E_HIP;
             }
         }
-        if (R) hipLaunchKernelGGL(tree_decode_kernel, dim3(row_grid(R)), dim3(TB), 0, st, Dd, Bd, x, R);
+        if (R) hipLaunchKernelGGL(tree_decode_kernel, dim3(row_grid(R)), dim3(TB), TREE_LDS, st, Dd, Bd, x, R);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
