@@ -599,6 +599,8 @@ __device__ __forceinline__ Pos emit_message(const EncFields &a, const Sink &k, P
 struct RuntimeEnc {
     struct Rec {};
     static __device__ __forceinline__ Rec load(const EncFields &, uint64_t) { return Rec{}; }
+    static __device__ __forceinline__ void load_cols(const EncFields &, uint64_t, Rec &) {}
+    static __device__ __forceinline__ void load_heaps(const EncFields &, Rec &) {}
     template <class Lists = NoLists>
     static __device__ __forceinline__ RecSize size(const EncFields &f, const Rec &, uint64_t r, bool check,
                                                    bool &err, const Lists &lists = Lists()) {
@@ -710,6 +712,9 @@ struct SpecEnc {
         load_heap<0>(f, x);
         return x;
     }
+    // the two halves of load(), for pipelines that issue them an iteration apart
+    static __device__ __forceinline__ void load_cols(const EncFields &f, uint64_t r, Rec &x) { load_col<0>(f, r, x); }
+    static __device__ __forceinline__ void load_heaps(const EncFields &f, Rec &x) { load_heap<0>(f, x); }
 
     template <int F, class Lists>
     static __device__ __forceinline__ uint64_t data_size(const EncFields &f, const Rec &x, uint64_t r, bool check,

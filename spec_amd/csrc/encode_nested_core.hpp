@@ -291,8 +291,10 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
     uint8_t *slab = (uint8_t *)pre + NENC_PRE;
 
     bool err = false;
+    // the outer record's loads first: in flight while the item prefix is built
+    const uint64_t r0 = (uint64_t)blockIdx.x * NENC_BLOCK + threadIdx.x;
+    const typename OP::Rec orec = OP::load(a.outer, r0 < a.n ? r0 : a.n - 1);
     const LaneRecord L = lane_record<IP>(a, pre, lane, false, err);
-    const typename OP::Rec orec = OP::load(a.outer, L.valid ? L.r : a.n - 1);
     ListSize ls;
     RecSize rs = lane_record_size<OP>(a, L, orec, pre, false, err, ls);
     if (!L.valid) rs.total = 0;
@@ -334,17 +336,20 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
     const bool fix = L.valid && ls.count > 0 && (lst & 3);
     const uint32_t saved = fix ? *(const uint32_t *)(slab + (lst & ~3)) : 0u;
     wave_sync();
-    // B: items, last chunk first; the next chunk's loads issued before this chunk is emitted
+    // B: items, last chunk first, three chunks in flight: the column loads of chunk c-128 and
+    // the heap loads of chunk c-64 (addressed by the spans its column loads brought one
+    // iteration earlier) are issued before chunk c is emitted
     const int lbase = lst - (int)pre[L.b - L.I0];
     int c = ((int)L.cnt - 1) & ~63;
-    typename IP::Rec cur;
+    typename IP::Rec cur, nxt, nn;
     if (c >= 0) {
         const uint32_t kk = (uint32_t)c + lane;
         cur = IP::load(a.item, L.I0 + (kk < L.cnt ? kk : L.cnt - 1));
     }
+    if (c >= 64) IP::load_cols(a.item, L.I0 + (uint32_t)(c - 64) + lane, nxt);
     for (; c >= 0; c -= 64) {
-        typename IP::Rec nxt;
-        if (c >= 64) nxt = IP::load(a.item, L.I0 + (uint32_t)(c - 64) + lane);
+        if (c >= 128) IP::load_cols(a.item, L.I0 + (uint32_t)(c - 128) + lane, nn);
+        if (c >= 64) IP::load_heaps(a.item, nxt);
         const uint32_t kk = (uint32_t)c + lane;
         const bool iv = kk < L.cnt;
         const uint32_t i = L.I0 + (iv ? kk : 0u);
@@ -359,6 +364,7 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
         }
         wave_sync();
         cur = nxt;
+        nxt = nn;
     }
     // C: the bytes under the list start that the first item's head store overwrote
     if (fix) {
