@@ -408,9 +408,13 @@ int spec_decode_nested_onepass(const spec_nested_schema *schema, const uint8_t *
                                uint32_t *item_begin, void *const *item_columns, uint8_t *item_status,
                                uint64_t item_cap, void *workspace, size_t workspace_size, uint64_t *total_items,
                                void *stream);
-/* spec_set_nested_mode: the kernel of spec_decode_nested's decode pass (results never differ):
- * 1 items found by an owner search over the group's record prefix sums (default; 0.097 ms on
- * config 4), 2 items read from ranges their records' lanes precomputed into LDS (0.108 ms). */
+/* spec_set_nested_mode: the kernels of spec_decode_nested_index / spec_decode_nested (results
+ * never differ; times per 1M config-4 records, index + decode):
+ * 4 (default) count pass from each record's last 64 bytes, decode with items found by an owner
+ *   search over the group's record prefix sums (0.127 ms);
+ * 1 count pass over the staged 64-record span, decode as 4 (0.140 ms);
+ * 2 as 1, items read from ranges their records' lanes precomputed into LDS (0.141 ms);
+ * 3 as 1 with LDS slabs for half a group (0.160 ms). */
 void spec_set_nested_mode(int mode);
 /* spec_decode_nested_jit_compile: compile (hiprtc, no GPU needed) the schema-specialised one-pass
  * kernel; code-object size, 0 if neither schema has a fast path. */

@@ -3,8 +3,9 @@
 // one-pass kernel specialised to the outer and item schemas.
 //
 // Two ways to place the items (include/spec_amd.h):
-//   spec_decode_nested_index + spec_decode_nested: nested_count_kernel (per 64-record group:
-//     item total) + nested_scan_kernel (exclusive scan of group totals, total items), then
+//   spec_decode_nested_index + spec_decode_nested: nested_count_tail_kernel (per 64-record
+//     group: item total, from each record's last 64 bytes; nested_count_kernel parses the staged
+//     span instead) + nested_scan_kernel (exclusive scan of group totals, total items), then
 //     nested_decode_kernel;
 //   spec_decode_nested_onepass: nested_onepass_kernel alone (decoupled look-back over the
 //     groups' item counts), after zeroing the look-back words.
@@ -19,6 +20,11 @@ namespace spec {
 namespace {
 
 __global__ __launch_bounds__(256) void nested_count_kernel(NestedArgs a) { nested_count_body(a); }
+
+__global__ __launch_bounds__(256) void nested_count_tail_kernel(NestedArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t wins[256 * TAIL_WIN];
+    nested_count_tail_body(a, wins);
+}
 
 // Exclusive scan of the group totals + total items: one 1024-thread workgroup.  Tiles of
 // 16 x 1024 totals: loaded coalesced (all 16 loads in flight) into LDS as u32 (item counts of
@@ -94,19 +100,30 @@ __global__ __launch_bounds__(256) void nested_decode_ranges_kernel(NestedArgs a)
     nested_decode_body<RuntimeSpec, RuntimeSpec, false, true>(a);
 }
 
-int g_nested_mode = NESTED_GROUPS;
+int g_nested_mode = NESTED_TAILCOUNT;
 
 } // namespace
+
+// NESTED_HALVES: slabs sized for half a group (32 records), so twice the waves fit a CU's LDS;
+// every group is then staged and decoded as two halves (the path a group larger than its
+// slab takes anyway).
+uint32_t nested_slab_for_mode(double avg_record) {
+    return nested_slab_bytes(g_nested_mode == NESTED_HALVES ? avg_record * 0.5 : avg_record);
+}
 
 int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream) {
     if (a.n == 0) {
         (void)hipMemsetAsync(a.total, 0, sizeof(uint64_t), stream);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    a.slab = nested_slab_bytes(avg_record);
+    a.slab = nested_slab_for_mode(avg_record);
     const uint64_t groups = (a.n + 63) / 64;
-    dim3 grid((unsigned)((groups + DEC_WAVES - 1) / DEC_WAVES)), block(64 * DEC_WAVES);
-    hipLaunchKernelGGL(nested_count_kernel, grid, block, (size_t)DEC_WAVES * a.slab, stream, a);
+    if (g_nested_mode == NESTED_TAILCOUNT) {
+        hipLaunchKernelGGL(nested_count_tail_kernel, dim3((unsigned)((groups + 3) / 4)), dim3(256), 0, stream, a);
+    } else {
+        dim3 grid((unsigned)((groups + DEC_WAVES - 1) / DEC_WAVES)), block(64 * DEC_WAVES);
+        hipLaunchKernelGGL(nested_count_kernel, grid, block, (size_t)DEC_WAVES * a.slab, stream, a);
+    }
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(nested_scan_kernel, dim3(1), dim3(1024), 0, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -116,8 +133,8 @@ int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream) {
 // owner search (NESTED_GROUPS, default) or from ranges precomputed into LDS (NESTED_RANGES).
 int launch_nested_decode(const spec_nested_schema *schema, NestedArgs a, double avg_record, hipStream_t stream) {
     if (a.n == 0) return 0;
-    a.slab = nested_slab_bytes(avg_record);
-    const int mode = g_nested_mode;
+    a.slab = nested_slab_for_mode(avg_record);
+    const int mode = g_nested_mode >= NESTED_HALVES ? NESTED_GROUPS : g_nested_mode;
     const int j = jit_launch_nested(schema, a, mode, stream);
     if (j != 0) return j > 0 ? 0 : -1;
     const uint64_t groups = (a.n + 63) / 64;
@@ -164,5 +181,7 @@ int launch_nested_onepass(const spec_nested_schema *schema, NestedArgs a, double
 } // namespace spec
 
 extern "C" void spec_set_nested_mode(int mode) {
-    if (mode == spec::NESTED_GROUPS || mode == spec::NESTED_RANGES) spec::g_nested_mode = mode;
+    if (mode == spec::NESTED_GROUPS || mode == spec::NESTED_RANGES || mode == spec::NESTED_HALVES ||
+        mode == spec::NESTED_TAILCOUNT)
+        spec::g_nested_mode = mode;
 }

@@ -241,11 +241,10 @@ __device__ __forceinline__ ListInfo item_owner(const ListInfo &li, uint32_t excl
 #ifndef NESTED_ITEM_U
 #define NESTED_ITEM_U 2
 #endif
-template <class ISpec, class Src>
+template <class ISpec, int U = NESTED_ITEM_U, class Src>
 __device__ __forceinline__ void decode_group_items(const Src &s, const ListInfo &li, uint32_t excl, uint32_t total,
                                                    uint64_t item_base, int lane, long long to_stream,
                                                    const NestedArgs &a) {
-    constexpr int U = NESTED_ITEM_U;
     for (uint32_t j0 = 0; j0 < total; j0 += 64 * U) {
         ListInfo own[U];
         uint32_t idx[U];
@@ -403,7 +402,7 @@ __device__ __forceinline__ uint64_t lookback(uint64_t *state, uint64_t g, uint64
 
 // Decode a group: outer records (lane = record), then items (item-parallel).  item_base =
 // the group's first item; ONEPASS: item_base is found here by look-back (state = a.group_base).
-template <class OSpec, class ISpec, bool ONEPASS, class Src>
+template <class OSpec, class ISpec, bool ONEPASS, int U = NESTED_ITEM_U, class Src>
 __device__ __forceinline__ uint32_t nested_group_body(const Src &s, long long rs, long long re, bool valid,
                                                       uint64_t r, uint64_t g, uint64_t item_base, int lane,
                                                       long long to_stream, const NestedArgs &a,
@@ -427,13 +426,13 @@ __device__ __forceinline__ uint32_t nested_group_body(const Src &s, long long rs
             return total;
         }
     }
-    decode_group_items<ISpec>(s, li, excl, total, item_base, lane, to_stream, a);
+    decode_group_items<ISpec, U>(s, li, excl, total, item_base, lane, to_stream, a);
     return total;
 }
 
 // A part of a group (lanes [l0, l1)) from the slab when it fits, from HBM otherwise; the part's items
 // start at item_base.  Returns the part's item count.
-template <class OSpec, class ISpec, bool RANGES>
+template <class OSpec, class ISpec, bool RANGES, int U = NESTED_ITEM_U>
 __device__ __forceinline__ uint32_t nested_decode_part(const NestedArgs &a, __amdgpu_buffer_rsrc_t rsrc,
                                                        uint8_t *slab, uint64_t g, uint64_t item_base, int lane,
                                                        int l0, int l1) {
@@ -443,20 +442,20 @@ __device__ __forceinline__ uint32_t nested_decode_part(const NestedArgs &a, __am
     const bool valid = r < a.n && lane >= l0 && lane < l1;
     if (gr.in_lds) {
         LdsSrc s{(lds_u8 *)slab};
-        return nested_group_body<OSpec, ISpec, false>(s, SLAB_GUARD + (long long)(gr.rec_lo - gr.aligned_lo),
+        return nested_group_body<OSpec, ISpec, false, U>(s, SLAB_GUARD + (long long)(gr.rec_lo - gr.aligned_lo),
                                                       SLAB_GUARD + (long long)(gr.rec_hi - gr.aligned_lo), valid, r,
                                                       g, item_base, lane, (long long)gr.aligned_lo - SLAB_GUARD, a,
                                                       RANGES ? (uint32_t *)(slab + a.slab) : nullptr);
     }
     GlobalSrc s{rsrc, a.stream_len};
-    return nested_group_body<OSpec, ISpec, false>(s, (long long)gr.rec_lo, (long long)gr.rec_hi, valid, r, g,
+    return nested_group_body<OSpec, ISpec, false, U>(s, (long long)gr.rec_lo, (long long)gr.rec_hi, valid, r, g,
                                                   item_base, lane, 0, a);
 }
 
 // Kernel body for one group per wave.  ONEPASS: group = ticket order (a.group_base = state
 // words, ticket at state[ngroups], both zeroed by the launcher); else group = wave index and
 // a.group_base holds the exclusive item offsets from the index kernels.
-template <class OSpec, class ISpec, bool ONEPASS, bool RANGES = false>
+template <class OSpec, class ISpec, bool ONEPASS, bool RANGES = false, int U = NESTED_ITEM_U>
 __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -483,17 +482,17 @@ __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
         const uint64_t r = base + lane;
         if (whole.in_lds) {
             LdsSrc s{(lds_u8 *)slab};
-            nested_group_body<OSpec, ISpec, false>(s, SLAB_GUARD + (long long)(whole.rec_lo - whole.aligned_lo),
+            nested_group_body<OSpec, ISpec, false, U>(s, SLAB_GUARD + (long long)(whole.rec_lo - whole.aligned_lo),
                                                    SLAB_GUARD + (long long)(whole.rec_hi - whole.aligned_lo),
                                                    r < a.n, r, g, item_base, lane,
                                                    (long long)whole.aligned_lo - SLAB_GUARD, a,
                                                    RANGES ? (uint32_t *)(slab + a.slab) : nullptr);
             return;
         }
-        const uint32_t first = nested_decode_part<OSpec, ISpec, RANGES>(a, rsrc, slab, g, item_base, lane, 0, 32);
+        const uint32_t first = nested_decode_part<OSpec, ISpec, RANGES, U>(a, rsrc, slab, g, item_base, lane, 0, 32);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the first half's LDS reads done
         __builtin_amdgcn_wave_barrier();
-        nested_decode_part<OSpec, ISpec, RANGES>(a, rsrc, slab, g, item_base + first, lane, 32, 64);
+        nested_decode_part<OSpec, ISpec, RANGES, U>(a, rsrc, slab, g, item_base + first, lane, 32, 64);
         return;
     }
     const Group gr = nested_stage(a, rsrc, slab, base, lane);
@@ -550,6 +549,80 @@ __device__ __forceinline__ void nested_count_body(const NestedArgs &a) {
         if (whole) break;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // this half's LDS reads done
         __builtin_amdgcn_wave_barrier();
+    }
+    const uint32_t sum = wave_sum(cnt);
+    if (lane == 0) a.group_base[g] = sum;
+}
+
+// ---- count from tail windows --------------------------------------------------------------
+// The count pass needs, per record, only OpenMessage's trailer and table, the list field's
+// table entry and the list's own trailer.  A Writer emits the table and trailer last and, for a
+// record whose list is its last field, the list's trailer right below the table: all within the
+// record's last few dozen bytes.  So instead of staging the whole span, each lane loads the 64
+// bytes [a, a + 64) (a = (end - 48) & ~15: at least the last 48 bytes) into its own LDS window
+// and parses from there; a read outside the window (big tables, a list followed by other fields,
+// malformed records) goes to HBM through the same range-checked loads GlobalSrc uses, so the
+// count is the same whatever the record looks like.  One 64-byte window per record touches one
+// or two 128-byte lines of the ~210-byte config-4 records instead of all of them.
+constexpr int TAIL_WIN = 64;
+
+struct WinSrc {
+    using pos_t = long long;
+    lds_u8 *lds;  // this lane's window: stream bytes [a, a + TAIL_WIN)
+    long long a;
+    GlobalSrc g;
+    __device__ __forceinline__ uint32_t u8(long long p) const {
+        const unsigned long long k = (unsigned long long)(p - a);
+        return k < (unsigned long long)TAIL_WIN ? (uint32_t)lds[k] : g.u8(p);
+    }
+    __device__ __forceinline__ uint64_t d64(long long p) const {
+        const unsigned long long k = (unsigned long long)(p - a);
+        if (k <= (unsigned long long)(TAIL_WIN - 8) && !(k & 7)) return *(lds_u64 *)(lds + k);
+        return g.d64(p);
+    }
+    __device__ __forceinline__ uint32_t d32(long long p) const {
+        const unsigned long long k = (unsigned long long)(p - a);
+        if (k <= (unsigned long long)(TAIL_WIN - 4) && !(k & 3)) return *(lds_u32 *)(lds + k);
+        return g.d32(p);
+    }
+};
+
+// 16 stream bytes at o as GlobalSrc reads them (a piece straddling the end bytewise, beyond: 0)
+__device__ __forceinline__ uint4 win_piece(__amdgpu_buffer_rsrc_t rsrc, uint64_t o, uint64_t len) {
+    const uint32_t o32 = (uint32_t)o;
+    if ((uint64_t)o32 + 16 <= len) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o32, 0, 0);
+        return make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    return make_uint4(buf_ld32(rsrc, o32, len), buf_ld32(rsrc, o32 + 4, len), buf_ld32(rsrc, o32 + 8, len),
+                      buf_ld32(rsrc, o32 + 12, len));
+}
+
+__device__ __forceinline__ void nested_count_tail_body(const NestedArgs &a, uint8_t *wins) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    const uint64_t base = g * 64;
+    if (base >= a.n) return;
+    __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
+    DecodeArgs d;
+    d.ends = a.ends;
+    d.n = a.n;
+    d.head = 0;
+    uint64_t lo, hi;
+    load_group_ends(d, base, lane, lo, hi);
+    if (hi < lo) hi = lo; // malformed ends: an empty record (make_group)
+    uint32_t cnt = 0;
+    if (base + lane < a.n) {
+        const uint64_t w0 = hi >= 48 ? (hi - 48) & ~15ull : 0;
+        uint8_t *win = wins + threadIdx.x * TAIL_WIN;
+        uint4 v[TAIL_WIN / 16];
+#pragma unroll
+        for (int k = 0; k < TAIL_WIN / 16; k++) v[k] = win_piece(rsrc, w0 + 16 * k, a.stream_len);
+#pragma unroll
+        for (int k = 0; k < TAIL_WIN / 16; k++) *(uint4 *)(win + 16 * k) = v[k];
+        WinSrc s{(lds_u8 *)win, (long long)w0, GlobalSrc{rsrc, a.stream_len}};
+        cnt = record_count(s, (long long)lo, (long long)hi, a);
     }
     const uint32_t sum = wave_sum(cnt);
     if (lane == 0) a.group_base[g] = sum;
