@@ -56,11 +56,7 @@ __device__ __forceinline__ void tree_wave_fence() {
 }
 
 // Every wave of the grid over the rows of table x, 64 at a time: body(src, row, lo, hi, panic)
-// for its valid rows.  The 64 rows' bytes usually span more than a slab (pkg1 records are ~470
-// bytes: 64 of them ~30 KiB), so the wave stages them in ROUNDS: each round stages the slab's
-// worth of bytes from the lowest pending row's start, and the rows whose bytes lie inside run
-// from LDS; a row larger than a slab runs alone from HBM; rows with no bytes run in the first
-// round.  The same bytes either way (SlabSrc reads outside the staged range go to HBM).
+// for its valid rows, src = the staged slab when the wave's span fits, else HBM.
 template <class Body>
 __device__ __forceinline__ void tree_rows(const TreeBufs &B, uint32_t x, uint64_t rows, Body body) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -75,31 +71,17 @@ __device__ __forceinline__ void tree_rows(const TreeBufs &B, uint32_t x, uint64_
         bool panic = false;
         if (valid) row_range(B, x, row, lo, hi, panic);
         const bool some = valid && hi > lo;
-        bool todo = valid;
-        while (true) {
-            const uint64_t pb = __ballot(todo && some);
-            if (!pb) { // rows with no bytes left only: they read (next to) nothing
-                if (todo) body(gs, row, lo, hi, panic);
-                break;
-            }
-            const int l0 = __builtin_ctzll(pb);
-            const long long slo = (long long)uniform64((uint64_t)__shfl(lo, l0));
-            const long long shi0 = (long long)uniform64((uint64_t)__shfl(hi, l0));
-            const long long sb = (slo > 64 ? slo - 64 : 0) & ~15ll;
-            if (shi0 + 16 > sb + TSLAB) { // row l0 alone exceeds a slab
-                if (lane == l0) body(gs, row, lo, hi, panic);
-                todo = todo && lane != l0;
-                continue;
-            }
-            const bool run = todo && (!some || (lo >= slo && hi + 16 <= sb + TSLAB));
-            long long shi = run && some ? hi : 0;
+        long long slo = some ? lo : (long long)B.stream_len, shi = some ? hi : 0;
 #pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) {
-                const long long b2 = __shfl_xor(shi, d);
-                shi = b2 > shi ? b2 : shi;
-            }
-            shi = (long long)uniform64((uint64_t)shi);
-            const long long se = (shi + 16 + 15) & ~15ll; // <= sb + TSLAB
+        for (int d = 32; d >= 1; d >>= 1) {
+            const long long a = __shfl_xor(slo, d), b2 = __shfl_xor(shi, d);
+            slo = a < slo ? a : slo;
+            shi = b2 > shi ? b2 : shi;
+        }
+        slo = (long long)uniform64((uint64_t)slo);
+        shi = (long long)uniform64((uint64_t)shi);
+        const long long sb = (slo > 64 ? slo - 64 : 0) & ~15ll, se = (shi + 16 + 15) & ~15ll;
+        if (slo < shi && se - sb <= TSLAB) {
             for (long long off = 16ll * lane; off < se - sb; off += 1024) {
                 const long long p = sb + off;
                 uint4 v;
@@ -113,10 +95,11 @@ __device__ __forceinline__ void tree_rows(const TreeBufs &B, uint32_t x, uint64_
             }
             tree_wave_fence();
             const SlabSrc ss{(lds_u8 *)slab, sb, se, gs};
-            if (run) body(ss, row, lo, hi, panic);
-            todo = todo && !run;
-            tree_wave_fence(); // the slab is read before the next round overwrites it
+            if (valid) body(ss, row, lo, hi, panic);
+        } else if (valid) {
+            body(gs, row, lo, hi, panic);
         }
+        tree_wave_fence(); // the slab is read before the next rows overwrite it
     }
 }
 
