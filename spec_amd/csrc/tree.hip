@@ -32,7 +32,16 @@ unsigned row_grid(uint64_t rows) {
 // go to HBM (GlobalSrc) — the same bytes either way.
 
 constexpr int TSLAB = 16384 + 128; // per wave
-constexpr int TREE_LDS = (TB / 64) * TSLAB;
+
+// LDS per wave for the rows of a table: a slab when 64 consecutive rows are expected to fit it
+// (mean span of 64 rows, estimated as if the table's rows covered the whole stream, + 10 %),
+// else none: staging would almost never happen and the slab only halves the waves a CU holds
+// (the row kernels are latency-bound gathers: pkg1's ~470-byte records never fit).
+uint32_t tree_slab(uint64_t stream_len, uint64_t rows) {
+    if (!rows) return 0;
+    const double span = 64.0 * (double)stream_len / (double)rows;
+    return span * 1.1 + 256 <= TSLAB ? (uint32_t)TSLAB : 0u;
+}
 
 struct SlabSrc {
     using pos_t = long long;
@@ -58,10 +67,11 @@ __device__ __forceinline__ void tree_wave_fence() {
 // Every wave of the grid over the rows of table x, 64 at a time: body(src, row, lo, hi, panic)
 // for its valid rows, src = the staged slab when the wave's span fits, else HBM.
 template <class Body>
-__device__ __forceinline__ void tree_rows(const TreeBufs &B, uint32_t x, uint64_t rows, Body body) {
+__device__ __forceinline__ void tree_rows(const TreeBufs &B, uint32_t x, uint64_t rows, uint32_t slab_bytes,
+                                          Body body) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint8_t *slab = smem + wave * TSLAB;
+    uint8_t *slab = smem + wave * slab_bytes;
     const GlobalSrc gs{stream_rsrc(B), B.stream_len};
     const uint64_t wstride = (uint64_t)gridDim.x * (TB / 64) * 64;
     for (uint64_t base = ((uint64_t)blockIdx.x * (TB / 64) + wave) * 64; base < rows; base += wstride) {
@@ -81,7 +91,7 @@ __device__ __forceinline__ void tree_rows(const TreeBufs &B, uint32_t x, uint64_
         slo = (long long)uniform64((uint64_t)slo);
         shi = (long long)uniform64((uint64_t)shi);
         const long long sb = (slo > 64 ? slo - 64 : 0) & ~15ll, se = (shi + 16 + 15) & ~15ll;
-        if (slo < shi && se - sb <= TSLAB) {
+        if (slab_bytes && slo < shi && se - sb <= (long long)slab_bytes) {
             for (long long off = 16ll * lane; off < se - sb; off += 1024) {
                 const long long p = sb + off;
                 uint4 v;
@@ -107,11 +117,11 @@ __device__ __forceinline__ void tree_rows(const TreeBufs &B, uint32_t x, uint64_
 // element count of every list field (m.field(tag), internal/types/msg.go:466-475; OpenList,
 // internal/types/list.go:22-25: errors => an empty list).
 __global__ __launch_bounds__(TB) void tree_index_kernel(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x,
-                                                         uint64_t rows) {
+                                                         uint64_t rows, uint32_t slab) {
     const TreeDesc &D = *Dp;
     const TreeBufs &B = *Bp;
     const TTable &T = D.t[x];
-    tree_rows(B, x, rows, [&](const auto &s, uint64_t row, long long lo, long long hi, bool) {
+    tree_rows(B, x, rows, slab, [&](const auto &s, uint64_t row, long long lo, long long hi, bool) {
         const RecInfo ri = rec_open(s, lo, hi);
         const long long ds = ri.tr.dstart;
         for (uint32_t k = 0; k < T.nd; k++) {
@@ -128,44 +138,49 @@ __global__ __launch_bounds__(TB) void tree_index_kernel(const TreeDesc *Dp, cons
     });
 }
 
-// Per owner row: the range of every element of list table y (List.GetBytes,
-// internal/types/list.go:100-116: end > dataSize => nil; start > end => Go panics).
+// Per owner row of table x: the range of every element of each of x's list tables y (one pass
+// over the owner rows for all of them: List.GetBytes, internal/types/list.go:100-116: end >
+// dataSize => nil; start > end => Go panics).
 __global__ __launch_bounds__(TB) void tree_expand_kernel(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x,
-                                                          uint32_t y, uint64_t rows) {
+                                                          uint64_t rows, uint32_t slab) {
     const TreeDesc &D = *Dp;
     const TreeBufs &B = *Bp;
-    const TField &F = D.f[D.t[y].field];
-    tree_rows(B, x, rows, [&](const auto &s, uint64_t row, long long lo, long long hi, bool) {
+    tree_rows(B, x, rows, slab, [&](const auto &s, uint64_t row, long long lo, long long hi, bool) {
         const RecInfo ri = rec_open(s, lo, hi);
         const long long ds = ri.tr.dstart;
-        const long long end = rec_field_end(s, ri, F.tag, F.rank);
-        const ListInfo li = list_at(s, (long long)ds, end >= 0 ? ds + end : ds);
-        uint2 *out = B.rng[y] + B.cnt[y][row];
-        for (uint32_t j = 0; j < li.count; j++) {
-            uint32_t a, b;
-            if (li.big) {
-                b = be32_at(s, li.tstart + 4ll * j);
-                a = j ? be32_at(s, li.tstart + 4ll * (j - 1)) : 0;
-            } else {
-                b = be16_at(s, li.tstart + 2ll * j);
-                a = j ? be16_at(s, li.tstart + 2ll * (j - 1)) : 0;
+        for (uint32_t y = x + 1; y < D.ntables; y++) {
+            const TTable &Ty = D.t[y];
+            if (Ty.parent != (int)x || Ty.rel != REL_MANY) continue;
+            const TField &F = D.f[Ty.field];
+            const long long end = rec_field_end(s, ri, F.tag, F.rank);
+            const ListInfo li = list_at(s, (long long)ds, end >= 0 ? ds + end : ds);
+            uint2 *out = B.rng[y] + B.cnt[y][row];
+            for (uint32_t j = 0; j < li.count; j++) {
+                uint32_t a, b;
+                if (li.big) {
+                    b = be32_at(s, li.tstart + 4ll * j);
+                    a = j ? be32_at(s, li.tstart + 4ll * (j - 1)) : 0;
+                } else {
+                    b = be16_at(s, li.tstart + 2ll * j);
+                    a = j ? be16_at(s, li.tstart + 2ll * (j - 1)) : 0;
+                }
+                uint2 r;
+                if (b > li.dsize) r = make_uint2(0, 0);           // nil element
+                else if (a > b) r = make_uint2(RNG_PANIC, 0);      // Go panics on the slice
+                else r = make_uint2((uint32_t)(li.dstart + a), (uint32_t)(li.dstart + b));
+                out[j] = r;
             }
-            uint2 r;
-            if (b > li.dsize) r = make_uint2(0, 0);           // nil element
-            else if (a > b) r = make_uint2(RNG_PANIC, 0);      // Go panics on the slice
-            else r = make_uint2((uint32_t)(li.dstart + a), (uint32_t)(li.dstart + b));
-            out[j] = r;
         }
     });
 }
 
 // Every column of table x.
 __global__ __launch_bounds__(TB) void tree_decode_kernel(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x,
-                                                          uint64_t rows) {
+                                                          uint64_t rows, uint32_t slab) {
     const TreeDesc &D = *Dp;
     const TreeBufs &B = *Bp;
     const TTable &T = D.t[x];
-    tree_rows(B, x, rows, [&](const auto &s, uint64_t row, long long lo, long long hi, bool panic) {
+    tree_rows(B, x, rows, slab, [&](const auto &s, uint64_t row, long long lo, long long hi, bool panic) {
         uint32_t st = ST_OK;
         if (T.shape == SHAPE_VALUE) {
             const TField &F = D.f[T.field];
@@ -426,11 +441,75 @@ __global__ __launch_bounds__(SCAN_T) void scan_apply_kernel(const uint32_t *in, 
     if (out32 && blockIdx.x == 0 && threadIdx.x == 0) out32[n] = (uint32_t)*total;
 }
 
+// The same three passes over several u32 arrays of n elements at once (the list tables of one
+// owner table): array j = blockIdx.y (tiles, apply) / blockIdx.x (top); out32 in place allowed.
+struct ScanMulti {
+    const uint32_t *in[TREE_MAX_T];
+    uint32_t *out32[TREE_MAX_T];
+    uint64_t *ws[TREE_MAX_T];
+    uint64_t *total[TREE_MAX_T];
+};
+
+__global__ __launch_bounds__(SCAN_T) void scan_tiles_multi_kernel(ScanMulti m, uint64_t n) {
+    __shared__ uint64_t sh[17];
+    const uint32_t j = blockIdx.y;
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_PER;
+    uint64_t v = 0;
+    for (int k = 0; k < SCAN_PER; k++)
+        if (base + k < n) v += m.in[j][base + k];
+    uint64_t tot;
+    block_excl_scan(v, sh, tot);
+    if (threadIdx.x == 0) m.ws[j][blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SCAN_T) void scan_top_multi_kernel(ScanMulti m, uint64_t ntiles) {
+    __shared__ uint64_t sh[17];
+    const uint32_t j = blockIdx.x;
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < ntiles; b += SCAN_T) {
+        const uint64_t i = b + threadIdx.x;
+        const uint64_t v = i < ntiles ? m.ws[j][i] : 0;
+        uint64_t tot;
+        const uint64_t e = block_excl_scan(v, sh, tot);
+        if (i < ntiles) m.ws[j][i] = carry + e;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) *m.total[j] = carry;
+}
+
+__global__ __launch_bounds__(SCAN_T) void scan_apply_multi_kernel(ScanMulti m, uint64_t n) {
+    __shared__ uint64_t sh[17];
+    const uint32_t j = blockIdx.y;
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_PER;
+    uint32_t v[SCAN_PER];
+    uint64_t sum = 0;
+    for (int k = 0; k < SCAN_PER; k++) {
+        v[k] = base + k < n ? m.in[j][base + k] : 0;
+        sum += v[k];
+    }
+    uint64_t tot;
+    uint64_t p = m.ws[j][blockIdx.x] + block_excl_scan(sum, sh, tot);
+    for (int k = 0; k < SCAN_PER; k++) {
+        if (base + k < n) m.out32[j][base + k] = (uint32_t)p;
+        p += v[k];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) m.out32[j][n] = (uint32_t)*m.total[j];
+}
+
 __global__ void tree_err_kernel(const uint32_t *err, uint64_t *total) {
     if (*err) *total = ~0ull;
 }
 
 size_t scan_ws_bytes(uint64_t n) { return ((n + SCAN_TILE - 1) / SCAN_TILE + 1) * sizeof(uint64_t); }
+
+// k exclusive scans of n >= 1 elements each (ScanMulti filled for j < k), three launches
+int launch_scan_multi(const ScanMulti &m, uint32_t k, uint64_t n, hipStream_t st) {
+    const uint64_t tiles = std::max<uint64_t>(1, (n + SCAN_TILE - 1) / SCAN_TILE);
+    hipLaunchKernelGGL(scan_tiles_multi_kernel, dim3((unsigned)tiles, k), dim3(SCAN_T), 0, st, m, n);
+    hipLaunchKernelGGL(scan_top_multi_kernel, dim3(k), dim3(SCAN_T), 0, st, m, tiles);
+    hipLaunchKernelGGL(scan_apply_multi_kernel, dim3((unsigned)tiles, k), dim3(SCAN_T), 0, st, m, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 // exclusive scan of in[0, n) (in place allowed for out32); *total (device) = the sum
 int launch_scan(const uint32_t *in, uint64_t n, uint32_t *out32, uint64_t *out64, uint64_t *ends64, uint64_t *ws,
@@ -704,23 +783,31 @@ int spec_tree_decoder_index(spec_tree_decoder *d, const uint8_t *stream_bytes, u
             }
         }
         if (!upload()) return SPEC_E_HIP;
-        if (R) hipLaunchKernelGGL(tree_index_kernel, dim3(row_grid(R)), dim3(TB), TREE_LDS, st, Dd, Bd, x, R);
-        // every list child: counts -> begin (in place), its total into totals[y]; then ONE copy of
-        // the totals to the host and one sync for all of this table's lists
-        bool lists = false;
+        const uint32_t slab = tree_slab(stream_len, R);
+        if (R) hipLaunchKernelGGL(tree_index_kernel, dim3(row_grid(R)), dim3(TB), (TB / 64) * slab, st, Dd, Bd, x, R, slab);
+        // every list child: counts -> begin (in place), its total into totals[y] (one batched scan
+        // for all of them); then ONE copy of the totals to the host and one sync
+        ScanMulti sm;
+        uint32_t nl = 0;
         for (uint32_t y = x + 1; y < L.nt; y++) {
             if (L.desc.t[y].parent != (int)x || L.desc.t[y].rel != REL_MANY) continue;
-            lists = true;
-            if (d->scan_ws.reserve(scan_ws_bytes(R))) return SPEC_E_HIP;
             uint64_t *tot_y = (uint64_t *)d->total.p + y;
             if (R == 0) {
                 (void)hipMemsetAsync(B.cnt[y], 0, sizeof(uint32_t), st);
                 (void)hipMemsetAsync(tot_y, 0, sizeof(uint64_t), st);
-            } else if (launch_scan(B.cnt[y], R, B.cnt[y], nullptr, nullptr, (uint64_t *)d->scan_ws.p, tot_y, st)) {
-                return SPEC_E_HIP;
             }
+            sm.in[nl] = B.cnt[y];
+            sm.out32[nl] = B.cnt[y];
+            sm.total[nl] = tot_y;
+            nl++;
         }
-        if (!lists) continue;
+        if (!nl) continue;
+        if (R) {
+            const size_t wsb = (scan_ws_bytes(R) + 255) & ~(size_t)255;
+            if (d->scan_ws.reserve(wsb * nl)) return SPEC_E_HIP;
+            for (uint32_t j = 0; j < nl; j++) sm.ws[j] = (uint64_t *)((uint8_t *)d->scan_ws.p + wsb * j);
+            if (launch_scan_multi(sm, nl, R, st)) return SPEC_E_HIP;
+        }
         uint64_t tot[TREE_MAX_T];
         if (hipMemcpyAsync(tot, d->total.p, sizeof(uint64_t) * L.nt, hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)
@@ -732,10 +819,7 @@ int spec_tree_decoder_index(spec_tree_decoder *d, const uint8_t *stream_bytes, u
             B.rng[y] = (uint2 *)d->rng[y].p;
         }
         if (!upload()) return SPEC_E_HIP;
-        for (uint32_t y = x + 1; y < L.nt; y++) {
-            if (L.desc.t[y].parent != (int)x || L.desc.t[y].rel != REL_MANY) continue;
-            if (R) hipLaunchKernelGGL(tree_expand_kernel, dim3(row_grid(R)), dim3(TB), TREE_LDS, st, Dd, Bd, x, y, R);
-        }
+        if (R) hipLaunchKernelGGL(tree_expand_kernel, dim3(row_grid(R)), dim3(TB), (TB / 64) * slab, st, Dd, Bd, x, R, slab);
     }
     // tables whose owner has no rows to index (empty batch / no message children) keep 0 rows
     for (uint32_t y = 1; y < L.nt; y++)
@@ -781,7 +865,8 @@ int spec_tree_decoder_decode(spec_tree_decoder *d, void *const *columns, void *s
                 return SPEC_E_HIP;
             }
         }
-        if (R) hipLaunchKernelGGL(tree_decode_kernel, dim3(row_grid(R)), dim3(TB), TREE_LDS, st, Dd, Bd, x, R);
+        const uint32_t slab = tree_slab(B.stream_len, R);
+        if (R) hipLaunchKernelGGL(tree_decode_kernel, dim3(row_grid(R)), dim3(TB), (TB / 64) * slab, st, Dd, Bd, x, R, slab);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
