@@ -282,33 +282,37 @@ __global__ __launch_bounds__(TB) void tree_write_kernel(const TreeDesc *Dp, cons
     const TreeBufs &B = *Bp;
     const TTable &T = D.t[x];
     if (!B.out || *B.err || *B.total > B.out_cap) return;
+    extern __shared__ uint32_t tw_ends[]; // MESSAGE tables: [wave][field][lane]
+    uint32_t *ends = tw_ends + (threadIdx.x >> 6) * (uint32_t)T.nd * 64 + (threadIdx.x & 63);
     for (uint64_t row = grid_first(); row < rows; row += grid_stride()) {
         const uint64_t start = x == 0 ? B.offsets[row] : B.pos[x][row];
         if (start == ~0ull) continue; // a row no written owner placed (absent message / list)
         if (x == 0 && B.ends_out) B.ends_out[row] = start + B.size[0][row];
-        BEmit em{B.out, start};
+        BEmit em{B.out, start, start};
         if (T.shape == SHAPE_VALUE) {
             const TField &F = D.f[T.field];
             emit_value(em, B, D, F.col, F.elem, row);
+            em.finish();
             continue;
         }
         if (T.shape == SHAPE_STRUCT) {
             emit_struct(em, B, D, T.field, row);
+            em.finish();
             continue;
         }
         // a message (internal/writer/writer.go:376-553): fields in write order, each field's
-        // end offset (relative to the message start) kept for the table
-        uint32_t ends[TREE_MAX_D];
+        // end offset (relative to the message start) kept for the table, in LDS
+        // ([field][lane] per wave: a per-lane array indexed at run time would live in scratch)
         uint32_t maxtag = 0, nf = 0;
         for (uint32_t k = 0; k < T.nd; k++) {
             const uint32_t fi = D.direct[T.d0 + k];
             const TField &F = D.f[fi];
-            ends[k] = 0xffffffffu; // absent
+            ends[k * 64] = 0xffffffffu; // absent
             if (F.kind == K_MESSAGE || F.kind == K_LIST) {
                 if (!cell(B, D, F.present, row)[0]) continue;
                 if (F.kind == K_MESSAGE) {
                     B.pos[F.table][row] = em.pos; // the sub-message, written by table F.table
-                    em.pos += B.size[F.table][row];
+                    em.skip(B.size[F.table][row]);
                 } else {
                     // elements (written by table F.table), then EncodeListTable's table and trailer
                     bool e2 = false;
@@ -318,7 +322,7 @@ __global__ __launch_bounds__(TB) void tree_write_kernel(const TreeDesc *Dp, cons
                     const uint64_t lstart = em.pos;
                     for (uint32_t j = j0; j < j1; j++) {
                         B.pos[F.table][j] = em.pos;
-                        em.pos += B.size[F.table][j];
+                        em.skip(B.size[F.table][j]);
                     }
                     uint64_t off = 0;
                     for (uint32_t j = j0; j < j1; j++) {
@@ -336,7 +340,7 @@ __global__ __launch_bounds__(TB) void tree_write_kernel(const TreeDesc *Dp, cons
                 if (F.kind == K_ANY && ((const uint2 *)cell(B, D, F.col, row))->y == 0) continue;
                 emit_value(em, B, D, F.col, F.kind, row);
             }
-            ends[k] = (uint32_t)(em.pos - start);
+            ends[k * 64] = (uint32_t)(em.pos - start);
             nf++;
             maxtag = F.tag > maxtag ? F.tag : maxtag;
         }
@@ -346,15 +350,15 @@ __global__ __launch_bounds__(TB) void tree_write_kernel(const TreeDesc *Dp, cons
         // internal/writer/stack_msg.go:37-61), present fields only (encode/msg.go:58-72)
         for (uint32_t k = 0; k < T.nd; k++) {
             const uint32_t fi = D.sorted[T.d0 + k];
-            uint32_t slot = 0;
-            while (D.direct[T.d0 + slot] != fi) slot++;
-            if (ends[slot] == 0xffffffffu) continue;
+            const uint32_t e = ends[D.sslot[T.d0 + k] * 64];
+            if (e == 0xffffffffu) continue;
             em.be(D.f[fi].tag, big ? 2 : 1);
-            em.be(ends[slot], big ? 4 : 2);
+            em.be(e, big ? 4 : 2);
         }
         em.rvarint(data);
         em.rvarint((uint64_t)nf * (big ? 6 : 3));
         em.put1(big ? T_BIG_MESSAGE : T_MESSAGE);
+        em.finish();
     }
 }
 
@@ -666,6 +670,9 @@ bool build_layout(const spec_tree *tr, Layout &L) {
                 for (int q = (int)k; q > 0 && D.f[srt[q - 1]].tag >= D.f[srt[q]].tag; q--) std::swap(srt[q - 1], srt[q]);
             }
             for (uint32_t k = 0; k < T.nd; k++) D.f[srt[k]].rank = (uint16_t)k;
+            for (uint32_t k = 0; k < T.nd; k++)
+                for (uint32_t q = 0; q < T.nd; q++)
+                    if (D.direct[T.d0 + q] == srt[k]) D.sslot[T.d0 + k] = (uint16_t)q;
         }
         if ((T.status_col = (int16_t)add_col(L, x, d, SPEC_COL_STATUS, 0, 1)) < 0) return false;
         t.ncolumns = (uint16_t)(L.nc - t.first_column);
@@ -997,7 +1004,11 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
     for (uint32_t x = 1; ok && out && x < L.nt; x++)
         if (rows[x]) ok = hipMemsetAsync(B->pos[x], 0xff, rows[x] * sizeof(uint64_t), st) == hipSuccess;
     for (uint32_t x = 0; ok && out && x < L.nt; x++)
-        if (rows[x]) hipLaunchKernelGGL(tree_write_kernel, dim3(row_grid(rows[x])), dim3(TB), 0, st, Dd, Bd, x, rows[x]);
+        if (rows[x]) {
+            const TTable &T = L.desc.t[x];
+            const size_t lds = T.shape == SHAPE_MESSAGE ? (size_t)(TB / 64) * T.nd * 64 * sizeof(uint32_t) : 0;
+            hipLaunchKernelGGL(tree_write_kernel, dim3(row_grid(rows[x])), dim3(TB), lds, st, Dd, Bd, x, rows[x]);
+        }
     const hipError_t e = hipGetLastError();
     delete B;
     delete Lp;

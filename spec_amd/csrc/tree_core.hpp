@@ -52,6 +52,7 @@ struct TreeDesc {
     TTable t[TREE_MAX_T];
     uint16_t direct[TREE_MAX_F];
     uint16_t sorted[TREE_MAX_F];
+    uint16_t sslot[TREE_MAX_F]; // sorted[d0 + k]'s index in direct[d0 ..] (its write slot)
     uint16_t members[TREE_MAX_F];
     uint16_t width[TREE_MAX_C];
 };
@@ -427,10 +428,45 @@ __device__ __forceinline__ TreeListSize list_size(const TreeBufs &B, const TreeD
 
 // Byte emitter over the output (one lane writes one row's own bytes; child rows are written by
 // later launches into the gaps this one skips).
+// A row's bytes at out[pos..]: bytes are merged into the dword they fall in and stored as whole
+// dwords (a byte store per byte costs a VMEM instruction per byte); the row's first and last
+// dwords, which it shares with the neighbouring rows (other lanes), are stored bytewise from
+// `lo` (the row start) and up to the end (finish()).  skip(n) jumps over a child's bytes (a
+// sub-message, list elements) written by a LATER launch: a dword stored across such a gap may
+// hold zeros for the child's bytes, which the child's own launch then overwrites.
 struct BEmit {
     uint8_t *out;
     uint64_t pos;
-    __device__ __forceinline__ void put1(uint32_t b) { out[pos++] = (uint8_t)b; }
+    uint64_t lo;    // first byte of the row (bytes below belong to another row)
+    uint32_t w = 0; // pending bytes of the dword holding pos
+    __device__ __forceinline__ void store_pending(uint64_t base, uint64_t end) { // bytes [base, end) of w
+        if (base >= lo && end == base + 4) {
+            *(uint32_t *)(out + base) = w;
+        } else {
+            for (uint64_t q = base > lo ? base : lo; q < end; q++) out[q] = (uint8_t)(w >> (8 * (q - base)));
+        }
+    }
+    __device__ __forceinline__ void put1(uint32_t b) {
+        w |= (b & 0xffu) << (8 * (pos & 3));
+        pos++;
+        if ((pos & 3) == 0) {
+            store_pending(pos - 4, pos);
+            w = 0;
+        }
+    }
+    __device__ __forceinline__ void skip(uint64_t n) {
+        if (!n) return;
+        const uint64_t np = pos + n;
+        if ((np & ~3ull) != (pos & ~3ull)) {
+            if (pos & 3) store_pending(pos & ~3ull, (pos & ~3ull) + 4); // the gap's bytes: the child's
+            w = 0;
+        }
+        pos = np;
+    }
+    __device__ __forceinline__ void finish() {
+        if (pos & 3) store_pending(pos & ~3ull, pos);
+        w = 0;
+    }
     __device__ __forceinline__ void rvarint(uint64_t v) { // oracle/compactint.c so_put_reverse_*
         const uint32_t L = vlen64(v);
         for (uint32_t i = 0; i < L; i++) put1(((uint32_t)(v >> (7 * (L - 1 - i))) & 0x7f) | (i ? 0x80 : 0));
