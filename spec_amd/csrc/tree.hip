@@ -500,6 +500,17 @@ __global__ __launch_bounds__(SCAN_T) void scan_apply_multi_kernel(ScanMulti m, u
     if (blockIdx.x == 0 && threadIdx.x == 0) m.out32[j][n] = (uint32_t)*m.total[j];
 }
 
+// Every child table's row positions to ~0 (unplaced) in one launch: table blockIdx.y
+struct PosFill {
+    uint64_t *p[TREE_MAX_T];
+    uint64_t n[TREE_MAX_T];
+};
+__global__ __launch_bounds__(256) void tree_pos_fill_kernel(PosFill f) {
+    uint64_t *p = f.p[blockIdx.y];
+    const uint64_t n = f.n[blockIdx.y];
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) p[i] = ~0ull;
+}
+
 __global__ void tree_err_kernel(const uint32_t *err, uint64_t *total) {
     if (*err) *total = ~0ull;
 }
@@ -1001,8 +1012,19 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
     // an encoder error: total = all-ones
     if (ok) hipLaunchKernelGGL(tree_err_kernel, dim3(1), dim3(1), 0, st, (const uint32_t *)B->err, total);
     // child rows start unplaced: only rows their owner writes get a position
-    for (uint32_t x = 1; ok && out && x < L.nt; x++)
-        if (rows[x]) ok = hipMemsetAsync(B->pos[x], 0xff, rows[x] * sizeof(uint64_t), st) == hipSuccess;
+    if (ok && out && L.nt > 1) {
+        PosFill pf;
+        uint64_t most = 0;
+        for (uint32_t x = 1; x < L.nt; x++) {
+            pf.p[x - 1] = B->pos[x];
+            pf.n[x - 1] = rows[x];
+            most = std::max(most, rows[x]);
+        }
+        if (most) {
+            const unsigned gx = (unsigned)std::min<uint64_t>((most + 255) / 256, 1024);
+            hipLaunchKernelGGL(tree_pos_fill_kernel, dim3(gx, L.nt - 1), dim3(256), 0, st, pf);
+        }
+    }
     for (uint32_t x = 0; ok && out && x < L.nt; x++)
         if (rows[x]) {
             const TTable &T = L.desc.t[x];
