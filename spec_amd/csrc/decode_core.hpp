@@ -489,14 +489,30 @@ __device__ __forceinline__ RecInfo rec_open(const Src &s, typename Src::pos_t rs
         ri.nent = ri.tr.tsize / (ri.tr.big ? 6u : 3u);
     }
     if (ri.ok) {
+        // the tags 8 entries at a time, every read of a step issued before any is compared (one
+        // dependent read per entry costs a memory round trip per entry when parsing from HBM)
         const pos_t tstart = (pos_t)ri.tr.tstart;
+        const uint32_t esz = ri.tr.big ? 6u : 3u;
         uint32_t prev = 0;
-        for (uint32_t i = 0; i < ri.nent; i++) {
-            pos_t p = tstart + (pos_t)i * (ri.tr.big ? 6 : 3);
-            uint32_t tg = ri.tr.big ? ((s.u8(p) << 8) | s.u8(p + 1)) : s.u8(p);
-            if (i > 0 && tg <= prev) ri.sorted = false;
-            prev = tg;
+        bool sorted = true;
+        for (uint32_t i0 = 0; i0 < ri.nent; i0 += 8) {
+            uint32_t tg[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint32_t i = i0 + u < ri.nent ? i0 + u : ri.nent - 1;
+                const pos_t p = tstart + (pos_t)(i * esz);
+                const uint32_t b0 = s.u8(p), b1 = s.u8(p + 1);
+                tg[u] = ri.tr.big ? ((b0 << 8) | b1) : b0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint32_t i = i0 + u;
+                const bool in = i < ri.nent;
+                sorted = sorted & !(in & (i > 0) & (tg[u] <= prev));
+                prev = in ? tg[u] : prev;
+            }
         }
+        ri.sorted = sorted;
     }
     return ri;
 }
