@@ -145,6 +145,7 @@ def dist_setup(args):
 
 
 _COLL_DEV = "cuda"
+_RESULT_OUT = None  # multi-rank: the original stdout (fd 1 itself goes to stderr)
 
 
 def barrier(dist):
@@ -595,6 +596,13 @@ def main(argv=None):
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         launch_ranks(args, argv if argv is not None else sys.argv[1:])
         return
+    global _RESULT_OUT
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        # the collective libraries print to fd 1 (gloo: "[Gloo] Rank k is connected ..."): send
+        # everything but the result line to stderr, so stdout carries exactly one JSON line
+        sys.stdout.flush()
+        _RESULT_OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
     run(args, env)
 
 
@@ -739,7 +747,7 @@ def run(args, env):
             "checks": checks,
         }
         line.update(extras)
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=_RESULT_OUT or sys.stdout, flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
