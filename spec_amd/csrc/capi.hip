@@ -323,7 +323,7 @@ static int nested_args(spec::NestedArgs &a, const spec_nested_schema *schema, co
 int spec_decode_nested_index(const spec_nested_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
                              const uint64_t *ends, uint64_t n, void *workspace, size_t workspace_size,
                              uint64_t *total_items, void *stream) {
-    spec::NestedArgs a;
+    spec::NestedArgs a{};
     int rc = nested_args(a, schema, stream_bytes, stream_len, ends, n, workspace, workspace_size);
     if (rc) return rc;
     if (!total_items) return SPEC_E_INVALID_ARGUMENT;
@@ -337,7 +337,7 @@ int spec_decode_nested(const spec_nested_schema *schema, const uint8_t *stream_b
                        const uint64_t *ends, uint64_t n, void *const *outer_columns, uint8_t *status,
                        uint32_t *item_begin, void *const *item_columns, uint8_t *item_status, uint64_t item_cap,
                        void *workspace, size_t workspace_size, void *stream) {
-    spec::NestedArgs a;
+    spec::NestedArgs a{};
     int rc = nested_args(a, schema, stream_bytes, stream_len, ends, n, workspace, workspace_size);
     if (rc) return rc;
     if (n == 0) return SPEC_OK;
@@ -365,7 +365,7 @@ int spec_decode_nested_onepass(const spec_nested_schema *schema, const uint8_t *
                                uint32_t *item_begin, void *const *item_columns, uint8_t *item_status,
                                uint64_t item_cap, void *workspace, size_t workspace_size, uint64_t *total_items,
                                void *stream) {
-    spec::NestedArgs a;
+    spec::NestedArgs a{};
     int rc = nested_args(a, schema, stream_bytes, stream_len, ends, n, workspace, workspace_size);
     if (rc) return rc;
     if (!total_items) return SPEC_E_INVALID_ARGUMENT;

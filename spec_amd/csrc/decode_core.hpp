@@ -74,6 +74,7 @@ struct NestedArgs {
     uint64_t *group_base; // workspace: per 64-record group item total, then exclusive offsets
     uint64_t *total;      // device: total items
     uint32_t slab;        // LDS bytes per wave
+    uint32_t xcd;         // decode pass: 1 = XCD-aware block order (grid a multiple of 8)
 };
 
 constexpr int DEC_WAVES = 4; // waves per block of the nested kernels

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void nested_decode_ranges_kernel(NestedArgs a)
     nested_decode_body<RuntimeSpec, RuntimeSpec, false, true>(a);
 }
 
-int g_nested_mode = NESTED_TAILCOUNT;
+int g_nested_mode = NESTED_XCD;
 
 } // namespace
 
@@ -118,7 +118,7 @@ int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream) {
     }
     a.slab = nested_slab_for_mode(avg_record);
     const uint64_t groups = (a.n + 63) / 64;
-    if (g_nested_mode == NESTED_TAILCOUNT) {
+    if (g_nested_mode == NESTED_TAILCOUNT || g_nested_mode == NESTED_XCD) {
         hipLaunchKernelGGL(nested_count_tail_kernel, dim3((unsigned)((groups + 3) / 4)), dim3(256), 0, stream, a);
     } else {
         dim3 grid((unsigned)((groups + DEC_WAVES - 1) / DEC_WAVES)), block(64 * DEC_WAVES);
@@ -134,11 +134,14 @@ int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream) {
 int launch_nested_decode(const spec_nested_schema *schema, NestedArgs a, double avg_record, hipStream_t stream) {
     if (a.n == 0) return 0;
     a.slab = nested_slab_for_mode(avg_record);
+    a.xcd = g_nested_mode == NESTED_XCD ? 1u : 0u;
     const int mode = g_nested_mode >= NESTED_HALVES ? NESTED_GROUPS : g_nested_mode;
     const int j = jit_launch_nested(schema, a, mode, stream);
     if (j != 0) return j > 0 ? 0 : -1;
     const uint64_t groups = (a.n + 63) / 64;
-    dim3 grid((unsigned)((groups + DEC_WAVES - 1) / DEC_WAVES)), block(64 * DEC_WAVES);
+    unsigned blocks = (unsigned)((groups + DEC_WAVES - 1) / DEC_WAVES);
+    if (a.xcd) blocks = (blocks + 7) / 8 * 8;
+    dim3 grid(blocks), block(64 * DEC_WAVES);
     if (mode == NESTED_RANGES)
         hipLaunchKernelGGL(nested_decode_ranges_kernel, grid, block,
                            (size_t)DEC_WAVES * (a.slab + NESTED_RANGE_BYTES), stream, a);
@@ -182,6 +185,6 @@ int launch_nested_onepass(const spec_nested_schema *schema, NestedArgs a, double
 
 extern "C" void spec_set_nested_mode(int mode) {
     if (mode == spec::NESTED_GROUPS || mode == spec::NESTED_RANGES || mode == spec::NESTED_HALVES ||
-        mode == spec::NESTED_TAILCOUNT)
+        mode == spec::NESTED_TAILCOUNT || mode == spec::NESTED_XCD)
         spec::g_nested_mode = mode;
 }

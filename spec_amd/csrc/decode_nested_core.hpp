@@ -466,7 +466,15 @@ __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
         if (lane == 0) t = atomicAdd((unsigned int *)&a.group_base[ngroups], 1u);
         g = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
     } else {
-        g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+        // blocks are dealt round-robin to the 8 XCDs: with xcd = 1, block b takes the b/8-th slot
+        // of XCD b%8's contiguous share, so neighbouring groups (sharing the item columns' cache
+        // lines) are written through one L2
+        uint64_t blk = blockIdx.x;
+        if (a.xcd) {
+            const uint64_t per = (gridDim.x + 7) / 8;
+            blk = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+        }
+        g = blk * (blockDim.x >> 6) + wave;
     }
     const uint64_t base = g * 64;
     if (base >= a.n) return;

@@ -455,7 +455,9 @@ int jit_launch_nested(const spec_nested_schema *schema, const NestedArgs &a, int
     size_t size = sizeof(args);
     void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                      HIP_LAUNCH_PARAM_END};
-    const unsigned grid = (unsigned)((a.n + 63) / 64);
+    unsigned grid = (unsigned)((a.n + 63) / 64);
+    if (args.xcd && mode != NESTED_ONEPASS) grid = (grid + 7) / 8 * 8; // 8 equal XCD shares
+    else args.xcd = 0;
     const size_t lds = a.slab + (mode == NESTED_RANGES ? NESTED_RANGE_BYTES : 0u);
     hipError_t rc = hipModuleLaunchKernel(e->fn[mode], grid, 1, 1, 64, 1, 1, (unsigned)lds, stream, nullptr, extra);
     return rc == hipSuccess ? 1 : -1;

@@ -45,8 +45,9 @@ int launch_nested_onepass(const spec_nested_schema *schema, NestedArgs a, double
 // mode: NESTED_ONEPASS (look-back kernel), NESTED_GROUPS (a wave per group after the index
 // kernels, items found by an owner search), NESTED_RANGES (same, items from ranges precomputed
 // into LDS by their records' lanes), NESTED_HALVES (as GROUPS, slabs for half a group),
-// NESTED_TAILCOUNT (as GROUPS, the count pass from each record's last 64 bytes: the default)
-enum { NESTED_ONEPASS = 0, NESTED_GROUPS = 1, NESTED_RANGES = 2, NESTED_HALVES = 3, NESTED_TAILCOUNT = 4 };
+// NESTED_TAILCOUNT (as GROUPS, the count pass from each record's last 64 bytes), NESTED_XCD (as
+// TAILCOUNT with an XCD-aware block order for the decode pass: the default)
+enum { NESTED_ONEPASS = 0, NESTED_GROUPS = 1, NESTED_RANGES = 2, NESTED_HALVES = 3, NESTED_TAILCOUNT = 4, NESTED_XCD = 5 };
 int jit_launch_nested(const spec_nested_schema *schema, const NestedArgs &a, int mode, hipStream_t stream);
 bool nested_lookback(); // SPEC_AMD_LOOKBACK=1: spec_decode_nested_onepass runs the look-back kernel
 long long jit_compile_only_nested(const spec_nested_schema *schema);

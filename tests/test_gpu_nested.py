@@ -25,14 +25,14 @@ def kernel(request):
     spec_amd.set_jit(True)
 
 
-MODE_IDS = {"twopass": 1, "twopass-ranges": 2, "twopass-halves": 3, "twopass-tail": 4}
+MODE_IDS = {"twopass": 1, "twopass-ranges": 2, "twopass-halves": 3, "twopass-tail": 4, "twopass-xcd": 5}
 
 
 def check_nested(dev, stream, ends, label="",
-                 modes=("twopass", "twopass-ranges", "twopass-halves", "twopass-tail", "onepass", "onepass-small-cap")):
+                 modes=("twopass", "twopass-ranges", "twopass-halves", "twopass-tail", "twopass-xcd", "onepass", "onepass-small-cap")):
     """Every decode mode against the oracle: index + decode (items found by the owner search,
     items from precomputed LDS ranges, half-group slabs, the count pass from tail windows vs
-    the staged-span count: spec_set_nested_mode 1 / 2 / 3 / 4), one pass with room for
+    the staged-span count, XCD-aware decode order: spec_set_nested_mode 1 / 2 / 3 / 4 / 5), one pass with room for
     every item, one pass that first runs out of item room (and decodes again with the total)."""
     stream = np.ascontiguousarray(stream, dtype=np.uint8)
     ends = np.ascontiguousarray(ends, dtype=np.uint64)
@@ -43,12 +43,12 @@ def check_nested(dev, stream, ends, label="",
     L = spec_amd.lib()
     for mode in modes:
         cap = 1 if mode == "onepass-small-cap" else None
-        L.spec_set_nested_mode(MODE_IDS.get(mode, 4))
+        L.spec_set_nested_mode(MODE_IDS.get(mode, 5))
         try:
             got = _check_nested_mode(dev, d_stream, d_ends, want, len(ends), f"{label} [{mode}]",
                                      onepass=not mode.startswith("twopass"), item_cap=cap)
         finally:
-            L.spec_set_nested_mode(4)
+            L.spec_set_nested_mode(5)
     return got, want
 
 

@@ -42,7 +42,7 @@ def main():
     L = spec_amd.lib()
     modes = {}
     ref_items = [c.clone() for c in d.items]
-    for mode, name in ((1, "groups"), (2, "ranges"), (3, "halves"), (4, "tailcount")):
+    for mode, name in ((1, "groups"), (2, "ranges"), (3, "halves"), (4, "tailcount"), (5, "xcd")):
         L.spec_set_nested_mode(mode)
         for c in d.items:
             c.zero_()
@@ -53,7 +53,7 @@ def main():
         same = all(torch.equal(a_, b_) for a_, b_ in zip(d.items, ref_items)) and int(d.status.sum()) == 0
         modes[name] = {"decode_ms": round(dec_ms, 4), "index_ms": round(idx_ms, 4), "twopass_ms": round(both_ms, 4),
                        "same": bool(same)}
-    L.spec_set_nested_mode(4)
+    L.spec_set_nested_mode(5)
     res["modes"] = modes
     one_ms, _ = bench.kernel_time_events(d.decode_onepass, 20)
     torch.cuda.synchronize()
