@@ -431,7 +431,7 @@ int spec_encode_nested(const spec_nested_schema *schema, const void *const *oute
     if (nitems && !item_columns) return SPEC_E_INVALID_ARGUMENT;
     if (out && !ends && n) return SPEC_E_INVALID_ARGUMENT;
     if (workspace_size < spec_encode_nested_workspace_size(n)) return SPEC_E_WORKSPACE;
-    spec::NestedEncodeArgs a;
+    spec::NestedEncodeArgs a{};
     memset(&a, 0, sizeof(a));
     a.n = n;
     fill_enc_fields(a.outer, &schema->outer, outer_columns);
@@ -466,7 +466,7 @@ int spec_encode_flat_size(const spec_schema *schema, const void *const *columns,
     if (rc) return rc;
     if (!columns || !workspace) return SPEC_E_INVALID_ARGUMENT;
     if (workspace_size < spec_encode_flat_workspace_size(n)) return SPEC_E_WORKSPACE;
-    spec::EncodeArgs a;
+    spec::EncodeArgs a{};
     fill_encode_args(a, schema, columns, n);
     a.block_sums = (uint64_t *)workspace;
     a.total = total;
@@ -482,7 +482,7 @@ int spec_encode_flat(const spec_schema *schema, const void *const *columns,
     if (rc) return rc;
     if (!columns || !workspace || (n && (!ends || !out))) return SPEC_E_INVALID_ARGUMENT;
     if (workspace_size < spec_encode_flat_workspace_size(n)) return SPEC_E_WORKSPACE;
-    spec::EncodeArgs a;
+    spec::EncodeArgs a{};
     fill_encode_args(a, schema, columns, n);
     for (uint32_t f = 0; f < schema->nfields; f++) {
         int k = schema->fields[f].kind;

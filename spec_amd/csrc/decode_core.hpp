@@ -929,7 +929,7 @@ __device__ __forceinline__ void decode_flat_entry(const DecodeArgs &a) {
         decode_flat_once<Spec>(a);
 }
 
-bool xcd_swizzle_decode(); // SPEC_AMD_XCD=1 (decode_flat.hip)
+bool xcd_swizzle_decode(); // XCD-aware block order, default on; SPEC_AMD_XCD=0 off (decode_flat.hip)
 
 // Launch shape of the flat decode: per-wave slab, waves per block, grid.
 struct DecodeLaunch {
