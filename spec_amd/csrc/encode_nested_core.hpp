@@ -47,6 +47,7 @@ struct NestedEncodeArgs {
     uint64_t *block_sums;
     uint64_t nblocks;
     uint64_t *total;
+    uint32_t xcd; // write pass: 1 = XCD-aware block order (grid padded to a multiple of 8)
 };
 
 constexpr int NENC_BLOCK = 256;               // records per block (4 waves, one record per lane)
@@ -219,9 +220,9 @@ struct LaneRecord {
 
 template <class IP>
 __device__ __forceinline__ LaneRecord lane_record(const NestedEncodeArgs &a, uint32_t *pre, int lane, bool check,
-                                                  bool &err) {
+                                                  bool &err, uint64_t blk) {
     LaneRecord L;
-    L.r = (uint64_t)blockIdx.x * NENC_BLOCK + threadIdx.x;
+    L.r = blk * NENC_BLOCK + threadIdx.x;
     L.valid = L.r < a.n;
     L.b = a.item_begin[L.valid ? L.r : a.n];
     L.e = L.valid ? a.item_begin[L.r + 1] : L.b;
@@ -261,7 +262,7 @@ __device__ __forceinline__ void nested_enc_size_body(const NestedEncodeArgs &a, 
     if (threadIdx.x == 0) *errs = 0;
     __syncthreads();
     bool err = false;
-    const LaneRecord L = lane_record<IP>(a, pre, lane, a.check_heaps, err);
+    const LaneRecord L = lane_record<IP>(a, pre, lane, a.check_heaps, err, blockIdx.x);
     const typename OP::Rec orec = OP::load(a.outer, L.valid ? L.r : a.n - 1);
     ListSize ls;
     const RecSize rs = lane_record_size<OP>(a, L, orec, pre, a.check_heaps, err, ls);
@@ -285,6 +286,11 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
     const uint64_t total = a.block_sums[a.nblocks];
     if (total > a.out_cap) return; // capacity error or encoder error (total == ~0)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // blocks dealt to the 8 XCDs in contiguous shares (xcd = 1): neighbouring blocks, whose
+    // outputs share a cache line at each boundary, write through one L2
+    uint64_t blk = blockIdx.x;
+    if (a.xcd) blk = (blockIdx.x & 7) * ((gridDim.x + 7) / 8) + (blockIdx.x >> 3);
+    if (blk >= a.nblocks) return;
     if (threadIdx.x < a.outer.nfields) inv_outer[a.outer.order[threadIdx.x]] = (uint8_t)threadIdx.x;
     if (threadIdx.x < a.item.nfields) inv_item[a.item.order[threadIdx.x]] = (uint8_t)threadIdx.x;
     uint32_t *pre = (uint32_t *)(smem + NENC_HEAD + wave * NENC_WAVE_LDS);
@@ -292,9 +298,9 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
 
     bool err = false;
     // the outer record's loads first: in flight while the item prefix is built
-    const uint64_t r0 = (uint64_t)blockIdx.x * NENC_BLOCK + threadIdx.x;
+    const uint64_t r0 = blk * NENC_BLOCK + threadIdx.x;
     const typename OP::Rec orec = OP::load(a.outer, r0 < a.n ? r0 : a.n - 1);
-    const LaneRecord L = lane_record<IP>(a, pre, lane, false, err);
+    const LaneRecord L = lane_record<IP>(a, pre, lane, false, err, blk);
     ListSize ls;
     RecSize rs = lane_record_size<OP>(a, L, orec, pre, false, err, ls);
     if (!L.valid) rs.total = 0;
@@ -305,12 +311,12 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
     }
     if (lane == 63) wsum[wave] = x;
     __syncthreads();
-    uint64_t pre_b = a.block_sums[blockIdx.x];
+    uint64_t pre_b = a.block_sums[blk];
     for (int w = 0; w < wave; w++) pre_b += wsum[w];
     const uint64_t start = pre_b + x - rs.total;
     if (L.valid) a.ends[L.r] = start + rs.total;
 
-    const uint64_t wbase = (uint64_t)blockIdx.x * NENC_BLOCK + wave * 64;
+    const uint64_t wbase = blk * NENC_BLOCK + wave * 64;
     if (wbase >= a.n) return;
     const uint64_t S = __builtin_amdgcn_readfirstlane((uint32_t)start) |
                        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(start >> 32)) << 32);

@@ -473,11 +473,13 @@ int jit_launch_nested_encode(const spec_nested_schema *schema, const NestedEncod
     const Entry *e = lookup_nested_encode(schema);
     if (!e) return 0;
     NestedEncodeArgs args = a;
+    args.xcd = write && xcd_swizzle_decode() ? 1u : 0u;
     size_t size = sizeof(args);
     void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                      HIP_LAUNCH_PARAM_END};
     const unsigned lds = (unsigned)(write ? nenc_write_lds_bytes() : nenc_size_lds_bytes());
-    hipError_t rc = hipModuleLaunchKernel(e->fn[write ? 1 : 0], (unsigned)a.nblocks, 1, 1, NENC_BLOCK, 1, 1, lds,
+    const unsigned grid = (unsigned)(args.xcd ? (a.nblocks + 7) / 8 * 8 : a.nblocks);
+    hipError_t rc = hipModuleLaunchKernel(e->fn[write ? 1 : 0], grid, 1, 1, NENC_BLOCK, 1, 1, lds,
                                           stream, nullptr, extra);
     return rc == hipSuccess ? 1 : -1;
 }
