@@ -96,14 +96,18 @@ def launch_ranks(args, argv):
     for p in procs:
         p.start()
     rc = 0
-    for p in procs:
+    live = list(procs)
+    while live and not rc:  # poll all ranks: the first failure ends the others at once
+        for p in list(live):
+            p.join(timeout=0.2)
+            if p.exitcode is not None:
+                live.remove(p)
+                if p.exitcode:
+                    rc = p.exitcode
+                    break
+    for p in live:
+        p.kill()
         p.join()
-        if p.exitcode and not rc:
-            rc = p.exitcode
-    if rc:
-        for p in procs:
-            if p.is_alive():
-                p.kill()
     sys.exit(rc if rc > 0 else (1 if rc else 0))
 
 
@@ -146,6 +150,27 @@ def dist_setup(args):
 
 _COLL_DEV = "cuda"
 _RESULT_OUT = None  # multi-rank: the original stdout (fd 1 itself goes to stderr)
+
+
+def device_key(dev) -> int:
+    """A 63-bit key of the physical GPU this rank runs on (its UUID, else host + index)."""
+    import hashlib
+    import socket
+
+    try:
+        ident = str(torch.cuda.get_device_properties(dev).uuid)
+    except Exception:
+        ident = f"{socket.gethostname()}:{dev.index}"
+    return int.from_bytes(hashlib.sha1(ident.encode()).digest()[:8], "little") >> 1
+
+
+def distinct_devices(dist, dev) -> int:
+    """How many physical GPUs the ranks use (a gloo rehearsal puts every rank on one)."""
+    if dist is None:
+        return 1
+    keys = [torch.zeros(1, dtype=torch.int64, device=_COLL_DEV) for _ in range(dist.get_world_size())]
+    dist.all_gather(keys, torch.tensor([device_key(dev)], dtype=torch.int64, device=_COLL_DEV))
+    return len({int(k.item()) for k in keys})
 
 
 def barrier(dist):
@@ -447,8 +472,8 @@ def shard_leg(args, dist, rank, world, dev):
     if dist is None:
         out["gather"] = "n/a (one rank: the columns are already on rank 0)"
         return out
-    sizes = [shard_bounds(nblocks, world, k) for k in range(world)]
-    sizes = [(k1 - k0) * bsz * row for k0, k1 in sizes]
+    recs = [(k1 - k0) * bsz for k0, k1 in (shard_bounds(nblocks, world, k) for k in range(world))]
+    sizes = [PackedColumns.nbytes_for(FLAT16, r) for r in recs]
 
     def step():
         decode_all()
@@ -462,7 +487,7 @@ def shard_leg(args, dist, rank, world, dev):
     barrier(dist)
     dg_s = max_over_ranks(dist, (time.perf_counter() - t0) / reps)
     out.update({"decode_gather_ms": round(dg_s * 1e3, 3), "decode_gather_mmsg_s": round(nblocks * bsz / dg_s / 1e6, 1),
-                "gathered_gb_s": round(sum(sizes[1:]) / dg_s / 1e9, 1),
+                "gathered_gb_s": round(sum(recs[1:]) * row / dg_s / 1e9, 1),
                 "gather": "one dist.gather of each rank's packed columns+status (RCCL grouped send/recv)"})
     if rank == 0 and not args.no_verify:
         from oracle import oracle as O
@@ -473,7 +498,7 @@ def shard_leg(args, dist, rank, world, dev):
         st, en = O.encode_flat_batch(FLAT16.tags, FLAT16.kinds, [c[:m] for c in cols],
                                      [heaps.get(f) for f in range(16)], m)
         want, wst = O.decode_flat_batch(FLAT16.tags, FLAT16.kinds, st, en, FLAT16.widths, host_cores())
-        last = PackedColumns(FLAT16, sizes[-1] // row, "cpu", buf=parts[-1].cpu())
+        last = PackedColumns(FLAT16, recs[-1], "cpu", buf=parts[-1].cpu())
         r0 = last.n - bsz
         ok = all(np.array_equal(last.cols[f][r0:r0 + m].numpy(), want[f]) for f in range(16))
         out["gathered_sample_vs_oracle"] = bool(ok and np.array_equal(last.status[r0:r0 + m].numpy(), wst))
@@ -608,6 +633,7 @@ def main(argv=None):
 
 def run(args, env):
     dist, rank, world, dev = dist_setup(args)
+    devices = distinct_devices(dist, dev)
     n = args.records
     cols, heaps, d_cols, d_heaps, stream, ends = make_batch(n, args.seed + rank, dev)
     stream_bytes = stream.numel()
@@ -723,7 +749,7 @@ def run(args, env):
             "metric": METRIC,
             "value": round(value, 2),
             "unit": "Mmsg/s",
-            "n_gpus": world,
+            "n_gpus": devices,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
@@ -735,6 +761,8 @@ def run(args, env):
             "config": {"workload": "flat16-decode", "records_per_gpu": n,
                        "mean_record_bytes": round(mean_rec, 1), "stream_bytes_per_gpu": stream_bytes,
                        "parallelism": f"record-sharded x{world}, no collective",
+                       "ranks": world, "distinct_devices": devices,
+                       "rehearsal": devices < world,
                        "backend": args.backend if world > 1 else None, "env": env},
             "gb_s": round(total_records * (mean_rec + 8 + COLUMN_BYTES + 1) / elapsed / 1e9, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

@@ -117,11 +117,16 @@ typedef struct spec_nested_schema {
  * A spec_tree describes a record message as fields in PRE-ORDER: each field names its enclosing
  * field (`parent`, an earlier index; -1 = the record).  Enclosing fields are
  *   SPEC_KIND_MESSAGE            its children are the sub-message's fields (write order);
- *   SPEC_KIND_STRUCT             its children are the struct's members (scalar kinds, declaration
- *                                order; the struct is decoded members-last-first, as generated
- *                                Decode does: internal/lang/generator/struct.go:75-113);
+ *   SPEC_KIND_STRUCT             its children are the struct's members in declaration order:
+ *                                scalar kinds or other structs ("structs support only value
+ *                                types or other structs", internal/lang/model/struct_field.go:
+ *                                57-70), at most SPEC_TREE_MAX_STRUCT_DEPTH structs deep; a
+ *                                struct is decoded members-last-first, an inner struct through its
+ *                                own DecodeXxx, as generated Decode does
+ *                                (internal/lang/generator/struct.go:75-113), and encoded members-
+ *                                first then EncodeStruct (struct.go:115-142);
  *   SPEC_KIND_LIST, elem MESSAGE its children are the item message's fields;
- *   SPEC_KIND_LIST, elem STRUCT  its children are the struct's members.
+ *   SPEC_KIND_LIST, elem STRUCT  its children are the struct's members (as above).
  * A list of scalars (elem = a scalar kind) has no children.  Enums are SPEC_KIND_INT32
  * (internal/lang/generator/enum.go:69-92).  Recursive types (pkg1.spec Submessage.next) are
  * unrolled to the depth the caller reads, exactly as a reader only opens what it accesses.
@@ -133,11 +138,12 @@ typedef struct spec_nested_schema {
  *   [BEGIN]  (LIST tables) uint32 [owner rows + 1]: row i's elements are [begin[i], begin[i+1])
  *   per direct field, in field order:
  *     scalar          VALUE  m.<Kind>(tag)                          (internal/types/msg.go:219-421)
- *     STRUCT          VALUE per member: OpenXxx(m.FieldRaw(tag))    (msg.go:139-150)
+ *     STRUCT          VALUE per scalar member, inner structs' members in place (pre-order):
+ *                     OpenXxx(m.FieldRaw(tag))                       (msg.go:139-150)
  *     ANY             VALUE spec_span of m.Field(tag) = OpenValue   (msg.go:108-124, value.go:18-31)
  *     MESSAGE, LIST   PRESENT uint8 m.HasField(tag)                 (msg.go:101-106)
  *   a list of scalars: VALUE = ValueList.Get(i) (list_value.go:87-92); a list of structs: a
- *   VALUE per member;
+ *   VALUE per scalar member (pre-order);
  *   STATUS uint8: records OpenMessageErr's class; sub-messages MessageErr's class (0 if absent);
  *   list items OpenItemErr's class or SPEC_STATUS_PANIC (Go panics: element start > end);
  *   list values / structs SPEC_STATUS_INVALID_VALUE when GetErr fails; any row whose struct or
@@ -149,6 +155,7 @@ typedef struct spec_nested_schema {
 #define SPEC_TREE_MAX_TABLES 64
 #define SPEC_TREE_MAX_COLUMNS 512
 #define SPEC_TREE_MAX_DIRECT 64 /* direct fields of one message / members of one struct */
+#define SPEC_TREE_MAX_STRUCT_DEPTH 8 /* structs nested in structs (the outermost counts 1) */
 
 typedef struct spec_tree_field {
     uint16_t tag;    /* field tag (ignored for struct members) */

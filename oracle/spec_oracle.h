@@ -263,6 +263,12 @@ so_err so_field_struct(so_writer *w, uint16_t tag, int nm, const uint8_t *kinds,
                        const uint8_t *const *heaps);
 so_err so_elem_struct(so_writer *w, int nm, const uint8_t *kinds, const uint8_t *const *vals,
                       const uint8_t *const *heaps);
+/* structs with inner structs: nm members in pre-order, an inner struct = SO_KIND_STRUCT followed
+ * by its nmem[i] direct members; `top` = the outer struct's direct members */
+so_err so_field_struct_tree(so_writer *w, uint16_t tag, int top, int nm, const uint8_t *kinds,
+                            const uint8_t *const *vals, const uint8_t *const *heaps, const int *nmem);
+so_err so_elem_struct_tree(so_writer *w, int top, int nm, const uint8_t *kinds, const uint8_t *const *vals,
+                           const uint8_t *const *heaps, const int *nmem);
 so_err so_value_int64(so_writer *w, int64_t v);
 so_err so_value_string(so_writer *w, const char *v, size_t len);
 /* end(): MessageWriter.Build / ListWriter.Build / ValueWriter.Build (writer.go:141-188) */

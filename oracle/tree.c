@@ -67,6 +67,21 @@ static int add_col(tree *t, int table, int field, int role, int kind, int width)
     return t->nc++;
 }
 
+/* The columns of struct field sf in table x: its members in declaration order, an inner
+ * struct's members (recursively) in its place. */
+static int struct_cols(tree *t, int x, int sf) {
+    for (int j = sf + 1; j < t->nf; j++) {
+        if (t->f[j].parent != sf) continue;
+        int c;
+        if (t->f[j].kind == SO_KIND_STRUCT)
+            c = struct_cols(t, x, j);
+        else
+            c = t->col_of[j] = add_col(t, x, j, ROLE_VALUE, t->f[j].kind, so_kind_width(t->f[j].kind));
+        if (c < 0) return -1;
+    }
+    return 0;
+}
+
 static int build(tree *t, const so_tree_field *f, int nf) {
     memset(t, 0, sizeof(*t));
     t->f = f;
@@ -82,11 +97,19 @@ static int build(tree *t, const so_tree_field *f, int nf) {
             return -1;
         if (p >= 0) {
             int pk = f[p].kind;
-            if (pk == SO_KIND_STRUCT && !scalar(k)) return -1;
-            if (pk == SO_KIND_LIST && f[p].elem == SO_KIND_STRUCT && !scalar(k)) return -1;
+            /* struct members: value types or other structs (model/struct_field.go:57-70) */
+            if (pk == SO_KIND_STRUCT && !scalar(k) && k != SO_KIND_STRUCT) return -1;
+            if (pk == SO_KIND_LIST && f[p].elem == SO_KIND_STRUCT && !scalar(k) && k != SO_KIND_STRUCT) return -1;
             if (pk == SO_KIND_LIST && scalar(f[p].elem)) return -1;
             if (pk != SO_KIND_STRUCT && pk != SO_KIND_MESSAGE && pk != SO_KIND_LIST) return -1;
         }
+    }
+    /* struct nesting depth (at most 8 structs deep, spec_amd.h SPEC_TREE_MAX_STRUCT_DEPTH) */
+    for (int i = 0; i < nf; i++) {
+        int depth = f[i].kind == SO_KIND_STRUCT;
+        for (int p = f[i].parent; p >= 0; p = f[p].parent)
+            depth += f[p].kind == SO_KIND_STRUCT || (f[p].kind == SO_KIND_LIST && f[p].elem == SO_KIND_STRUCT);
+        if (depth > 8) return -1;
     }
     /* tables: the root, then one per MESSAGE / LIST field in field order */
     so_tree_table root = {-1, -1, REL_ROOT, SHAPE_MESSAGE, 0, 0};
@@ -115,6 +138,8 @@ static int build(tree *t, const so_tree_field *f, int nf) {
         if (tb->rel == REL_MANY && (t->begin_col[x] = add_col(t, x, d, ROLE_BEGIN, 0, 4)) < 0) return -1;
         if (tb->shape == SHAPE_VALUE) {
             if ((t->col_of[d] = add_col(t, x, d, ROLE_VALUE, f[d].elem, so_kind_width(f[d].elem))) < 0) return -1;
+        } else if (tb->shape == SHAPE_STRUCT) {
+            if (struct_cols(t, x, d) < 0) return -1;
         } else {
             for (int i = d + 1; i < nf; i++) {
                 if (f[i].parent != d) continue;
@@ -126,9 +151,8 @@ static int build(tree *t, const so_tree_field *f, int nf) {
                     c = t->col_of[i] = add_col(t, x, i, ROLE_VALUE, k, 8);
                 } else if (k == SO_KIND_MESSAGE || k == SO_KIND_LIST) {
                     c = t->present_of[i] = add_col(t, x, i, ROLE_PRESENT, 0, 1);
-                } else { /* struct: one column per member */
-                    for (int j = i + 1; j < nf && c >= 0; j++)
-                        if (f[j].parent == i) c = t->col_of[j] = add_col(t, x, j, ROLE_VALUE, f[j].kind, so_kind_width(f[j].kind));
+                } else { /* struct: one column per scalar member, inner structs' members in place */
+                    c = struct_cols(t, x, i);
                 }
                 if (c < 0) return -1;
             }
@@ -217,32 +241,58 @@ static so_err decode_kind(tree *t, int kind, const uint8_t *b, size_t len, uint8
     return e;
 }
 
+/* Zero the columns of every scalar member of struct sf (inner structs' too). */
+static void zero_struct(tree *t, int sf, uint64_t row) {
+    uint8_t zero[32] = {0};
+    for (int j = sf + 1; j < t->nf; j++) {
+        if (t->f[j].parent != sf) continue;
+        if (t->f[j].kind == SO_KIND_STRUCT)
+            zero_struct(t, j, row);
+        else
+            put(t, t->col_of[j], row, zero, so_kind_width(t->f[j].kind));
+    }
+}
+
 /* Xxx.Decode(b) of a generated struct (generator/struct.go:75-113) over the value ending at
  * b+len, members = the fields whose parent is `sf`.  Members decoded from the LAST to the
- * first; the first error stops the decode, members decoded so far keep their values.
- * Returns ST_OK, ST_INVALID_VALUE (an error), or ST_PANIC (b[len(b)-size:] with size > len). */
-static int decode_struct(tree *t, int sf, const uint8_t *b, size_t len, uint64_t row) {
+ * first over b[:off]; an inner struct member through its own DecodeXxx(b[:off]) = this function
+ * (n = its size); the first error stops the decode, members decoded so far keep their values.
+ * Returns ST_OK, ST_INVALID_VALUE (an error), or ST_PANIC (b[len(b)-size:] with size > len),
+ * and the struct's size in *nsize. */
+static int decode_struct_n(tree *t, int sf, const uint8_t *b, size_t len, uint64_t row, int *nsize) {
     int mem[MAX_F], nm = 0;
     for (int j = sf + 1; j < t->nf; j++)
         if (t->f[j].parent == sf) mem[nm++] = j;
-    uint8_t zero[32] = {0};
-    for (int k = 0; k < nm; k++) put(t, t->col_of[mem[k]], row, zero, so_kind_width(t->f[mem[k]].kind));
+    zero_struct(t, sf, row);
+    *nsize = 0;
     int ds = 0, size = 0;
     if (so_decode_struct(b, len, &ds, &size)) return ST_INVALID_VALUE;
     if (size == 0) return ST_OK;
     if ((size_t)size > len) return ST_PANIC;
+    *nsize = size;
     b = b + len - (size_t)size;
     int n = size - ds;
     int64_t off = (int64_t)size - n; /* = dataSize */
     for (int k = nm - 1; k >= 0; k--) {
-        uint8_t v[32];
+        const int mk = t->f[mem[k]].kind;
         int m = 0;
-        so_err e = decode_kind(t, t->f[mem[k]].kind, b, (size_t)off, v, &m);
-        put(t, t->col_of[mem[k]], row, v, so_kind_width(t->f[mem[k]].kind));
-        if (e) return ST_INVALID_VALUE;
+        if (mk == SO_KIND_STRUCT) {
+            const int st = decode_struct_n(t, mem[k], b, (size_t)off, row, &m);
+            if (st != ST_OK) return st;
+        } else {
+            uint8_t v[32];
+            so_err e = decode_kind(t, mk, b, (size_t)off, v, &m);
+            put(t, t->col_of[mem[k]], row, v, so_kind_width(mk));
+            if (e) return ST_INVALID_VALUE;
+        }
         off -= m;
     }
     return ST_OK;
+}
+
+static int decode_struct(tree *t, int sf, const uint8_t *b, size_t len, uint64_t row) {
+    int n;
+    return decode_struct_n(t, sf, b, len, row, &n);
 }
 
 static void decode_message(tree *t, int x, uint64_t row, const uint8_t *b, size_t len, int item);
@@ -383,19 +433,36 @@ static const uint8_t *cell(tree *t, int c, uint64_t row) {
     return (const uint8_t *)t->cols[c] + row * t->C[c].width;
 }
 
+/* The member list of struct sf for the Writer's struct calls: pre-order (an inner struct is
+ * SO_KIND_STRUCT followed by its members; nmem[] = direct member counts of the structs). */
+static void struct_members(tree *t, int sf, uint64_t row, uint8_t *kinds, const uint8_t **vals, const uint8_t **heaps,
+                           int *nmem, int *nm) {
+    for (int j = sf + 1; j < t->nf; j++) {
+        if (t->f[j].parent != sf) continue;
+        const int at = (*nm)++;
+        kinds[at] = t->f[j].kind;
+        nmem[at] = 0;
+        if (t->f[j].kind == SO_KIND_STRUCT) {
+            vals[at] = NULL;
+            heaps[at] = NULL;
+            for (int q = j + 1; q < t->nf; q++) nmem[at] += t->f[q].parent == j;
+            struct_members(t, j, row, kinds, vals, heaps, nmem, nm);
+        } else {
+            const int c = t->col_of[j];
+            vals[at] = cell(t, c, row);
+            heaps[at] = t->heaps ? t->heaps[c] : NULL;
+        }
+    }
+}
+
 static so_err write_struct(tree *t, so_writer *w, int sf, uint64_t row, int field, uint16_t tag) {
     uint8_t kinds[MAX_F];
     const uint8_t *vals[MAX_F], *heaps[MAX_F];
-    int nm = 0;
-    for (int j = sf + 1; j < t->nf; j++)
-        if (t->f[j].parent == sf) {
-            const int c = t->col_of[j];
-            kinds[nm] = t->f[j].kind;
-            vals[nm] = cell(t, c, row);
-            heaps[nm] = t->heaps ? t->heaps[c] : NULL;
-            nm++;
-        }
-    return field ? so_field_struct(w, tag, nm, kinds, vals, heaps) : so_elem_struct(w, nm, kinds, vals, heaps);
+    int nmem[MAX_F], nm = 0, top = 0;
+    for (int j = sf + 1; j < t->nf; j++) top += t->f[j].parent == sf;
+    struct_members(t, sf, row, kinds, vals, heaps, nmem, &nm);
+    return field ? so_field_struct_tree(w, tag, top, nm, kinds, vals, heaps, nmem)
+                 : so_elem_struct_tree(w, top, nm, kinds, vals, heaps, nmem);
 }
 
 static uint32_t begin_at(tree *t, int y, uint64_t row) {

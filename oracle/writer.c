@@ -496,13 +496,18 @@ static so_err encode_kind(so_buf *b, int kind, const uint8_t *v, const uint8_t *
 
 /* The generated EncodeXxxTo of a struct (internal/lang/generator/struct.go:115-142): every
  * member through its encoder in declaration order, then EncodeStruct(dataSize)
- * (internal/encode/struct.go:14-21). */
-static so_err encode_struct(so_buf *b, int nm, const uint8_t *kinds, const uint8_t *const *vals,
-                            const uint8_t *const *heaps, int *n) {
+ * (internal/encode/struct.go:14-21).  An inner struct member (kinds[i] == SO_KIND_STRUCT,
+ * nmem[i] direct members following it in the arrays) is its own EncodeXxxTo in place.
+ * `top` members from *at on; *at advances past them. */
+static so_err encode_struct_at(so_buf *b, int top, int *at, int nm, const uint8_t *kinds, const uint8_t *const *vals,
+                               const uint8_t *const *heaps, const int *nmem, int *n) {
     int64_t data = 0;
-    for (int i = 0; i < nm; i++) {
+    for (int i = 0; i < top; i++) {
+        if (*at >= nm) return "encode struct: member list too short";
+        const int j = (*at)++;
         int k = 0;
-        so_err e = encode_kind(b, kinds[i], vals[i], heaps ? heaps[i] : NULL, &k);
+        so_err e = kinds[j] == SO_KIND_STRUCT ? encode_struct_at(b, nmem ? nmem[j] : 0, at, nm, kinds, vals, heaps, nmem, &k)
+                                              : encode_kind(b, kinds[j], vals[j], heaps ? heaps[j] : NULL, &k);
         if (e) return e;
         data += k;
     }
@@ -511,6 +516,19 @@ static so_err encode_struct(so_buf *b, int nm, const uint8_t *kinds, const uint8
     if (e) return e;
     *n = (int)(data + k);
     return NULL;
+}
+
+static so_err encode_struct(so_buf *b, int nm, const uint8_t *kinds, const uint8_t *const *vals,
+                            const uint8_t *const *heaps, int *n) {
+    int at = 0;
+    return encode_struct_at(b, nm, &at, nm, kinds, vals, heaps, NULL, n);
+}
+
+static so_err encode_struct_tree(so_buf *b, int top, int nm, const uint8_t *kinds, const uint8_t *const *vals,
+                                 const uint8_t *const *heaps, const int *nmem, int *n) {
+    int at = 0;
+    so_err e = encode_struct_at(b, top, &at, nm, kinds, vals, heaps, nmem, n);
+    return e ? e : (at == nm ? NULL : "encode struct: member list too long");
 }
 
 /* FieldWriter.<Kind>(v) (internal/writer/msg.go:99-211) by column kind */
@@ -534,4 +552,15 @@ so_err so_field_struct(so_writer *w, uint16_t tag, int nm, const uint8_t *kinds,
 so_err so_elem_struct(so_writer *w, int nm, const uint8_t *kinds, const uint8_t *const *vals,
                       const uint8_t *const *heaps) {
     ELEM_OF(encode_struct(w->buf, nm, kinds, vals, heaps, &n_));
+}
+
+/* Structs with inner structs: members in pre-order (see encode_struct_at) */
+so_err so_field_struct_tree(so_writer *w, uint16_t tag, int top, int nm, const uint8_t *kinds,
+                            const uint8_t *const *vals, const uint8_t *const *heaps, const int *nmem) {
+    FIELD_OF(encode_struct_tree(w->buf, top, nm, kinds, vals, heaps, nmem, &n_));
+}
+
+so_err so_elem_struct_tree(so_writer *w, int top, int nm, const uint8_t *kinds, const uint8_t *const *vals,
+                           const uint8_t *const *heaps, const int *nmem) {
+    ELEM_OF(encode_struct_tree(w->buf, top, nm, kinds, vals, heaps, nmem, &n_));
 }

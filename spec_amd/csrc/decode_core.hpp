@@ -92,7 +92,14 @@ __host__ __device__ inline uint32_t decode_slab_bytes(double avg_record, double 
     if (chunks > SLAB_MAX_CHUNKS) return 0;
     return (uint32_t)(SLAB_GUARD + chunks * 1024 + 32);
 }
-__host__ __device__ inline uint32_t nested_slab_bytes(double avg_record) { return decode_slab_bytes(avg_record, 1.16); }
+// The nested kernels run DEC_WAVES waves per block, each with its slab plus (RANGES mode) a 1 KiB
+// item-range window: the block's LDS must stay within gfx950's 160 KiB, so a slab over
+// NESTED_SLAB_MAX is not used (0: the groups parse from HBM).
+constexpr uint32_t NESTED_SLAB_MAX = 163840 / DEC_WAVES - 1024;
+__host__ __device__ inline uint32_t nested_slab_bytes(double avg_record) {
+    const uint32_t s = decode_slab_bytes(avg_record, 1.16);
+    return s <= NESTED_SLAB_MAX ? s : 0u;
+}
 
 // ---- message table lookup --------------------------------------------------------------
 

@@ -580,9 +580,11 @@ bool build_layout(const spec_tree *tr, Layout &L) {
         if (p >= 0) {
             const int pk = f[p].kind;
             if (pk != SPEC_KIND_STRUCT && pk != SPEC_KIND_MESSAGE && pk != SPEC_KIND_LIST) return false;
-            if (pk == SPEC_KIND_STRUCT && !is_scalar(k)) return false;
+            // struct members: value types or other structs (internal/lang/model/struct_field.go:57-70)
+            if (pk == SPEC_KIND_STRUCT && !is_scalar(k) && k != SPEC_KIND_STRUCT) return false;
             if (pk == SPEC_KIND_LIST && is_scalar(f[p].elem)) return false;
-            if (pk == SPEC_KIND_LIST && f[p].elem == SPEC_KIND_STRUCT && !is_scalar(k)) return false;
+            if (pk == SPEC_KIND_LIST && f[p].elem == SPEC_KIND_STRUCT && !is_scalar(k) && k != SPEC_KIND_STRUCT)
+                return false;
         }
         TField &F = D.f[i];
         F.tag = f[i].tag;
@@ -590,7 +592,30 @@ bool build_layout(const spec_tree *tr, Layout &L) {
         F.elem = f[i].elem;
         F.parent = (int16_t)p;
         F.table = F.col = F.present = -1;
+        F.send = (uint16_t)(i + 1);
     }
+    // subtree ends (pre-order: a field's descendants follow it) and struct nesting depth
+    for (uint32_t i = 0; i < nf; i++) {
+        int depth = 0;
+        for (int p = f[i].parent; p >= 0; p = f[p].parent) {
+            D.f[p].send = (uint16_t)std::max<uint32_t>(D.f[p].send, i + 1);
+            if (f[p].kind == SPEC_KIND_STRUCT || (f[p].kind == SPEC_KIND_LIST && f[p].elem == SPEC_KIND_STRUCT)) depth++;
+        }
+        if (f[i].kind == SPEC_KIND_STRUCT) {
+            depth++;
+            if (f[i].parent >= 0 && (f[f[i].parent].kind == SPEC_KIND_STRUCT ||
+                                     (f[f[i].parent].kind == SPEC_KIND_LIST && f[f[i].parent].elem == SPEC_KIND_STRUCT)))
+                D.f[f[i].parent].nested = 1;
+        }
+        if (depth > TREE_MAX_SD) return false;
+    }
+    // a field's subtree must be contiguous (pre-order): every field inside [i + 1, send) descends from i
+    for (uint32_t i = 0; i < nf; i++)
+        for (uint32_t j = i + 1; j < D.f[i].send; j++) {
+            int p = f[j].parent;
+            while (p > (int)i) p = f[p].parent;
+            if (p != (int)i) return false;
+        }
     auto owner = [&](int i) {
         int p = f[i].parent;
         while (p >= 0 && f[p].kind == SPEC_KIND_STRUCT) p = f[p].parent;
@@ -643,9 +668,9 @@ bool build_layout(const spec_tree *tr, Layout &L) {
             if (c < 0) return false;
             D.f[d].col = (int16_t)c;
         } else if (t.shape == SPEC_SHAPE_STRUCT) {
-            for (uint32_t k = 0; k < D.f[d].nmem; k++) {
-                const int j = D.members[D.f[d].mem0 + k];
-                const int c = add_col(L, x, j, SPEC_COL_VALUE, f[j].kind, spec_kind_width(f[j].kind));
+            for (uint32_t j = (uint32_t)d + 1; j < D.f[d].send; j++) { // scalar members, pre-order
+                if (!is_scalar(f[j].kind)) continue;
+                const int c = add_col(L, x, (int)j, SPEC_COL_VALUE, f[j].kind, spec_kind_width(f[j].kind));
                 if (c < 0) return false;
                 D.f[j].col = (int16_t)c;
             }
@@ -663,10 +688,10 @@ bool build_layout(const spec_tree *tr, Layout &L) {
                 } else if (k == SPEC_KIND_MESSAGE || k == SPEC_KIND_LIST) {
                     c = D.f[i].present = (int16_t)add_col(L, x, i, SPEC_COL_PRESENT, 0, 1);
                     T.has_children = 1;
-                } else {
-                    for (uint32_t m = 0; m < D.f[i].nmem && c >= 0; m++) {
-                        const int j = D.members[D.f[i].mem0 + m];
-                        c = D.f[j].col = (int16_t)add_col(L, x, j, SPEC_COL_VALUE, f[j].kind, spec_kind_width(f[j].kind));
+                } else { // a struct: its scalar members (inner structs' in place), pre-order
+                    for (uint32_t j = i + 1; j < D.f[i].send && c >= 0; j++) {
+                        if (!is_scalar(f[j].kind)) continue;
+                        c = D.f[j].col = (int16_t)add_col(L, x, (int)j, SPEC_COL_VALUE, f[j].kind, spec_kind_width(f[j].kind));
                     }
                 }
                 if (c < 0) return false;
@@ -971,7 +996,10 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
         const spec_tree_column &col = L.cols[c];
         const bool spans = col.role == SPEC_COL_VALUE && (col.kind == SPEC_KIND_STRING || col.kind == SPEC_KIND_BYTES ||
                                                          col.kind == SPEC_KIND_ANY);
-        if (col.role != SPEC_COL_STATUS && !columns[c] && rows[col.table]) rc = SPEC_E_INVALID_ARGUMENT;
+        // a BEGIN column has owner rows + 1 entries: needed whenever the owner table has rows
+        // (an owner whose lists are all empty still reads begin[row], begin[row + 1])
+        const uint64_t col_rows = col.role == SPEC_COL_BEGIN ? rows[L.tables[col.table].parent] : rows[col.table];
+        if (col.role != SPEC_COL_STATUS && !columns[c] && col_rows) rc = SPEC_E_INVALID_ARGUMENT;
         if (spans && rows[col.table] && !B->heaps[c]) rc = SPEC_E_INVALID_ARGUMENT;
     }
     for (uint32_t x = 0; x < L.nt; x++) {

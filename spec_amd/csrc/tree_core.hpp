@@ -23,6 +23,7 @@
 namespace spec {
 
 constexpr int TREE_MAX_F = 256, TREE_MAX_T = 64, TREE_MAX_C = 512, TREE_MAX_D = 64;
+constexpr int TREE_MAX_SD = 8; // structs nested in structs (include/spec_amd.h SPEC_TREE_MAX_STRUCT_DEPTH)
 enum : uint32_t { K_STRUCT = 17, K_MESSAGE = 18, K_ANY = 19 };
 enum : uint32_t { REL_ROOT = 0, REL_ONE = 1, REL_MANY = 2 };
 enum : uint32_t { SHAPE_MESSAGE = 0, SHAPE_VALUE = 1, SHAPE_STRUCT = 2 };
@@ -37,6 +38,9 @@ struct TField {
     int16_t present; // MESSAGE / LIST: PRESENT column
     uint16_t rank;   // index of the tag in the writer's table of all direct fields (lookup probe)
     uint16_t nmem, mem0; // STRUCT / LIST<STRUCT>: members[mem0 .. mem0 + nmem)
+    uint16_t send;       // one past the last field of this field's subtree (pre-order)
+    uint8_t nested;      // STRUCT / LIST<STRUCT>: some member is itself a struct
+    uint8_t pad;
 };
 
 struct TTable {
@@ -236,39 +240,93 @@ __device__ __forceinline__ bool decode_value_n(const Src &s, uint32_t kind, type
     return true;
 }
 
+// DecodeStruct (internal/decode/struct.go:14-42) of the value ending at e over [lo, e), then
+// the generated Decode's `b = b[len(b)-size:]` (a panic when size > len(b)): the struct's start S
+// and data size; ST_OK, ST_INVALID_VALUE or ST_PANIC.  e > lo.
+template <class Src>
+__device__ __forceinline__ uint32_t struct_open(const Src &s, long long lo, long long e, long long &S, uint32_t &ds) {
+    if (s.u8((typename Src::pos_t)(e - 1)) != T_STRUCT) return ST_INVALID_VALUE; // invalid type
+    const Tail t = load_tail(s, (typename Src::pos_t)e);
+    int m;
+    ds = (uint32_t)rvarint_bf(tail_r(t), tail_r2(t), e - 1 - lo, 5, m);
+    if (m < 0) return ST_INVALID_VALUE; // invalid data size
+    const long long size = 1 + m + (long long)ds;
+    if (size > e - lo) return ST_PANIC;
+    S = e - size;
+    return ST_OK;
+}
+
 // A generated struct's Decode (internal/lang/generator/struct.go:75-113) over [lo, e):
 // DecodeStruct, then the members from the LAST to the first over b[:off]; the first error
-// stops it and members decoded so far keep their values.  Returns ST_OK, ST_INVALID_VALUE, or
-// ST_PANIC where Go slices b[len(b)-size:] with size > len(b).
+// stops it and members decoded so far keep their values.  An inner struct member is decoded by
+// its own DecodeXxx over b[:off] (its bytes end at off, its lower bound is the outer struct's
+// start), consuming its size.  Returns ST_OK, ST_INVALID_VALUE, or ST_PANIC where Go slices
+// b[len(b)-size:] with size > len(b) (at any depth).
 template <class Src>
 __device__ __forceinline__ uint32_t tree_struct(const Src &s, const TreeDesc &D, const TreeBufs &B, uint32_t sf,
                                                 long long lo, long long e, uint64_t row, long long to_stream) {
     const TField &F = D.f[sf];
     const Val zero = {0, 0, 0, 0};
-    for (uint32_t k = 0; k < F.nmem; k++) {
-        const TField &M = D.f[D.members[F.mem0 + k]];
-        store_kind(B.cols[M.col], row, M.kind, zero);
+    for (uint32_t i = sf + 1; i < F.send; i++) {
+        const TField &M = D.f[i];
+        if (M.kind != K_STRUCT) store_kind(B.cols[M.col], row, M.kind, zero);
     }
     if (e <= lo) return ST_OK;
-    if (s.u8(e - 1) != T_STRUCT) return ST_INVALID_VALUE; // DecodeStruct: invalid type
-    const Tail t = load_tail(s, (typename Src::pos_t)e);
-    int m;
-    const uint32_t ds = (uint32_t)rvarint_bf(tail_r(t), tail_r2(t), e - 1 - lo, 5, m);
-    if (m < 0) return ST_INVALID_VALUE;
-    const long long size = 1 + m + (long long)ds;
-    if (size > e - lo) return ST_PANIC;
-    const long long S = e - size;
+    long long S;
+    uint32_t ds;
+    uint32_t st = struct_open(s, lo, e, S, ds);
+    if (st != ST_OK) return st;
     long long off = S + ds;
-    for (int k = (int)F.nmem - 1; k >= 0; k--) {
-        const TField &M = D.f[D.members[F.mem0 + k]];
-        Val v;
-        int n;
-        const bool ok = decode_value_n(s, M.kind, (typename Src::pos_t)S, (typename Src::pos_t)off, to_stream, v, n);
-        store_kind(B.cols[M.col], row, M.kind, v);
-        if (!ok) return ST_INVALID_VALUE;
-        off -= n;
+    if (!F.nested) {
+        for (int k = (int)F.nmem - 1; k >= 0; k--) {
+            const TField &M = D.f[D.members[F.mem0 + k]];
+            Val v;
+            int n;
+            const bool ok = decode_value_n(s, M.kind, (typename Src::pos_t)S, (typename Src::pos_t)off, to_stream, v, n);
+            store_kind(B.cols[M.col], row, M.kind, v);
+            if (!ok) return ST_INVALID_VALUE;
+            off -= n;
+        }
+        return ST_OK;
     }
-    return ST_OK;
+    // structs inside structs: an explicit stack of the open structs (field, next member, start)
+    uint16_t sfi[TREE_MAX_SD];
+    int16_t kk[TREE_MAX_SD];
+    long long Sb[TREE_MAX_SD];
+    int d = 0;
+    sfi[0] = (uint16_t)sf;
+    kk[0] = (int16_t)F.nmem - 1;
+    Sb[0] = S;
+    for (;;) {
+        if (kk[d] < 0) { // this struct is done: its parent continues below its start
+            if (d == 0) return ST_OK;
+            off = Sb[d];
+            d--;
+            continue;
+        }
+        const uint32_t mi = D.members[D.f[sfi[d]].mem0 + kk[d]];
+        kk[d]--;
+        const TField &M = D.f[mi];
+        if (M.kind == K_STRUCT) {
+            if (off <= Sb[d]) continue; // empty input: DecodeStruct => size 0, the members stay zero
+            long long S2;
+            uint32_t ds2;
+            st = struct_open(s, Sb[d], off, S2, ds2);
+            if (st != ST_OK) return st;
+            d++;
+            sfi[d] = (uint16_t)mi;
+            kk[d] = (int16_t)M.nmem - 1;
+            Sb[d] = S2;
+            off = S2 + ds2;
+        } else {
+            Val v;
+            int n;
+            const bool ok = decode_value_n(s, M.kind, (typename Src::pos_t)Sb[d], (typename Src::pos_t)off, to_stream, v, n);
+            store_kind(B.cols[M.col], row, M.kind, v);
+            if (!ok) return ST_INVALID_VALUE;
+            off -= n;
+        }
+    }
 }
 
 // compactint.ReverseSize (oracle/compactint.c so_reverse_size) over the bytes below e down to lo
@@ -380,16 +438,45 @@ __device__ __forceinline__ uint64_t value_size(const TreeBufs &B, const TreeDesc
     return 0;
 }
 
+// The generated EncodeXxxTo's size (internal/lang/generator/struct.go:115-142): the members'
+// encoded sizes, then EncodeStruct's rvarint(dataSize) | TypeStruct; inner structs likewise.
 __device__ __forceinline__ uint64_t struct_size(const TreeBufs &B, const TreeDesc &D, uint32_t sf, uint64_t row,
                                                 bool &err) {
     const TField &F = D.f[sf];
-    uint64_t data = 0;
-    for (uint32_t k = 0; k < F.nmem; k++) {
-        const TField &M = D.f[D.members[F.mem0 + k]];
-        data += value_size(B, D, M.col, M.kind, row, err);
+    if (!F.nested) {
+        uint64_t data = 0;
+        for (uint32_t k = 0; k < F.nmem; k++) {
+            const TField &M = D.f[D.members[F.mem0 + k]];
+            data += value_size(B, D, M.col, M.kind, row, err);
+        }
+        if (data > MAX_SIZE) err = true; // EncodeStruct: struct too large
+        return data + vlen64(data) + 1;
     }
-    if (data > MAX_SIZE) err = true; // EncodeStruct: struct too large
-    return data + vlen64(data) + 1;
+    uint64_t acc[TREE_MAX_SD];
+    uint16_t endi[TREE_MAX_SD];
+    int d = 0;
+    acc[0] = 0;
+    endi[0] = F.send;
+    auto close = [&]() {
+        const uint64_t data = acc[d];
+        if (data > MAX_SIZE) err = true;
+        d--;
+        acc[d] += data + vlen64(data) + 1;
+    };
+    for (uint32_t i = sf + 1; i < F.send; i++) { // the subtree in pre-order = declaration order
+        while (d > 0 && i >= endi[d]) close();
+        const TField &M = D.f[i];
+        if (M.kind == K_STRUCT) {
+            d++;
+            acc[d] = 0;
+            endi[d] = M.send;
+        } else {
+            acc[d] += value_size(B, D, M.col, M.kind, row, err);
+        }
+    }
+    while (d > 0) close();
+    if (acc[0] > MAX_SIZE) err = true;
+    return acc[0] + vlen64(acc[0]) + 1;
 }
 
 // [begin[row], begin[row + 1]) of list table y, from its BEGIN column (checked)
@@ -538,13 +625,42 @@ __device__ __forceinline__ void emit_value(BEmit &em, const TreeBufs &B, const T
 
 __device__ __forceinline__ void emit_struct(BEmit &em, const TreeBufs &B, const TreeDesc &D, uint32_t sf, uint64_t row) {
     const TField &F = D.f[sf];
-    const uint64_t start = em.pos;
-    for (uint32_t k = 0; k < F.nmem; k++) {
-        const TField &M = D.f[D.members[F.mem0 + k]];
-        emit_value(em, B, D, M.col, M.kind, row);
+    if (!F.nested) {
+        const uint64_t start = em.pos;
+        for (uint32_t k = 0; k < F.nmem; k++) {
+            const TField &M = D.f[D.members[F.mem0 + k]];
+            emit_value(em, B, D, M.col, M.kind, row);
+        }
+        em.rvarint(em.pos - start); // EncodeStruct: rvarint(dataSize) | TypeStruct
+        em.put1(T_STRUCT);
+        return;
     }
-    em.rvarint(em.pos - start); // EncodeStruct: rvarint(dataSize) | TypeStruct
-    em.put1(T_STRUCT);
+    // members in declaration order; an inner struct is its own EncodeXxxTo (members, then
+    // EncodeStruct) in place
+    uint64_t st[TREE_MAX_SD];
+    uint16_t endi[TREE_MAX_SD];
+    int d = 0;
+    st[0] = em.pos;
+    endi[0] = F.send;
+    for (uint32_t i = sf + 1; i < F.send; i++) {
+        while (d > 0 && i >= endi[d]) {
+            em.rvarint(em.pos - st[d]);
+            em.put1(T_STRUCT);
+            d--;
+        }
+        const TField &M = D.f[i];
+        if (M.kind == K_STRUCT) {
+            d++;
+            st[d] = em.pos;
+            endi[d] = M.send;
+        } else {
+            emit_value(em, B, D, M.col, M.kind, row);
+        }
+    }
+    for (; d >= 0; d--) {
+        em.rvarint(em.pos - st[d]);
+        em.put1(T_STRUCT);
+    }
 }
 
 } // namespace spec

@@ -36,22 +36,37 @@ def shard_batch(stream, ends, world: int, rank: int):
     return s, e, b0, (r0, r1)
 
 
+PACK_ALIGN = 256  # column starts in a packed buffer: aligned for the kernels' 4/8/16-byte stores
+
+
+def packed_layout(widths, n: int):
+    """Byte offsets of the columns of n records packed one after another (each start rounded up
+    to PACK_ALIGN), then the status bytes: -> (column offsets, status offset, total bytes)."""
+    offs, off = [], 0
+    for w in widths:
+        offs.append(off)
+        off = (off + n * w + PACK_ALIGN - 1) // PACK_ALIGN * PACK_ALIGN
+    return offs, off, off + n
+
+
 class PackedColumns:
     """Decoded columns + status of n records in one contiguous uint8 buffer (record-major per
-    column): `cols[f]` is a [n, width_f] view, `status` a [n] view.  Pass `cols`/`status` to
-    spec_amd.Decoder so the decode writes the packed layout directly."""
+    column, every column starting on a PACK_ALIGN boundary): `cols[f]` is a [n, width_f] view,
+    `status` a [n] view.  Pass `cols`/`status` to spec_amd.Decoder so the decode writes the
+    packed layout directly."""
 
     def __init__(self, schema: Schema, n: int, device="cuda", buf: torch.Tensor | None = None):
         self.schema, self.n = schema, n
-        self.nbytes = n * (schema.column_bytes + 1)
+        offs, soff, self.nbytes = packed_layout(schema.widths, n)
         self.buf = buf if buf is not None else torch.empty(max(self.nbytes, 1), dtype=torch.uint8, device=device)
         if self.buf.numel() < self.nbytes:
             raise ValueError("packed buffer too small")
-        self.cols, off = [], 0
-        for w in schema.widths:
-            self.cols.append(self.buf[off: off + n * w].view(n, w))
-            off += n * w
-        self.status = self.buf[off: off + n]
+        self.cols = [self.buf[o: o + n * w].view(n, w) for o, w in zip(offs, schema.widths)]
+        self.status = self.buf[soff: soff + n]
+
+    @staticmethod
+    def nbytes_for(schema: Schema, n: int) -> int:
+        return packed_layout(schema.widths, n)[2]
 
 
 def _gather_sizes(nbytes: int, dist, group, device):
@@ -94,16 +109,18 @@ def gather_columns(cols, dist, dst: int = 0, group=None):
         return [] if dist.get_rank(group) == dst else None
     widths = [int(c.shape[1]) for c in cols]
     n_local = int(cols[0].shape[0])
-    packed = torch.cat([c.reshape(-1) for c in cols]) if n_local else cols[0].new_empty(0)
+    offs, cbytes, _ = packed_layout(widths, n_local)
+    packed = cols[0].new_zeros(cbytes + 8)  # the columns, then the record count (int64)
+    for o, c in zip(offs, cols):
+        packed[o: o + c.numel()] = c.reshape(-1)
+    packed[cbytes:].view(torch.int64)[0] = n_local
     parts = gather_packed(packed, dist, dst, group)
     if parts is None:
         return None
-    row = sum(widths)
     out = [[] for _ in cols]
     for p in parts:
-        n_k = p.numel() // row if row else 0
-        off = 0
+        n_k = int(p[-8:].cpu().view(torch.int64)[0])
+        po, _, _ = packed_layout(widths, n_k)
         for f, w in enumerate(widths):
-            out[f].append(p[off: off + n_k * w].view(n_k, w))
-            off += n_k * w
+            out[f].append(p[po[f]: po[f] + n_k * w].view(n_k, w))
     return out

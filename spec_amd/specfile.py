@@ -334,13 +334,7 @@ class SpecSet:
             if kind == "enum":
                 return Kind.INT32
             if kind == "struct":
-                members = []
-                for mname, mtyp in self.files[p].structs[n]:
-                    mk = self.scalar_kind(p, mtyp)
-                    if mk is None:
-                        raise ValueError(f"spec: struct {n}.{mname}: only scalar members have a column kind")
-                    members.append((mname, mk))
-                return Struct(f"{p}.{n}", members)
+                return self.struct(n, p)
             return self.message(n, p, cache)
 
         fields = []
@@ -351,6 +345,24 @@ class SpecSet:
                 fields.append((fname, tag, resolve(typ)))
         msg.fields = fields
         return msg
+
+    def struct(self, name: str, package: str, _seen=()):
+        """tree.Struct of struct `name`: members are value types (scalars, enums) or other structs
+        (internal/lang/model/struct_field.go:57-70); a struct that contains itself is an error."""
+        from .tree import Struct
+
+        if (package, name) in _seen:
+            raise ValueError(f"spec: struct {name} contains itself")
+        members = []
+        for mname, mtyp in self.files[package].structs[name]:
+            mk = self.scalar_kind(package, mtyp)
+            if mk is None:
+                kind, p, n = self._lookup(package, mtyp)
+                if kind != "struct":
+                    raise ValueError(f"spec: struct {name}.{mname}: structs support only value types or other structs")
+                mk = self.struct(n, p, _seen + ((package, name),))
+            members.append((mname, mk))
+        return Struct(f"{package}.{name}", members)
 
     def scalar_kind(self, pkg, typ):
         """Kind of a scalar or enum type name in package pkg, else None."""

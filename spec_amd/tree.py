@@ -36,14 +36,16 @@ ROLE_VALUE, ROLE_PRESENT, ROLE_BEGIN, ROLE_STATUS = 0, 1, 2, 3
 
 
 class Struct:
-    """A .spec struct: members in declaration order (scalar kinds)."""
+    """A .spec struct: members in declaration order, each a scalar kind (Kind.INT32 for an enum)
+    or another Struct ("structs support only value types or other structs",
+    internal/lang/model/struct_field.go:57-70)."""
 
     def __init__(self, name: str, members):
         self.name = name
-        self.members = [(m, Kind(k)) for m, k in members]
+        self.members = [(m, k if isinstance(k, Struct) else Kind(k)) for m, k in members]
         for _, k in self.members:
-            if k not in SCALARS:
-                raise ValueError(f"struct {name}: members must be scalar kinds")
+            if not isinstance(k, Struct) and k not in SCALARS:
+                raise ValueError(f"struct {name}: members must be scalar kinds or structs")
 
 
 class Message:
@@ -148,8 +150,7 @@ class Tree:
                     self._add_message(e, i, path + "[].", d2, max_depth)
                 elif isinstance(e, Struct):
                     i = self._add(path, tag, Kind.LIST, Kind.STRUCT, parent)
-                    for m, k in e.members:
-                        self._add(f"{path}[].{m}", 0, k, 0, i)
+                    self._add_members(e, i, f"{path}[].")
                 else:
                     self._add(path, tag, Kind.LIST, Kind(e), parent)
             elif isinstance(typ, Message):
@@ -161,10 +162,19 @@ class Tree:
                 self._add_message(typ, i, path + ".", d2, max_depth)
             elif isinstance(typ, Struct):
                 i = self._add(path, tag, Kind.STRUCT, 0, parent)
-                for m, k in typ.members:
-                    self._add(f"{path}.{m}", 0, k, 0, i)
+                self._add_members(typ, i, path + ".")
             else:
                 self._add(path, tag, Kind(typ), 0, parent)
+
+    def _add_members(self, struct, parent, prefix):
+        """A struct's members in declaration order (pre-order: a struct member's own members
+        follow it)."""
+        for m, k in struct.members:
+            if isinstance(k, Struct):
+                j = self._add(prefix + m, 0, Kind.STRUCT, 0, parent)
+                self._add_members(k, j, f"{prefix}{m}.")
+            else:
+                self._add(prefix + m, 0, k, 0, parent)
 
     # -- layout (spec_tree_layout) --
     def _layout(self):
@@ -338,6 +348,9 @@ class TreeEncoder:
                 h = heaps.get(c.name)
                 if h is None:
                     raise ValueError(f"missing heap for {c.name}")
+                if not isinstance(h, torch.Tensor) or h.dtype != torch.uint8 or not h.is_contiguous() \
+                        or h.device != v.device:
+                    raise ValueError(f"heap {c.name} must be a contiguous uint8 tensor on {v.device}")
                 keep.append(h)
                 hp[c.index] = h.data_ptr()
                 hl[c.index] = h.numel()

@@ -57,6 +57,28 @@ def test_argument_validation_without_gpu():
     assert L.spec_encode_flat_size(C.byref(s), cols, 1000, C.c_void_p(1), ws - 1, None, None) == -5
 
 
+def test_encode_tree_requires_begin_columns_without_gpu():
+    """spec_encode_tree: a list table's BEGIN column has owner rows + 1 entries, so it is required
+    whenever the OWNER has rows, even when every list is empty (0 element rows); rejected before
+    any HIP call."""
+    from spec_amd.tree import ROLE_BEGIN, ROLE_STATUS, ListOf, Message, Tree
+
+    L = spec_amd.lib()
+    tree = Tree(Message("M", [("a", 1, spec_amd.Kind.INT32), ("l", 2, ListOf(spec_amd.Kind.INT64))]))
+    rows = (C.c_uint64 * len(tree.tables))(5, 0)  # 5 records, no list elements
+    nc = len(tree.columns)
+    cols = (C.c_void_p * nc)()
+    for c in tree.columns:
+        if c.role != ROLE_STATUS:
+            cols[c.index] = 1  # never dereferenced: validation fails first
+    begin = next(c for c in tree.columns if c.role == ROLE_BEGIN)
+    cols[begin.index] = None
+    ws = L.spec_encode_tree_workspace_size(C.byref(tree.c), rows)
+    total = (C.c_uint64 * 1)()
+    rc = L.spec_encode_tree(C.byref(tree.c), cols, None, None, rows, None, 0, None, C.c_void_p(1), ws, C.c_void_p(C.addressof(total)), None)
+    assert rc == -1
+
+
 def test_schema_limits():
     import pytest
 

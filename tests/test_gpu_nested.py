@@ -80,6 +80,20 @@ def test_nested_parity(dev, kernel, n):
     check_nested(dev, stream, ends, f"nested n={n}")
 
 
+@pytest.mark.parametrize("name_len", [(330, 368), (300, 330), (360, 420)])
+def test_nested_large_records_generic(dev, name_len):
+    """Mean records of ~510-600 B on the precompiled generic kernels: the slab a 4-wave block
+    would need crosses the 160 KiB LDS of a workgroup around 545 B, where the nested slab falls
+    back to 0 (parse from HBM) instead of failing the launch."""
+    spec_amd.set_jit(False)
+    try:
+        w = workload.nested(3000, seed=len(name_len) + name_len[0], name_len=name_len)
+        stream, ends = O.encode_nested_batch(w)
+        check_nested(dev, stream, ends, f"large records {name_len}")
+    finally:
+        spec_amd.set_jit(True)
+
+
 def test_nested_golden(dev):
     g = np.load(os.path.join(GOLDEN, "nested_small.npz"), allow_pickle=False)
     got, _ = check_nested(dev, g["stream"], g["ends"], "golden")

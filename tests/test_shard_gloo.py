@@ -93,3 +93,20 @@ def test_shard_and_gather_world2():
         p.join(timeout=240)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=5) is True
+
+
+def test_packed_columns_aligned():
+    """Every packed column starts on a 256-byte boundary (the decode kernels store 4/8/16-byte
+    elements; odd shard sizes such as 2049 records must not misalign the later columns)."""
+    from spec_amd import FLAT16
+    from spec_amd.shard import PACK_ALIGN, PackedColumns
+
+    for n in (0, 1, 2049, 2050, 100_003):
+        pc = PackedColumns(FLAT16, n, "cpu")
+        base = pc.buf.data_ptr()
+        assert all((c.data_ptr() - base) % PACK_ALIGN == 0 for c in pc.cols)
+        assert (pc.status.data_ptr() - base) % PACK_ALIGN == 0
+        assert pc.nbytes == PackedColumns.nbytes_for(FLAT16, n) >= n * (FLAT16.column_bytes + 1)
+        assert [tuple(c.shape) for c in pc.cols] == [(n, w) for w in FLAT16.widths]
+        ends = [c.data_ptr() - base + c.numel() for c in pc.cols]
+        assert all(e <= s for e, s in zip(ends, [c.data_ptr() - base for c in pc.cols[1:]] + [pc.status.data_ptr() - base]))

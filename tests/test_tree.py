@@ -202,3 +202,107 @@ def test_oracle_struct_reverse_decode_partial():
     rec = val + bytes([1, 0, len(val), len(val), 3, 0x50])
     rows, got = oracle_decode(tree, np.frombuffer(rec, np.uint8), np.array([len(rec)], np.uint64))
     assert got[1].view(np.int32)[0, 0] == 2 and got[0].view(np.int32)[0, 0] == 0
+
+
+# ---- structs inside structs (internal/lang/model/struct_field.go:57-70) ----
+
+def _nested_tree():
+    from tests.tree_helpers import nested_struct_tree
+
+    return nested_struct_tree()
+
+
+def test_layout_matches_oracle_nested_structs():
+    tree = _nested_tree()
+    _layout_equal(tree)
+    # inner structs' members sit in place, pre-order, with dotted names
+    names = [c.name for c in tree.tables[0].columns]
+    assert names[:6] == ["id", "outer.a", "outer.in.x", "outer.in.y", "outer.s", "outers?"]
+    assert "deep.m.j.y" in names and "deep.o.in.x" in names
+    assert [c.name for c in tree.tables[1].columns][:4] == ["outers#begin", "outers[].a", "outers[].in.x", "outers[].in.y"]
+
+
+def test_nested_struct_known_bytes():
+    """Outer{a 1, in Inner{x -1, y "hi"}, s ""}: the inner struct is Inner's own EncodeInnerTo
+    (members, then EncodeStruct) inside Outer's data (generator/struct.go:115-142)."""
+    inner = Struct("Inner", [("x", Kind.INT32), ("y", Kind.STRING)])
+    tree = Tree(Message("M", [("o", 1, Struct("Outer", [("a", Kind.INT32), ("in", inner), ("s", Kind.STRING)]))]))
+    heaps = {"o.in.y": np.frombuffer(b"hi", np.uint8).copy(), "o.s": np.zeros(1, np.uint8)}
+    cols = {"o.a": np.array([[1, 0, 0, 0]], np.uint8), "o.in.x": np.full((1, 4), 0xff, np.uint8),
+            "o.in.y": np.array([[0, 2]], np.uint32).view(np.uint8), "o.s": np.zeros((1, 8), np.uint8),
+            "#status": np.zeros((1, 1), np.uint8)}
+    stream, ends = oracle_encode(tree, cols, heaps, 1)
+    inner_b = bytes([0x01, 0x0B]) + b"hi" + bytes([0x00, 0x02, 0x3C])
+    inner_b += bytes([len(inner_b), 0x5A])
+    outer_data = bytes([0x02, 0x0B]) + inner_b + bytes([0x00, 0x00, 0x3C])
+    outer_b = outer_data + bytes([len(outer_data), 0x5A])
+    assert bytes(stream) == outer_b + bytes([1, 0, len(outer_b), len(outer_b), 3, 0x50])
+    rows, got = oracle_decode(tree, stream, ends)
+    g = {c.name: v for c, v in zip(tree.columns, got)}
+    assert g["o.a"].view(np.int32)[0, 0] == 1 and g["o.in.x"].view(np.int32)[0, 0] == -1
+    off, ln = g["o.in.y"].view(np.uint32)[0]
+    assert bytes(stream[off:off + ln]) == b"hi" and g["#status"][0, 0] == 0
+
+
+def test_nested_struct_reverse_decode_partial():
+    """An inner struct's Decode errs: the outer stops there; members decoded before (the ones
+    after it in declaration order) keep their values, and the inner struct keeps what it decoded
+    (generator/struct.go:83-107 at both levels)."""
+    inner = Struct("Inner", [("x", Kind.INT32), ("y", Kind.INT32)])
+    tree = Tree(Message("M", [("o", 1, Struct("Outer", [("a", Kind.INT32), ("in", inner), ("s", Kind.INT32)]))]))
+    ib = bytes([0x02, 0x33]) + bytes([0x06, 0x0B])   # x: bad type, y = 3
+    ib += bytes([len(ib), 0x5A])
+    ob = bytes([0x04, 0x0B]) + ib + bytes([0x08, 0x0B])  # a = 2, in, s = 4
+    ob += bytes([len(ob), 0x5A])
+    rec = ob + bytes([1, 0, len(ob), len(ob), 3, 0x50])
+    rows, got = oracle_decode(tree, np.frombuffer(rec, np.uint8), np.array([len(rec)], np.uint64))
+    g = {c.name: v.view(np.int32)[0, 0] for c, v in zip(tree.columns, got) if c.name.startswith("o.")}
+    assert g == {"o.a": 0, "o.in.x": 0, "o.in.y": 3, "o.s": 4}
+
+
+@pytest.mark.parametrize("seed,n", [(1, 200), (2, 1), (3, 57)])
+def test_oracle_roundtrip_nested_structs(seed, n):
+    tree = _nested_tree()
+    cols, heaps, rows = workload.tree_batch(tree, n, seed)
+    stream, ends = oracle_encode(tree, cols, heaps, n)
+    st, _ = O.parse_batch(stream, ends)
+    assert not st.any()
+    got_rows, got = oracle_decode(tree, stream, ends)
+    assert got_rows == rows
+    assert roundtrip_mismatches(tree, cols, heaps, got, stream) == []
+
+
+def test_struct_depth_limit():
+    """At most 8 structs deep (SPEC_TREE_MAX_STRUCT_DEPTH); both the engine and the oracle
+    reject a 9th level."""
+    def chain(levels):
+        s = Struct("L0", [("v", Kind.INT32)])
+        for k in range(1, levels):
+            s = Struct(f"L{k}", [("s", s), ("v", Kind.INT32)])
+        return Message("M", [("s", 1, s)])
+
+    t8 = Tree(chain(8))
+    _layout_equal(t8)
+    with pytest.raises(spec_amd.SpecError):
+        Tree(chain(9))
+    assert O.tree_layout(O.tree_fields([(1, Kind.STRUCT, 0, -1)] + [(0, Kind.STRUCT, 0, i) for i in range(8)]
+                                       + [(0, Kind.INT32, 0, 8)])) is None
+
+
+def test_specfile_nested_struct():
+    from spec_amd import specfile
+
+    sf = specfile.SpecSet()
+    sf.add(specfile.load("""
+        message M { o Outer 1; l []Outer 2; }
+        struct Outer { a int32; in Inner; e Color; }
+        struct Inner { x int64; y string; }
+        enum Color { RED = 0; }
+    """, "p"))
+    tree = sf.tree("M", "p")
+    names = [c.name for c in tree.columns]
+    assert "o.in.x" in names and "l[].in.y" in names and "o.e" in names
+    bad = specfile.SpecSet()
+    bad.add(specfile.load("message M { o A 1; } struct A { b B; } struct B { a A; }", "q"))
+    with pytest.raises(ValueError):
+        bad.tree("M", "q")

@@ -76,3 +76,18 @@ def shapes_tree() -> Tree:
         ("seq", 65535, Kind.INT64),
     ])
     return Tree(root)
+
+
+def nested_struct_tree() -> Tree:
+    """Structs inside structs (internal/lang/model/struct_field.go:57-70): a struct field of a
+    message, a list of such structs, a sub-message holding one, and three levels of nesting."""
+    inner = Struct("Inner", [("x", Kind.INT32), ("y", Kind.STRING)])
+    mid = Struct("Mid", [("i", inner), ("f", Kind.FLOAT64), ("j", inner)])
+    outer = Struct("Outer", [("a", Kind.INT32), ("in", inner), ("s", Kind.STRING)])
+    deep = Struct("Deep", [("m", mid), ("b", Kind.BIN64), ("o", outer)])
+    sub = Message("Sub", [("o", 1, outer), ("n", 2, Kind.UINT16)])
+    root = Message("Root", [
+        ("id", 1, Kind.INT64), ("outer", 2, outer), ("outers", 3, ListOf(outer)), ("sub", 4, sub),
+        ("deep", 5, deep), ("deeps", 6, ListOf(deep)), ("tail", 7, Kind.STRING),
+    ])
+    return Tree(root)
