@@ -140,15 +140,23 @@ typedef struct spec_nested_schema {
  *     scalar          VALUE  m.<Kind>(tag)                          (internal/types/msg.go:219-421)
  *     STRUCT          VALUE per scalar member, inner structs' members in place (pre-order):
  *                     OpenXxx(m.FieldRaw(tag))                       (msg.go:139-150)
- *     ANY             VALUE spec_span of m.Field(tag) = OpenValue   (msg.go:108-124, value.go:18-31)
+ *     ANY             VALUE spec_span of m.Field(tag) = OpenValue   (msg.go:108-124, value.go:18-31),
+ *                     then TYPE uint8 m.Field(tag).Type() (value.go:115-119: the value's last
+ *                     byte, 0 for nil); Field(tag).<Kind>() / .Message(): spec_decode_values,
+ *                     spec_tree_decoder_index_spans
  *     MESSAGE, LIST   PRESENT uint8 m.HasField(tag)                 (msg.go:101-106)
  *   a list of scalars: VALUE = ValueList.Get(i) (list_value.go:87-92); a list of structs: a
  *   VALUE per scalar member (pre-order);
+ *   ERRMASK uint64 (MESSAGE-shaped tables: records, sub-messages, message-list items): bit k
+ *   set when the k-th direct field's (write order, k < 64) *Err getter errs — scalars
+ *   <Kind>Err (msg.go:233-459), ANY OpenValueErr (value.go:35-46), MESSAGE MessageErr, LIST
+ *   ListErr (msg.go:453-463), STRUCT DecodeXxx (generator/struct.go:60-64); an absent field never
+ *   errs;
  *   STATUS uint8: records OpenMessageErr's class; sub-messages MessageErr's class (0 if absent);
  *   list items OpenItemErr's class or SPEC_STATUS_PANIC (Go panics: element start > end);
  *   list values / structs SPEC_STATUS_INVALID_VALUE when GetErr fails; any row whose struct or
  *   any field would make Go panic (slice out of range) SPEC_STATUS_PANIC.
- * Encode input uses the same columns (STATUS ignored): scalars and structs are always written,
+ * Encode input uses the same columns (STATUS, ERRMASK, TYPE ignored): scalars and structs are always written,
  * MESSAGE / LIST fields when PRESENT is non-zero (a present list may be empty), ANY when its span
  * is non-empty (FieldWriter.Any copies the bytes: internal/writer/writer.go:438-456). */
 #define SPEC_TREE_MAX_FIELDS 256
@@ -173,7 +181,8 @@ typedef struct spec_tree {
 typedef enum spec_tree_rel { SPEC_REL_ROOT = 0, SPEC_REL_ONE = 1, SPEC_REL_MANY = 2 } spec_tree_rel;
 typedef enum spec_tree_shape { SPEC_SHAPE_MESSAGE = 0, SPEC_SHAPE_VALUE = 1, SPEC_SHAPE_STRUCT = 2 } spec_tree_shape;
 typedef enum spec_tree_role {
-    SPEC_COL_VALUE = 0, SPEC_COL_PRESENT = 1, SPEC_COL_BEGIN = 2, SPEC_COL_STATUS = 3
+    SPEC_COL_VALUE = 0, SPEC_COL_PRESENT = 1, SPEC_COL_BEGIN = 2, SPEC_COL_STATUS = 3,
+    SPEC_COL_ERRMASK = 4, SPEC_COL_TYPE = 5
 } spec_tree_role;
 
 typedef struct spec_tree_table {
@@ -209,6 +218,20 @@ void spec_tree_decoder_destroy(spec_tree_decoder *d);
 int spec_tree_decoder_index(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len,
                             const uint64_t *ends, uint64_t n, uint64_t *rows, void *stream);
 int spec_tree_decoder_decode(spec_tree_decoder *d, void *const *columns, void *stream);
+/* spec_tree_decoder_index over VALUE SPANS instead of contiguous records: row i of the root table
+ * is the message spans[i] holds — what m.Field(tag).Message() opens (an `any` / `message` field,
+ * internal/lang/generator/message.go:145-148; Value.Message() = OpenMessage,
+ * internal/types/value.go:318-321).  A nil span is an empty message; a span past the stream
+ * is a Go panic (STATUS SPEC_STATUS_PANIC).  Decode with spec_tree_decoder_decode as usual. */
+int spec_tree_decoder_index_spans(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len,
+                                  const spec_span *spans, uint64_t n, uint64_t *rows, void *stream);
+
+/* Value.<Kind>() / Value.<Kind>Err() (internal/types/value.go:120-310) over n value spans (an
+ * `any` column): out[i] = Decode<Kind>(the span's bytes) (n * spec_kind_width(kind) bytes;
+ * string/bytes as spans into the stream), err[i] (optional) = 1 where the decoder errs, 2 where
+ * the span lies past the stream (Go would panic), else 0. */
+int spec_decode_values(int kind, const uint8_t *stream_bytes, uint64_t stream_len, const spec_span *spans, uint64_t n,
+                       void *out, uint8_t *err, void *stream);
 
 /* Encode: for every record, the generated Write() over the tree, Build() (writer.go:141-188),
  * appended into out[] with ends[i] = record i's end.  rows[t] = rows of table t (host);
@@ -258,7 +281,8 @@ int spec_decode_flat(const spec_schema *schema, const uint8_t *stream_bytes, uin
  * return an error (internal/types/msg.go:233-459: Int32Err, StringErr, ...): errmask[i] bit f
  * is set when field f is present and Decode<Kind> fails on it (an absent field is no error;
  * the record-level OpenMessageErr class is in status).  Fields >= 64 are not reported.
- * Runs the generic kernel (the schema-specialised one does not track field errors). */
+ * Runs the schema-specialised kernel's errmask variant where the schema has one (else the
+ * generic kernel): the same columns and status as spec_decode_flat. */
 int spec_decode_flat_errors(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
                             const uint64_t *ends, uint64_t n, void *const *columns, uint8_t *status, uint64_t *errmask,
                             void *stream);

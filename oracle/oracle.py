@@ -222,6 +222,10 @@ def _declare(L):
                                         C.c_void_p]
     L.so_tree_layout.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_int), C.c_void_p, C.POINTER(C.c_int)]
     L.so_decode_tree_batch.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+    L.so_decode_tree_spans.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p,
+                                       C.c_void_p]
+    L.so_kind_width.argtypes = [C.c_int]
+    L.so_decode_values.argtypes = [C.c_int, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
     L.so_encode_tree_batch.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                                        C.c_void_p]
     L.so_frames_read.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
@@ -687,6 +691,39 @@ def decode_tree_batch(fields: np.ndarray, stream: np.ndarray, ends: np.ndarray):
     lib().so_decode_tree_batch(_ptr(fields), len(fields), sp, _ptr(ends) if n else None, n, ptrs, _ptr(rows2))
     assert [int(r) for r in rows2] == rows
     return rows, [o[: _entries(tables, c, rows)] for o, c in zip(out, cols)]
+
+
+def decode_tree_spans(fields: np.ndarray, stream: np.ndarray, spans: np.ndarray):
+    """Generated reader over value spans (m.Field(tag).Message() of each) -> (rows, columns)."""
+    tables, cols = tree_layout(fields)
+    stream = np.ascontiguousarray(stream, dtype=np.uint8)
+    spans = np.ascontiguousarray(spans, dtype=np.uint32).reshape(-1, 2)
+    n = len(spans)
+    rows = np.zeros(len(tables), np.uint64)
+    sp = _ptr(stream) if stream.size else None
+    lib().so_decode_tree_spans(_ptr(fields), len(fields), sp, stream.size, _ptr(spans) if n else None, n, None,
+                               _ptr(rows))
+    rows = [int(r) for r in rows]
+    out = [np.zeros((max(_entries(tables, c, rows), 1), int(c["width"])), np.uint8) for c in cols]
+    ptrs = (C.c_void_p * len(out))(*[o.ctypes.data for o in out])
+    rows2 = np.zeros(len(tables), np.uint64)
+    lib().so_decode_tree_spans(_ptr(fields), len(fields), sp, stream.size, _ptr(spans) if n else None, n, ptrs,
+                               _ptr(rows2))
+    assert [int(r) for r in rows2] == rows
+    return rows, [o[: _entries(tables, c, rows)] for o, c in zip(out, cols)]
+
+
+def decode_values(kind: int, stream: np.ndarray, spans: np.ndarray):
+    """Value.<Kind>Err() over value spans -> (values uint8 [n, width], err uint8 [n])."""
+    stream = np.ascontiguousarray(stream, dtype=np.uint8)
+    spans = np.ascontiguousarray(spans, dtype=np.uint32).reshape(-1, 2)
+    n = len(spans)
+    out = np.zeros((max(n, 1), int(lib().so_kind_width(int(kind)))), np.uint8)
+    err = np.zeros(max(n, 1), np.uint8)
+    rc = lib().so_decode_values(int(kind), _ptr(stream) if stream.size else None, stream.size,
+                                _ptr(spans) if n else None, n, _ptr(out), _ptr(err))
+    assert rc == 0
+    return out[:n], err[:n]
 
 
 def encode_tree_batch(fields: np.ndarray, columns, heaps, n: int, cap=None):

@@ -378,6 +378,10 @@ int so_tree_layout(const so_tree_field *f, int nf, so_tree_table *tables, int *n
  * table t; columns (may be NULL: rows only) in layout order, sized by rows. */
 int so_decode_tree_batch(const so_tree_field *f, int nf, const uint8_t *stream, const uint64_t *ends, uint64_t n,
                          void *const *columns, uint64_t *rows);
+int so_decode_tree_spans(const so_tree_field *f, int nf, const uint8_t *stream, uint64_t stream_len,
+                         const uint32_t *spans, uint64_t n, void *const *columns, uint64_t *rows);
+int so_decode_values(int kind, const uint8_t *stream, uint64_t stream_len, const uint32_t *spans, uint64_t n,
+                     uint8_t *out, uint8_t *err);
 /* Per record: the generated Write() over the tree (scalars always written; sub-messages and
  * lists when their PRESENT byte is set; any when its span is non-empty), Build().
  * heaps[c] backs string/bytes/any column c.  0 ok, -1 writer error, -2 out too small. */

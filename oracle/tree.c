@@ -30,7 +30,7 @@
 
 enum { REL_ROOT = 0, REL_ONE = 1, REL_MANY = 2 };
 enum { SHAPE_MESSAGE = 0, SHAPE_VALUE = 1, SHAPE_STRUCT = 2 };
-enum { ROLE_VALUE = 0, ROLE_PRESENT = 1, ROLE_BEGIN = 2, ROLE_STATUS = 3 };
+enum { ROLE_VALUE = 0, ROLE_PRESENT = 1, ROLE_BEGIN = 2, ROLE_STATUS = 3, ROLE_ERRMASK = 4, ROLE_TYPE = 5 };
 enum { ST_OK = 0, ST_PANIC = 6, ST_INVALID_VALUE = 7 };
 #define MAX_F 256
 #define MAX_T 64
@@ -47,7 +47,8 @@ typedef struct {
     int table_of[MAX_F]; /* table a MESSAGE / LIST field defines */
     int col_of[MAX_F];   /* VALUE column of a field (a struct member: its own; a value list: its elements) */
     int present_of[MAX_F]; /* PRESENT column of a MESSAGE / LIST field */
-    int status_col[MAX_T], begin_col[MAX_T];
+    int status_col[MAX_T], begin_col[MAX_T], err_col[MAX_T];
+    int type_of[MAX_F]; /* TYPE column of an ANY field */
     const uint8_t *stream;
     void *const *cols;
     const uint8_t *const *heaps;
@@ -147,8 +148,9 @@ static int build(tree *t, const so_tree_field *f, int nf) {
                 int c = 0;
                 if (scalar(k)) {
                     c = t->col_of[i] = add_col(t, x, i, ROLE_VALUE, k, so_kind_width(k));
-                } else if (k == SO_KIND_ANY) {
+                } else if (k == SO_KIND_ANY) { /* the span, then Value.Type() */
                     c = t->col_of[i] = add_col(t, x, i, ROLE_VALUE, k, 8);
+                    if (c >= 0) c = t->type_of[i] = add_col(t, x, i, ROLE_TYPE, 0, 1);
                 } else if (k == SO_KIND_MESSAGE || k == SO_KIND_LIST) {
                     c = t->present_of[i] = add_col(t, x, i, ROLE_PRESENT, 0, 1);
                 } else { /* struct: one column per scalar member, inner structs' members in place */
@@ -157,6 +159,8 @@ static int build(tree *t, const so_tree_field *f, int nf) {
                 if (c < 0) return -1;
             }
         }
+        t->err_col[x] = -1;
+        if (tb->shape == SHAPE_MESSAGE && (t->err_col[x] = add_col(t, x, d, ROLE_ERRMASK, 0, 8)) < 0) return -1;
         if ((t->status_col[x] = add_col(t, x, d, ROLE_STATUS, 0, 1)) < 0) return -1;
         tb->ncolumns = (uint16_t)(t->nc - tb->first_column);
     }
@@ -336,35 +340,45 @@ static void zero_row(tree *t, int x, uint64_t row) {
 
 /* A message row of table x over the value ending at b+len: OpenMessageErr (root, sub-message)
  * or OpenItemErr (item) — status = its error class, errors => an empty message — then every
- * field's getter. */
+ * field's getter, and (ERRMASK) whether each direct field's *Err getter errs (msg.go:233-463,
+ * value.go:35-46, generator/struct.go:60-64). */
 static void decode_message(tree *t, int x, uint64_t row, const uint8_t *b, size_t len, int item) {
     (void)item;
     so_message m;
     so_err e = so_open_message_err(b, len, &m);
     if (e) memset(&m, 0, sizeof(m));
     uint8_t st = classify(e);
+    uint64_t errs = 0;
+    int kth = 0;
     const int d = t->T[x].field;
     for (int i = d + 1; i < t->nf; i++) {
         if (t->f[i].parent != d) continue;
         const so_tree_field *fi = &t->f[i];
         const int k = fi->kind;
+        const int bit = kth++;
+        int bad = 0;
         size_t rl = 0;
         const uint8_t *raw = so_message_field_raw(&m, fi->tag, &rl);
         if (scalar(k)) {
             uint8_t v[32];
             int n;
-            decode_kind(t, k, raw, rl, v, &n); /* m.<Kind>(tag): the error is swallowed */
+            bad = decode_kind(t, k, raw, rl, v, &n) != NULL; /* m.<Kind>(tag) swallows it; <Kind>Err not */
             put(t, t->col_of[i], row, v, so_kind_width(k));
         } else if (k == SO_KIND_STRUCT) {
-            if (decode_struct(t, i, raw, rl, row) == ST_PANIC) st = ST_PANIC;
+            const int sst = decode_struct(t, i, raw, rl, row); /* DecodeXxx(m.FieldRaw(tag)) */
+            if (sst == ST_PANIC) st = ST_PANIC;
+            bad = sst != ST_OK;
         } else if (k == SO_KIND_ANY) {
             /* OpenValue(bytes[:end]) (value.go:18-31): nil on error or len < n; Go slices
-             * b[len(b)-n:] with n < 0 (DecodeTypeSize's struct quirk) and panics */
+             * b[len(b)-n:] with n < 0 (DecodeTypeSize's struct quirk) and panics; OpenValueErr
+             * errs with DecodeTypeSize only (value.go:35-46) */
             uint32_t span[2] = {0, 0};
             uint8_t ty;
             int n = 0;
-            if (rl && !so_decode_type_size(raw, rl, &ty, &n)) {
-                if (n < 0) {
+            if (rl) {
+                if (so_decode_type_size(raw, rl, &ty, &n)) {
+                    bad = 1;
+                } else if (n < 0) {
                     st = ST_PANIC;
                 } else if ((size_t)n <= rl && n > 0) {
                     span[0] = (uint32_t)(raw + rl - (size_t)n - t->stream);
@@ -372,14 +386,21 @@ static void decode_message(tree *t, int x, uint64_t row, const uint8_t *b, size_
                 }
             }
             put(t, t->col_of[i], row, span, 8);
+            /* Value.Type() = DecodeType(v) (value.go:115-119): the last byte, Undefined for nil */
+            put_u8(t, t->type_of[i], row, span[1] ? t->stream[span[0] + span[1] - 1] : 0);
         } else if (k == SO_KIND_MESSAGE) {
             put_u8(t, t->present_of[i], row, (uint8_t)so_message_has_field(&m, fi->tag));
+            so_message sm;
+            bad = so_open_message_err(raw, rl, &sm) != NULL; /* MessageErr(tag) */
             decode_message(t, t->table_of[i], row, raw, rl, 0);
         } else { /* list */
             const int y = t->table_of[i];
             put_u8(t, t->present_of[i], row, (uint8_t)so_message_has_field(&m, fi->tag));
             so_list l;
-            if (so_open_list_err(raw, rl, &l)) memset(&l, 0, sizeof(l)); /* m.List(tag): errors => empty */
+            if (so_open_list_err(raw, rl, &l)) { /* m.List(tag): errors => empty; ListErr errs */
+                memset(&l, 0, sizeof(l));
+                bad = 1;
+            }
             const int cnt = so_list_len(&l);
             uint32_t b0 = (uint32_t)t->rows[y];
             put(t, t->begin_col[y], row, &b0, 4);
@@ -395,12 +416,17 @@ static void decode_message(tree *t, int x, uint64_t row, const uint8_t *b, size_
                 decode_element(t, y, er, p, plen);
             }
         }
+        if (bad && bit < 64) errs |= 1ull << bit;
     }
+    put(t, t->err_col[x], row, &errs, 8);
     put_u8(t, t->status_col[x], row, st);
 }
 
-int so_decode_tree_batch(const so_tree_field *f, int nf, const uint8_t *stream, const uint64_t *ends, uint64_t n,
-                         void *const *columns, uint64_t *rows) {
+/* The generated reader over n messages: record r = [ends[r-1], ends[r]) of the stream, or
+ * (spans != NULL) the value span r — m.Field(tag).Message() = OpenMessage(value)
+ * (internal/types/value.go:318-321); a span past the stream is a Go panic. */
+static int decode_tree(const so_tree_field *f, int nf, const uint8_t *stream, uint64_t stream_len, const uint64_t *ends,
+                       const uint32_t *spans, uint64_t n, void *const *columns, uint64_t *rows) {
     tree *t = (tree *)malloc(sizeof(tree));
     if (build(t, f, nf)) {
         free(t);
@@ -410,8 +436,15 @@ int so_decode_tree_batch(const so_tree_field *f, int nf, const uint8_t *stream, 
     t->cols = columns;
     t->rows[0] = n;
     for (uint64_t r = 0; r < n; r++) {
-        const uint64_t s = r ? ends[r - 1] : 0;
-        decode_message(t, 0, r, stream + s, (size_t)(ends[r] - s), 0);
+        if (spans) {
+            const uint64_t off = spans[2 * r], len = spans[2 * r + 1];
+            const int past = off + len > stream_len;
+            decode_message(t, 0, r, past ? stream : stream + off, past ? 0 : (size_t)len, 0);
+            if (past) put_u8(t, t->status_col[0], r, ST_PANIC);
+        } else {
+            const uint64_t s = r ? ends[r - 1] : 0;
+            decode_message(t, 0, r, stream + s, (size_t)(ends[r] - s), 0);
+        }
     }
     /* CSR closers: begin[parent rows] = total */
     for (int x = 1; x < t->nt; x++) {
@@ -423,6 +456,35 @@ int so_decode_tree_batch(const so_tree_field *f, int nf, const uint8_t *stream, 
         put(t, t->begin_col[x], t->rows[t->T[x].parent], &tot, 4);
     }
     memcpy(rows, t->rows, sizeof(uint64_t) * (size_t)t->nt);
+    free(t);
+    return 0;
+}
+
+int so_decode_tree_batch(const so_tree_field *f, int nf, const uint8_t *stream, const uint64_t *ends, uint64_t n,
+                         void *const *columns, uint64_t *rows) {
+    return decode_tree(f, nf, stream, 0, ends, NULL, n, columns, rows);
+}
+
+int so_decode_tree_spans(const so_tree_field *f, int nf, const uint8_t *stream, uint64_t stream_len,
+                         const uint32_t *spans, uint64_t n, void *const *columns, uint64_t *rows) {
+    return decode_tree(f, nf, stream, stream_len, NULL, spans, n, columns, rows);
+}
+
+/* Value.<Kind>Err() over value spans (internal/types/value.go:120-310): Decode<Kind> of the
+ * span's bytes; err = 1 on a decoder error, 2 for a span past the stream (a Go panic). */
+int so_decode_values(int kind, const uint8_t *stream, uint64_t stream_len, const uint32_t *spans, uint64_t n,
+                     uint8_t *out, uint8_t *err) {
+    if (!scalar(kind)) return -1;
+    tree *t = (tree *)calloc(1, sizeof(tree));
+    t->stream = stream;
+    const int w = so_kind_width(kind);
+    for (uint64_t r = 0; r < n; r++) {
+        const uint64_t off = spans[2 * r], len = spans[2 * r + 1];
+        const int past = off + len > stream_len;
+        int m;
+        so_err e = decode_kind(t, kind, past ? stream : stream + off, past ? 0 : (size_t)len, out + r * (uint64_t)w, &m);
+        err[r] = past ? 2 : (e ? 1 : 0);
+    }
     free(t);
     return 0;
 }

@@ -13,13 +13,13 @@ from .frames import decode_frames, frames_index, frames_index_device, make_frame
 from .pipeline import HostDecoder
 from .nested import NestedColumns, NestedDecoder, NestedEncoder, decode_nested, encode_nested
 from .schema import FLAT16, NESTED, Field, Kind, NestedSchema, Schema
-from .tree import (ListOf, Message, Struct, Tree, TreeColumns, TreeDecoder, TreeEncoder, decode_tree, encode_tree,
-                   pkg1_message, pkg1_tree, tree_rows)
+from .tree import (ListOf, Message, Struct, Tree, TreeColumns, TreeDecoder, TreeEncoder, decode_tree, decode_values,
+                   encode_tree, pkg1_message, pkg1_tree, tree_rows)
 
 __all__ = [
     "HostDecoder", "decode_frames", "frames_index", "frames_index_device", "make_frames", "make_frames_device", "LIB_PATH", "SpecError", "header_symbols", "lib", "set_jit", "Columns", "Decoder", "Encoder", "alloc_columns",
     "decode_flat", "decode_flat_errors", "encode_flat", "parse_messages", "FLAT16", "Field", "Kind", "Schema",
     "NESTED", "NestedSchema", "NestedColumns", "NestedDecoder", "NestedEncoder", "decode_nested",
     "encode_nested", "ListOf", "Message", "Struct", "Tree", "TreeColumns", "TreeDecoder", "TreeEncoder", "decode_tree",
-    "encode_tree", "pkg1_message", "pkg1_tree", "tree_rows",
+    "decode_values", "encode_tree", "pkg1_message", "pkg1_tree", "tree_rows",
 ]

@@ -154,6 +154,8 @@ def _declare(L):
     L.spec_tree_decoder_destroy.restype = None
     L.spec_tree_decoder_index.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.POINTER(C.c_uint64), vp]
     L.spec_tree_decoder_decode.argtypes = [vp, C.POINTER(vp), vp]
+    L.spec_tree_decoder_index_spans.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.POINTER(C.c_uint64), vp]
+    L.spec_decode_values.argtypes = [C.c_int, vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp]
     L.spec_encode_tree_workspace_size.argtypes = [C.POINTER(SpecTree), C.POINTER(C.c_uint64)]
     L.spec_encode_tree_workspace_size.restype = C.c_size_t
     L.spec_encode_tree.argtypes = [C.POINTER(SpecTree), C.POINTER(vp), C.POINTER(vp), C.POINTER(C.c_uint64),

@@ -187,8 +187,8 @@ static int decode_flat_impl(const spec_schema *schema, const uint8_t *stream_byt
     // LDS slab from the mean record size of the range (the caller knows the range's bytes;
     // for a whole batch it is stream_len / n)
     double avg = range_bytes ? (double)range_bytes / (double)(r1 - r0) : (double)stream_len / (double)r1;
-    // field error masks come from the generic path (the specialised kernels do not track them)
-    int j = errmask ? 0 : spec::jit_launch_decode_flat(schema, a, avg, (hipStream_t)stream);
+    // field error masks: the schema-specialised kernel's errmask variant (or the generic path)
+    int j = spec::jit_launch_decode_flat(schema, a, avg, (hipStream_t)stream);
     if (j < 0) return hip_rc(hipGetLastError());
     if (j == 0 && spec::launch_decode_flat(a, avg, (hipStream_t)stream)) return hip_rc(hipGetLastError());
     return SPEC_OK;

@@ -38,7 +38,7 @@ namespace spec {
 // The fields a record decode produces: one column per schema field + the status column.
 struct FieldSet {
     uint8_t *status;
-    uint64_t *errmask; // optional: bit f = field f's <Kind>Err getter errs (generic path only)
+    uint64_t *errmask; // optional: bit f = field f's <Kind>Err getter errs
     uint32_t nfields;
     uint16_t tags[SPEC_MAX_FIELDS];
     uint8_t kinds[SPEC_MAX_FIELDS];
@@ -636,17 +636,21 @@ struct FieldNat {
     }
 };
 
-template <class Spec, int F>
+// ERR: also collect field F's <Kind>Err outcome into bit F of errs (a present, non-empty field
+// whose decoder errs; internal/types/msg.go:233-459)
+template <class Spec, int F, bool ERR = false>
 struct FieldStore {
     static __device__ __forceinline__ void run(const FastRec<Spec> &fr, long long to_stream, const FieldSet &fs,
-                                               uint64_t r) {
+                                               uint64_t r, uint64_t &errs) {
         if constexpr (F < Spec::N) {
             constexpr uint32_t K = Spec::kind[F];
             if constexpr (K != K_LIST) {
-                const Val v = decode_tail_k<K, true>(fr.w[F], fr.lo[F], fr.e[F], to_stream);
+                bool ok = true;
+                const Val v = decode_tail_k<K, true>(fr.w[F], fr.lo[F], fr.e[F], to_stream, ERR ? &ok : nullptr);
                 store_value_k<K>(fs.cols[F], r, v);
+                if constexpr (ERR && F < 64) errs |= (!ok & (fr.e[F] > fr.lo[F])) ? (1ull << F) : 0ull;
             }
-            FieldStore<Spec, F + 1>::run(fr, to_stream, fs, r);
+            FieldStore<Spec, F + 1, ERR>::run(fr, to_stream, fs, r, errs);
         }
     }
 };
@@ -731,11 +735,13 @@ __device__ __forceinline__ bool fast_prepare(const LdsSrc &s, int rs, int re, Fa
 }
 
 // Fast path, part 2: decode every field from registers and store the columns.
-template <class Spec>
+template <class Spec, bool ERR = false>
 __device__ __forceinline__ void fast_finish(const FastRec<Spec> &fr, uint64_t r, const FieldSet &fs,
                                             long long to_stream) {
-    FieldStore<Spec, 0>::run(fr, to_stream, fs, r);
+    uint64_t errs = 0;
+    FieldStore<Spec, 0, ERR>::run(fr, to_stream, fs, r, errs);
     if (fs.status) fs.status[r] = ST_OK;
+    if constexpr (ERR) fs.errmask[r] = errs;
 }
 
 // ---- kernel body -------------------------------------------------------------------------
@@ -807,7 +813,7 @@ __device__ __forceinline__ void fix_stream_tail(const DecodeArgs &a, __amdgpu_bu
 //   wait for its DMA -> fast_prepare (trailer, table, all field windows into registers) and
 //   the generic path for any rejected record -> the slab is free: issue the NEXT group's DMA
 //   -> decode + store this group from registers while that DMA is in flight.
-template <class Spec>
+template <class Spec, bool ERR = false>
 __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int nw = blockDim.x >> 6;
@@ -852,7 +858,7 @@ __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // every LDS read of this group done
                 if (has_next && nxt.in_lds) issue_dma(rsrc, slab, nxt, lane);
                 if (g2 < ngroups) load_group_ends(a, a.r0 + g2 * 64, lane, lo2, hi2);
-                if (fast) fast_finish<Spec>(fr, r, a.f, to_stream);
+                if (fast) fast_finish<Spec, ERR>(fr, r, a.f, to_stream);
             } else {
                 if (valid) decode_record_generic(s, rs, re, r, a.f, to_stream);
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -879,7 +885,7 @@ __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
 // One group per wave (the default grid): stage, decode, done.  Same steps as one iteration of
 // decode_flat_body without the hand-off to a next group, so nothing fences the fast path's
 // LDS reads from its decode and stores.
-template <class Spec>
+template <class Spec, bool ERR = false>
 __device__ __forceinline__ void decode_flat_once(const DecodeArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6;
@@ -916,7 +922,7 @@ __device__ __forceinline__ void decode_flat_once(const DecodeArgs &a) {
         if constexpr (Spec::N > 0) {
             FastRec<Spec> fr;
             if (fast_prepare<Spec>(s, rs, re, fr)) {
-                fast_finish<Spec>(fr, r, a.f, to_stream);
+                fast_finish<Spec, ERR>(fr, r, a.f, to_stream);
                 return;
             }
         }
@@ -927,13 +933,14 @@ __device__ __forceinline__ void decode_flat_once(const DecodeArgs &a) {
     }
 }
 
-// Kernel entry: PERSIST selects the persistent, software-pipelined loop.
-template <bool PERSIST, class Spec>
+// Kernel entry: PERSIST selects the persistent, software-pipelined loop; ERR the variant that
+// also writes the per-record field error masks (a.f.errmask, spec_decode_flat_errors).
+template <bool PERSIST, class Spec, bool ERR = false>
 __device__ __forceinline__ void decode_flat_entry(const DecodeArgs &a) {
     if constexpr (PERSIST)
-        decode_flat_body<Spec>(a);
+        decode_flat_body<Spec, ERR>(a);
     else
-        decode_flat_once<Spec>(a);
+        decode_flat_once<Spec, ERR>(a);
 }
 
 bool xcd_swizzle_decode(); // XCD-aware block order, default on; SPEC_AMD_XCD=0 off (decode_flat.hip)

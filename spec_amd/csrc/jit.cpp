@@ -126,8 +126,11 @@ std::string generate_decode(const spec_schema *s) {
     std::ostringstream o;
     o << "#include \"decode_core.hpp\"\n";
     emit_spec(o, "GenSpec", s);
+    const char *pers = spec::persistent_decode() ? "true" : "false";
     o << "extern \"C\" __global__ __launch_bounds__(256) void spec_decode_flat_jit(spec::DecodeArgs a) {\n"
-      << "  spec::decode_flat_entry<" << (spec::persistent_decode() ? "true" : "false") << ", GenSpec>(a);\n}\n";
+      << "  spec::decode_flat_entry<" << pers << ", GenSpec>(a);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void spec_decode_flat_err_jit(spec::DecodeArgs a) {\n"
+      << "  spec::decode_flat_entry<" << pers << ", GenSpec, true>(a);\n}\n";
     return o.str();
 }
 
@@ -341,7 +344,7 @@ Entry load(const std::vector<char> &code, Prog p) {
         e.failed = true;
         return e;
     }
-    const char *names[4][4] = {{"spec_decode_flat_jit", nullptr, nullptr, nullptr},
+    const char *names[4][4] = {{"spec_decode_flat_jit", "spec_decode_flat_err_jit", nullptr, nullptr},
                                {"spec_encode_size_jit", "spec_encode_write_jit", nullptr, nullptr},
                                {"spec_decode_nested_jit", "spec_decode_nested2_jit", "spec_decode_nested3_jit", nullptr},
                                {"spec_encode_nested_size_jit", "spec_encode_nested_write_jit", nullptr, nullptr}};
@@ -417,7 +420,7 @@ int jit_launch_decode_flat(const spec_schema *schema, const DecodeArgs &a, doubl
     if (decode_slab_bytes(avg_record) == 0) return 0; // records too large for LDS: generic kernel
     const Entry *ent = lookup(schema, DECODE);
     if (!ent) return 0;
-    hipFunction_t fn = ent->fn[0];
+    hipFunction_t fn = ent->fn[a.f.errmask ? 1 : 0]; // the errmask variant for spec_decode_flat_errors
     if (a.n <= a.r0) return 1;
     const DecodeLaunch L = decode_launch(a.n - a.r0, avg_record, device_cus(), persistent_decode(), decode_wpb());
     DecodeArgs args = a;

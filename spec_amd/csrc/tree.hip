@@ -196,36 +196,79 @@ __global__ __launch_bounds__(TB) void tree_decode_kernel(const TreeDesc *Dp, con
             const RecInfo ri = rec_open(s, lo, hi); // empty (or panicked) range => empty message
             st = ri.tr.st;
             const long long ds = ri.tr.dstart;
+            uint64_t *errp = (uint64_t *)B.cols[T.err_col];
+            uint64_t errs = 0;
             for (uint32_t k = 0; k < T.nd; k++) {
                 const uint32_t fi = D.direct[T.d0 + k];
                 const TField &F = D.f[fi];
                 const long long end = rec_field_end(s, ri, F.tag, F.rank);
                 const long long e = end >= 0 ? ds + end : ds;
+                bool bad = false; // the field's *Err getter errs
                 switch (F.kind) {
                 case K_MESSAGE:
-                case K_LIST: store_u8(B.cols[F.present], row, end >= 0 ? 1u : 0u); break;
-                case K_STRUCT:
-                    if (tree_struct(s, D, B, fi, ds, e, row, 0) == ST_PANIC) st = ST_PANIC;
+                case K_LIST:
+                    store_u8(B.cols[F.present], row, end >= 0 ? 1u : 0u);
+                    // MessageErr / ListErr: OpenMessageErr / OpenListErr of m.field(tag)
+                    if (errp && e > ds)
+                        bad = (F.kind == K_MESSAGE ? parse_trailer<false>(s, ds, e).st : parse_trailer<true>(s, ds, e).st) != ST_OK;
                     break;
+                case K_STRUCT: {
+                    const uint32_t sst = tree_struct(s, D, B, fi, ds, e, row, 0);
+                    if (sst == ST_PANIC) st = ST_PANIC;
+                    bad = sst != ST_OK;
+                    break;
+                }
                 case K_ANY: {
                     // Field(tag) = OpenValue(bytes[:end]): nil on error or len < n; n < 0 panics
                     long long n = 0;
                     uint2 sp = make_uint2(0, 0);
-                    if (e > ds && type_size(s, ds, e, n)) {
-                        if (n < 0) st = ST_PANIC;
-                        else if (n > 0 && n <= e - ds) sp = make_uint2((uint32_t)(e - n), (uint32_t)n);
+                    if (e > ds) {
+                        if (type_size(s, ds, e, n)) {
+                            if (n < 0) st = ST_PANIC;
+                            else if (n > 0 && n <= e - ds) sp = make_uint2((uint32_t)(e - n), (uint32_t)n);
+                        } else {
+                            bad = true; // OpenValueErr: DecodeTypeSize's error
+                        }
                     }
                     if (B.cols[F.col]) ((uint2 *)B.cols[F.col])[row] = sp;
+                    // Value.Type(): the value's last byte (DecodeType), 0 for a nil value
+                    store_u8(B.cols[F.present], row, sp.y ? s.u8((long long)sp.x + sp.y - 1) : 0u);
                     break;
                 }
                 default:
-                    if (B.cols[F.col]) decode_store(s, F.kind, (long long)ds, end, 0, B.cols[F.col], row);
+                    if (B.cols[F.col]) bad = !decode_store(s, F.kind, (long long)ds, end, 0, B.cols[F.col], row);
+                    else if (errp) {
+                        Val v;
+                        int n;
+                        bad = !decode_value_n(s, F.kind, (long long)ds, e, 0, v, n);
+                    }
                 }
+                if (bad && k < 64) errs |= 1ull << k;
             }
+            if (errp) errp[row] = errs;
             if (panic) st = ST_PANIC;
         }
         store_u8(B.cols[T.status_col], row, st);
     });
+}
+
+// Value.<Kind>() / <Kind>Err() over value spans (internal/types/value.go:120-310): Decode<Kind>
+// of exactly the span's bytes; err[row] = 1 where the decoder errs.  A span past the stream
+// (Go would panic slicing it) decodes as empty and reports 2.
+__global__ __launch_bounds__(256) void values_kernel(const uint8_t *stream, uint64_t stream_len, const uint2 *spans,
+                                                     uint64_t n, uint32_t kind, void *out, uint8_t *err) {
+    const GlobalSrc gs{__builtin_amdgcn_make_buffer_rsrc((void *)stream, (short)0, (int)(uint32_t)stream_len, 0x00020000),
+                       stream_len};
+    for (uint64_t row = grid_first(); row < n; row += grid_stride()) {
+        const uint2 sp = spans[row];
+        const bool past = (uint64_t)sp.x + sp.y > stream_len;
+        const long long lo = past ? 0 : sp.x, e = past ? 0 : (long long)sp.x + sp.y;
+        Val v;
+        int nn;
+        const bool ok = decode_value_n(gs, kind, lo, e, 0, v, nn);
+        store_kind(out, row, kind, v);
+        if (err) err[row] = past ? 2 : (ok ? 0 : 1);
+    }
 }
 
 // ---- encode kernels ------------------------------------------------------------------------
@@ -685,6 +728,7 @@ bool build_layout(const spec_tree *tr, Layout &L) {
                     c = D.f[i].col = (int16_t)add_col(L, x, i, SPEC_COL_VALUE, k, spec_kind_width(k));
                 } else if (k == SPEC_KIND_ANY) {
                     c = D.f[i].col = (int16_t)add_col(L, x, i, SPEC_COL_VALUE, k, 8);
+                    if (c >= 0) c = D.f[i].present = (int16_t)add_col(L, x, i, SPEC_COL_TYPE, 0, 1);
                 } else if (k == SPEC_KIND_MESSAGE || k == SPEC_KIND_LIST) {
                     c = D.f[i].present = (int16_t)add_col(L, x, i, SPEC_COL_PRESENT, 0, 1);
                     T.has_children = 1;
@@ -710,6 +754,9 @@ bool build_layout(const spec_tree *tr, Layout &L) {
                 for (uint32_t q = 0; q < T.nd; q++)
                     if (D.direct[T.d0 + q] == srt[k]) D.sslot[T.d0 + k] = (uint16_t)q;
         }
+        T.err_col = -1;
+        if (t.shape == SPEC_SHAPE_MESSAGE && (T.err_col = (int16_t)add_col(L, x, d, SPEC_COL_ERRMASK, 0, 8)) < 0)
+            return false;
         if ((T.status_col = (int16_t)add_col(L, x, d, SPEC_COL_STATUS, 0, 1)) < 0) return false;
         t.ncolumns = (uint16_t)(L.nc - t.first_column);
     }
@@ -791,9 +838,9 @@ int spec_tree_decoder_create(const spec_tree *tree, spec_tree_decoder **out) {
 
 void spec_tree_decoder_destroy(spec_tree_decoder *d) { delete d; }
 
-int spec_tree_decoder_index(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len,
-                            const uint64_t *ends, uint64_t n, uint64_t *rows, void *stream) {
-    if (!d || (n && (!stream_bytes || !ends))) return SPEC_E_INVALID_ARGUMENT;
+static int tree_index_impl(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len,
+                           const uint64_t *ends, const uint2 *spans, uint64_t n, uint64_t *rows, void *stream) {
+    if (!d || (n && (!stream_bytes || (!ends && !spans)))) return SPEC_E_INVALID_ARGUMENT;
     if (stream_len >= (1ull << 32)) return SPEC_E_TOO_LARGE;
     hipStream_t st = (hipStream_t)stream;
     Layout &L = d->L;
@@ -801,6 +848,7 @@ int spec_tree_decoder_index(spec_tree_decoder *d, const uint8_t *stream_bytes, u
     B.stream = stream_bytes;
     B.stream_len = stream_len;
     B.ends = ends;
+    B.spans = spans;
     B.n = n;
     B.rows[0] = n;
     const TreeDesc *Dd = (const TreeDesc *)d->desc.p;
@@ -877,6 +925,17 @@ int spec_tree_decoder_index(spec_tree_decoder *d, const uint8_t *stream_bytes, u
     return SPEC_OK;
 }
 
+int spec_tree_decoder_index(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len,
+                            const uint64_t *ends, uint64_t n, uint64_t *rows, void *stream) {
+    return tree_index_impl(d, stream_bytes, stream_len, ends, nullptr, n, rows, stream);
+}
+
+int spec_tree_decoder_index_spans(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len,
+                                  const spec_span *spans, uint64_t n, uint64_t *rows, void *stream) {
+    if (n && !spans) return SPEC_E_INVALID_ARGUMENT;
+    return tree_index_impl(d, stream_bytes, stream_len, nullptr, (const uint2 *)spans, n, rows, stream);
+}
+
 int spec_tree_decoder_decode(spec_tree_decoder *d, void *const *columns, void *stream) {
     if (!d || !d->indexed || !columns) return SPEC_E_INVALID_ARGUMENT;
     hipStream_t st = (hipStream_t)stream;
@@ -911,6 +970,22 @@ int spec_tree_decoder_decode(spec_tree_decoder *d, void *const *columns, void *s
         const uint32_t slab = tree_slab(B.stream_len, R);
         if (R) hipLaunchKernelGGL(tree_decode_kernel, dim3(row_grid(R)), dim3(TB), (TB / 64) * slab, st, Dd, Bd, x, R, slab);
     }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        note_hip_error(e);
+        return SPEC_E_HIP;
+    }
+    return SPEC_OK;
+}
+
+int spec_decode_values(int kind, const uint8_t *stream_bytes, uint64_t stream_len, const spec_span *spans, uint64_t n,
+                       void *out, uint8_t *err, void *stream) {
+    if (!is_scalar(kind)) return SPEC_E_INVALID_ARGUMENT;
+    if (n == 0) return SPEC_OK;
+    if (!spans || !out || (!stream_bytes && stream_len)) return SPEC_E_INVALID_ARGUMENT;
+    if (stream_len >= (1ull << 32)) return SPEC_E_TOO_LARGE;
+    hipLaunchKernelGGL(values_kernel, dim3(row_grid(n)), dim3(TB), 0, (hipStream_t)stream, stream_bytes, stream_len,
+                       (const uint2 *)spans, n, (uint32_t)kind, out, err);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         note_hip_error(e);
@@ -999,7 +1074,8 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
         // a BEGIN column has owner rows + 1 entries: needed whenever the owner table has rows
         // (an owner whose lists are all empty still reads begin[row], begin[row + 1])
         const uint64_t col_rows = col.role == SPEC_COL_BEGIN ? rows[L.tables[col.table].parent] : rows[col.table];
-        if (col.role != SPEC_COL_STATUS && !columns[c] && col_rows) rc = SPEC_E_INVALID_ARGUMENT;
+        const bool input = col.role == SPEC_COL_VALUE || col.role == SPEC_COL_PRESENT || col.role == SPEC_COL_BEGIN;
+        if (input && !columns[c] && col_rows) rc = SPEC_E_INVALID_ARGUMENT;
         if (spans && rows[col.table] && !B->heaps[c]) rc = SPEC_E_INVALID_ARGUMENT;
     }
     for (uint32_t x = 0; x < L.nt; x++) {

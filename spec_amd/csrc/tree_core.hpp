@@ -35,7 +35,7 @@ struct TField {
     int16_t parent;
     int16_t table;   // MESSAGE / LIST: the table it defines
     int16_t col;     // VALUE column (scalar, any, struct member; a value list's element column)
-    int16_t present; // MESSAGE / LIST: PRESENT column
+    int16_t present; // MESSAGE / LIST: PRESENT column; ANY: TYPE column
     uint16_t rank;   // index of the tag in the writer's table of all direct fields (lookup probe)
     uint16_t nmem, mem0; // STRUCT / LIST<STRUCT>: members[mem0 .. mem0 + nmem)
     uint16_t send;       // one past the last field of this field's subtree (pre-order)
@@ -48,6 +48,8 @@ struct TTable {
     uint8_t rel, shape, has_children, pad;
     int16_t begin_col, status_col;
     uint16_t nd, d0; // MESSAGE shape: direct[d0 .. d0 + nd) (write order), sorted[...] (table order)
+    int16_t err_col; // MESSAGE shape: ERRMASK column
+    int16_t pad2;
 };
 
 struct TreeDesc {
@@ -73,6 +75,7 @@ struct TreeBufs {
     const uint8_t *stream;
     uint64_t stream_len;
     const uint64_t *ends;
+    const uint2 *spans; // decode over spans (Field(tag).Message() values) instead of ends
     uint64_t n;
     uint8_t *out;
     uint64_t out_cap;
@@ -96,6 +99,14 @@ __device__ __forceinline__ void row_range(const TreeBufs &B, uint32_t x, uint64_
                                           bool &panic) {
     panic = false;
     if (x == 0) {
+        if (B.spans) { // a value span (off, len); one past the stream would panic in Go
+            const uint2 sp = B.spans[row];
+            const bool out = (uint64_t)sp.x + sp.y > B.stream_len;
+            panic = out;
+            lo = out ? 0 : sp.x;
+            hi = out ? 0 : (long long)sp.x + sp.y;
+            return;
+        }
         lo = row ? (long long)B.ends[row - 1] : 0;
         hi = (long long)B.ends[row];
         if (hi < lo) hi = lo;

@@ -16,7 +16,8 @@ Decoded output is a set of tables (spec_tree_layout): the records, one table per
 field (a row per owner row) and one per list field (a row per element, CSR `#begin`).  Column
 names: `a.b` (a field), `a.b.m` (struct member), `l[]` (value list elements), `l[].x` (item
 field / struct member), `a?` (HasField of a message or list field), `l#begin`, `<table>#status`
-(`#status` for the records).
+(`#status` for the records), `<table>#errmask` (per message row: bit k = the k-th direct
+field's *Err getter errs), `a#type` (Value.Type() of an `any` field).
 """
 from __future__ import annotations
 
@@ -32,7 +33,8 @@ from .schema import WIDTH, Kind
 SCALARS = tuple(Kind(k) for k in range(1, 16))
 REL_ROOT, REL_ONE, REL_MANY = 0, 1, 2
 SHAPE_MESSAGE, SHAPE_VALUE, SHAPE_STRUCT = 0, 1, 2
-ROLE_VALUE, ROLE_PRESENT, ROLE_BEGIN, ROLE_STATUS = 0, 1, 2, 3
+ROLE_VALUE, ROLE_PRESENT, ROLE_BEGIN, ROLE_STATUS, ROLE_ERRMASK, ROLE_TYPE = 0, 1, 2, 3, 4, 5
+INPUT_ROLES = (ROLE_VALUE, ROLE_PRESENT, ROLE_BEGIN)  # what spec_encode_tree reads
 
 
 class Struct:
@@ -200,6 +202,10 @@ class Tree:
                 name = f"{f.path}#begin"
             elif k.role == ROLE_STATUS:
                 name = f"{tb.path}#status"
+            elif k.role == ROLE_ERRMASK:
+                name = f"{tb.path}#errmask"
+            elif k.role == ROLE_TYPE:
+                name = f"{f.path}#type"
             elif k.role == ROLE_PRESENT:
                 name = f"{f.path}?"
             elif f is not None and f.kind == Kind.LIST:  # a value list's elements
@@ -241,8 +247,10 @@ class TreeColumns:
     def numpy(self, name: str) -> np.ndarray:
         c = self.tree.by_name[name]
         a = self.cols[c.index].cpu().numpy()
-        if c.role in (ROLE_PRESENT, ROLE_STATUS):
+        if c.role in (ROLE_PRESENT, ROLE_STATUS, ROLE_TYPE):
             return a.reshape(-1)
+        if c.role == ROLE_ERRMASK:
+            return a.view(np.uint64).reshape(-1)
         if c.role == ROLE_BEGIN:
             return a.view(np.uint32).reshape(-1)
         return a
@@ -277,6 +285,24 @@ class TreeDecoder:
         self.rows = [int(r) for r in rows]
         return self.rows
 
+    def index_spans(self, stream: torch.Tensor, spans: torch.Tensor, cuda_stream=None) -> list:
+        """index() over value spans (an `any` / `message` column, int32/uint32 [n, 2] or uint8
+        [n, 8]): row i of the root table = m.Field(tag).Message() of record i
+        (spec_tree_decoder_index_spans)."""
+        if not (stream.is_cuda and spans.is_cuda and stream.dtype == torch.uint8 and spans.is_contiguous()):
+            raise ValueError("stream uint8 and contiguous spans device tensors")
+        if spans.numel() * spans.element_size() % 8:
+            raise ValueError("spans: 8 bytes (off, len) per value")
+        n = spans.numel() * spans.element_size() // 8
+        self._keep = (stream, spans)
+        rows = (C.c_uint64 * len(self.tree.tables))()
+        rc = _lib.lib().spec_tree_decoder_index_spans(self._h, C.c_void_p(stream.data_ptr()), stream.numel(),
+                                                       C.c_void_p(spans.data_ptr()), n, rows,
+                                                       _stream_handle(cuda_stream))
+        _lib.check(rc, "spec_tree_decoder_index_spans")
+        self.rows = [int(r) for r in rows]
+        return self.rows
+
     def alloc(self, device) -> list:
         return [torch.empty((max(self.tree.column_rows(c, self.rows), 1), c.width), dtype=torch.uint8, device=device)
                 for c in self.tree.columns]
@@ -298,6 +324,22 @@ def decode_tree(tree: Tree, stream: torch.Tensor, ends: torch.Tensor, cuda_strea
     d = TreeDecoder(tree)
     d.index(stream, ends, cuda_stream)
     return d.decode(cuda_stream=cuda_stream)
+
+
+def decode_values(kind, stream: torch.Tensor, spans: torch.Tensor, cuda_stream=None):
+    """Value.<Kind>() / <Kind>Err() over value spans (an `any` column): -> (values uint8 [n,
+    width], err uint8 [n]: 1 decoder error, 2 span past the stream) (spec_decode_values)."""
+    kind = Kind(kind)
+    if not (stream.is_cuda and spans.is_cuda and stream.dtype == torch.uint8 and spans.is_contiguous()):
+        raise ValueError("stream uint8 and contiguous spans device tensors")
+    n = spans.numel() * spans.element_size() // 8
+    out = torch.empty((max(n, 1), WIDTH[kind]), dtype=torch.uint8, device=stream.device)
+    err = torch.empty(max(n, 1), dtype=torch.uint8, device=stream.device)
+    rc = _lib.lib().spec_decode_values(int(kind), C.c_void_p(stream.data_ptr()), stream.numel(),
+                                       C.c_void_p(spans.data_ptr()), n, C.c_void_p(out.data_ptr()),
+                                       C.c_void_p(err.data_ptr()), _stream_handle(cuda_stream))
+    _lib.check(rc, "spec_decode_values")
+    return out[:n], err[:n]
 
 
 def tree_rows(tree: Tree, n: int, cols: dict) -> list:
@@ -334,8 +376,10 @@ class TreeEncoder:
         keep = []
         for c in t.columns:
             v = cols.get(c.name)
+            if c.role not in INPUT_ROLES:
+                continue  # decode outputs (STATUS, ERRMASK, TYPE): not read by the encoder
             if v is None:
-                if c.role != ROLE_STATUS and t.column_rows(c, self.rows) > 0:
+                if t.column_rows(c, self.rows) > 0:
                     raise ValueError(f"missing column {c.name}")
                 continue
             if not v.is_cuda or not v.is_contiguous():
@@ -418,4 +462,5 @@ def pkg1_tree(max_depth: int = 2) -> Tree:
 
 
 __all__ = ["Struct", "Message", "ListOf", "Tree", "TreeDecoder", "TreeEncoder", "TreeColumns", "decode_tree",
+           "decode_values",
            "encode_tree", "tree_rows", "pkg1_message", "pkg1_tree", "WIDTH"]

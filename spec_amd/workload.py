@@ -176,7 +176,7 @@ def tree_batch(tree, n: int, seed: int = SEED, count=(0, 4), present: float = 0.
     """Random columns for a spec_amd.Tree (canonical: a field under an absent sub-message or list
     holds zeros, so decode(encode(x)) == x up to span offsets).  Returns (cols {name: uint8
     [entries, width]}, heaps {name: uint8[]}, rows per table)."""
-    from .tree import REL_MANY, REL_ONE, ROLE_BEGIN, ROLE_PRESENT, ROLE_STATUS
+    from .tree import REL_MANY, REL_ONE, ROLE_BEGIN, ROLE_ERRMASK, ROLE_PRESENT, ROLE_STATUS, ROLE_TYPE
 
     rng = np.random.default_rng(seed)
     T = tree.tables
@@ -204,6 +204,13 @@ def tree_batch(tree, n: int, seed: int = SEED, count=(0, 4), present: float = 0.
                 continue
             if c.role == ROLE_STATUS:
                 cols[c.name] = np.zeros((R, 1), np.uint8)
+            elif c.role == ROLE_ERRMASK:
+                cols[c.name] = np.zeros((R, 8), np.uint8)  # values written by their own kinds: no errors
+            elif c.role == ROLE_TYPE:  # Value.Type() of the any value before it: its last byte
+                v = tree.fields[c.field].path
+                sp, h = cols[v].view(np.uint32).reshape(-1, 2), heaps[v]
+                last = np.where(sp[:, 1] > 0, sp[:, 0].astype(np.int64) + sp[:, 1] - 1, 0)
+                cols[c.name] = np.where(sp[:, 1] > 0, h[last], 0).astype(np.uint8).reshape(R, 1)
             elif c.role == ROLE_PRESENT:
                 cols[c.name] = ((rng.random(R) < present) & live).astype(np.uint8).reshape(R, 1)
             elif c.kind == Kind.ANY:

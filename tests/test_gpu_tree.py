@@ -182,3 +182,111 @@ def test_reference_spec_trees_at_scale(dev, name):
     n = 100_000
     cols, heaps, rows = workload.tree_batch(tree, n, 91, count=(0, 4))
     check_encode_decode(tree, cols, heaps, rows, dev, n)
+
+
+@pytest.mark.parametrize("shift", [1, 4, 9])
+def test_errmask_cross_kind(dev, shift):
+    """Per-row *Err masks (ERRMASK columns) of every message table: records written by pkg1's
+    writer and read through a tree whose scalar fields have other kinds (range / type errors at
+    every level: records, sub-messages, list items), plus ListErr / MessageErr / struct /
+    OpenValueErr bits from fuzzed bytes — identical to the oracle's *Err getters."""
+    tree = spec_amd.pkg1_tree()
+    n = 3000
+    cols, heaps, rows = workload.tree_batch(tree, n, 500 + shift, count=(0, 3))
+    stream, ends = oracle_encode(tree, cols, heaps, n)
+    fields = []
+    for p, tag, k, e, par in tree.to_fields():
+        if 1 <= k <= 15:
+            k = (k - 1 + shift) % 15 + 1
+        fields.append((p, tag, k, e, par))
+    reader = spec_amd.Tree.from_fields(fields)
+    for s, e in ((stream, ends), _fuzz(stream, ends, shift, n)):
+        want_rows, want = oracle_decode(reader, s, e)
+        got_rows, got = gpu_decode(reader, s, e, dev)
+        assert got_rows == want_rows
+        assert mismatches(reader, got, want) == []
+    masks = [g for c, g in zip(reader.columns, got) if c.name.endswith("#errmask")]
+    assert any(np.any(m) for m in masks)
+
+
+def _spec_tree(name):
+    import json
+    import os
+
+    d = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "spec_trees.json")))
+    return spec_amd.Tree.from_fields(d[name])
+
+
+def test_any_message_field_as_sub_table(dev):
+    """pkg1.spec `message1 message 52` (internal/tests/pkg1/pkg1.spec:30): the generated getter is
+    m.msg.Field(52).Message() (generator/message.go:145-148) — an `any` span, then OpenMessage
+    over it (Value.Message, internal/types/value.go:318-321).  The span column of the record
+    decode feeds a second tree decode (spec_tree_decoder_index_spans) under the caller's schema
+    for it; identical to the oracle's OpenValue(...).Message() + getters, and the values written
+    come back."""
+    from oracle import oracle as O
+    from spec_amd import Kind
+    from spec_amd.tree import ListOf, Message
+
+    tree = _spec_tree("pkg1.Message")
+    assert tree.column("message1").kind == Kind.ANY
+    sub = spec_amd.Tree(Message("message1", [("f1", 1, Kind.INT32), ("f2", 2, Kind.INT32),
+                                             ("f3", 3, Kind.INT32), ("l", 4, ListOf(Kind.STRING))]))
+    n = 4000
+    scols, sheaps, srows = workload.tree_batch(sub, n, 31, count=(0, 3))
+    sub_stream, sub_ends = oracle_encode(sub, scols, sheaps, n)
+    cols, heaps, rows = workload.tree_batch(tree, n, 32, count=(0, 2))
+    starts = np.concatenate([[0], sub_ends[:-1]]).astype(np.uint32)
+    sp = np.stack([starts, (sub_ends - starts).astype(np.uint32)], 1)
+    empty = np.random.default_rng(5).random(n) < 0.1  # the field not written
+    sp[empty] = 0
+    cols["message1"] = sp.astype(np.uint32).view(np.uint8)
+    heaps["message1"] = sub_stream
+    cols["message1#type"] = np.where(sp[:, 1] > 0, 0x50, 0).astype(np.uint8).reshape(n, 1)
+    stream, ends = check_encode_decode(tree, cols, heaps, rows, dev, n)
+    # the record decode's message1 spans (oracle == GPU, checked above)
+    _, want = oracle_decode(tree, stream, ends)
+    spans = want[tree.column("message1").index]
+    want_rows, want_sub = O.decode_tree_spans(tree_fields_of(sub), stream, spans)
+    d = spec_amd.TreeDecoder(sub)
+    got_rows = d.index_spans(torch.from_numpy(stream).to(dev), torch.from_numpy(np.ascontiguousarray(spans)).to(dev))
+    got = [c.cpu().numpy() for c in d.decode().cols]
+    torch.cuda.synchronize()
+    assert got_rows == want_rows
+    assert mismatches(sub, got, want_sub) == []
+    g = {c.name: v for c, v in zip(sub.columns, got)}
+    assert np.array_equal(g["f1"][~empty], scols["f1"][~empty]) and not g["f1"][empty].any()
+    assert not g["#status"].any()
+
+
+def tree_fields_of(tree):
+    from tests.tree_helpers import oracle_fields
+
+    return oracle_fields(tree)
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_typed_values_of_any(dev, seed):
+    """Value.<Kind>() / <Kind>Err() (internal/types/value.go:120-310) over pkg1's `any` spans for
+    every kind (type errors where the value has another type), spans past the stream, fuzzed
+    bytes — spec_decode_values == the oracle."""
+    from oracle import oracle as O
+    from spec_amd import Kind
+
+    tree = spec_amd.pkg1_tree()
+    n = 3000
+    cols, heaps, rows = workload.tree_batch(tree, n, 600 + seed)
+    stream, ends = oracle_encode(tree, cols, heaps, n)
+    if seed:
+        stream, _ = _fuzz(stream, ends, seed, n)
+    _, want = oracle_decode(tree, stream, ends)
+    spans = np.ascontiguousarray(want[tree.column("any").index]).view(np.uint32).reshape(-1, 2).copy()
+    spans[::97] = (len(stream) - 3, 9)  # past the stream: a Go panic
+    d_stream = torch.from_numpy(stream).to(dev)
+    d_spans = torch.from_numpy(spans).to(dev)
+    for k in range(1, 16):
+        wv, we = O.decode_values(k, stream, spans)
+        gv, ge = spec_amd.decode_values(Kind(k), d_stream, d_spans)
+        torch.cuda.synchronize()
+        assert np.array_equal(ge.cpu().numpy(), we), Kind(k)
+        assert np.array_equal(gv.cpu().numpy(), wv), Kind(k)

@@ -81,7 +81,8 @@ def test_value_list_known_bytes():
     lst = bytes([0x00, 0x0C, 0x02, 0x0C, 0x04, 0x0C, 0, 2, 0, 4, 0, 6, 6, 6, 0x46])
     assert bytes(stream) == lst + bytes([70, 0, len(lst), len(lst), 3, 0x50])
     rows, got = oracle_decode(tree, stream, ends)
-    assert rows == [1, 3] and list(got[3].view(np.int64).ravel()) == [0, 1, 2]
+    g = {c.name: v for c, v in zip(tree.columns, got)}
+    assert rows == [1, 3] and list(g["ints[]"].view(np.int64).ravel()) == [0, 1, 2]
 
 
 def _test_object_columns(tree: Tree):
@@ -306,3 +307,40 @@ def test_specfile_nested_struct():
     bad.add(specfile.load("message M { o A 1; } struct A { b B; } struct B { a A; }", "q"))
     with pytest.raises(ValueError):
         bad.tree("M", "q")
+
+
+def test_oracle_errmask_and_type():
+    """ERRMASK bits (the direct fields' *Err getters, write order) and Value.Type() of any: an
+    int32 field holding a string errs; a bool never errs; an absent field never errs; a list
+    field holding an int64 errs (ListErr); an any field's type is its value's last byte."""
+    wr = O.Writer()
+    wr.message()
+    wr.field(1, "string", "not an int")  # read as int32 -> Int32Err
+    wr.field(2, "bool", True)
+    wr.field(4, "int64", 5)              # read as a list -> ListErr
+    wr.field(5, "float64", 2.5)          # any: type 41
+    b, err = wr.end()
+    assert err is None
+    tree = Tree(Message("M", [("a", 1, Kind.INT32), ("b", 2, Kind.BOOL), ("c", 3, Kind.INT64),
+                              ("l", 4, ListOf(Kind.INT32)), ("v", 5, Kind.ANY)]))
+    rows, got = oracle_decode(tree, np.frombuffer(b, np.uint8), np.array([len(b)], np.uint64))
+    g = {c.name: v for c, v in zip(tree.columns, got)}
+    assert int(g["#errmask"].view(np.uint64)[0, 0]) == 0b01001
+    assert g["v#type"][0, 0] == 41 and g["#status"][0, 0] == 0
+
+
+def test_oracle_spans_equal_records():
+    """The oracle's decode over value spans (Field(tag).Message()) equals its decode over the same
+    messages as contiguous records; a span past the stream is a panic row."""
+    tree = spec_amd.pkg1_tree()
+    cols, heaps, rows = workload.tree_batch(tree, 200, 12)
+    stream, ends = oracle_encode(tree, cols, heaps, 200)
+    starts = np.concatenate([[0], ends[:-1]])
+    spans = np.stack([starts, ends - starts], 1).astype(np.uint32)
+    r1, a = oracle_decode(tree, stream, ends)
+    r2, b = O.decode_tree_spans(oracle_fields(tree), stream, spans)
+    assert r1 == r2 and all(np.array_equal(x, y) for x, y in zip(a, b))
+    spans[7] = (len(stream) - 1, 5)
+    _, c = O.decode_tree_spans(oracle_fields(tree), stream, spans)
+    st = {cc.name: v for cc, v in zip(tree.columns, c)}["#status"]
+    assert st[7, 0] == 6 and not np.delete(st, 7).any()

@@ -6,7 +6,8 @@ import numpy as np
 
 from oracle import oracle as O
 from spec_amd.schema import Kind
-from spec_amd.tree import ROLE_BEGIN, ROLE_PRESENT, ROLE_STATUS, ROLE_VALUE, ListOf, Message, Struct, Tree
+from spec_amd.tree import (ROLE_BEGIN, ROLE_ERRMASK, ROLE_PRESENT, ROLE_STATUS, ROLE_TYPE, ROLE_VALUE, ListOf, Message,
+                           Struct, Tree)
 
 SPAN_KINDS = (Kind.STRING, Kind.BYTES, Kind.ANY)
 
@@ -34,11 +35,18 @@ def span_bytes(col: np.ndarray, buf: np.ndarray):
 
 def roundtrip_mismatches(tree: Tree, inputs: dict, heaps: dict, got: list, stream: np.ndarray):
     """Decoded columns `got` (layout order, numpy) vs the encode inputs: values, PRESENT and
-    BEGIN equal; spans by their bytes; STATUS all zero."""
+    BEGIN equal; spans by their bytes; STATUS and ERRMASK all zero; an any field's TYPE = the last
+    byte of its input value (0 if empty)."""
     bad = []
     for c, g in zip(tree.columns, got):
-        if c.role == ROLE_STATUS:
+        if c.role in (ROLE_STATUS, ROLE_ERRMASK):
             if np.any(g):
+                bad.append(c.name)
+            continue
+        if c.role == ROLE_TYPE:
+            v = tree.fields[c.field].path
+            want = np.array([b[-1] if b else 0 for b in span_bytes(inputs[v], heaps[v])], np.uint8)
+            if not np.array_equal(np.asarray(g).reshape(-1), want):
                 bad.append(c.name)
             continue
         want = inputs[c.name]
