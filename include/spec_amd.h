@@ -207,17 +207,26 @@ int spec_tree_layout(const spec_tree *tree, spec_tree_table *tables, uint32_t *n
                      uint32_t *ncolumns);
 
 /* Decode: for every record, the generated reader's getters over the whole tree.  A decoder
- * owns its device workspace (grown on demand, on its device).
- *   spec_tree_decoder_index: the table row counts (host rows[ntables]); synchronises with the
- *     stream once per LIST table (a list's row count sizes the tables below it);
- *   spec_tree_decoder_decode: every column (columns[c] sized by spec_tree_layout and rows;
- *     NULL skips a column), asynchronous on `stream`; the batch must be the one indexed. */
+ * owns its device workspace (grown on demand, on its device) and is used on one stream at a time.
+ * The decode is one asynchronous pass (row counts of list tables stay on the device):
+ *   spec_tree_decoder_index: the pass without columns, then the table row counts on the host
+ *     (rows[ntables]; one synchronisation); it also sizes the list buffers for the batch;
+ *   spec_tree_decoder_decode: the pass with columns (columns[c] sized by spec_tree_layout and
+ *     rows; NULL skips a column), asynchronous; the batch must be the one indexed;
+ *   spec_tree_decoder_run: the pass over a new batch with columns, asynchronous, no host
+ *     synchronisation: rows_out (device, ntables uint64) receives the row counts, ~0 for a list
+ *     table that outgrew the decoder's capacity for it (its rows beyond capacity are not
+ *     decoded: index a batch of that shape first, or spec_tree_decoder_reserve);
+ *   spec_tree_decoder_reserve: list-table capacities of at least rows[t] (host). */
 typedef struct spec_tree_decoder spec_tree_decoder;
 int spec_tree_decoder_create(const spec_tree *tree, spec_tree_decoder **out);
 void spec_tree_decoder_destroy(spec_tree_decoder *d);
 int spec_tree_decoder_index(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len,
                             const uint64_t *ends, uint64_t n, uint64_t *rows, void *stream);
 int spec_tree_decoder_decode(spec_tree_decoder *d, void *const *columns, void *stream);
+int spec_tree_decoder_run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, const uint64_t *ends,
+                          uint64_t n, void *const *columns, uint64_t *rows_out, void *stream);
+int spec_tree_decoder_reserve(spec_tree_decoder *d, const uint64_t *rows);
 /* spec_tree_decoder_index over VALUE SPANS instead of contiguous records: row i of the root table
  * is the message spans[i] holds — what m.Field(tag).Message() opens (an `any` / `message` field,
  * internal/lang/generator/message.go:145-148; Value.Message() = OpenMessage,
@@ -243,6 +252,41 @@ size_t spec_encode_tree_workspace_size(const spec_tree *tree, const uint64_t *ro
 int spec_encode_tree(const spec_tree *tree, const void *const *columns, const uint8_t *const *heaps,
                      const uint64_t *heap_lens, const uint64_t *rows, uint8_t *out, uint64_t out_cap, uint64_t *ends,
                      void *workspace, size_t workspace_size, uint64_t *total, void *stream);
+
+/* ---- several devices in one process (the reference has no multi-device code) ----
+ * Records are independent, so a batch splits into contiguous record shards, one per device.  A
+ * spec_shard holds one stream and one RCCL communicator per device (ncclCommInitAll: one rank
+ * per GPU, no duplicates; librccl is loaded on first use).  Per device, a shard decodes into ONE
+ * packed buffer: the schema's columns back to back, each starting on a 256-byte boundary, then
+ * the status bytes (spec_packed_layout; what spec_amd.shard.PackedColumns lays out), so the
+ * gather to the root device is one grouped RCCL send/recv per device over xGMI.  String/bytes
+ * spans stay shard-relative (a 16M-record batch is > 4 GiB): the shard's byte base travels
+ * alongside (spec_shard_decode_host reports it).
+ *   spec_packed_layout: column offsets / status offset of n records; returns the bytes;
+ *   spec_shard_bounds: shard k's records [r0, r1) of n (sizes differ by at most one);
+ *   spec_shard_decode: device i decodes its device-resident shard (streams[i], ends[i] relative
+ *     to streams[i], ns[i] records) into packed[i] (on device i), asynchronously on its stream;
+ *   spec_shard_decode_host: a host batch (pinned memory for overlap) split by spec_shard_bounds:
+ *     each shard copied to its device (ends rebased there), then spec_shard_decode;
+ *     byte_bases[i] (optional) = shard i's first byte in the batch;
+ *   spec_shard_gather: every device's packed buffer (nbytes[i]) to `gathered` on device `root`,
+ *     part i at the sum of the earlier parts' sizes, ordered after the decodes on each stream;
+ *   spec_shard_stream: device k's stream; spec_shard_sync: wait for every device's stream. */
+#define SPEC_SHARD_MAX_DEVICES 16
+typedef struct spec_shard spec_shard;
+uint64_t spec_packed_layout(const spec_schema *schema, uint64_t n, uint64_t *col_offsets, uint64_t *status_offset);
+void spec_shard_bounds(uint64_t n, int nshards, int k, uint64_t *r0, uint64_t *r1);
+int spec_shard_create(const int *devices, int ndev, spec_shard **out);
+void spec_shard_destroy(spec_shard *c);
+int spec_shard_ndev(const spec_shard *c);
+void *spec_shard_stream(const spec_shard *c, int k);
+int spec_shard_decode(spec_shard *c, const spec_schema *schema, const uint8_t *const *streams,
+                      const uint64_t *stream_lens, const uint64_t *const *ends, const uint64_t *ns,
+                      uint8_t *const *packed);
+int spec_shard_decode_host(spec_shard *c, const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
+                           const uint64_t *ends, uint64_t n, uint8_t *const *packed, uint64_t *byte_bases);
+int spec_shard_gather(spec_shard *c, const uint64_t *nbytes, uint8_t *const *packed, int root, uint8_t *gathered);
+int spec_shard_sync(spec_shard *c);
 
 /* ---- introspection ---- */
 int spec_abi_version(void);

@@ -693,11 +693,19 @@ def decode_tree_batch(fields: np.ndarray, stream: np.ndarray, ends: np.ndarray):
     return rows, [o[: _entries(tables, c, rows)] for o, c in zip(out, cols)]
 
 
+def _spans_u32(spans: np.ndarray) -> np.ndarray:
+    """(off, len) pairs as uint32 [n, 2]: a span column (uint8 [n, 8]) is viewed, not converted."""
+    a = np.ascontiguousarray(spans)
+    if a.dtype == np.uint8:
+        a = a.view(np.uint32)
+    return np.ascontiguousarray(a, dtype=np.uint32).reshape(-1, 2)
+
+
 def decode_tree_spans(fields: np.ndarray, stream: np.ndarray, spans: np.ndarray):
     """Generated reader over value spans (m.Field(tag).Message() of each) -> (rows, columns)."""
     tables, cols = tree_layout(fields)
     stream = np.ascontiguousarray(stream, dtype=np.uint8)
-    spans = np.ascontiguousarray(spans, dtype=np.uint32).reshape(-1, 2)
+    spans = _spans_u32(spans)
     n = len(spans)
     rows = np.zeros(len(tables), np.uint64)
     sp = _ptr(stream) if stream.size else None
@@ -716,7 +724,7 @@ def decode_tree_spans(fields: np.ndarray, stream: np.ndarray, spans: np.ndarray)
 def decode_values(kind: int, stream: np.ndarray, spans: np.ndarray):
     """Value.<Kind>Err() over value spans -> (values uint8 [n, width], err uint8 [n])."""
     stream = np.ascontiguousarray(stream, dtype=np.uint8)
-    spans = np.ascontiguousarray(spans, dtype=np.uint32).reshape(-1, 2)
+    spans = _spans_u32(spans)
     n = len(spans)
     out = np.zeros((max(n, 1), int(lib().so_kind_width(int(kind)))), np.uint8)
     err = np.zeros(max(n, 1), np.uint8)

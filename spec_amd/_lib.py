@@ -154,6 +154,24 @@ def _declare(L):
     L.spec_tree_decoder_destroy.restype = None
     L.spec_tree_decoder_index.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.POINTER(C.c_uint64), vp]
     L.spec_tree_decoder_decode.argtypes = [vp, C.POINTER(vp), vp]
+    L.spec_packed_layout.argtypes = [C.POINTER(SpecSchema), C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    L.spec_packed_layout.restype = C.c_uint64
+    L.spec_shard_bounds.argtypes = [C.c_uint64, C.c_int, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    L.spec_shard_bounds.restype = None
+    L.spec_shard_create.argtypes = [C.POINTER(C.c_int), C.c_int, C.POINTER(vp)]
+    L.spec_shard_destroy.argtypes = [vp]
+    L.spec_shard_destroy.restype = None
+    L.spec_shard_ndev.argtypes = [vp]
+    L.spec_shard_stream.argtypes = [vp, C.c_int]
+    L.spec_shard_stream.restype = vp
+    L.spec_shard_decode.argtypes = [vp, C.POINTER(SpecSchema), C.POINTER(vp), C.POINTER(C.c_uint64), C.POINTER(vp),
+                                    C.POINTER(C.c_uint64), C.POINTER(vp)]
+    L.spec_shard_decode_host.argtypes = [vp, C.POINTER(SpecSchema), vp, C.c_uint64, vp, C.c_uint64, C.POINTER(vp),
+                                         C.POINTER(C.c_uint64)]
+    L.spec_shard_gather.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(vp), C.c_int, vp]
+    L.spec_shard_sync.argtypes = [vp]
+    L.spec_tree_decoder_run.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.POINTER(vp), vp, vp]
+    L.spec_tree_decoder_reserve.argtypes = [vp, C.POINTER(C.c_uint64)]
     L.spec_tree_decoder_index_spans.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.POINTER(C.c_uint64), vp]
     L.spec_decode_values.argtypes = [C.c_int, vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp]
     L.spec_encode_tree_workspace_size.argtypes = [C.POINTER(SpecTree), C.POINTER(C.c_uint64)]

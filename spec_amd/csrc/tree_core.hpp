@@ -50,6 +50,11 @@ struct TTable {
     uint16_t nd, d0; // MESSAGE shape: direct[d0 .. d0 + nd) (write order), sorted[...] (table order)
     int16_t err_col; // MESSAGE shape: ERRMASK column
     int16_t pad2;
+    // decode groups: a group root (the records or a list table) and the sub-message tables
+    // hanging off it 1:1, decoded in one pass (tree_decode.hip)
+    uint16_t groot;  // this table's group root
+    uint16_t gslot;  // a sub-message table: its range slot within the group (0-based)
+    uint16_t g0, gn; // a group root: its tables group[g0 .. g0 + gn), pre-order, itself first
 };
 
 struct TreeDesc {
@@ -61,14 +66,19 @@ struct TreeDesc {
     uint16_t sslot[TREE_MAX_F]; // sorted[d0 + k]'s index in direct[d0 ..] (its write slot)
     uint16_t members[TREE_MAX_F];
     uint16_t width[TREE_MAX_C];
+    uint16_t group[TREE_MAX_T];
 };
 
 struct TreeBufs {
     void *cols[TREE_MAX_C];
     const uint8_t *heaps[TREE_MAX_C];
     uint64_t heap_lens[TREE_MAX_C];
-    uint2 *rng[TREE_MAX_T];     // decode: row ranges (stream offsets lo, hi) of tables 1..
-    uint32_t *cnt[TREE_MAX_T];  // decode: LIST tables: counts per owner row, scanned into begin
+    uint2 *rng[TREE_MAX_T];     // decode: LIST tables: element ranges (stream offsets lo, hi)
+    uint32_t *cnt[TREE_MAX_T];  // decode: LIST tables: element count per owner row
+    uint4 *lh[TREE_MAX_T];      // decode: LIST tables: per owner row (table start, data start, data size, count | big << 31)
+    uint64_t caps[TREE_MAX_T];  // decode: row capacity per table (a list table's buffers)
+    uint64_t *rowsd;            // decode: device row counts of the list tables
+    uint32_t *ovf;              // decode: set when a list outgrew its capacity
     uint32_t *size[TREE_MAX_T]; // encode: encoded bytes per row
     uint64_t *pos[TREE_MAX_T];  // encode: start of each row in out (tables 1..)
     uint64_t rows[TREE_MAX_T];
@@ -150,7 +160,7 @@ __device__ __forceinline__ void store_u8(void *colp, uint64_t r, uint32_t v) {
 // Decode<Kind>(b) of the value [lo, e) with Go's (value, n, err) (internal/decode/...; the
 // value rules are decode_tail_k's, n = bytes consumed from the end).  Returns !err.
 template <class Src>
-__device__ __forceinline__ bool decode_value_n(const Src &s, uint32_t kind, typename Src::pos_t lo,
+__device__ __noinline__ bool decode_value_n(const Src &s, uint32_t kind, typename Src::pos_t lo,
                                                typename Src::pos_t e, long long to_stream, Val &v, int &n) {
     v = Val{0, 0, 0, 0};
     n = 0;
@@ -274,7 +284,7 @@ __device__ __forceinline__ uint32_t struct_open(const Src &s, long long lo, long
 // start), consuming its size.  Returns ST_OK, ST_INVALID_VALUE, or ST_PANIC where Go slices
 // b[len(b)-size:] with size > len(b) (at any depth).
 template <class Src>
-__device__ __forceinline__ uint32_t tree_struct(const Src &s, const TreeDesc &D, const TreeBufs &B, uint32_t sf,
+__device__ __noinline__ uint32_t tree_struct(const Src &s, const TreeDesc &D, const TreeBufs &B, uint32_t sf,
                                                 long long lo, long long e, uint64_t row, long long to_stream) {
     const TField &F = D.f[sf];
     const Val zero = {0, 0, 0, 0};
@@ -365,7 +375,7 @@ __device__ __forceinline__ uint32_t rsize32(const Src &s, long long lo, long lon
 // returns false on an error; n may be negative (the struct case checks n, not m: the bug is
 // kept, type.go:185-191).
 template <class Src>
-__device__ __forceinline__ bool type_size(const Src &s, long long lo, long long e, long long &n) {
+__device__ __noinline__ bool type_size(const Src &s, long long lo, long long e, long long &n) {
     n = 0;
     if (e <= lo) return true;
     const uint32_t t = s.u8((typename Src::pos_t)(e - 1));

@@ -1,0 +1,717 @@
+// tree_decode.hip — the generated readers of a schema tree over a batch (include/spec_amd.h
+// spec_tree_decoder_*, spec_decode_values): internal/lang/generator/message.go:97-186 (getters),
+// struct.go:75-113 (struct Decode), list_msg.go / list_value.go (lists), value.go (any).
+//
+// One pass over the batch, no host round trip (device-resident row counts):
+//   for every GROUP in pre-order — the records, or one list table — with the sub-message tables
+//   hanging off it 1:1 (a sub-message's bytes lie inside its owner row's bytes):
+//     decode   a lane per row: the group's tables top-down within the row (getters, structs,
+//              any, PRESENT / TYPE / ERRMASK / STATUS), and for every list owned in the group
+//              its element count and table position (List.Len, internal/types/list.go:22-67);
+//     scan     the group's list counts -> CSR begin (BEGIN columns), row counts of the lists;
+//              every element's byte range (List.GetBytes: end > dataSize => nil, start > end =>
+//              Go panics) while the offsets are in registers.
+// A wave's 64 rows are staged in LDS before they are parsed: the rows' whole span with LDS-DMA
+// when it fits the wave's slab (consecutive records; the elements of neighbouring lists), else
+// each row in its own lane window (small rows far apart), else the rows parse from HBM through
+// range-checked loads.  Parsing from LDS turns the field walk's chain of dependent reads from
+// HBM-latency round trips into LDS round trips.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+
+#include "spec_internal.hpp"
+#include "tree_internal.hpp"
+
+namespace spec {
+namespace {
+
+constexpr int LANE_W = 256;          // bytes of a lane's window (lane staging)
+constexpr int LANE_CHUNKS = LANE_W / 16;
+constexpr int GUARD = 64;            // bytes staged below a row (value windows read below its start)
+
+// Staged stream bytes [off, off + size) at lds: reads are clamped into the window (every read
+// of a row's parse lies in [lo - 64, hi + 16), which the staging covers).
+struct TreeLds {
+    using pos_t = long long;
+    lds_u8 *lds;
+    long long off;
+    int size;
+    __device__ __forceinline__ int at(long long p, int n) const {
+        long long i = p - off;
+        i = i < 0 ? 0 : i;
+        return (int)(i > size - n ? size - n : i);
+    }
+    __device__ __forceinline__ uint32_t u8(long long p) const { return lds[at(p, 1)]; }
+    __device__ __forceinline__ uint64_t d64(long long p) const {
+        int i = at(p, 8);
+        asm("" : "+v"(i)); // one ds_read_b64 per qword (LdsSrc::d64)
+        return *(lds_u64 *)(lds + i);
+    }
+    __device__ __forceinline__ uint32_t d32(long long p) const { return *(lds_u32 *)(lds + at(p, 4)); }
+};
+
+__device__ __forceinline__ void wave_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Rows of table x during a decode: the records (n) or a list table's device-counted rows,
+// capped by its capacity (a sub-message table has its owner's rows).
+__device__ __forceinline__ uint64_t dec_rows(const TreeDesc &D, const TreeBufs &B, uint32_t x) {
+    const uint32_t g = D.t[x].groot;
+    if (g == 0) return B.n;
+    const uint64_t r = B.rowsd[g];
+    return r < B.caps[g] ? r : B.caps[g];
+}
+
+// Every wave of the grid over the rows of group root x, 64 at a time:
+// body(src, row, lo, hi, panic) for its valid rows, src = the staged bytes or HBM.
+template <class Body>
+__device__ __forceinline__ void tree_rows(const TreeBufs &B, uint32_t x, uint64_t rows, uint32_t slab_bytes,
+                                          uint32_t wave_bytes, Body body) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint8_t *slab = smem + wave * wave_bytes;
+    const __amdgpu_buffer_rsrc_t rsrc = stream_rsrc(B);
+    const GlobalSrc gs{rsrc, B.stream_len};
+    const uint64_t wstride = (uint64_t)gridDim.x * (TB / 64) * 64;
+    for (uint64_t base = ((uint64_t)blockIdx.x * (TB / 64) + wave) * 64; base < rows; base += wstride) {
+        const uint64_t row = base + lane;
+        const bool valid = row < rows;
+        long long lo = 0, hi = 0;
+        bool panic = false;
+        if (valid) row_range(B, x, row, lo, hi, panic);
+        const bool some = valid && hi > lo;
+        long long slo = some ? lo : (long long)B.stream_len, shi = some ? hi : 0, len = some ? hi - lo : 0;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const long long a = __shfl_xor(slo, d), b2 = __shfl_xor(shi, d), l2 = __shfl_xor(len, d);
+            slo = a < slo ? a : slo;
+            shi = b2 > shi ? b2 : shi;
+            len = l2 > len ? l2 : len;
+        }
+        slo = (long long)uniform64((uint64_t)slo);
+        shi = (long long)uniform64((uint64_t)shi);
+        len = (long long)uniform64((uint64_t)len);
+        const long long sb = (slo > GUARD ? slo - GUARD : 0) & ~15ll, se = (shi + 16 + 15) & ~15ll;
+        if (slab_bytes && slo < shi && se - sb + 16 <= (long long)slab_bytes) {
+            // the span: LDS-DMA, 1 KiB per instruction, all in flight at once
+            const uint32_t chunks = (uint32_t)((se - sb + 1023) >> 10);
+            for (uint32_t c = 0; c < chunks; c++)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(slab + c * 1024),
+                                                         16, (uint32_t)sb + c * 1024 + lane * 16, 0, 0, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // a 16-byte chunk straddling the stream end comes back zeroed: refill it bytewise
+            const uint64_t tail = B.stream_len & ~15ull;
+            if (tail < B.stream_len && (long long)tail >= sb && (long long)tail < sb + (long long)chunks * 1024 &&
+                lane < 16 && tail + lane < B.stream_len)
+                slab[tail - sb + lane] = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)(tail + lane), 0, 0);
+            wave_fence();
+            if (valid) body(TreeLds{(lds_u8 *)slab, sb, (int)slab_bytes}, row, lo, hi, panic);
+        } else if (slab_bytes >= 64 * LANE_W && len + GUARD + 48 <= LANE_W) {
+            // each row in its lane's window: its 16-byte chunks, all loads issued before the stores
+            uint8_t *win = slab + lane * LANE_W;
+            const long long lb = (lo > GUARD ? lo - GUARD : 0) & ~15ll;
+            const int nch = some ? (int)((((hi + 16 + 15) & ~15ll) - lb) >> 4) : 0;
+            uint4 v[LANE_CHUNKS];
+#pragma unroll
+            for (int c = 0; c < LANE_CHUNKS; c++) {
+                const long long p = lb + 16ll * c;
+                if (c < nch) {
+                    if ((uint64_t)p + 16 <= B.stream_len) {
+                        const auto q = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)p, 0, 0);
+                        v[c] = make_uint4(q[0], q[1], q[2], q[3]);
+                    } else {
+                        v[c] = make_uint4(gs.d32(p), gs.d32(p + 4), gs.d32(p + 8), gs.d32(p + 12));
+                    }
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < LANE_CHUNKS; c++)
+                if (c < nch) *(uint4 *)(win + 16 * c) = v[c];
+            wave_fence();
+            if (valid) body(TreeLds{(lds_u8 *)win, lb, LANE_W}, row, lo, hi, panic);
+        } else if (valid) {
+            body(gs, row, lo, hi, panic);
+        }
+        wave_fence(); // the staged bytes are read before the next rows overwrite them
+    }
+}
+
+// A message row of table t over [lo, hi): OpenMessageErr, every direct field's getter into its
+// column, *Err bits, and for its children: sub-message ranges (into the group's LDS range
+// slots), list counts + list table positions (for the scan).  Returns the row's status.
+// Out of line, once per source: the generic row code is large (every kind's decoder), and one
+// copy per call site overflowed the instruction cache (98K instructions: the waves of one
+// kernel executing different fields' code missed it constantly).
+template <class Src>
+__device__ __forceinline__ bool tree_scalar(const Src &s, uint32_t kind, long long ds, long long end, void *col,
+                                            uint64_t row, bool want_err) {
+    if (!col && !want_err) return true;
+    Val v;
+    int n;
+    const bool ok = decode_value_n(s, kind, ds, end >= 0 ? ds + end : ds, 0, v, n); // m.<Kind>(tag)
+    store_kind(col, row, kind, v);
+    return ok;
+}
+
+template <class Src>
+__device__ __noinline__ uint32_t tree_message_row(const Src &s, const TreeDesc &D, const TreeBufs &B, uint32_t t,
+                                                  uint64_t row, long long lo, long long hi, uint2 *gr) {
+    const TTable &T = D.t[t];
+    const RecInfo ri = rec_open(s, lo, hi); // empty (or panicked) range => empty message
+    uint32_t st = ri.tr.st;
+    const long long ds = ri.tr.dstart;
+    uint64_t *errp = T.err_col >= 0 ? (uint64_t *)B.cols[T.err_col] : nullptr;
+    uint64_t errs = 0;
+    for (uint32_t k = 0; k < T.nd; k++) {
+        const uint32_t fi = D.direct[T.d0 + k];
+        const TField &F = D.f[fi];
+        const long long end = rec_field_end(s, ri, F.tag, F.rank);
+        const long long e = end >= 0 ? ds + end : ds;
+        bool bad = false; // the field's *Err getter errs
+        switch (F.kind) {
+        case K_MESSAGE: {
+            store_u8(B.cols[F.present], row, end >= 0 ? 1u : 0u);
+            // its table decodes next in this group, over m.field(tag) (Message(tag), msg.go:447-451)
+            gr[D.t[F.table].gslot * 64] = end >= 0 ? make_uint2((uint32_t)ds, (uint32_t)e) : make_uint2(0, 0);
+            if (errp && e > ds) bad = parse_trailer<false>(s, ds, e).st != ST_OK; // MessageErr
+            break;
+        }
+        case K_LIST: {
+            store_u8(B.cols[F.present], row, end >= 0 ? 1u : 0u);
+            // OpenList(m.field(tag)): errors => an empty list (internal/types/list.go:22-25)
+            ListInfo li = {0, 0, 0, 0, false};
+            if (e > ds) {
+                const Trailer lt = parse_trailer<true>(s, ds, e);
+                if (lt.st == ST_OK) {
+                    li.big = lt.big;
+                    li.count = lt.tsize / (lt.big ? 4u : 2u);
+                    li.dstart = lt.dstart;
+                    li.tstart = lt.tstart;
+                    li.dsize = lt.dsize;
+                } else {
+                    bad = true; // ListErr
+                }
+            }
+            B.cnt[F.table][row] = li.count;
+            B.lh[F.table][row] = make_uint4((uint32_t)li.tstart, (uint32_t)li.dstart, li.dsize,
+                                            li.count | (li.big ? 0x80000000u : 0u));
+            break;
+        }
+        case K_STRUCT: {
+            const uint32_t sst = tree_struct(s, D, B, fi, ds, e, row, 0);
+            if (sst == ST_PANIC) st = ST_PANIC;
+            bad = sst != ST_OK;
+            break;
+        }
+        case K_ANY: {
+            // Field(tag) = OpenValue(bytes[:end]): nil on error or len < n; n < 0 panics
+            long long n = 0;
+            uint2 sp = make_uint2(0, 0);
+            if (e > ds) {
+                if (type_size(s, ds, e, n)) {
+                    if (n < 0) st = ST_PANIC;
+                    else if (n > 0 && n <= e - ds) sp = make_uint2((uint32_t)(e - n), (uint32_t)n);
+                } else {
+                    bad = true; // OpenValueErr: DecodeTypeSize's error
+                }
+            }
+            if (B.cols[F.col]) ((uint2 *)B.cols[F.col])[row] = sp;
+            // Value.Type(): the value's last byte (DecodeType), 0 for a nil value
+            store_u8(B.cols[F.present], row, sp.y ? s.u8((long long)sp.x + sp.y - 1) : 0u);
+            break;
+        }
+        default:
+            bad = !tree_scalar(s, F.kind, ds, end, B.cols[F.col], row, errp != nullptr);
+        }
+        if (bad && k < 64) errs |= 1ull << k;
+    }
+    if (errp) errp[row] = errs;
+    return st;
+}
+
+// Group root x (the records or a list table) and the sub-message tables below it, a lane per
+// row.  LDS per wave: the staging slab, then a range slot per sub-message table of the group.
+__global__ __launch_bounds__(TB) void tree_group_kernel(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x,
+                                                         uint32_t slab, uint32_t wave_bytes) {
+    const TreeDesc &D = *Dp;
+    const TreeBufs &B = *Bp;
+    const TTable &T = D.t[x];
+    const uint64_t rows = dec_rows(D, B, x);
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint2 *gr = (uint2 *)(smem + (threadIdx.x >> 6) * wave_bytes + slab) + (threadIdx.x & 63);
+    tree_rows(B, x, rows, slab, wave_bytes, [&](const auto &s, uint64_t row, long long lo, long long hi, bool panic) {
+        uint32_t st;
+        if (T.shape == SHAPE_VALUE) {
+            const TField &F = D.f[T.field];
+            Val v;
+            int n;
+            const bool ok = decode_value_n(s, F.elem, lo, hi, 0, v, n);
+            store_kind(B.cols[F.col], row, F.elem, v);
+            st = panic ? ST_PANIC : (ok ? ST_OK : ST_INVALID_VALUE);
+            store_u8(B.cols[T.status_col], row, st);
+            return;
+        }
+        if (T.shape == SHAPE_STRUCT) {
+            st = tree_struct(s, D, B, T.field, lo, hi, row, 0);
+            store_u8(B.cols[T.status_col], row, panic ? ST_PANIC : st);
+            return;
+        }
+        st = tree_message_row(s, D, B, x, row, lo, hi, gr);
+        store_u8(B.cols[T.status_col], row, panic ? ST_PANIC : st);
+        // the sub-message tables of the group, pre-order: each over the range its owner found
+        for (uint32_t g = 1; g < T.gn; g++) {
+            const uint32_t y = D.group[T.g0 + g];
+            const uint2 r = gr[D.t[y].gslot * 64];
+            const uint32_t sy = tree_message_row(s, D, B, y, row, (long long)r.x, (long long)r.y, gr);
+            store_u8(B.cols[D.t[y].status_col], row, sy);
+        }
+    });
+}
+
+// ---- the group's list counts -> CSR begin, row counts, element ranges ----------------------
+
+constexpr int SCAN_T = 1024, SCAN_PER = 4, SCAN_TILE = SCAN_T * SCAN_PER;
+
+__device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t *sh, uint64_t &block_total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t t = __shfl_up(incl, d);
+        if (lane >= d) incl += t;
+    }
+    if (lane == 63) sh[wave] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t acc = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); w++) {
+            const uint64_t t = sh[w];
+            sh[w] = acc;
+            acc += t;
+        }
+        sh[16] = acc;
+    }
+    __syncthreads();
+    const uint64_t r = sh[wave] + incl - v;
+    block_total = sh[16];
+    __syncthreads();
+    return r;
+}
+
+// The list tables scanned together (every list owned in one group: same owner rows).
+struct ListSet {
+    uint32_t n;                 // lists
+    uint32_t owner;             // the group root (its rows are the lists' owner rows)
+    uint32_t y[TREE_MAX_T];     // the list tables
+    uint64_t *ws[TREE_MAX_T];   // per list: tile sums, then their exclusive offsets
+};
+
+// pass 1: per tile of 4096 owner rows and list j (blockIdx.y), the tile's element total
+__global__ __launch_bounds__(SCAN_T) void list_tiles_kernel(const TreeDesc *Dp, const TreeBufs *Bp, ListSet m) {
+    __shared__ uint64_t sh[17];
+    const TreeDesc &D = *Dp;
+    const TreeBufs &B = *Bp;
+    const uint64_t rows = dec_rows(D, B, m.owner);
+    if ((uint64_t)blockIdx.x * SCAN_TILE >= rows && blockIdx.x) return;
+    const uint32_t *cnt = B.cnt[m.y[blockIdx.y]];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_PER;
+    uint64_t v = 0;
+    for (int k = 0; k < SCAN_PER; k++)
+        if (base + k < rows) v += cnt[base + k];
+    uint64_t tot;
+    block_scan(v, sh, tot);
+    if (threadIdx.x == 0) m.ws[blockIdx.y][blockIdx.x] = tot;
+}
+
+// pass 2: per list j (blockIdx.x), exclusive offsets of the tile totals; the list's row count
+// (and a capacity overflow flag)
+__global__ __launch_bounds__(SCAN_T) void list_top_kernel(const TreeDesc *Dp, const TreeBufs *Bp, ListSet m) {
+    __shared__ uint64_t sh[17];
+    const TreeDesc &D = *Dp;
+    const TreeBufs &B = *Bp;
+    const uint64_t rows = dec_rows(D, B, m.owner);
+    const uint64_t ntiles = (rows + SCAN_TILE - 1) / SCAN_TILE;
+    uint64_t *ws = m.ws[blockIdx.x];
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < ntiles; b += SCAN_T) {
+        const uint64_t i = b + threadIdx.x;
+        const uint64_t v = i < ntiles ? ws[i] : 0;
+        uint64_t tot;
+        const uint64_t e = block_scan(v, sh, tot);
+        if (i < ntiles) ws[i] = carry + e;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        const uint32_t y = m.y[blockIdx.x];
+        B.rowsd[y] = carry;
+        if (carry > B.caps[y] || carry > 0xffffffffull) *B.ovf = 1;
+    }
+}
+
+// pass 3: per tile, every owner row's begin (BEGIN column) and its elements' byte ranges
+__global__ __launch_bounds__(SCAN_T) void list_apply_kernel(const TreeDesc *Dp, const TreeBufs *Bp, ListSet m) {
+    __shared__ uint64_t sh[17];
+    const TreeDesc &D = *Dp;
+    const TreeBufs &B = *Bp;
+    const uint64_t rows = dec_rows(D, B, m.owner);
+    if ((uint64_t)blockIdx.x * SCAN_TILE >= rows && blockIdx.x) return;
+    const uint32_t y = m.y[blockIdx.y];
+    const uint32_t *cnt = B.cnt[y];
+    uint32_t *beg = (uint32_t *)B.cols[D.t[y].begin_col];
+    const uint64_t cap = B.caps[y];
+    uint2 *rng = B.rng[y];
+    const uint4 *lh = B.lh[y];
+    const GlobalSrc gs{stream_rsrc(B), B.stream_len};
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_PER;
+    uint32_t v[SCAN_PER];
+    uint64_t sum = 0;
+    for (int k = 0; k < SCAN_PER; k++) {
+        v[k] = base + k < rows ? cnt[base + k] : 0;
+        sum += v[k];
+    }
+    uint64_t tot;
+    uint64_t p = m.ws[blockIdx.y][blockIdx.x] + block_scan(sum, sh, tot);
+    for (int k = 0; k < SCAN_PER; k++) {
+        const uint64_t r = base + k;
+        if (r >= rows) break;
+        if (beg) beg[r] = (uint32_t)p;
+        if (v[k]) {
+            // List.GetBytes(i) (internal/types/list.go:100-116, format/list.go:152-176)
+            const uint4 h = lh[r];
+            const bool big = (h.w & 0x80000000u) != 0;
+            uint32_t a = 0;
+            for (uint32_t j = 0; j < v[k] && p + j < cap; j++) {
+                const uint32_t b = big ? be32_at(gs, (long long)h.x + 4ll * j) : be16_at(gs, (long long)h.x + 2ll * j);
+                uint2 rr;
+                if (b > h.z) rr = make_uint2(0, 0);               // end > dataSize: nil element
+                else if (a > b) rr = make_uint2(RNG_PANIC, 0);     // start > end: Go panics
+                else rr = make_uint2(h.y + a, h.y + b);
+                rng[p + j] = rr;
+                a = b;
+            }
+        }
+        p += v[k];
+    }
+    if (beg && blockIdx.x == 0 && threadIdx.x == 0) {
+        const uint64_t tr = B.rowsd[y];
+        beg[rows] = (uint32_t)tr; // the closing entry: the list's row count
+    }
+}
+
+// Value.<Kind>() / <Kind>Err() over value spans (internal/types/value.go:120-310): Decode<Kind>
+// of exactly the span's bytes; err[row] = 1 where the decoder errs.  A span past the stream
+// (Go would panic slicing it) decodes as empty and reports 2.
+__global__ __launch_bounds__(256) void values_kernel(const uint8_t *stream, uint64_t stream_len, const uint2 *spans,
+                                                     uint64_t n, uint32_t kind, void *out, uint8_t *err) {
+    const GlobalSrc gs{__builtin_amdgcn_make_buffer_rsrc((void *)stream, (short)0, (int)(uint32_t)stream_len, 0x00020000),
+                       stream_len};
+    for (uint64_t row = grid_first(); row < n; row += grid_stride()) {
+        const uint2 sp = spans[row];
+        const bool past = (uint64_t)sp.x + sp.y > stream_len;
+        const long long lo = past ? 0 : sp.x, e = past ? 0 : (long long)sp.x + sp.y;
+        Val v;
+        int nn;
+        const bool ok = decode_value_n(gs, kind, lo, e, 0, v, nn);
+        store_kind(out, row, kind, v);
+        if (err) err[row] = past ? 2 : (ok ? 0 : 1);
+    }
+}
+
+// rows_out[t] = rows of table t, or ~0 where a list table overflowed its capacity
+__global__ void rows_out_kernel(const TreeDesc *Dp, const TreeBufs *Bp, uint64_t *out) {
+    const TreeDesc &D = *Dp;
+    const TreeBufs &B = *Bp;
+    const uint32_t t = threadIdx.x;
+    if (t >= D.ntables) return;
+    const uint32_t g = D.t[t].groot;
+    out[t] = g == 0 ? B.n : (B.rowsd[g] > B.caps[g] ? ~0ull : B.rowsd[g]);
+}
+
+} // namespace
+} // namespace spec
+
+using namespace spec;
+
+// ---- host side ------------------------------------------------------------------------------
+
+struct spec_tree_decoder {
+    Layout L;
+    int device = 0;
+    DevBuf desc, bufs, misc, ws_scan;
+    DevBuf rng[TREE_MAX_T], cnt[TREE_MAX_T], lh[TREE_MAX_T];
+    uint64_t caps[TREE_MAX_T] = {0}; // capacities of the list tables' row buffers
+    TreeBufs B;          // host copy of the call's device block
+    TreeBufs uploaded;   // what the device block holds
+    bool have_upload = false;
+    TreeBufs *pinned = nullptr;     // staging for the async upload (ring of slots)
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    int slot = 0;
+    uint64_t rows[TREE_MAX_T] = {0}; // from the last index
+    bool indexed = false;
+    ~spec_tree_decoder() {
+        for (hipEvent_t &e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (pinned) (void)hipHostFree(pinned);
+    }
+};
+
+namespace {
+
+// LDS per wave of group x: the staging slab and one range slot per sub-message table
+struct GroupShape {
+    uint32_t slab, wave_bytes;
+};
+
+// A block's 4 waves share a CU's 160 KiB: a wave gets at most 40 KiB.
+constexpr uint32_t WAVE_LDS_MAX = 40960;
+
+GroupShape group_shape(const Layout &L, uint32_t x, uint64_t stream_len, uint64_t n) {
+    const TTable &T = L.desc.t[x];
+    const uint32_t extra = 512u * (T.gn > 1 ? T.gn - 1 : 0) + 16; // sub-message range slots
+    GroupShape g;
+    g.slab = 64 * LANE_W; // 16 KiB: small rows (list elements, sub-messages) stage, lane windows
+    if (x == 0 && n) {
+        // the records: a wave's 64 consecutive records (mean + 15 %)
+        const double span = 64.0 * (double)stream_len / (double)n * 1.15 + 128;
+        if (span > g.slab) g.slab = span + extra <= WAVE_LDS_MAX ? ((uint32_t)span + 1023) & ~1023u : g.slab;
+    }
+    if (g.slab + extra > WAVE_LDS_MAX) g.slab = extra < WAVE_LDS_MAX ? (WAVE_LDS_MAX - extra) & ~1023u : 0;
+    g.wave_bytes = (g.slab + extra + 15) & ~15u;
+    return g;
+}
+
+int grow(DevBuf &b, size_t bytes) { return b.reserve(std::max<size_t>(bytes, 256)); }
+
+// Buffers for the batch (n records) and the current list capacities; fills d->B.
+int prepare(spec_tree_decoder *d, uint64_t n) {
+    Layout &L = d->L;
+    TreeBufs &B = d->B;
+    const TreeDesc &D = L.desc;
+    for (uint32_t x = 1; x < L.nt; x++) {
+        const TTable &T = D.t[x];
+        const uint64_t cap = T.groot == 0 ? n : d->caps[T.groot];
+        B.caps[x] = cap;
+        if (T.rel == REL_MANY) {
+            const uint32_t o = T.parent;
+            const uint64_t ocap = D.t[o].groot == 0 ? n : d->caps[D.t[o].groot];
+            if (grow(d->rng[x], std::max<uint64_t>(cap, 1) * sizeof(uint2)) ||
+                grow(d->cnt[x], (ocap + 1) * sizeof(uint32_t)) || grow(d->lh[x], std::max<uint64_t>(ocap, 1) * sizeof(uint4)))
+                return SPEC_E_HIP;
+            B.rng[x] = (uint2 *)d->rng[x].p;
+            B.cnt[x] = (uint32_t *)d->cnt[x].p;
+            B.lh[x] = (uint4 *)d->lh[x].p;
+        }
+    }
+    B.caps[0] = n;
+    // scan workspace: per list table, the tile sums of its owner rows
+    size_t ws = 0;
+    for (uint32_t x = 1; x < L.nt; x++) {
+        if (D.t[x].rel != REL_MANY) continue;
+        const uint32_t o = D.t[D.t[x].parent].groot;
+        const uint64_t ocap = o == 0 ? n : d->caps[o];
+        ws += ((ocap + SCAN_TILE - 1) / SCAN_TILE + 1) * sizeof(uint64_t) + 256;
+    }
+    if (grow(d->ws_scan, ws)) return SPEC_E_HIP;
+    return SPEC_OK;
+}
+
+// Upload d->B if it differs from what the device holds (stream-ordered, from pinned staging).
+int upload(spec_tree_decoder *d, hipStream_t st) {
+    if (d->have_upload && memcmp(&d->uploaded, &d->B, sizeof(TreeBufs)) == 0) return SPEC_OK;
+    const int k = d->slot;
+    d->slot = (d->slot + 1) & 3;
+    if (d->ev[k] && hipEventSynchronize(d->ev[k]) != hipSuccess) return SPEC_E_HIP; // slot's last copy done
+    memcpy(&d->pinned[k], &d->B, sizeof(TreeBufs));
+    if (hipMemcpyAsync(d->bufs.p, &d->pinned[k], sizeof(TreeBufs), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipEventRecord(d->ev[k], st) != hipSuccess)
+        return SPEC_E_HIP;
+    memcpy(&d->uploaded, &d->B, sizeof(TreeBufs));
+    d->have_upload = true;
+    return SPEC_OK;
+}
+
+// The whole decode of a batch, asynchronous on st: every group's kernel, then its lists' scans.
+int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, const uint64_t *ends,
+        const uint2 *spans, uint64_t n, void *const *columns, hipStream_t st) {
+    if (stream_len >= (1ull << 32)) return SPEC_E_TOO_LARGE;
+    if (n && (!stream_bytes || (!ends && !spans))) return SPEC_E_INVALID_ARGUMENT;
+    Layout &L = d->L;
+    TreeBufs &B = d->B;
+    const TreeDesc &D = L.desc;
+    int rc = prepare(d, n);
+    if (rc) return rc;
+    B.stream = stream_bytes;
+    B.stream_len = stream_len;
+    B.ends = ends;
+    B.spans = spans;
+    B.n = n;
+    B.rowsd = (uint64_t *)d->misc.p;
+    B.ovf = (uint32_t *)((uint8_t *)d->misc.p + TREE_MAX_T * sizeof(uint64_t));
+    for (uint32_t c = 0; c < L.nc; c++) B.cols[c] = columns ? columns[c] : nullptr;
+    if ((rc = upload(d, st))) return rc;
+    if (hipMemsetAsync(B.ovf, 0, sizeof(uint32_t), st) != hipSuccess) return SPEC_E_HIP;
+    if (n == 0) {
+        if (hipMemsetAsync(B.rowsd, 0, TREE_MAX_T * sizeof(uint64_t), st) != hipSuccess) return SPEC_E_HIP;
+    }
+    const TreeDesc *Dd = (const TreeDesc *)d->desc.p;
+    const TreeBufs *Bd = (const TreeBufs *)d->bufs.p;
+    uint8_t *wsp = (uint8_t *)d->ws_scan.p;
+    for (uint32_t x = 0; x < L.nt; x++) {
+        const TTable &T = D.t[x];
+        if (T.groot != x) continue; // decoded inside its group
+        const uint64_t cap = x == 0 ? n : d->caps[x];
+        if (cap == 0 && x) continue;
+        if (n) {
+            const GroupShape gs = group_shape(L, x, stream_len, n);
+            const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((cap + TB - 1) / TB, 1u << 20));
+            hipLaunchKernelGGL(tree_group_kernel, dim3((unsigned)blocks), dim3(TB), (size_t)(TB / 64) * gs.wave_bytes, st,
+                               Dd, Bd, x, gs.slab, gs.wave_bytes);
+        }
+        // every list owned in the group: one batched scan
+        ListSet m;
+        m.n = 0;
+        m.owner = x;
+        for (uint32_t y = x + 1; y < L.nt; y++) {
+            if (D.t[y].rel != REL_MANY || D.t[D.t[y].parent].groot != x) continue;
+            m.y[m.n] = y;
+            m.ws[m.n] = (uint64_t *)wsp;
+            wsp += (((cap + SCAN_TILE - 1) / SCAN_TILE + 1) * sizeof(uint64_t) + 255) & ~(size_t)255;
+            m.n++;
+        }
+        if (!m.n || !n) continue;
+        const uint64_t tiles = std::max<uint64_t>(1, (cap + SCAN_TILE - 1) / SCAN_TILE);
+        hipLaunchKernelGGL(list_tiles_kernel, dim3((unsigned)tiles, m.n), dim3(SCAN_T), 0, st, Dd, Bd, m);
+        hipLaunchKernelGGL(list_top_kernel, dim3(m.n), dim3(SCAN_T), 0, st, Dd, Bd, m);
+        hipLaunchKernelGGL(list_apply_kernel, dim3((unsigned)tiles, m.n), dim3(SCAN_T), 0, st, Dd, Bd, m);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        note_hip_error(e);
+        return SPEC_E_HIP;
+    }
+    return SPEC_OK;
+}
+
+// index: a decode without columns, then the row counts on the host; list capacities grow and
+// the pass reruns when a list outgrew them (at most once per growth).
+int index(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, const uint64_t *ends,
+          const uint2 *spans, uint64_t n, uint64_t *rows, hipStream_t st) {
+    Layout &L = d->L;
+    for (int attempt = 0; attempt < 8; attempt++) {
+        int rc = run(d, stream_bytes, stream_len, ends, spans, n, nullptr, st);
+        if (rc) return rc;
+        uint64_t got[TREE_MAX_T];
+        if (hipMemcpyAsync(got, d->B.rowsd, sizeof(uint64_t) * TREE_MAX_T, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return SPEC_E_HIP;
+        bool again = false;
+        for (uint32_t x = 1; x < L.nt; x++) {
+            const TTable &T = L.desc.t[x];
+            if (T.rel != REL_MANY) continue;
+            if (n && got[x] > d->caps[x]) {
+                if (got[x] > 0xffffffffull) return SPEC_E_TOO_LARGE;
+                d->caps[x] = got[x] + got[x] / 8 + 64;
+                again = true;
+            }
+        }
+        if (again) continue;
+        for (uint32_t x = 0; x < L.nt; x++) {
+            const uint32_t g = L.desc.t[x].groot;
+            d->rows[x] = n == 0 ? 0 : (g == 0 ? n : got[g]);
+        }
+        if (rows) memcpy(rows, d->rows, sizeof(uint64_t) * L.nt);
+        d->indexed = true;
+        return SPEC_OK;
+    }
+    return SPEC_E_HIP;
+}
+
+} // namespace
+
+extern "C" {
+
+int spec_tree_decoder_create(const spec_tree *tree, spec_tree_decoder **out) {
+    if (!out) return SPEC_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    spec_tree_decoder *d = new (std::nothrow) spec_tree_decoder();
+    if (!d) return SPEC_E_INVALID_ARGUMENT;
+    if (!build_layout(tree, d->L)) {
+        delete d;
+        return SPEC_E_INVALID_ARGUMENT;
+    }
+    memset(&d->B, 0, sizeof(d->B));
+    memset(&d->uploaded, 0, sizeof(d->uploaded));
+    bool ok = hipGetDevice(&d->device) == hipSuccess && !d->desc.reserve(sizeof(TreeDesc)) &&
+              !d->bufs.reserve(sizeof(TreeBufs)) && !d->misc.reserve(TREE_MAX_T * sizeof(uint64_t) + 256) &&
+              hipHostMalloc((void **)&d->pinned, 4 * sizeof(TreeBufs), hipHostMallocDefault) == hipSuccess &&
+              hipMemcpy(d->desc.p, &d->L.desc, sizeof(TreeDesc), hipMemcpyHostToDevice) == hipSuccess;
+    for (hipEvent_t &e : d->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        note_hip_error(hipGetLastError());
+        delete d;
+        return SPEC_E_HIP;
+    }
+    *out = d;
+    return SPEC_OK;
+}
+
+void spec_tree_decoder_destroy(spec_tree_decoder *d) { delete d; }
+
+int spec_tree_decoder_index(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len,
+                            const uint64_t *ends, uint64_t n, uint64_t *rows, void *stream) {
+    if (!d) return SPEC_E_INVALID_ARGUMENT;
+    return index(d, stream_bytes, stream_len, ends, nullptr, n, rows, (hipStream_t)stream);
+}
+
+int spec_tree_decoder_index_spans(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len,
+                                  const spec_span *spans, uint64_t n, uint64_t *rows, void *stream) {
+    if (!d || (n && !spans)) return SPEC_E_INVALID_ARGUMENT;
+    return index(d, stream_bytes, stream_len, nullptr, (const uint2 *)spans, n, rows, (hipStream_t)stream);
+}
+
+int spec_tree_decoder_decode(spec_tree_decoder *d, void *const *columns, void *stream) {
+    if (!d || !d->indexed || !columns) return SPEC_E_INVALID_ARGUMENT;
+    const TreeBufs &B = d->B;
+    return run(d, B.stream, B.stream_len, B.ends, B.spans, B.n, columns, (hipStream_t)stream);
+}
+
+int spec_tree_decoder_run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, const uint64_t *ends,
+                          uint64_t n, void *const *columns, uint64_t *rows_out, void *stream) {
+    if (!d || !columns) return SPEC_E_INVALID_ARGUMENT;
+    const int rc = run(d, stream_bytes, stream_len, ends, nullptr, n, columns, (hipStream_t)stream);
+    if (rc || !rows_out) return rc;
+    hipLaunchKernelGGL(rows_out_kernel, dim3(1), dim3(TREE_MAX_T), 0, (hipStream_t)stream,
+                       (const TreeDesc *)d->desc.p, (const TreeBufs *)d->bufs.p, rows_out);
+    return hipGetLastError() == hipSuccess ? SPEC_OK : SPEC_E_HIP;
+}
+
+int spec_tree_decoder_reserve(spec_tree_decoder *d, const uint64_t *rows) {
+    if (!d || !rows) return SPEC_E_INVALID_ARGUMENT;
+    for (uint32_t x = 1; x < d->L.nt; x++)
+        if (d->L.desc.t[x].rel == REL_MANY) d->caps[x] = std::max(d->caps[x], rows[x]);
+    return SPEC_OK;
+}
+
+int spec_decode_values(int kind, const uint8_t *stream_bytes, uint64_t stream_len, const spec_span *spans, uint64_t n,
+                       void *out, uint8_t *err, void *stream) {
+    if (!is_scalar(kind)) return SPEC_E_INVALID_ARGUMENT;
+    if (n == 0) return SPEC_OK;
+    if (!spans || !out || (!stream_bytes && stream_len)) return SPEC_E_INVALID_ARGUMENT;
+    if (stream_len >= (1ull << 32)) return SPEC_E_TOO_LARGE;
+    hipLaunchKernelGGL(values_kernel, dim3(row_grid(n)), dim3(TB), 0, (hipStream_t)stream, stream_bytes, stream_len,
+                       (const uint2 *)spans, n, (uint32_t)kind, out, err);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        note_hip_error(e);
+        return SPEC_E_HIP;
+    }
+    return SPEC_OK;
+}
+
+} // extern "C"

@@ -14,6 +14,8 @@ as grouped ncclSend/ncclRecv; "gloo" (CPU tests) gets host copies.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 import torch
 
@@ -124,3 +126,67 @@ def gather_columns(cols, dist, dst: int = 0, group=None):
         for f, w in enumerate(widths):
             out[f].append(p[po[f]: po[f] + n_k * w].view(n_k, w))
     return out
+
+
+class NativeShard:
+    """One process driving several devices through the C ABI (include/spec_amd.h spec_shard_*):
+    a stream and an RCCL communicator per device, shards decoded into packed buffers
+    (PackedColumns' layout, spec_packed_layout), one grouped RCCL send/recv gather to a root
+    device.  What a cgo caller of INTEGRATION.md drives, without torch.distributed."""
+
+    def __init__(self, devices):
+        from . import _lib
+
+        self._lib = _lib
+        self.devices = list(devices)
+        arr = (C.c_int * len(self.devices))(*self.devices)
+        self._h = C.c_void_p()
+        _lib.check(_lib.lib().spec_shard_create(arr, len(self.devices), C.byref(self._h)), "spec_shard_create")
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h and h.value:
+            try:
+                self._lib.lib().spec_shard_destroy(h)
+            except Exception:
+                pass
+
+    @property
+    def ndev(self) -> int:
+        return len(self.devices)
+
+    def bounds(self, n: int, k: int):
+        r0, r1 = C.c_uint64(), C.c_uint64()
+        self._lib.lib().spec_shard_bounds(n, self.ndev, k, C.byref(r0), C.byref(r1))
+        return r0.value, r1.value
+
+    def decode_host(self, schema: Schema, stream: np.ndarray, ends: np.ndarray):
+        """Split a host batch over the devices, decode each shard on its device: -> (packed
+        buffers [PackedColumns per device], byte bases)."""
+        stream = np.ascontiguousarray(stream, dtype=np.uint8)
+        ends = np.ascontiguousarray(ends, dtype=np.uint64)
+        n = len(ends)
+        packs = []
+        for k, d in enumerate(self.devices):
+            r0, r1 = self.bounds(n, k)
+            packs.append(PackedColumns(schema, r1 - r0, torch.device("cuda", d)))
+        ptrs = (C.c_void_p * self.ndev)(*[p.buf.data_ptr() for p in packs])
+        bases = (C.c_uint64 * self.ndev)()
+        rc = self._lib.lib().spec_shard_decode_host(self._h, C.byref(schema.c), stream.ctypes.data, stream.size,
+                                                    ends.ctypes.data, n, ptrs, bases)
+        self._lib.check(rc, "spec_shard_decode_host")
+        self._keep = (stream, ends)
+        return packs, list(bases)
+
+    def gather(self, packs, root: int = 0) -> torch.Tensor:
+        """Every device's packed buffer to one buffer on device `root` (parts back to back)."""
+        sizes = [p.nbytes for p in packs]
+        out = torch.empty(max(sum(sizes), 1), dtype=torch.uint8, device=torch.device("cuda", self.devices[root]))
+        ptrs = (C.c_void_p * self.ndev)(*[p.buf.data_ptr() for p in packs])
+        nb = (C.c_uint64 * self.ndev)(*sizes)
+        self._lib.check(self._lib.lib().spec_shard_gather(self._h, nb, ptrs, root, C.c_void_p(out.data_ptr())),
+                        "spec_shard_gather")
+        return out
+
+    def sync(self):
+        self._lib.check(self._lib.lib().spec_shard_sync(self._h), "spec_shard_sync")

@@ -307,6 +307,30 @@ class TreeDecoder:
         return [torch.empty((max(self.tree.column_rows(c, self.rows), 1), c.width), dtype=torch.uint8, device=device)
                 for c in self.tree.columns]
 
+    def run(self, stream: torch.Tensor, ends: torch.Tensor, cols: list, rows_out: torch.Tensor | None = None,
+            cuda_stream=None) -> torch.Tensor:
+        """Decode a new batch into `cols` in one asynchronous pass (spec_tree_decoder_run): no
+        host synchronisation; returns the device row counts (int64 [ntables], -1 where a list
+        table outgrew the decoder's capacity: index() a batch of that shape first)."""
+        if not (stream.is_cuda and ends.is_cuda and stream.dtype == torch.uint8 and ends.dtype == torch.int64):
+            raise ValueError("stream uint8 and ends int64 device tensors")
+        if len(cols) != len(self.tree.columns):
+            raise ValueError("one entry per column (None skips it)")
+        if rows_out is None:
+            rows_out = torch.empty(len(self.tree.tables), dtype=torch.int64, device=stream.device)
+        self._keep = (stream, ends)
+        ptrs = (C.c_void_p * len(cols))(*[c.data_ptr() if c is not None else 0 for c in cols])
+        rc = _lib.lib().spec_tree_decoder_run(self._h, C.c_void_p(stream.data_ptr()), stream.numel(),
+                                               C.c_void_p(ends.data_ptr()), ends.numel(), ptrs,
+                                               C.c_void_p(rows_out.data_ptr()), _stream_handle(cuda_stream))
+        _lib.check(rc, "spec_tree_decoder_run")
+        return rows_out
+
+    def reserve(self, rows):
+        """List-table capacities of at least rows[t] (spec_tree_decoder_reserve)."""
+        r = (C.c_uint64 * len(self.tree.tables))(*rows)
+        _lib.check(_lib.lib().spec_tree_decoder_reserve(self._h, r), "spec_tree_decoder_reserve")
+
     def decode(self, cols=None, cuda_stream=None) -> TreeColumns:
         if self.rows is None:
             raise RuntimeError("index() first")

@@ -290,3 +290,28 @@ def test_typed_values_of_any(dev, seed):
         torch.cuda.synchronize()
         assert np.array_equal(ge.cpu().numpy(), we), Kind(k)
         assert np.array_equal(gv.cpu().numpy(), wv), Kind(k)
+
+
+def test_run_async_and_capacity(dev):
+    """spec_tree_decoder_run: a new batch decoded in one pass with no host synchronisation, row
+    counts on the device == index(); a batch whose lists outgrow the capacity reports -1 for
+    those tables (and decodes the rest), then fits after reserve()."""
+    tree = spec_amd.pkg1_tree()
+    small_cols, small_heaps, _ = workload.tree_batch(tree, 500, 71, count=(0, 2))
+    s1, e1 = oracle_encode(tree, small_cols, small_heaps, 500)
+    cols, heaps, rows = workload.tree_batch(tree, 500, 72, count=(3, 6))
+    s2, e2 = oracle_encode(tree, cols, heaps, 500)
+    want_rows, want = oracle_decode(tree, s2, e2)
+    d = spec_amd.TreeDecoder(tree)
+    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    d.index(to(s1), to(e1.view(np.int64)))               # sizes the lists for the small batch
+    out = [torch.zeros((max(tree.column_rows(c, want_rows), 1), c.width), dtype=torch.uint8, device=dev)
+           for c in tree.columns]
+    got_rows = d.run(to(s2), to(e2.view(np.int64)), out).cpu().numpy()
+    lists = [t.index for t in tree.tables if t.rel == 2]
+    assert all(got_rows[t] == -1 for t in lists if want_rows[t] > d.rows[t] * 9 // 8 + 64)
+    d.reserve(want_rows)
+    got_rows = d.run(to(s2), to(e2.view(np.int64)), out).cpu().numpy()
+    assert list(got_rows) == want_rows
+    got = [c[: tree.column_rows(tc, want_rows)].cpu().numpy() for c, tc in zip(out, tree.columns)]
+    assert mismatches(tree, got, want) == []

@@ -113,3 +113,28 @@ def test_packed_columns_aligned():
         assert [tuple(c.shape) for c in pc.cols] == [(n, w) for w in FLAT16.widths]
         ends = [c.data_ptr() - base + c.numel() for c in pc.cols]
         assert all(e <= s for e, s in zip(ends, [c.data_ptr() - base for c in pc.cols[1:]] + [pc.status.data_ptr() - base]))
+
+
+def test_packed_layout_matches_c_abi():
+    """spec_amd.shard.PackedColumns and the C ABI's spec_packed_layout (what spec_shard_decode
+    writes) lay the packed buffer out identically; spec_shard_bounds == shard_bounds."""
+    import ctypes as C
+
+    import spec_amd
+    from spec_amd import FLAT16, Kind, Schema
+    from spec_amd.shard import packed_layout
+
+    L = spec_amd.lib()
+    for schema in (FLAT16, Schema([(1, Kind.BOOL), (9, Kind.BIN256), (3, Kind.INT16)])):
+        for n in (0, 1, 2049, 1 << 21):
+            offs = (C.c_uint64 * 64)()
+            soff = C.c_uint64()
+            total = L.spec_packed_layout(C.byref(schema.c), n, offs, C.byref(soff))
+            po, ps, pt = packed_layout(schema.widths, n)
+            assert (list(offs[: len(schema)]), soff.value, total) == (po, ps, pt)
+    for n in (0, 7, 16 << 20):
+        for world in (1, 3, 8):
+            for k in range(world):
+                r0, r1 = C.c_uint64(), C.c_uint64()
+                L.spec_shard_bounds(n, world, k, C.byref(r0), C.byref(r1))
+                assert (r0.value, r1.value) == shard_bounds(n, world, k)
