@@ -22,7 +22,7 @@ namespace {
 __global__ __launch_bounds__(256) void nested_count_kernel(NestedArgs a) { nested_count_body(a); }
 
 __global__ __launch_bounds__(256) void nested_count_tail_kernel(NestedArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t wins[256 * TAIL_WIN];
+    __shared__ __attribute__((aligned(16))) uint8_t wins[256 * TAIL_STRIDE];
     nested_count_tail_body(a, wins);
 }
 

@@ -573,10 +573,14 @@ __device__ __forceinline__ void nested_count_body(const NestedArgs &a) {
 // count is the same whatever the record looks like.  One 64-byte window per record touches one
 // or two 128-byte lines of the ~210-byte config-4 records instead of all of them.
 constexpr int TAIL_WIN = 64;
+// Windows sit TAIL_STRIDE = 17 dwords apart: lane i's byte k is in bank (17 i + k / 4) mod 32,
+// so the 32 lanes of a ds_write_b32 / ds_read group never share a bank at equal k (a 16-dword
+// stride put every other lane on the same 4 banks: 10.4 conflict cycles per LDS instruction).
+constexpr int TAIL_STRIDE = TAIL_WIN + 4;
 
 struct WinSrc {
     using pos_t = long long;
-    lds_u8 *lds;  // this lane's window: stream bytes [a, a + TAIL_WIN)
+    lds_u8 *lds;  // this lane's window (4-byte aligned): stream bytes [a, a + TAIL_WIN)
     long long a;
     GlobalSrc g;
     __device__ __forceinline__ uint32_t u8(long long p) const {
@@ -585,7 +589,8 @@ struct WinSrc {
     }
     __device__ __forceinline__ uint64_t d64(long long p) const {
         const unsigned long long k = (unsigned long long)(p - a);
-        if (k <= (unsigned long long)(TAIL_WIN - 8) && !(k & 7)) return *(lds_u64 *)(lds + k);
+        if (k <= (unsigned long long)(TAIL_WIN - 8) && !(k & 7))
+            return (uint64_t)*(lds_u32 *)(lds + k) | ((uint64_t)*(lds_u32 *)(lds + k + 4) << 32);
         return g.d64(p);
     }
     __device__ __forceinline__ uint32_t d32(long long p) const {
@@ -623,12 +628,18 @@ __device__ __forceinline__ void nested_count_tail_body(const NestedArgs &a, uint
     uint32_t cnt = 0;
     if (base + lane < a.n) {
         const uint64_t w0 = hi >= 48 ? (hi - 48) & ~15ull : 0;
-        uint8_t *win = wins + threadIdx.x * TAIL_WIN;
+        uint8_t *win = wins + threadIdx.x * TAIL_STRIDE;
         uint4 v[TAIL_WIN / 16];
 #pragma unroll
         for (int k = 0; k < TAIL_WIN / 16; k++) v[k] = win_piece(rsrc, w0 + 16 * k, a.stream_len);
 #pragma unroll
-        for (int k = 0; k < TAIL_WIN / 16; k++) *(uint4 *)(win + 16 * k) = v[k];
+        for (int k = 0; k < TAIL_WIN / 16; k++) {
+            uint32_t *d = (uint32_t *)(win + 16 * k);
+            d[0] = v[k].x;
+            d[1] = v[k].y;
+            d[2] = v[k].z;
+            d[3] = v[k].w;
+        }
         WinSrc s{(lds_u8 *)win, (long long)w0, GlobalSrc{rsrc, a.stream_len}};
         cnt = record_count(s, (long long)lo, (long long)hi, a);
     }
