@@ -227,6 +227,10 @@ int spec_tree_decoder_decode(spec_tree_decoder *d, void *const *columns, void *s
 int spec_tree_decoder_run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, const uint64_t *ends,
                           uint64_t n, void *const *columns, uint64_t *rows_out, void *stream);
 int spec_tree_decoder_reserve(spec_tree_decoder *d, const uint64_t *rows);
+/* spec_tree_jit_compile: compile (hiprtc, no GPU needed) the decoder's schema-specialised group
+ * kernels for this tree into the code-object cache (a decoder compiles them on first use
+ * otherwise); returns the code object's size, or <= 0 (SPEC_E_INVALID_ARGUMENT: invalid tree). */
+long long spec_tree_jit_compile(const spec_tree *tree);
 /* spec_tree_decoder_index over VALUE SPANS instead of contiguous records: row i of the root table
  * is the message spans[i] holds — what m.Field(tag).Message() opens (an `any` / `message` field,
  * internal/lang/generator/message.go:145-148; Value.Message() = OpenMessage,

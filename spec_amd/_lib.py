@@ -172,6 +172,8 @@ def _declare(L):
     L.spec_shard_sync.argtypes = [vp]
     L.spec_tree_decoder_run.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.POINTER(vp), vp, vp]
     L.spec_tree_decoder_reserve.argtypes = [vp, C.POINTER(C.c_uint64)]
+    L.spec_tree_jit_compile.argtypes = [C.POINTER(SpecTree)]
+    L.spec_tree_jit_compile.restype = C.c_longlong
     L.spec_tree_decoder_index_spans.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.POINTER(C.c_uint64), vp]
     L.spec_decode_values.argtypes = [C.c_int, vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp]
     L.spec_encode_tree_workspace_size.argtypes = [C.POINTER(SpecTree), C.POINTER(C.c_uint64)]

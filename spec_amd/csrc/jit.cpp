@@ -23,6 +23,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <mutex>
 #include <sstream>
 #include <string>
@@ -33,6 +34,7 @@
 #include <cstring>
 
 #include "spec_internal.hpp"
+#include "tree_core.hpp"
 
 namespace {
 
@@ -96,7 +98,7 @@ bool has_encoder(const spec_schema *s) {
     return true;
 }
 
-enum Prog { DECODE = 0, ENCODE = 1, NESTED = 2, NESTED_ENC = 3 };
+enum Prog { DECODE = 0, ENCODE = 1, NESTED = 2, NESTED_ENC = 3, TREE = 4 };
 
 std::string key_of(const spec_schema *s, int device, Prog p) {
     std::ostringstream k;
@@ -211,6 +213,7 @@ std::string generate_encode(const spec_schema *s) {
 
 const char *prog_name(Prog p) {
     return p == ENCODE       ? "spec_encode_jit.hip"
+           : p == TREE       ? "spec_tree_jit.hip"
            : p == NESTED     ? "spec_decode_nested_jit.hip"
            : p == NESTED_ENC ? "spec_encode_nested_jit.hip"
                              : "spec_decode_flat_jit.hip";
@@ -218,12 +221,12 @@ const char *prog_name(Prog p) {
 
 // hiprtc compile only; returns the code object (empty on failure)
 std::vector<char> compile_uncached(const std::string &src, Prog p, const char *const *opts_in, int nopts) {
-    const char *hdr_src[5] = {kSpecDeviceHpp, kDecodeCoreHpp, kEncodeCoreHpp, kDecodeNestedCoreHpp,
-                              kEncodeNestedCoreHpp};
-    const char *hdr_name[5] = {"spec_device.hpp", "decode_core.hpp", "encode_core.hpp", "decode_nested_core.hpp",
-                               "encode_nested_core.hpp"};
+    const char *hdr_src[7] = {kSpecDeviceHpp, kDecodeCoreHpp, kEncodeCoreHpp, kDecodeNestedCoreHpp,
+                              kEncodeNestedCoreHpp, kTreeCoreHpp, kTreeDecodeCoreHpp};
+    const char *hdr_name[7] = {"spec_device.hpp", "decode_core.hpp", "encode_core.hpp", "decode_nested_core.hpp",
+                               "encode_nested_core.hpp", "tree_core.hpp", "tree_decode_core.hpp"};
     hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), prog_name(p), 5, hdr_src, hdr_name) != HIPRTC_SUCCESS) return {};
+    if (hiprtcCreateProgram(&prog, src.c_str(), prog_name(p), 7, hdr_src, hdr_name) != HIPRTC_SUCCESS) return {};
     // the product kernels are compiled with fixed options only: no environment variable can
     // change what a kernel computes
     std::vector<const char *> opts(opts_in, opts_in + nopts);
@@ -250,6 +253,7 @@ std::vector<char> compile_uncached(const std::string &src, Prog p, const char *c
     // SPEC_AMD_JIT_DUMP=prefix: write the source and code object (ISA inspection)
     if (const char *d = getenv("SPEC_AMD_JIT_DUMP")) {
         std::string base = std::string(d) + (p == ENCODE       ? "encode"
+                                             : p == TREE       ? "tree"
                                              : p == NESTED     ? "nested"
                                              : p == NESTED_ENC ? "nested_encode"
                                                                : "decode");
@@ -307,7 +311,8 @@ bool read_file(const std::string &path, std::vector<char> &out) {
 void write_cache(const std::string &name, const std::vector<char> &code) {
     for (const std::string &d : cache_dirs()) {
         mkdir(d.c_str(), 0755); // best effort; a missing parent makes the open below fail
-        const std::string tmp = d + "/." + name + "." + std::to_string(getpid());
+        static std::atomic<unsigned> seq{0}; // concurrent compiles (threads) of one process
+        const std::string tmp = d + "/." + name + "." + std::to_string(getpid()) + "." + std::to_string(seq++);
         FILE *f = fopen(tmp.c_str(), "wb");
         if (!f) continue;
         bool ok = fwrite(code.data(), 1, code.size(), f) == code.size();
@@ -321,7 +326,8 @@ std::vector<char> compile_source(const std::string &src, Prog p) {
     static const char *const kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
     uint64_t h = 0xcbf29ce484222325ull;
     h = fnv1a(h, src.data(), src.size());
-    for (const char *hs : {kSpecDeviceHpp, kDecodeCoreHpp, kEncodeCoreHpp, kDecodeNestedCoreHpp, kEncodeNestedCoreHpp})
+    for (const char *hs : {kSpecDeviceHpp, kDecodeCoreHpp, kEncodeCoreHpp, kDecodeNestedCoreHpp, kEncodeNestedCoreHpp,
+                           kTreeCoreHpp, kTreeDecodeCoreHpp})
         h = fnv1a(h, hs, strlen(hs) + 1);
     for (const char *o : kOpts) h = fnv1a(h, o, strlen(o) + 1);
     char name[64];
@@ -398,11 +404,278 @@ const Entry *lookup_nested_encode(const spec_nested_schema *s) {
     return lookup_key(k, NESTED_ENC, [&] { return compile_source(generate_nested_encode(s), NESTED_ENC); });
 }
 
+
+// ---- schema trees: the generated readers, one kernel per decode group -------------------------
+// For every group root x (the records or a list table) whose message tables qualify (direct
+// tags unique and <= 255), a kernel spec_tree_group_<x> whose row code is the generated reader
+// of internal/lang/generator/message.go:97-186 with every tag, kind, rank and column index a
+// constant: tree_open checks the table against the schema's tag set once, every getter is then
+// one table read and a kind-specialised decode; a row whose table does not qualify (unsorted,
+// big, foreign tags) runs the run-time reader (tree_message_row), so results never depend on
+// which path ran.  Structs are the generated Decode (struct.go:75-113), members last-first.
+
+using spec::TreeDesc;
+using spec::TField;
+using spec::TTable;
+
+bool tree_table_ok(const TreeDesc &D, uint32_t t) {
+    const TTable &T = D.t[t];
+    if (T.shape != spec::SHAPE_MESSAGE) return true;
+    if (T.nd > 64) return false;
+    bool seen[256] = {false};
+    for (uint32_t k = 0; k < T.nd; k++) {
+        const uint32_t tag = D.f[D.direct[T.d0 + k]].tag;
+        if (tag > 255 || seen[tag]) return false;
+        seen[tag] = true;
+    }
+    return true;
+}
+
+bool tree_group_ok(const TreeDesc &D, uint32_t x) {
+    const TTable &T = D.t[x];
+    for (uint32_t g = 0; g < T.gn; g++)
+        if (!tree_table_ok(D, D.group[T.g0 + g])) return false;
+    return true;
+}
+
+std::string col_expr(int c) {
+    if (c < 0) return "(void *)nullptr";
+    return "B.cols[" + std::to_string(c) + "]";
+}
+
+// the members of struct field sf, last first, decoded below OFF down to LB (depth d variables)
+void gen_struct_members(std::ostringstream &o, const TreeDesc &D, uint32_t sf, const std::string &LB,
+                        const std::string &OFF, int d, const std::string &ind) {
+    const TField &F = D.f[sf];
+    for (int k = (int)F.nmem - 1; k >= 0; k--) {
+        const uint32_t mi = D.members[F.mem0 + k];
+        const TField &M = D.f[mi];
+        if (M.kind == spec::K_STRUCT) {
+            const std::string S = "S" + std::to_string(d + 1), Z = "dz" + std::to_string(d + 1),
+                              O2 = "off" + std::to_string(d + 1);
+            o << ind << "if (" << OFF << " > " << LB << ") { // inner struct, field " << mi << "\n"
+              << ind << "  long long " << S << "; uint32_t " << Z << ";\n"
+              << ind << "  sst = struct_open(s, " << LB << ", " << OFF << ", " << S << ", " << Z << ");\n"
+              << ind << "  if (sst != ST_OK) break;\n"
+              << ind << "  long long " << O2 << " = " << S << " + " << Z << ";\n";
+            gen_struct_members(o, D, mi, S, O2, d + 1, ind + "  ");
+            o << ind << "  " << OFF << " = " << S << ";\n" << ind << "}\n";
+        } else {
+            o << ind << "{ Val v; int n; const bool ok = decode_value_kn<" << (int)M.kind << ">(s, " << LB << ", " << OFF
+              << ", 0, v, n);\n"
+              << ind << "  if (" << col_expr(M.col) << ") store_value_k<" << (int)M.kind << ">(" << col_expr(M.col)
+              << ", row, v);\n"
+              << ind << "  if (!ok) { sst = ST_INVALID_VALUE; break; }\n"
+              << ind << "  " << OFF << " -= n; }\n";
+        }
+    }
+}
+
+// sst = the generated Decode of struct field sf over [LO, E) (tree_core.hpp tree_struct)
+void gen_struct(std::ostringstream &o, const TreeDesc &D, uint32_t sf, const std::string &LO, const std::string &E,
+                const std::string &ind) {
+    const TField &F = D.f[sf];
+    for (uint32_t i = sf + 1; i < F.send; i++) {
+        const TField &M = D.f[i];
+        if (M.kind == spec::K_STRUCT || M.col < 0) continue;
+        o << ind << "if (" << col_expr(M.col) << ") store_value_k<" << (int)M.kind << ">(" << col_expr(M.col)
+          << ", row, Val{0, 0, 0, 0});\n";
+    }
+    o << ind << "if (" << E << " > " << LO << ") do {\n"
+      << ind << "  long long S0; uint32_t dz0;\n"
+      << ind << "  sst = struct_open(s, " << LO << ", " << E << ", S0, dz0);\n"
+      << ind << "  if (sst != ST_OK) break;\n"
+      << ind << "  long long off0 = S0 + dz0;\n";
+    gen_struct_members(o, D, sf, "S0", "off0", 0, ind + "  ");
+    o << ind << "} while (0);\n";
+}
+
+// a message table's row: lo/hi expressions, its status column written (root: a panicked range
+// is ST_PANIC)
+void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, const std::string &lo,
+                       const std::string &hi, bool root) {
+    const TTable &T = D.t[t];
+    uint64_t m[4] = {0, 0, 0, 0};
+    for (uint32_t k = 0; k < T.nd; k++) {
+        const uint32_t tag = D.f[D.direct[T.d0 + k]].tag;
+        m[tag >> 6] |= 1ull << (tag & 63);
+    }
+    o << "  { // table " << t << "\n"
+      << "    const long long tlo = " << lo << ", thi = " << hi << ";\n"
+      << "    const TOpen o = tree_open<" << T.nd << ", 0x" << std::hex << m[0] << "ull, 0x" << m[1] << "ull, 0x" << m[2]
+      << "ull, 0x" << m[3] << "ull" << std::dec << ">(s, tlo, thi);\n"
+      << "    uint32_t st;\n"
+      << "    if (o.fast) {\n"
+      << "      st = o.st;\n"
+      << "      const long long ds = o.ds;\n"
+      << "      uint64_t *errp = " << (T.err_col >= 0 ? "(uint64_t *)" + col_expr(T.err_col) : std::string("nullptr"))
+      << ";\n"
+      << "      uint64_t errs = 0;\n";
+    for (uint32_t k = 0; k < T.nd; k++) {
+        const uint32_t fi = D.direct[T.d0 + k];
+        const TField &F = D.f[fi];
+        const std::string bit = k < 64 ? "(1ull << " + std::to_string(k) + ")" : "0ull";
+        o << "      { // field " << fi << " tag " << F.tag << " kind " << (int)F.kind << "\n"
+          << "        const long long end = tree_end<" << F.rank << ">(s, o);\n";
+        switch (F.kind) {
+        case spec::K_MESSAGE:
+            o << "        const long long e = end >= 0 ? ds + end : ds;\n"
+              << "        store_u8(" << col_expr(F.present) << ", row, end >= 0 ? 1u : 0u);\n"
+              << "        gr[" << D.t[F.table].gslot << " * 64] = end >= 0 ? make_uint2((uint32_t)ds, (uint32_t)e) : make_uint2(0, 0);\n"
+              << "        if (errp && e > ds && parse_trailer<false>(s, ds, e).st != ST_OK) errs |= " << bit << ";\n";
+            break;
+        case spec::K_LIST:
+            o << "        const long long e = end >= 0 ? ds + end : ds;\n"
+              << "        store_u8(" << col_expr(F.present) << ", row, end >= 0 ? 1u : 0u);\n"
+              << "        uint32_t cnt = 0;\n"
+              << "        uint4 h = make_uint4(0, 0, 0, 0);\n"
+              << "        if (e > ds) {\n"
+              << "          const Trailer lt = parse_trailer<true>(s, ds, e);\n"
+              << "          if (lt.st == ST_OK) {\n"
+              << "            cnt = lt.tsize / (lt.big ? 4u : 2u);\n"
+              << "            h = make_uint4((uint32_t)lt.tstart, (uint32_t)lt.dstart, lt.dsize, cnt | (lt.big ? 0x80000000u : 0u));\n"
+              << "          } else {\n"
+              << "            errs |= " << bit << ";\n"
+              << "          }\n"
+              << "        }\n"
+              << "        B.cnt[" << F.table << "][row] = cnt;\n"
+              << "        B.lh[" << F.table << "][row] = h;\n";
+            break;
+        case spec::K_STRUCT:
+            o << "        const long long e = end >= 0 ? ds + end : ds;\n"
+              << "        uint32_t sst = ST_OK;\n";
+            gen_struct(o, D, fi, "ds", "e", "        ");
+            o << "        if (sst == ST_PANIC) st = ST_PANIC;\n"
+              << "        if (sst != ST_OK) errs |= " << bit << ";\n";
+            break;
+        case spec::K_ANY:
+            o << "        const long long e = end >= 0 ? ds + end : ds;\n"
+              << "        long long n = 0;\n"
+              << "        uint2 sp = make_uint2(0, 0);\n"
+              << "        if (e > ds) {\n"
+              << "          if (type_size_inl(s, ds, e, n)) {\n"
+              << "            if (n < 0) st = ST_PANIC;\n"
+              << "            else if (n > 0 && n <= e - ds) sp = make_uint2((uint32_t)(e - n), (uint32_t)n);\n"
+              << "          } else {\n"
+              << "            errs |= " << bit << ";\n"
+              << "          }\n"
+              << "        }\n"
+              << "        if (" << col_expr(F.col) << ") ((uint2 *)" << col_expr(F.col) << ")[row] = sp;\n"
+              << "        store_u8(" << col_expr(F.present) << ", row, sp.y ? s.u8((long long)sp.x + sp.y - 1) : 0u);\n";
+            break;
+        default: // scalar kinds
+            o << "        void *col = " << col_expr(F.col) << ";\n"
+              << "        if ((col || errp) && !tree_field_k<" << (int)F.kind << ">(s, ds, end, col, row)) errs |= " << bit
+              << ";\n";
+        }
+        o << "      }\n";
+    }
+    o << "      if (errp) errp[row] = errs;\n"
+      << "    } else {\n"
+      << "      st = tree_message_row(s, D, B, " << t << "u, row, tlo, thi, gr);\n"
+      << "    }\n"
+      << "    store_u8(" << col_expr(T.status_col) << ", row, " << (root ? "panic ? (uint32_t)ST_PANIC : st" : "st")
+      << ");\n"
+      << "  }\n";
+}
+
+std::string generate_tree(const TreeDesc &D, bool *has) {
+    std::ostringstream o;
+    o << "#include \"tree_decode_core.hpp\"\nusing namespace spec;\n";
+    for (uint32_t x = 0; x < D.ntables; x++) {
+        const TTable &T = D.t[x];
+        has[x] = false;
+        if (T.groot != x || !tree_group_ok(D, x)) continue;
+        has[x] = true;
+        o << "template <class Src>\n__device__ __forceinline__ void gen_row_" << x
+          << "(const Src &s, const TreeDesc &D, const TreeBufs &B, uint64_t row, long long lo, long long hi, bool panic, "
+             "uint2 *gr) {\n";
+        if (T.shape == spec::SHAPE_VALUE) {
+            const TField &F = D.f[T.field];
+            o << "  Val v; int n;\n"
+              << "  const bool ok = decode_value_kn<" << (int)F.elem << ">(s, lo, hi, 0, v, n);\n"
+              << "  if (" << col_expr(F.col) << ") store_value_k<" << (int)F.elem << ">(" << col_expr(F.col) << ", row, v);\n"
+              << "  store_u8(" << col_expr(T.status_col) << ", row, panic ? ST_PANIC : (ok ? ST_OK : ST_INVALID_VALUE));\n";
+        } else if (T.shape == spec::SHAPE_STRUCT) {
+            o << "  uint32_t sst = ST_OK;\n";
+            gen_struct(o, D, T.field, "lo", "hi", "  ");
+            o << "  store_u8(" << col_expr(T.status_col) << ", row, panic ? (uint32_t)ST_PANIC : sst);\n";
+        } else {
+            gen_message_table(o, D, x, "lo", "hi", true);
+            for (uint32_t g = 1; g < T.gn; g++) {
+                const uint32_t y = D.group[T.g0 + g];
+                const std::string r = "gr[" + std::to_string(D.t[y].gslot) + " * 64]";
+                gen_message_table(o, D, y, "(long long)" + r + ".x", "(long long)" + r + ".y", false);
+            }
+        }
+        o << "}\n"
+          << "extern \"C\" __global__ __launch_bounds__(256) void spec_tree_group_" << x
+          << "(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x, uint32_t slab, uint32_t wave_bytes) {\n"
+          << "  const TreeDesc &D = *Dp;\n"
+          << "  const TreeBufs &B = *Bp;\n"
+          << "  const uint64_t rows = dec_rows(D, B, x);\n"
+          << "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+          << "  uint2 *gr = (uint2 *)(smem + (threadIdx.x >> 6) * wave_bytes + slab) + (threadIdx.x & 63);\n"
+          << "  tree_rows(B, x, rows, slab, wave_bytes,\n"
+          << "            [&](const TreeLds &s, uint64_t row, long long lo, long long hi, bool panic) {\n"
+          << "              gen_row_" << x << "(s, D, B, row, lo, hi, panic, gr);\n"
+          << "            },\n"
+          << "            [&](const GlobalSrc &s, uint64_t row, long long lo, long long hi, bool panic) {\n"
+          << "              tree_group_row(s, D, B, x, row, lo, hi, panic, gr);\n"
+          << "            });\n"
+          << "}\n";
+    }
+    return o.str();
+}
+
+struct TreeEntry {
+    hipModule_t mod = nullptr;
+    hipFunction_t fn[spec::TREE_MAX_T] = {};
+    bool failed = false;
+};
+std::unordered_map<std::string, TreeEntry> g_tree_cache;
+
 } // namespace
 
 namespace spec {
 
 void jit_set_enabled(int on) { g_enabled = on ? 1 : 0; }
+
+long long jit_compile_only_tree(const TreeDesc &D) {
+    bool has[TREE_MAX_T];
+    const std::string src = generate_tree(D, has);
+    return (long long)compile_source(src, TREE).size();
+}
+
+// The schema-specialised group kernels of a tree: fn[x] for each group root x that has one
+// (nullptr where the run-time kernel runs); nullptr when the JIT is off or failed.
+const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
+    if (!enabled()) return nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    bool has[TREE_MAX_T];
+    const std::string src = generate_tree(D, has);
+    const std::string key = "tree:" + std::to_string(dev) + ":" + src;
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_tree_cache.find(key);
+    if (it == g_tree_cache.end()) {
+        TreeEntry e;
+        const std::vector<char> code = compile_source(src, TREE);
+        bool ok = !code.empty() && hipModuleLoadData(&e.mod, code.data()) == hipSuccess;
+        for (uint32_t x = 0; ok && x < D.ntables; x++) {
+            if (!has[x]) continue;
+            const std::string name = "spec_tree_group_" + std::to_string(x);
+            ok = hipModuleGetFunction(&e.fn[x], e.mod, name.c_str()) == hipSuccess;
+        }
+        if (!ok) {
+            (void)hipGetLastError();
+            e.failed = true;
+            fprintf(stderr, "spec_amd jit: tree compile/load failed, run-time tree kernels in use\n");
+        }
+        it = g_tree_cache.emplace(key, e).first;
+    }
+    return it->second.failed ? nullptr : it->second.fn;
+}
 
 long long jit_compile_only(const spec_schema *schema, double) {
     if (!has_fast_path(schema)) return 0;

@@ -64,5 +64,9 @@ int launch_encode_write(const spec_schema *schema, const EncodeArgs &a, hipStrea
 // precompiled kernel, <0 HIP error.
 int jit_launch_encode(const spec_schema *schema, const EncodeArgs &a, bool write, hipStream_t stream);
 
+// jit.cpp: schema-specialised schema-tree group kernels (tree_decode.hip)
+struct TreeDesc;
+const hipFunction_t *jit_tree_kernels(const TreeDesc &D);
+long long jit_compile_only_tree(const TreeDesc &D);
 
 } // namespace spec

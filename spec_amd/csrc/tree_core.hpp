@@ -22,6 +22,7 @@
 
 namespace spec {
 
+constexpr int TB = 256; // threads per block of the row kernels
 constexpr int TREE_MAX_F = 256, TREE_MAX_T = 64, TREE_MAX_C = 512, TREE_MAX_D = 64;
 constexpr int TREE_MAX_SD = 8; // structs nested in structs (include/spec_amd.h SPEC_TREE_MAX_STRUCT_DEPTH)
 enum : uint32_t { K_STRUCT = 17, K_MESSAGE = 18, K_ANY = 19 };
@@ -158,10 +159,11 @@ __device__ __forceinline__ void store_u8(void *colp, uint64_t r, uint32_t v) {
 }
 
 // Decode<Kind>(b) of the value [lo, e) with Go's (value, n, err) (internal/decode/...; the
-// value rules are decode_tail_k's, n = bytes consumed from the end).  Returns !err.
-template <class Src>
-__device__ __noinline__ bool decode_value_n(const Src &s, uint32_t kind, typename Src::pos_t lo,
-                                               typename Src::pos_t e, long long to_stream, Val &v, int &n) {
+// value rules are decode_tail_k's, n = bytes consumed from the end).  Returns !err.  K is a
+// compile-time kind (the schema-specialised tree kernels); decode_value_n dispatches a run-time one.
+template <uint32_t K, class Src>
+__device__ __forceinline__ bool decode_value_kn(const Src &s, typename Src::pos_t lo, typename Src::pos_t e,
+                                                long long to_stream, Val &v, int &n) {
     v = Val{0, 0, 0, 0};
     n = 0;
     const long long flen = (long long)(e - lo);
@@ -173,73 +175,82 @@ __device__ __noinline__ bool decode_value_n(const Src &s, uint32_t kind, typenam
     const long long avail = flen - 1;
     int m = 0;
     bool ok = false;
-    switch (kind) {
-    case K_BOOL: n = 1; ok = true; break; // DecodeBool: any type, no error (byte.go:38-51)
-    case K_BYTE: ok = (type == T_BYTE) & (flen >= 2); n = 2; break;
-    case K_INT16:
-    case K_INT32:
-    case K_INT64: {
-        const bool w32 = (type == T_INT16) | (type == T_INT32);
-        if (!w32 && type != T_INT64) break;
-        const uint64_t u = rvarint_bf(R, R2, avail, w32 ? 5 : 10, m);
-        if (m < 0) break;
-        const long long x = w32 ? (long long)unzigzag32((uint32_t)u) : (long long)unzigzag64(u);
-        ok = kind == K_INT16 ? (x >= -32768) & (x <= 32767)
-             : kind == K_INT32 ? (w32 | ((x >= INT32_MIN) & (x <= INT32_MAX)))
-                               : true;
-        n = 1 + m;
-        break;
-    }
-    case K_UINT16:
-    case K_UINT32:
-    case K_UINT64: {
-        const bool w32 = (type == T_UINT16) | (type == T_UINT32);
-        if (!w32 && type != T_UINT64) break;
-        const uint64_t x = rvarint_bf(R, R2, avail, w32 ? 5 : 10, m);
-        if (m < 0) break;
-        ok = kind == K_UINT16 ? x <= 0xffffull : kind == K_UINT32 ? x <= 0xffffffffull : true;
-        n = 1 + m;
-        break;
-    }
-    case K_FLOAT32:
-    case K_FLOAT64: {
-        const bool f32 = (type == T_FLOAT32) & (flen >= 5), f64 = (type == T_FLOAT64) & (flen >= 9);
-        if (!f32 && !f64) break;
-        n = f32 ? 5 : 9;
+    if constexpr (K == K_BOOL) {
+        n = 1; // DecodeBool: any type, no error (byte.go:38-51)
         ok = true;
-        if (kind == K_FLOAT32) { // +-MaxFloat32 range check (float.go:15-32); NaN passes
-            if (f32) {
-                const uint32_t b = (uint32_t)(R & 0xffffffffu);
-                ok = !((((b >> 23) & 0xff) == 0xff) & ((b & 0x7fffff) == 0));
-            } else {
-                const bool nan = (((R >> 52) & 0x7ff) == 0x7ff) & ((R & 0xfffffffffffffull) != 0);
-                ok = nan | ((R & 0x7fffffffffffffffull) <= 0x47EFFFFFE0000000ull);
+    } else if constexpr (K == K_BYTE) {
+        ok = (type == T_BYTE) & (flen >= 2);
+        n = 2;
+    } else if constexpr (K == K_INT16 || K == K_INT32 || K == K_INT64) {
+        const bool w32 = (type == T_INT16) | (type == T_INT32);
+        if (w32 || type == T_INT64) {
+            const uint64_t u = rvarint_bf(R, R2, avail, w32 ? 5 : 10, m);
+            if (m >= 0) {
+                const long long x = w32 ? (long long)unzigzag32((uint32_t)u) : (long long)unzigzag64(u);
+                ok = K == K_INT16 ? (x >= -32768) & (x <= 32767)
+                     : K == K_INT32 ? (w32 | ((x >= INT32_MIN) & (x <= INT32_MAX)))
+                                    : true;
+                n = 1 + m;
             }
         }
-        break;
-    }
-    case K_BIN64: ok = (type == T_BIN64) & (flen >= 9); n = 9; break;
-    case K_BIN128: ok = (type == T_BIN128) & (flen >= 17); n = 17; break;
-    case K_BIN256: ok = (type == T_BIN256) & (flen >= 33); n = 33; break;
-    case K_STRING:
-    case K_BYTES: {
-        const bool str = kind == K_STRING;
-        if (type != (str ? T_STRING : T_BYTES)) break;
-        const uint32_t len = (uint32_t)rvarint_bf(R, R2, avail, 5, m);
-        if (m < 0) break;
-        const long long end = (long long)(e - 1) - m - (str ? 1 : 0);
-        const long long off = end - (long long)len;
-        ok = (end >= (long long)lo) & (off >= (long long)lo);
-        n = 1 + m + (str ? 1 : 0) + (int)len;
-        break;
-    }
+    } else if constexpr (K == K_UINT16 || K == K_UINT32 || K == K_UINT64) {
+        const bool w32 = (type == T_UINT16) | (type == T_UINT32);
+        if (w32 || type == T_UINT64) {
+            const uint64_t x = rvarint_bf(R, R2, avail, w32 ? 5 : 10, m);
+            if (m >= 0) {
+                ok = K == K_UINT16 ? x <= 0xffffull : K == K_UINT32 ? x <= 0xffffffffull : true;
+                n = 1 + m;
+            }
+        }
+    } else if constexpr (K == K_FLOAT32 || K == K_FLOAT64) {
+        const bool f32 = (type == T_FLOAT32) & (flen >= 5), f64 = (type == T_FLOAT64) & (flen >= 9);
+        if (f32 || f64) {
+            n = f32 ? 5 : 9;
+            ok = true;
+            if constexpr (K == K_FLOAT32) { // +-MaxFloat32 range check (float.go:15-32); NaN passes
+                if (f32) {
+                    const uint32_t b = (uint32_t)(R & 0xffffffffu);
+                    ok = !((((b >> 23) & 0xff) == 0xff) & ((b & 0x7fffff) == 0));
+                } else {
+                    const bool nan = (((R >> 52) & 0x7ff) == 0x7ff) & ((R & 0xfffffffffffffull) != 0);
+                    ok = nan | ((R & 0x7fffffffffffffffull) <= 0x47EFFFFFE0000000ull);
+                }
+            }
+        }
+    } else if constexpr (K == K_BIN64) {
+        ok = (type == T_BIN64) & (flen >= 9);
+        n = 9;
+    } else if constexpr (K == K_BIN128) {
+        ok = (type == T_BIN128) & (flen >= 17);
+        n = 17;
+    } else if constexpr (K == K_BIN256) {
+        ok = (type == T_BIN256) & (flen >= 33);
+        n = 33;
+    } else if constexpr (K == K_STRING || K == K_BYTES) {
+        constexpr bool str = K == K_STRING;
+        if (type == (str ? T_STRING : T_BYTES)) {
+            const uint32_t len = (uint32_t)rvarint_bf(R, R2, avail, 5, m);
+            if (m >= 0) {
+                const long long end = (long long)(e - 1) - m - (str ? 1 : 0);
+                const long long off = end - (long long)len;
+                ok = (end >= (long long)lo) & (off >= (long long)lo);
+                n = 1 + m + (str ? 1 : 0) + (int)len;
+            }
+        }
     }
     if (!ok) {
         n = 0;
         return false;
     }
+    v = decode_tail_k<K>(load_win<K>(s, e), lo, e, to_stream);
+    return true;
+}
+
+template <class Src>
+__device__ __noinline__ bool decode_value_n(const Src &s, uint32_t kind, typename Src::pos_t lo,
+                                            typename Src::pos_t e, long long to_stream, Val &v, int &n) {
 #define SPEC_CASE(K) \
-    case K: v = decode_tail_k<K>(load_win<K>(s, e), lo, e, to_stream); break;
+    case K: return decode_value_kn<K>(s, lo, e, to_stream, v, n);
     switch (kind) {
         SPEC_CASE(K_BOOL)
         SPEC_CASE(K_BYTE)
@@ -258,7 +269,9 @@ __device__ __noinline__ bool decode_value_n(const Src &s, uint32_t kind, typenam
         SPEC_CASE(K_BYTES)
     }
 #undef SPEC_CASE
-    return true;
+    v = Val{0, 0, 0, 0};
+    n = 0;
+    return e <= lo; // not a scalar kind: empty input decodes without error
 }
 
 // DecodeStruct (internal/decode/struct.go:14-42) of the value ending at e over [lo, e), then
@@ -375,7 +388,7 @@ __device__ __forceinline__ uint32_t rsize32(const Src &s, long long lo, long lon
 // returns false on an error; n may be negative (the struct case checks n, not m: the bug is
 // kept, type.go:185-191).
 template <class Src>
-__device__ __noinline__ bool type_size(const Src &s, long long lo, long long e, long long &n) {
+__device__ __forceinline__ bool type_size_inl(const Src &s, long long lo, long long e, long long &n) {
     n = 0;
     if (e <= lo) return true;
     const uint32_t t = s.u8((typename Src::pos_t)(e - 1));
@@ -422,6 +435,11 @@ __device__ __noinline__ bool type_size(const Src &s, long long lo, long long e, 
     }
     }
     return false;
+}
+
+template <class Src>
+__device__ __noinline__ bool type_size(const Src &s, long long lo, long long e, long long &n) {
+    return type_size_inl(s, lo, e, n);
 }
 
 // ---- encode helpers ----------------------------------------------------------------------

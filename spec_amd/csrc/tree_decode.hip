@@ -23,260 +23,32 @@
 #include <new>
 
 #include "spec_internal.hpp"
+#include "tree_decode_core.hpp"
 #include "tree_internal.hpp"
 
 namespace spec {
 namespace {
 
-constexpr int LANE_W = 256;          // bytes of a lane's window (lane staging)
-constexpr int LANE_CHUNKS = LANE_W / 16;
-constexpr int GUARD = 64;            // bytes staged below a row (value windows read below its start)
-
-// Staged stream bytes [off, off + size) at lds: reads are clamped into the window (every read
-// of a row's parse lies in [lo - 64, hi + 16), which the staging covers).
-struct TreeLds {
-    using pos_t = long long;
-    lds_u8 *lds;
-    long long off;
-    int size;
-    __device__ __forceinline__ int at(long long p, int n) const {
-        long long i = p - off;
-        i = i < 0 ? 0 : i;
-        return (int)(i > size - n ? size - n : i);
-    }
-    __device__ __forceinline__ uint32_t u8(long long p) const { return lds[at(p, 1)]; }
-    __device__ __forceinline__ uint64_t d64(long long p) const {
-        int i = at(p, 8);
-        asm("" : "+v"(i)); // one ds_read_b64 per qword (LdsSrc::d64)
-        return *(lds_u64 *)(lds + i);
-    }
-    __device__ __forceinline__ uint32_t d32(long long p) const { return *(lds_u32 *)(lds + at(p, 4)); }
-};
-
-__device__ __forceinline__ void wave_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Rows of table x during a decode: the records (n) or a list table's device-counted rows,
-// capped by its capacity (a sub-message table has its owner's rows).
-__device__ __forceinline__ uint64_t dec_rows(const TreeDesc &D, const TreeBufs &B, uint32_t x) {
-    const uint32_t g = D.t[x].groot;
-    if (g == 0) return B.n;
-    const uint64_t r = B.rowsd[g];
-    return r < B.caps[g] ? r : B.caps[g];
-}
-
-// Every wave of the grid over the rows of group root x, 64 at a time:
-// body(src, row, lo, hi, panic) for its valid rows, src = the staged bytes or HBM.
-template <class Body>
-__device__ __forceinline__ void tree_rows(const TreeBufs &B, uint32_t x, uint64_t rows, uint32_t slab_bytes,
-                                          uint32_t wave_bytes, Body body) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint8_t *slab = smem + wave * wave_bytes;
-    const __amdgpu_buffer_rsrc_t rsrc = stream_rsrc(B);
-    const GlobalSrc gs{rsrc, B.stream_len};
-    const uint64_t wstride = (uint64_t)gridDim.x * (TB / 64) * 64;
-    for (uint64_t base = ((uint64_t)blockIdx.x * (TB / 64) + wave) * 64; base < rows; base += wstride) {
-        const uint64_t row = base + lane;
-        const bool valid = row < rows;
-        long long lo = 0, hi = 0;
-        bool panic = false;
-        if (valid) row_range(B, x, row, lo, hi, panic);
-        const bool some = valid && hi > lo;
-        long long slo = some ? lo : (long long)B.stream_len, shi = some ? hi : 0, len = some ? hi - lo : 0;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            const long long a = __shfl_xor(slo, d), b2 = __shfl_xor(shi, d), l2 = __shfl_xor(len, d);
-            slo = a < slo ? a : slo;
-            shi = b2 > shi ? b2 : shi;
-            len = l2 > len ? l2 : len;
-        }
-        slo = (long long)uniform64((uint64_t)slo);
-        shi = (long long)uniform64((uint64_t)shi);
-        len = (long long)uniform64((uint64_t)len);
-        const long long sb = (slo > GUARD ? slo - GUARD : 0) & ~15ll, se = (shi + 16 + 15) & ~15ll;
-        if (slab_bytes && slo < shi && se - sb + 16 <= (long long)slab_bytes) {
-            // the span: LDS-DMA, 1 KiB per instruction, all in flight at once
-            const uint32_t chunks = (uint32_t)((se - sb + 1023) >> 10);
-            for (uint32_t c = 0; c < chunks; c++)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(slab + c * 1024),
-                                                         16, (uint32_t)sb + c * 1024 + lane * 16, 0, 0, 0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            // a 16-byte chunk straddling the stream end comes back zeroed: refill it bytewise
-            const uint64_t tail = B.stream_len & ~15ull;
-            if (tail < B.stream_len && (long long)tail >= sb && (long long)tail < sb + (long long)chunks * 1024 &&
-                lane < 16 && tail + lane < B.stream_len)
-                slab[tail - sb + lane] = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)(tail + lane), 0, 0);
-            wave_fence();
-            if (valid) body(TreeLds{(lds_u8 *)slab, sb, (int)slab_bytes}, row, lo, hi, panic);
-        } else if (slab_bytes >= 64 * LANE_W && len + GUARD + 48 <= LANE_W) {
-            // each row in its lane's window: its 16-byte chunks, all loads issued before the stores
-            uint8_t *win = slab + lane * LANE_W;
-            const long long lb = (lo > GUARD ? lo - GUARD : 0) & ~15ll;
-            const int nch = some ? (int)((((hi + 16 + 15) & ~15ll) - lb) >> 4) : 0;
-            uint4 v[LANE_CHUNKS];
-#pragma unroll
-            for (int c = 0; c < LANE_CHUNKS; c++) {
-                const long long p = lb + 16ll * c;
-                if (c < nch) {
-                    if ((uint64_t)p + 16 <= B.stream_len) {
-                        const auto q = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)p, 0, 0);
-                        v[c] = make_uint4(q[0], q[1], q[2], q[3]);
-                    } else {
-                        v[c] = make_uint4(gs.d32(p), gs.d32(p + 4), gs.d32(p + 8), gs.d32(p + 12));
-                    }
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < LANE_CHUNKS; c++)
-                if (c < nch) *(uint4 *)(win + 16 * c) = v[c];
-            wave_fence();
-            if (valid) body(TreeLds{(lds_u8 *)win, lb, LANE_W}, row, lo, hi, panic);
-        } else if (valid) {
-            body(gs, row, lo, hi, panic);
-        }
-        wave_fence(); // the staged bytes are read before the next rows overwrite them
-    }
-}
-
-// A message row of table t over [lo, hi): OpenMessageErr, every direct field's getter into its
-// column, *Err bits, and for its children: sub-message ranges (into the group's LDS range
-// slots), list counts + list table positions (for the scan).  Returns the row's status.
-// Out of line, once per source: the generic row code is large (every kind's decoder), and one
-// copy per call site overflowed the instruction cache (98K instructions: the waves of one
-// kernel executing different fields' code missed it constantly).
-template <class Src>
-__device__ __forceinline__ bool tree_scalar(const Src &s, uint32_t kind, long long ds, long long end, void *col,
-                                            uint64_t row, bool want_err) {
-    if (!col && !want_err) return true;
-    Val v;
-    int n;
-    const bool ok = decode_value_n(s, kind, ds, end >= 0 ? ds + end : ds, 0, v, n); // m.<Kind>(tag)
-    store_kind(col, row, kind, v);
-    return ok;
-}
-
-template <class Src>
-__device__ __noinline__ uint32_t tree_message_row(const Src &s, const TreeDesc &D, const TreeBufs &B, uint32_t t,
-                                                  uint64_t row, long long lo, long long hi, uint2 *gr) {
-    const TTable &T = D.t[t];
-    const RecInfo ri = rec_open(s, lo, hi); // empty (or panicked) range => empty message
-    uint32_t st = ri.tr.st;
-    const long long ds = ri.tr.dstart;
-    uint64_t *errp = T.err_col >= 0 ? (uint64_t *)B.cols[T.err_col] : nullptr;
-    uint64_t errs = 0;
-    for (uint32_t k = 0; k < T.nd; k++) {
-        const uint32_t fi = D.direct[T.d0 + k];
-        const TField &F = D.f[fi];
-        const long long end = rec_field_end(s, ri, F.tag, F.rank);
-        const long long e = end >= 0 ? ds + end : ds;
-        bool bad = false; // the field's *Err getter errs
-        switch (F.kind) {
-        case K_MESSAGE: {
-            store_u8(B.cols[F.present], row, end >= 0 ? 1u : 0u);
-            // its table decodes next in this group, over m.field(tag) (Message(tag), msg.go:447-451)
-            gr[D.t[F.table].gslot * 64] = end >= 0 ? make_uint2((uint32_t)ds, (uint32_t)e) : make_uint2(0, 0);
-            if (errp && e > ds) bad = parse_trailer<false>(s, ds, e).st != ST_OK; // MessageErr
-            break;
-        }
-        case K_LIST: {
-            store_u8(B.cols[F.present], row, end >= 0 ? 1u : 0u);
-            // OpenList(m.field(tag)): errors => an empty list (internal/types/list.go:22-25)
-            ListInfo li = {0, 0, 0, 0, false};
-            if (e > ds) {
-                const Trailer lt = parse_trailer<true>(s, ds, e);
-                if (lt.st == ST_OK) {
-                    li.big = lt.big;
-                    li.count = lt.tsize / (lt.big ? 4u : 2u);
-                    li.dstart = lt.dstart;
-                    li.tstart = lt.tstart;
-                    li.dsize = lt.dsize;
-                } else {
-                    bad = true; // ListErr
-                }
-            }
-            B.cnt[F.table][row] = li.count;
-            B.lh[F.table][row] = make_uint4((uint32_t)li.tstart, (uint32_t)li.dstart, li.dsize,
-                                            li.count | (li.big ? 0x80000000u : 0u));
-            break;
-        }
-        case K_STRUCT: {
-            const uint32_t sst = tree_struct(s, D, B, fi, ds, e, row, 0);
-            if (sst == ST_PANIC) st = ST_PANIC;
-            bad = sst != ST_OK;
-            break;
-        }
-        case K_ANY: {
-            // Field(tag) = OpenValue(bytes[:end]): nil on error or len < n; n < 0 panics
-            long long n = 0;
-            uint2 sp = make_uint2(0, 0);
-            if (e > ds) {
-                if (type_size(s, ds, e, n)) {
-                    if (n < 0) st = ST_PANIC;
-                    else if (n > 0 && n <= e - ds) sp = make_uint2((uint32_t)(e - n), (uint32_t)n);
-                } else {
-                    bad = true; // OpenValueErr: DecodeTypeSize's error
-                }
-            }
-            if (B.cols[F.col]) ((uint2 *)B.cols[F.col])[row] = sp;
-            // Value.Type(): the value's last byte (DecodeType), 0 for a nil value
-            store_u8(B.cols[F.present], row, sp.y ? s.u8((long long)sp.x + sp.y - 1) : 0u);
-            break;
-        }
-        default:
-            bad = !tree_scalar(s, F.kind, ds, end, B.cols[F.col], row, errp != nullptr);
-        }
-        if (bad && k < 64) errs |= 1ull << k;
-    }
-    if (errp) errp[row] = errs;
-    return st;
-}
-
 // Group root x (the records or a list table) and the sub-message tables below it, a lane per
-// row.  LDS per wave: the staging slab, then a range slot per sub-message table of the group.
+// row, run-time schema.  LDS per wave: the staging slab, then a range slot per sub-message table
+// of the group.
 __global__ __launch_bounds__(TB) void tree_group_kernel(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x,
                                                          uint32_t slab, uint32_t wave_bytes) {
     const TreeDesc &D = *Dp;
     const TreeBufs &B = *Bp;
-    const TTable &T = D.t[x];
     const uint64_t rows = dec_rows(D, B, x);
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint2 *gr = (uint2 *)(smem + (threadIdx.x >> 6) * wave_bytes + slab) + (threadIdx.x & 63);
-    tree_rows(B, x, rows, slab, wave_bytes, [&](const auto &s, uint64_t row, long long lo, long long hi, bool panic) {
-        uint32_t st;
-        if (T.shape == SHAPE_VALUE) {
-            const TField &F = D.f[T.field];
-            Val v;
-            int n;
-            const bool ok = decode_value_n(s, F.elem, lo, hi, 0, v, n);
-            store_kind(B.cols[F.col], row, F.elem, v);
-            st = panic ? ST_PANIC : (ok ? ST_OK : ST_INVALID_VALUE);
-            store_u8(B.cols[T.status_col], row, st);
-            return;
-        }
-        if (T.shape == SHAPE_STRUCT) {
-            st = tree_struct(s, D, B, T.field, lo, hi, row, 0);
-            store_u8(B.cols[T.status_col], row, panic ? ST_PANIC : st);
-            return;
-        }
-        st = tree_message_row(s, D, B, x, row, lo, hi, gr);
-        store_u8(B.cols[T.status_col], row, panic ? ST_PANIC : st);
-        // the sub-message tables of the group, pre-order: each over the range its owner found
-        for (uint32_t g = 1; g < T.gn; g++) {
-            const uint32_t y = D.group[T.g0 + g];
-            const uint2 r = gr[D.t[y].gslot * 64];
-            const uint32_t sy = tree_message_row(s, D, B, y, row, (long long)r.x, (long long)r.y, gr);
-            store_u8(B.cols[D.t[y].status_col], row, sy);
-        }
-    });
+    auto body = [&](const auto &s, uint64_t row, long long lo, long long hi, bool panic) {
+        tree_group_row(s, D, B, x, row, lo, hi, panic, gr);
+    };
+    tree_rows(B, x, rows, slab, wave_bytes, body, body);
 }
 
 // ---- the group's list counts -> CSR begin, row counts, element ranges ----------------------
 
-constexpr int SCAN_T = 1024, SCAN_PER = 4, SCAN_TILE = SCAN_T * SCAN_PER;
+// one owner row per thread: the apply pass's per-row element loads are the latency to hide
+constexpr int SCAN_T = 1024, SCAN_PER = 1, SCAN_TILE = SCAN_T * SCAN_PER;
 
 __device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t *sh, uint64_t &block_total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -312,7 +84,7 @@ struct ListSet {
     uint64_t *ws[TREE_MAX_T];   // per list: tile sums, then their exclusive offsets
 };
 
-// pass 1: per tile of 4096 owner rows and list j (blockIdx.y), the tile's element total
+// pass 1: per tile of SCAN_TILE owner rows and list j (blockIdx.y), the tile's element total
 __global__ __launch_bounds__(SCAN_T) void list_tiles_kernel(const TreeDesc *Dp, const TreeBufs *Bp, ListSet m) {
     __shared__ uint64_t sh[17];
     const TreeDesc &D = *Dp;
@@ -382,18 +154,28 @@ __global__ __launch_bounds__(SCAN_T) void list_apply_kernel(const TreeDesc *Dp, 
         if (r >= rows) break;
         if (beg) beg[r] = (uint32_t)p;
         if (v[k]) {
-            // List.GetBytes(i) (internal/types/list.go:100-116, format/list.go:152-176)
+            // List.GetBytes(i) (internal/types/list.go:100-116, format/list.go:152-176): the
+            // table's entries 16 bytes at a time (8 small / 4 big), both loads in flight at once
             const uint4 h = lh[r];
             const bool big = (h.w & 0x80000000u) != 0;
+            const uint32_t esz = big ? 4u : 2u, per = 16u / esz;
             uint32_t a = 0;
-            for (uint32_t j = 0; j < v[k] && p + j < cap; j++) {
-                const uint32_t b = big ? be32_at(gs, (long long)h.x + 4ll * j) : be16_at(gs, (long long)h.x + 2ll * j);
-                uint2 rr;
-                if (b > h.z) rr = make_uint2(0, 0);               // end > dataSize: nil element
-                else if (a > b) rr = make_uint2(RNG_PANIC, 0);     // start > end: Go panics
-                else rr = make_uint2(h.y + a, h.y + b);
-                rng[p + j] = rr;
-                a = b;
+            for (uint32_t j0 = 0; j0 < v[k] && p + j0 < cap; j0 += per) {
+                const long long q = (long long)h.x + (long long)j0 * esz;
+                const uint64_t w0 = load_le64(gs, q), w1 = load_le64(gs, q + 8);
+#pragma unroll
+                for (uint32_t u = 0; u < 8; u++) {
+                    const uint32_t j = j0 + u;
+                    if (u >= per || j >= v[k] || p + j >= cap) break;
+                    const uint64_t w = u * esz < 8 ? w0 >> (8 * (u * esz)) : w1 >> (8 * (u * esz - 8));
+                    const uint32_t b = big ? __builtin_bswap32((uint32_t)w) : (uint32_t)__builtin_bswap16((uint16_t)w);
+                    uint2 rr;
+                    if (b > h.z) rr = make_uint2(0, 0);               // end > dataSize: nil element
+                    else if (a > b) rr = make_uint2(RNG_PANIC, 0);     // start > end: Go panics
+                    else rr = make_uint2(h.y + a, h.y + b);
+                    rng[p + j] = rr;
+                    a = b;
+                }
             }
         }
         p += v[k];
@@ -454,6 +236,8 @@ struct spec_tree_decoder {
     int slot = 0;
     uint64_t rows[TREE_MAX_T] = {0}; // from the last index
     bool indexed = false;
+    const hipFunction_t *jit = nullptr; // schema-specialised group kernels (jit.cpp), per group root
+    bool jit_looked = false;
     ~spec_tree_decoder() {
         for (hipEvent_t &e : ev)
             if (e) (void)hipEventDestroy(e);
@@ -559,6 +343,10 @@ int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, 
     if (n == 0) {
         if (hipMemsetAsync(B.rowsd, 0, TREE_MAX_T * sizeof(uint64_t), st) != hipSuccess) return SPEC_E_HIP;
     }
+    if (!d->jit_looked) { // compiled (or read from the code-object cache) on first use
+        d->jit = jit_tree_kernels(D);
+        d->jit_looked = true;
+    }
     const TreeDesc *Dd = (const TreeDesc *)d->desc.p;
     const TreeBufs *Bd = (const TreeBufs *)d->bufs.p;
     uint8_t *wsp = (uint8_t *)d->ws_scan.p;
@@ -570,8 +358,17 @@ int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, 
         if (n) {
             const GroupShape gs = group_shape(L, x, stream_len, n);
             const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((cap + TB - 1) / TB, 1u << 20));
-            hipLaunchKernelGGL(tree_group_kernel, dim3((unsigned)blocks), dim3(TB), (size_t)(TB / 64) * gs.wave_bytes, st,
-                               Dd, Bd, x, gs.slab, gs.wave_bytes);
+            const size_t lds = (size_t)(TB / 64) * gs.wave_bytes;
+            if (d->jit && d->jit[x]) {
+                uint32_t xx = x, slab = gs.slab, wb = gs.wave_bytes;
+                void *args[] = {(void *)&Dd, (void *)&Bd, &xx, &slab, &wb};
+                if (hipModuleLaunchKernel(d->jit[x], (unsigned)blocks, 1, 1, TB, 1, 1, (unsigned)lds, st, args, nullptr) !=
+                    hipSuccess)
+                    return SPEC_E_HIP;
+            } else {
+                hipLaunchKernelGGL(tree_group_kernel, dim3((unsigned)blocks), dim3(TB), lds, st, Dd, Bd, x, gs.slab,
+                                   gs.wave_bytes);
+            }
         }
         // every list owned in the group: one batched scan
         ListSet m;
@@ -696,6 +493,15 @@ int spec_tree_decoder_reserve(spec_tree_decoder *d, const uint64_t *rows) {
     for (uint32_t x = 1; x < d->L.nt; x++)
         if (d->L.desc.t[x].rel == REL_MANY) d->caps[x] = std::max(d->caps[x], rows[x]);
     return SPEC_OK;
+}
+
+long long spec_tree_jit_compile(const spec_tree *tree) {
+    Layout *L = new (std::nothrow) Layout();
+    if (!L) return SPEC_E_INVALID_ARGUMENT;
+    long long r = SPEC_E_INVALID_ARGUMENT;
+    if (build_layout(tree, *L)) r = jit_compile_only_tree(L->desc);
+    delete L;
+    return r;
 }
 
 int spec_decode_values(int kind, const uint8_t *stream_bytes, uint64_t stream_len, const spec_span *spans, uint64_t n,

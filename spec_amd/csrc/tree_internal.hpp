@@ -12,8 +12,6 @@
 
 namespace spec {
 
-constexpr int TB = 256; // threads per block of the row kernels
-
 unsigned row_grid(uint64_t rows); // blocks for a grid-stride pass over `rows` rows
 bool is_scalar(int kind);
 
