@@ -65,6 +65,20 @@ def parse(argv=None):
     return p.parse_args(argv)
 
 
+def source_rev() -> str:
+    """Hash of the engine's device and host sources (spec_amd/csrc): the code revision a kernel
+    time or a PMC traffic figure belongs to."""
+    import hashlib
+
+    h = hashlib.sha1()
+    d = os.path.join(ROOT, "spec_amd", "csrc")
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".hpp", ".cpp", ".h")):
+            h.update(f.encode())
+            h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()[:12]
+
+
 def spec_env():
     return {k: v for k, v in sorted(os.environ.items()) if k.startswith("SPEC_AMD_")}
 
@@ -336,7 +350,9 @@ def nested_leg(n, seed, dev):
                            "launched back to back, no host sync",
             "decode_twopass_ms": round(two_ms, 4),
             "encode_mmsg_s": round(n / (enc_ms * 1e-3) / 1e6, 1), "encode_ms": round(enc_ms, 4),
-            "encode_gb_s": round(enc_alg / (enc_ms * 1e-3) / 1e9, 1), "roundtrip_ok": bool(ok)}
+            "encode_gb_s": round(enc_alg / (enc_ms * 1e-3) / 1e9, 1),
+            "encode_frac": round(enc_alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "encode_alg_bytes": int(enc_alg),
+            "roundtrip_ok": bool(ok)}
 
 
 def frames_leg(stream, ends, dev):
@@ -524,6 +540,37 @@ def generic_leg(stream, ends, want_cols, want_status, avg_jit_ms):
             "vs_specialised": round(ms / avg_jit_ms, 2), "same_columns": bool(same)}
 
 
+def errmask_leg(stream, ends, want_cols, want_status, avg_jit_ms):
+    """spec_decode_flat_errors on the headline batch (the schema-specialised errmask variant):
+    decode + a per-record uint64 of field *Err bits (internal/types/msg.go:233-459).  Same
+    columns as spec_decode_flat, masks all zero (every record is a Writer's)."""
+    import ctypes as C
+
+    from spec_amd import _lib
+    from spec_amd.batch import alloc_columns
+
+    n = ends.numel()
+    cols = alloc_columns(FLAT16, n, stream.device)
+    st = torch.empty(n, dtype=torch.uint8, device=stream.device)
+    em = torch.empty(n, dtype=torch.int64, device=stream.device)
+    ptrs = (C.c_void_p * len(cols))(*[c.data_ptr() for c in cols])
+    L = _lib.lib()
+    args = (C.byref(FLAT16.c), C.c_void_p(stream.data_ptr()), stream.numel(), C.c_void_p(ends.data_ptr()), n, ptrs,
+            C.c_void_p(st.data_ptr()), C.c_void_p(em.data_ptr()), None)
+
+    def run():
+        _lib.check(L.spec_decode_flat_errors(*args), "spec_decode_flat_errors")
+
+    run()
+    ms, _ = kernel_time_events(run, 20)
+    torch.cuda.synchronize()
+    same = torch.equal(st, want_status) and all(torch.equal(a, b) for a, b in zip(cols, want_cols))
+    alg = stream.numel() + n * (8 + COLUMN_BYTES + 1 + 8)
+    return {"ms": round(ms, 4), "mmsg_s": round(n / (ms * 1e-3) / 1e6, 1), "gb_s": round(alg / (ms * 1e-3) / 1e9, 1),
+            "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "vs_decode": round(ms / avg_jit_ms, 3),
+            "same_columns": bool(same), "masks_zero": bool(int((em != 0).sum().item()) == 0)}
+
+
 def verify_sample(cols, heaps, stream, ends, out_cols, status, m):
     """Oracle check of the first m records, outside any timed region: the oracle Writer's bytes
     for their columns == the GPU encoder's stream prefix, and the oracle's OpenMessageErr +
@@ -609,6 +656,8 @@ def tree_leg(dev, n=1 << 18, seed=7):
             "decode_note": "spec_tree_decoder_run: one asynchronous pass (group kernels + list scans), HIP events",
             "index_plus_decode_wall_ms": round(index_decode_s * 1e3, 3),
             "encode_ms": round(res["encode"] * 1e3, 3), "encode_mmsg_s": round(n / res["encode"] / 1e6, 1),
+            "encode_gb_s": round(alg / res["encode"] / 1e9, 1),
+            "encode_frac": round(alg / res["encode"] / 1e9 / HBM_PEAK_GBS, 4),
             "bit_exact_and_parity_vs_oracle": bool(ok),
             "note": "encode: generic row kernels, table by table, wall time incl. host syncs"}
 
@@ -674,12 +723,16 @@ def run(args, env):
 
     # HBM bytes per launch from the committed rocprofv3 PMC passes (tools/pmc_traffic.py):
     # FETCH_SIZE x 2 (gfx950 correction, MI355X_MICROARCH.md) + WRITE_SIZE, for this kernel
-    traffic = None
+    # The passes record the device-source revision they measured (source_rev): a traffic figure
+    # measured on other kernel code is not reported (traffic null, traffic_rev says which).
+    traffic, traffic_rev = None, None
     kname = "spec_decode_flat_jit" if jit else "decode_flat_kernel"
+    rev = source_rev()
     if os.path.exists(args.traffic):
         try:
             t = json.load(open(args.traffic)).get(kname, {})
-            if t.get("records") == n:
+            traffic_rev = t.get("source_rev")
+            if t.get("records") == n and traffic_rev == rev:
                 traffic = t.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -702,6 +755,7 @@ def run(args, env):
         enc_alg = n * (COLUMN_BYTES + 8) + heap_bytes + stream_bytes
         extras["encode"] = {"mmsg_s": round(n / (enc_ms * 1e-3) / 1e6, 1),
                             "gb_s": round(enc_alg / (enc_ms * 1e-3) / 1e9, 1),
+                            "frac": round(enc_alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "alg_bytes": int(enc_alg),
                             "ms": round(enc_ms, 4), "bit_exact_vs_decode_input": bool(enc_same)}
         if not args.no_jit and jit:
             try:
@@ -709,6 +763,11 @@ def run(args, env):
                 checks["generic_same_columns"] = extras["decode_generic"]["same_columns"]
             except Exception as e:  # an extra leg never hides the headline line
                 extras["decode_generic"] = {"error": repr(e)[:300]}
+        try:
+            extras["decode_errmask"] = errmask_leg(stream, ends, out_cols, status, avg_ms)
+            checks["errmask_same_columns"] = extras["decode_errmask"]["same_columns"]
+        except Exception as e:
+            extras["decode_errmask"] = {"error": repr(e)[:300]}
         if args.shard_total > 0:
             try:
                 extras["config5_sharded"] = shard_leg(args, dist, rank, world, dev)
@@ -784,7 +843,7 @@ def run(args, env):
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": kname, "kernel_ms_avg": round(avg_ms, 5),
                          "kernel_ms_median": round(med_ms, 5), "alg_bytes_per_launch": alg_bytes,
-                         "read_only_gb_s": round(read_only, 1)},
+                         "read_only_gb_s": round(read_only, 1), "source_rev": rev, "traffic_rev": traffic_rev},
             "cpu_baseline": cpu,
             "correct": bool(all(checks.values())),
             "checks": checks,

@@ -531,6 +531,9 @@ int spec_encode_flat(const spec_schema *schema, const void *const *columns,
  * (string/bytes > MaxSize or outside its heap, item_begin not monotonic or > nitems) makes
  * *total all-ones.  Workspace: spec_encode_nested_workspace_size(n) bytes. */
 size_t spec_encode_nested_workspace_size(uint64_t n);
+/* A workspace of at least spec_encode_nested_workspace_size_items(n, nitems) bytes also keeps the
+ * size pass's per-item prefixes for the write pass (faster; same bytes). */
+size_t spec_encode_nested_workspace_size_items(uint64_t n, uint64_t nitems);
 int spec_encode_nested(const spec_nested_schema *schema, const void *const *outer_columns,
                        const uint8_t *const *outer_heaps, const uint64_t *outer_heap_lens, const uint32_t *item_begin,
                        const void *const *item_columns, const uint8_t *const *item_heaps,

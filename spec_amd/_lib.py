@@ -172,6 +172,8 @@ def _declare(L):
     L.spec_shard_sync.argtypes = [vp]
     L.spec_tree_decoder_run.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.POINTER(vp), vp, vp]
     L.spec_tree_decoder_reserve.argtypes = [vp, C.POINTER(C.c_uint64)]
+    L.spec_encode_nested_workspace_size_items.argtypes = [C.c_uint64, C.c_uint64]
+    L.spec_encode_nested_workspace_size_items.restype = C.c_size_t
     L.spec_tree_jit_compile.argtypes = [C.POINTER(SpecTree)]
     L.spec_tree_jit_compile.restype = C.c_longlong
     L.spec_tree_decoder_index_spans.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.POINTER(C.c_uint64), vp]

@@ -407,6 +407,12 @@ long long spec_encode_nested_jit_compile(const spec_nested_schema *schema) {
 
 size_t spec_encode_nested_workspace_size(uint64_t n) { return spec_encode_flat_workspace_size(n); }
 
+// block sums | item prefixes (u32 per item) | wave verdicts (one byte per 64 records)
+static size_t nested_ws_base(uint64_t n) { return (spec_encode_flat_workspace_size(n) + 255) & ~(size_t)255; }
+size_t spec_encode_nested_workspace_size_items(uint64_t n, uint64_t nitems) {
+    return nested_ws_base(n) + (((size_t)nitems * 4 + 255) & ~(size_t)255) + (size_t)((n + 63) / 64);
+}
+
 static int heaps_of(spec::EncFields &e, const spec_schema *s, const uint8_t *const *heaps, const uint64_t *lens) {
     for (uint32_t f = 0; f < s->nfields; f++) {
         int k = s->fields[f].kind;
@@ -450,6 +456,10 @@ int spec_encode_nested(const spec_nested_schema *schema, const void *const *oute
     a.block_sums = (uint64_t *)workspace;
     a.nblocks = (n + spec::ENC_BLOCK - 1) / spec::ENC_BLOCK;
     a.total = total;
+    if (workspace_size >= spec_encode_nested_workspace_size_items(n, nitems)) {
+        a.item_pre = (uint32_t *)((uint8_t *)workspace + nested_ws_base(n));
+        a.wave_ok = (uint8_t *)a.item_pre + (((size_t)nitems * 4 + 255) & ~(size_t)255);
+    }
     if (spec::launch_nested_encode(schema, a, out != nullptr, (hipStream_t)stream))
         return hip_rc(hipGetLastError());
     return SPEC_OK;

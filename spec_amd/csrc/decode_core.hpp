@@ -825,7 +825,7 @@ __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
     if (g >= ngroups) return;
     uint8_t *slab = smem + wave * a.slab;
     __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
+        uniform_rsrc(a.stream, a.stream_len);
 
     uint64_t lo, hi;
     load_group_ends(a, a.r0 + g * 64, lane, lo, hi);
@@ -869,7 +869,7 @@ __device__ __forceinline__ void decode_flat_body(const DecodeArgs &a) {
             if (has_next && nxt.in_lds) issue_dma(rsrc, slab, nxt, lane);
             if (g2 < ngroups) load_group_ends(a, a.r0 + g2 * 64, lane, lo2, hi2);
             if (valid) {
-                GlobalSrc s{rsrc, a.stream_len};
+                GlobalSrc s{a.stream, a.stream_len};
                 decode_record_generic(s, (long long)cur.rec_lo, (long long)cur.rec_hi, r, a.f, 0);
             }
         }
@@ -904,7 +904,7 @@ __device__ __forceinline__ void decode_flat_once(const DecodeArgs &a) {
     const bool valid = r < a.n;
     uint8_t *slab = smem + wave * a.slab;
     __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
+        uniform_rsrc(a.stream, a.stream_len);
     const uint64_t hi = a.ends[valid ? r : a.n - 1];
     uint64_t lo = __shfl_up(hi, 1);
     if (lane == 0) lo = r == 0 ? 0 : a.ends[r - 1];
@@ -928,7 +928,7 @@ __device__ __forceinline__ void decode_flat_once(const DecodeArgs &a) {
         }
         decode_record_generic(s, rs, re, r, a.f, to_stream);
     } else if (valid) {
-        GlobalSrc s{rsrc, a.stream_len};
+        GlobalSrc s{a.stream, a.stream_len};
         decode_record_generic(s, (long long)cur.rec_lo, (long long)cur.rec_hi, r, a.f, 0);
     }
 }

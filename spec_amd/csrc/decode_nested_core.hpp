@@ -447,7 +447,7 @@ __device__ __forceinline__ uint32_t nested_decode_part(const NestedArgs &a, __am
                                                       g, item_base, lane, (long long)gr.aligned_lo - SLAB_GUARD, a,
                                                       RANGES ? (uint32_t *)(slab + a.slab) : nullptr);
     }
-    GlobalSrc s{rsrc, a.stream_len};
+    GlobalSrc s{a.stream, a.stream_len};
     return nested_group_body<OSpec, ISpec, false, U>(s, (long long)gr.rec_lo, (long long)gr.rec_hi, valid, r, g,
                                                   item_base, lane, 0, a);
 }
@@ -481,7 +481,7 @@ __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
     // per wave: the slab, then (RANGES) the item range window
     uint8_t *slab = smem + wave * (a.slab + (RANGES ? NESTED_RANGE_BYTES : 0u));
     __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
+        uniform_rsrc(a.stream, a.stream_len);
     if constexpr (!ONEPASS) {
         // the whole group in the slab; a group whose span exceeds it (a batch whose record sizes
         // vary a lot) as two halves of 32 records, each staged on its own
@@ -514,7 +514,7 @@ __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
                                                  item_base, lane, (long long)gr.aligned_lo - SLAB_GUARD, a,
                                                  RANGES ? (uint32_t *)(slab + a.slab) : nullptr);
     } else {
-        GlobalSrc s{rsrc, a.stream_len};
+        GlobalSrc s{a.stream, a.stream_len};
         nested_group_body<OSpec, ISpec, ONEPASS>(s, (long long)gr.rec_lo, (long long)gr.rec_hi, valid, r, g,
                                                  item_base, lane, 0, a);
     }
@@ -529,7 +529,7 @@ __device__ __forceinline__ void nested_count_body(const NestedArgs &a) {
     if (base >= a.n) return;
     uint8_t *slab = smem + wave * a.slab;
     __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
+        uniform_rsrc(a.stream, a.stream_len);
     uint32_t cnt = 0;
     // the whole group, or (span larger than the slab) two halves of 32 records
     for (int part = 0; part < 2; part++) {
@@ -550,7 +550,7 @@ __device__ __forceinline__ void nested_count_body(const NestedArgs &a) {
                 cnt = record_count(s, SLAB_GUARD + (long long)(h.rec_lo - h.aligned_lo),
                                    SLAB_GUARD + (long long)(h.rec_hi - h.aligned_lo), a);
             } else {
-                GlobalSrc s{rsrc, a.stream_len};
+                GlobalSrc s{a.stream, a.stream_len};
                 cnt = record_count(s, (long long)h.rec_lo, (long long)h.rec_hi, a);
             }
         }
@@ -617,7 +617,7 @@ __device__ __forceinline__ void nested_count_tail_body(const NestedArgs &a, uint
     const uint64_t base = g * 64;
     if (base >= a.n) return;
     __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
+        uniform_rsrc(a.stream, a.stream_len);
     DecodeArgs d;
     d.ends = a.ends;
     d.n = a.n;
@@ -640,7 +640,7 @@ __device__ __forceinline__ void nested_count_tail_body(const NestedArgs &a, uint
             d[2] = v[k].z;
             d[3] = v[k].w;
         }
-        WinSrc s{(lds_u8 *)win, (long long)w0, GlobalSrc{rsrc, a.stream_len}};
+        WinSrc s{(lds_u8 *)win, (long long)w0, GlobalSrc{a.stream, a.stream_len}};
         cnt = record_count(s, (long long)lo, (long long)hi, a);
     }
     const uint32_t sum = wave_sum(cnt);

@@ -549,9 +549,7 @@ __device__ __forceinline__ Pos emit_message(const EncFields &a, const Sink &k, P
         case K_STRING:
         case K_BYTES: {
             uint2 sp = ((const uint2 *)col)[r];
-            __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(
-                (void *)a.heaps[f], (short)0,
-                (int)(uint32_t)(a.heap_lens[f] > 0xffffffffull ? 0xffffffffull : a.heap_lens[f]), 0x00020000);
+            const __amdgpu_buffer_rsrc_t hr = uniform_rsrc(a.heaps[f], a.heap_lens[f]);
             emit_heap(em, hr, a.heap_lens[f], sp.x, sp.y);
             if (kind == K_STRING) em.put1(0);
             em.rvarint(sp.y);
@@ -615,10 +613,7 @@ struct RuntimeEnc {
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t heap_rsrc(const EncFields &f, int i) {
-    return __builtin_amdgcn_make_buffer_rsrc((void *)f.heaps[i], (short)0,
-                                             (int)(uint32_t)(f.heap_lens[i] > 0xffffffffull ? 0xffffffffull
-                                                                                             : f.heap_lens[i]),
-                                             0x00020000);
+    return uniform_rsrc(f.heaps[i], f.heap_lens[i]);
 }
 
 // Spec: N (1..), kind[N], tag[N] in write order, order[N] (table order, as EncFields.order),

@@ -48,6 +48,12 @@ struct NestedEncodeArgs {
     uint64_t nblocks;
     uint64_t *total;
     uint32_t xcd; // write pass: 1 = XCD-aware block order (grid padded to a multiple of 8)
+    // optional (workspace large enough): the size pass leaves every item's wave prefix
+    // (item_pre[i] = bytes of the wave's items up to and including item i) and each wave's
+    // item-parallel verdict (wave_ok), so the write pass reads them instead of reloading every
+    // item column and heap to recompute the sizes and scans
+    uint32_t *item_pre;
+    uint8_t *wave_ok;
 };
 
 constexpr int NENC_BLOCK = 256;               // records per block (4 waves, one record per lane)
@@ -164,6 +170,35 @@ struct WaveListEmit {
             em.acc = 0;
         }
         const uint32_t p0 = pre[0];
+        if constexpr (E::kHeadSt4) {
+            if (__ballot(count > 8 || big) == 0) { // wave-uniform: short small lists
+                // table {u16 BE end} x count | rvarint(data) (<= 3 bytes: data <= 65535) |
+                // rvarint(2 count) (1 byte) | TypeList as ONE run built in registers
+                // (internal/encode/list.go:36-75), appended with one store per dword
+                uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const bool in = j < (int)count;
+                    const uint32_t end = pre[in ? j + 1 : 0] - p0; // element offset = item end - list start
+                    w[j >> 1] |= (in ? (uint32_t)__builtin_bswap16((uint16_t)end) : 0u) << (16 * (j & 1));
+                }
+                const uint32_t L = vlen32(data);
+                uint64_t x = data & 0x1fffff; // 3 groups of 7 bits -> bytes (inverse of rvarint_bf)
+                x = (x & 0x7f) | ((x & 0x3f80) << 1) | ((x & 0x1fc000) << 2);
+                const uint64_t be = (__builtin_bswap32((uint32_t)x) >> 8) >> (8 * (3 - L)); // top group first
+                const uint64_t cont = (0x808080ull >> (8 * (3 - L))) & ~0xffull;
+                const uint64_t T = (be | cont) | ((uint64_t)(2 * count) << (8 * L)) | ((uint64_t)T_LIST << (8 * (L + 1)));
+                const uint32_t q = count >> 1;
+                const uint64_t Ts = T << (16 * (count & 1)); // the trailer starts at byte 2 count
+#pragma unroll
+                for (int d = 0; d < 7; d++) {
+                    w[d] |= d == (int)q ? (uint32_t)Ts : 0u;
+                    w[d] |= d == (int)q + 1 ? (uint32_t)(Ts >> 32) : 0u;
+                }
+                em.template put_heap_short<7>(w, 0u, 2 * count + L + 2);
+                return;
+            }
+        }
         for (uint32_t j = 0; j < count; j++) {
             const uint32_t end = pre[j + 1] - p0; // element offset = item end - list start
             em.put_n(big ? bswap32(end) : (uint32_t)__builtin_bswap16((uint16_t)end), big ? 4 : 2);
@@ -218,9 +253,10 @@ struct LaneRecord {
     bool fast; // wave-uniform: item-parallel path
 };
 
+// cached = the size pass's prefix is read from a.item_pre (write pass with the cache)
 template <class IP>
 __device__ __forceinline__ LaneRecord lane_record(const NestedEncodeArgs &a, uint32_t *pre, int lane, bool check,
-                                                  bool &err, uint64_t blk) {
+                                                  bool &err, uint64_t blk, bool cached = false) {
     LaneRecord L;
     L.r = blk * NENC_BLOCK + threadIdx.x;
     L.valid = L.r < a.n;
@@ -230,6 +266,15 @@ __device__ __forceinline__ LaneRecord lane_record(const NestedEncodeArgs &a, uin
     L.I0 = __builtin_amdgcn_readfirstlane(L.b);
     const uint32_t I1 = __builtin_amdgcn_readfirstlane(__shfl(L.e, 63));
     L.cnt = I1 - L.I0;
+    if (cached) {
+        const uint64_t w = (blk * NENC_BLOCK + threadIdx.x) >> 6;
+        L.fast = (w << 6) < a.n && a.wave_ok[w] != 0; // (waves past n return before using it)
+        if (L.fast) {
+            if (lane == 0) pre[0] = 0;
+            for (uint32_t k = lane; k < L.cnt; k += 64) pre[k + 1] = a.item_pre[L.I0 + k];
+        }
+        return L;
+    }
     L.fast = __ballot(bad) == 0 && L.cnt <= (uint32_t)NENC_ITEM_CAP;
     if (L.fast) L.fast = wave_item_prefix<IP>(a, L.I0, L.cnt, pre, lane, check, err);
     return L;
@@ -263,6 +308,13 @@ __device__ __forceinline__ void nested_enc_size_body(const NestedEncodeArgs &a, 
     __syncthreads();
     bool err = false;
     const LaneRecord L = lane_record<IP>(a, pre, lane, a.check_heaps, err, blockIdx.x);
+    if (a.item_pre && L.r - lane < a.n) { // this wave's prefix and verdict, for the write pass
+        if (lane == 0) a.wave_ok[L.r >> 6] = L.fast ? 1 : 0;
+        if (L.fast) {
+            wave_sync();
+            for (uint32_t k = lane; k < L.cnt; k += 64) a.item_pre[L.I0 + k] = pre[k + 1];
+        }
+    }
     const typename OP::Rec orec = OP::load(a.outer, L.valid ? L.r : a.n - 1);
     ListSize ls;
     const RecSize rs = lane_record_size<OP>(a, L, orec, pre, a.check_heaps, err, ls);
@@ -300,7 +352,8 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
     // the outer record's loads first: in flight while the item prefix is built
     const uint64_t r0 = blk * NENC_BLOCK + threadIdx.x;
     const typename OP::Rec orec = OP::load(a.outer, r0 < a.n ? r0 : a.n - 1);
-    const LaneRecord L = lane_record<IP>(a, pre, lane, false, err, blk);
+    const LaneRecord L = lane_record<IP>(a, pre, lane, false, err, blk, a.item_pre != nullptr);
+    wave_sync(); // the prefix (from the cache) is in LDS
     ListSize ls;
     RecSize rs = lane_record_size<OP>(a, L, orec, pre, false, err, ls);
     if (!L.valid) rs.total = 0;

@@ -21,6 +21,7 @@
 
 #include <dlfcn.h>
 #include <sys/stat.h>
+#include <utime.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -333,8 +334,12 @@ std::vector<char> compile_source(const std::string &src, Prog p) {
     char name[64];
     snprintf(name, sizeof name, "%016llx.co", (unsigned long long)h);
     std::vector<char> cached;
+    const bool dump = getenv("SPEC_AMD_JIT_DUMP") != nullptr; // diagnostic: always compile (and dump)
     for (const std::string &d : cache_dirs())
-        if (read_file(d + "/" + name, cached)) return cached;
+        if (!dump && read_file(d + "/" + name, cached)) {
+            utime((d + "/" + name).c_str(), nullptr); // in use: build() prunes entries it did not touch
+            return cached;
+        }
     std::vector<char> code = compile_uncached(src, p, kOpts, (int)(sizeof kOpts / sizeof kOpts[0]));
     if (!code.empty()) write_cache(name, code);
     return code;
@@ -511,9 +516,55 @@ void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, con
       << "      uint64_t *errp = " << (T.err_col >= 0 ? "(uint64_t *)" + col_expr(T.err_col) : std::string("nullptr"))
       << ";\n"
       << "      uint64_t errs = 0;\n";
+    // the scalar fields first, as straight-line code (the kernel runs only with every column
+    // present): every table read and value window of the table issued before any decode, so
+    // the LDS round trips overlap; windows are read for the type a Writer emits, and a field of
+    // another accepted type (ints of another width, float32 <-> float64) is decoded again
+    // with the general window below
+    bool any_nt = false;
+    for (uint32_t k = 0; k < T.nd; k++) {
+        const TField &F = D.f[D.direct[T.d0 + k]];
+        if (F.kind < spec::K_BOOL || F.kind > spec::K_BYTES) continue;
+        o << "      const long long end" << k << " = tree_end<" << F.rank << ">(s, o);\n"
+          << "      const long long e" << k << " = end" << k << " > 0 ? ds + end" << k << " : ds;\n"
+          << "      const Win w" << k << " = load_win<" << (int)F.kind << ", true>(s, e" << k << ");\n";
+    }
+    o << "      bool slow = false;\n";
+    for (uint32_t k = 0; k < T.nd; k++) {
+        const TField &F = D.f[D.direct[T.d0 + k]];
+        if (F.kind < spec::K_BOOL || F.kind > spec::K_BYTES) continue;
+        const uint32_t nt = spec::cross_kind_type(F.kind);
+        o << "      bool ok" << k << " = true;\n"
+          << "      Val v" << k << " = decode_tail_k<" << (int)F.kind << ", true>(w" << k << ", ds, e" << k << ", 0, &ok" << k
+          << ");\n";
+        if (nt) {
+            any_nt = true;
+            o << "      const bool nat" << k << " = end" << k << " <= 0 || ((uint32_t)w" << k << ".t.q0 & 0xff) == " << nt
+              << "u;\n"
+              << "      slow |= !nat" << k << ";\n";
+        }
+    }
+    if (any_nt) {
+        o << "      if (slow) {\n";
+        for (uint32_t k = 0; k < T.nd; k++) {
+            const TField &F = D.f[D.direct[T.d0 + k]];
+            if (F.kind < spec::K_BOOL || F.kind > spec::K_BYTES || !spec::cross_kind_type(F.kind)) continue;
+            o << "        if (!nat" << k << ") v" << k << " = decode_tail_k<" << (int)F.kind << ">(load_win<" << (int)F.kind
+              << ">(s, e" << k << "), ds, e" << k << ", 0, &ok" << k << ");\n";
+        }
+        o << "      }\n";
+    }
+    for (uint32_t k = 0; k < T.nd; k++) {
+        const TField &F = D.f[D.direct[T.d0 + k]];
+        if (F.kind < spec::K_BOOL || F.kind > spec::K_BYTES) continue;
+        const std::string bit = k < 64 ? "(1ull << " + std::to_string(k) + ")" : "0ull";
+        o << "      store_value_k<" << (int)F.kind << ">(" << col_expr(F.col) << ", row, v" << k << ");\n"
+          << "      errs |= (ok" << k << " || end" << k << " <= 0) ? 0ull : " << bit << ";\n";
+    }
     for (uint32_t k = 0; k < T.nd; k++) {
         const uint32_t fi = D.direct[T.d0 + k];
         const TField &F = D.f[fi];
+        if (F.kind >= spec::K_BOOL && F.kind <= spec::K_BYTES) continue;
         const std::string bit = k < 64 ? "(1ull << " + std::to_string(k) + ")" : "0ull";
         o << "      { // field " << fi << " tag " << F.tag << " kind " << (int)F.kind << "\n"
           << "        const long long end = tree_end<" << F.rank << ">(s, o);\n";
@@ -563,10 +614,8 @@ void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, con
               << "        if (" << col_expr(F.col) << ") ((uint2 *)" << col_expr(F.col) << ")[row] = sp;\n"
               << "        store_u8(" << col_expr(F.present) << ", row, sp.y ? s.u8((long long)sp.x + sp.y - 1) : 0u);\n";
             break;
-        default: // scalar kinds
-            o << "        void *col = " << col_expr(F.col) << ";\n"
-              << "        if ((col || errp) && !tree_field_k<" << (int)F.kind << ">(s, ds, end, col, row)) errs |= " << bit
-              << ";\n";
+        default:
+            break;
         }
         o << "      }\n";
     }
@@ -610,18 +659,18 @@ std::string generate_tree(const TreeDesc &D, bool *has) {
         }
         o << "}\n"
           << "extern \"C\" __global__ __launch_bounds__(256) void spec_tree_group_" << x
-          << "(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x, uint32_t slab, uint32_t wave_bytes) {\n"
+          << "(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x, uint32_t slab, uint32_t wave_bytes, uint32_t rpw) {\n"
           << "  const TreeDesc &D = *Dp;\n"
           << "  const TreeBufs &B = *Bp;\n"
           << "  const uint64_t rows = dec_rows(D, B, x);\n"
           << "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
           << "  uint2 *gr = (uint2 *)(smem + (threadIdx.x >> 6) * wave_bytes + slab) + (threadIdx.x & 63);\n"
-          << "  tree_rows(B, x, rows, slab, wave_bytes,\n"
+          << "  tree_rows(B, x, rows, slab, wave_bytes, rpw,\n"
           << "            [&](const TreeLds &s, uint64_t row, long long lo, long long hi, bool panic) {\n"
           << "              gen_row_" << x << "(s, D, B, row, lo, hi, panic, gr);\n"
           << "            },\n"
           << "            [&](const GlobalSrc &s, uint64_t row, long long lo, long long hi, bool panic) {\n"
-          << "              tree_group_row(s, D, B, x, row, lo, hi, panic, gr);\n"
+          << "              gen_row_" << x << "(s, D, B, row, lo, hi, panic, gr);\n"
           << "            });\n"
           << "}\n";
     }

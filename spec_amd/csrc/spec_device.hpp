@@ -99,12 +99,25 @@ __device__ __forceinline__ uint32_t buf_ld32(__amdgpu_buffer_rsrc_t r, uint32_t 
     return w;
 }
 
+// A range-checked buffer descriptor over [p, p + len) (len clamped to 4 GiB - 1), built from
+// readfirstlane'd scalars: the callers' p / len are wave-uniform, but a value that went through
+// memory or a call is not KNOWN to be, and every buffer load through a descriptor in VGPRs
+// becomes a waterfall loop (readfirstlane x 4, compare, loop).  Free when they sit in SGPRs.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void *p, uint64_t len) {
+    const uint64_t b = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    const uint32_t n = __builtin_amdgcn_readfirstlane(len > 0xffffffffull ? 0xffffffffu : (uint32_t)len);
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0, (int)n, 0x00020000);
+}
+
 struct GlobalSrc {
     using pos_t = long long;
-    __amdgpu_buffer_rsrc_t rsrc; // range-checked: reads outside [0, len) return 0
+    const uint8_t *base; // range-checked: reads outside [0, len) return 0
     uint64_t len;
+    __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const { return uniform_rsrc(base, len); }
     __device__ __forceinline__ uint32_t u8(long long p) const {
-        return __builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)p, 0, 0);
+        return __builtin_amdgcn_raw_buffer_load_b8(rsrc(), (uint32_t)p, 0, 0);
     }
     __device__ __forceinline__ uint64_t d64(long long p) const {
         // p may be negative near the stream start: wrap to a huge offset => range check => 0
@@ -113,11 +126,11 @@ struct GlobalSrc {
             for (int i = 0; i < 8; i++) v |= (uint64_t)u8(p + i) << (8 * i);
             return v;
         }
-        auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (uint32_t)p, 0, 0);
+        auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc(), (uint32_t)p, 0, 0);
         return (uint64_t)v[0] | ((uint64_t)v[1] << 32);
     }
     __device__ __forceinline__ uint32_t d32(long long p) const {
-        if (p >= 0) return buf_ld32(rsrc, (uint32_t)p, len);
+        if (p >= 0) return buf_ld32(rsrc(), (uint32_t)p, len);
         return 0;
     }
 };

@@ -102,7 +102,7 @@ __device__ __forceinline__ uint64_t grid_first() { return (uint64_t)blockIdx.x *
 // ---- decode helpers ----------------------------------------------------------------------
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t stream_rsrc(const TreeBufs &B) {
-    return __builtin_amdgcn_make_buffer_rsrc((void *)B.stream, (short)0, (int)(uint32_t)B.stream_len, 0x00020000);
+    return uniform_rsrc(B.stream, B.stream_len);
 }
 
 // The byte range of row `row` of table x (record, sub-message field slice, list element).
@@ -606,9 +606,7 @@ struct BEmit {
     // heap bytes [off, off + len): 16 at a time from four dword loads issued together
     // (range-checked: bytes past the heap read as 0 and are never used)
     __device__ __forceinline__ void heap(const uint8_t *h, uint64_t hlen, uint32_t off, uint32_t len) {
-        const __amdgpu_buffer_rsrc_t r =
-            __builtin_amdgcn_make_buffer_rsrc((void *)h, (short)0, (int)(uint32_t)(hlen < 0xffffffffull ? hlen : 0xffffffffull),
-                                              0x00020000);
+        const __amdgpu_buffer_rsrc_t r = uniform_rsrc(h, hlen);
         uint32_t i = 0;
         while (i < len) {
             const uint32_t a = (off + i) & ~3u;

@@ -33,7 +33,7 @@ namespace {
 // row, run-time schema.  LDS per wave: the staging slab, then a range slot per sub-message table
 // of the group.
 __global__ __launch_bounds__(TB) void tree_group_kernel(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x,
-                                                         uint32_t slab, uint32_t wave_bytes) {
+                                                         uint32_t slab, uint32_t wave_bytes, uint32_t rpw) {
     const TreeDesc &D = *Dp;
     const TreeBufs &B = *Bp;
     const uint64_t rows = dec_rows(D, B, x);
@@ -42,7 +42,7 @@ __global__ __launch_bounds__(TB) void tree_group_kernel(const TreeDesc *Dp, cons
     auto body = [&](const auto &s, uint64_t row, long long lo, long long hi, bool panic) {
         tree_group_row(s, D, B, x, row, lo, hi, panic, gr);
     };
-    tree_rows(B, x, rows, slab, wave_bytes, body, body);
+    tree_rows(B, x, rows, slab, wave_bytes, rpw, body, body);
 }
 
 // ---- the group's list counts -> CSR begin, row counts, element ranges ----------------------
@@ -139,30 +139,30 @@ __global__ __launch_bounds__(SCAN_T) void list_apply_kernel(const TreeDesc *Dp, 
     const uint64_t cap = B.caps[y];
     uint2 *rng = B.rng[y];
     const uint4 *lh = B.lh[y];
-    const GlobalSrc gs{stream_rsrc(B), B.stream_len};
+    const GlobalSrc gs{B.stream, B.stream_len};
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_PER;
-    uint32_t v[SCAN_PER];
-    uint64_t sum = 0;
-    for (int k = 0; k < SCAN_PER; k++) {
-        v[k] = base + k < rows ? cnt[base + k] : 0;
-        sum += v[k];
-    }
+    static_assert(SCAN_PER == 1, "one owner row per thread");
+    // the row's count, table position and first 16 table bytes are loaded before the block
+    // scan (they do not depend on it): only the element ranges' positions wait for it
+    const uint64_t r = base;
+    const uint32_t v0 = r < rows ? cnt[r] : 0;
+    const uint4 h = v0 ? lh[r] : make_uint4(0, 0, 0, 0);
+    const uint64_t t0 = v0 ? load_le64(gs, (long long)h.x) : 0, t1 = v0 ? load_le64(gs, (long long)h.x + 8) : 0;
     uint64_t tot;
-    uint64_t p = m.ws[blockIdx.y][blockIdx.x] + block_scan(sum, sh, tot);
+    uint64_t p = m.ws[blockIdx.y][blockIdx.x] + block_scan(v0, sh, tot);
+    const uint32_t v[1] = {v0};
     for (int k = 0; k < SCAN_PER; k++) {
-        const uint64_t r = base + k;
         if (r >= rows) break;
         if (beg) beg[r] = (uint32_t)p;
         if (v[k]) {
             // List.GetBytes(i) (internal/types/list.go:100-116, format/list.go:152-176): the
             // table's entries 16 bytes at a time (8 small / 4 big), both loads in flight at once
-            const uint4 h = lh[r];
             const bool big = (h.w & 0x80000000u) != 0;
             const uint32_t esz = big ? 4u : 2u, per = 16u / esz;
             uint32_t a = 0;
             for (uint32_t j0 = 0; j0 < v[k] && p + j0 < cap; j0 += per) {
                 const long long q = (long long)h.x + (long long)j0 * esz;
-                const uint64_t w0 = load_le64(gs, q), w1 = load_le64(gs, q + 8);
+                const uint64_t w0 = j0 ? load_le64(gs, q) : t0, w1 = j0 ? load_le64(gs, q + 8) : t1;
 #pragma unroll
                 for (uint32_t u = 0; u < 8; u++) {
                     const uint32_t j = j0 + u;
@@ -191,8 +191,7 @@ __global__ __launch_bounds__(SCAN_T) void list_apply_kernel(const TreeDesc *Dp, 
 // (Go would panic slicing it) decodes as empty and reports 2.
 __global__ __launch_bounds__(256) void values_kernel(const uint8_t *stream, uint64_t stream_len, const uint2 *spans,
                                                      uint64_t n, uint32_t kind, void *out, uint8_t *err) {
-    const GlobalSrc gs{__builtin_amdgcn_make_buffer_rsrc((void *)stream, (short)0, (int)(uint32_t)stream_len, 0x00020000),
-                       stream_len};
+    const GlobalSrc gs{stream, stream_len};
     for (uint64_t row = grid_first(); row < n; row += grid_stride()) {
         const uint2 sp = spans[row];
         const bool past = (uint64_t)sp.x + sp.y > stream_len;
@@ -249,23 +248,33 @@ namespace {
 
 // LDS per wave of group x: the staging slab and one range slot per sub-message table
 struct GroupShape {
-    uint32_t slab, wave_bytes;
+    uint32_t slab, wave_bytes, rpw; // rpw: rows per wave (tree_rows)
 };
 
 // A block's 4 waves share a CU's 160 KiB: a wave gets at most 40 KiB.
 constexpr uint32_t WAVE_LDS_MAX = 40960;
 
-GroupShape group_shape(const Layout &L, uint32_t x, uint64_t stream_len, uint64_t n) {
+GroupShape group_shape(const Layout &L, uint32_t x, uint64_t stream_len, uint64_t rows) {
     const TTable &T = L.desc.t[x];
     const uint32_t extra = 512u * (T.gn > 1 ? T.gn - 1 : 0) + 16; // sub-message range slots
     GroupShape g;
-    g.slab = 64 * LANE_W; // 16 KiB: small rows (list elements, sub-messages) stage, lane windows
-    if (x == 0 && n) {
-        // the records: a wave's 64 consecutive records (mean + 15 %)
-        const double span = 64.0 * (double)stream_len / (double)n * 1.15 + 128;
-        if (span > g.slab) g.slab = span + extra <= WAVE_LDS_MAX ? ((uint32_t)span + 1023) & ~1023u : g.slab;
+    g.slab = 0;
+    g.rpw = 64;
+    if (rows) {
+        // a wave's 64 consecutive rows span about 64 / rows of the stream (the records: 64 mean
+        // records; a list table's elements are spread over every record holding the list):
+        // staged when that fits a wave's share of the CU's LDS, else the rows parse straight
+        // from HBM (small rows far apart: a slab would hold mostly other rows' bytes, and
+        // without one the CU holds 8 waves per SIMD to cover the reads' latency)
+        const double span = 64.0 * (double)stream_len / (double)rows * 1.15 + 128 + GUARD;
+        const uint32_t lim = x == 0 ? WAVE_LDS_MAX : 16384u;
+        const double slab = (double)(((uint64_t)span + 1023) & ~1023ull);
+        // (32 rows per wave in half the slab, two waves per SIMD: measured slower for pkg1's
+        // 473-byte records, 183 vs 177 us: the waves are VALU-bound at half their lanes)
+        if (slab + extra <= lim) {
+            g.slab = (uint32_t)slab;
+        }
     }
-    if (g.slab + extra > WAVE_LDS_MAX) g.slab = extra < WAVE_LDS_MAX ? (WAVE_LDS_MAX - extra) & ~1023u : 0;
     g.wave_bytes = (g.slab + extra + 15) & ~15u;
     return g;
 }
@@ -337,7 +346,11 @@ int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, 
     B.n = n;
     B.rowsd = (uint64_t *)d->misc.p;
     B.ovf = (uint32_t *)((uint8_t *)d->misc.p + TREE_MAX_T * sizeof(uint64_t));
-    for (uint32_t c = 0; c < L.nc; c++) B.cols[c] = columns ? columns[c] : nullptr;
+    bool all_cols = columns != nullptr; // the schema-specialised kernels store every column unconditionally
+    for (uint32_t c = 0; c < L.nc; c++) {
+        B.cols[c] = columns ? columns[c] : nullptr;
+        all_cols = all_cols && B.cols[c];
+    }
     if ((rc = upload(d, st))) return rc;
     if (hipMemsetAsync(B.ovf, 0, sizeof(uint32_t), st) != hipSuccess) return SPEC_E_HIP;
     if (n == 0) {
@@ -356,18 +369,22 @@ int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, 
         const uint64_t cap = x == 0 ? n : d->caps[x];
         if (cap == 0 && x) continue;
         if (n) {
-            const GroupShape gs = group_shape(L, x, stream_len, n);
-            const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((cap + TB - 1) / TB, 1u << 20));
+            const GroupShape gs = group_shape(L, x, stream_len, cap);
+            const uint64_t per_block = (uint64_t)(TB / 64) * gs.rpw;
+            const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((cap + per_block - 1) / per_block, 1u << 20));
             const size_t lds = (size_t)(TB / 64) * gs.wave_bytes;
-            if (d->jit && d->jit[x]) {
-                uint32_t xx = x, slab = gs.slab, wb = gs.wave_bytes;
-                void *args[] = {(void *)&Dd, (void *)&Bd, &xx, &slab, &wb};
-                if (hipModuleLaunchKernel(d->jit[x], (unsigned)blocks, 1, 1, TB, 1, 1, (unsigned)lds, st, args, nullptr) !=
-                    hipSuccess)
+            if (d->jit && d->jit[x] && all_cols) {
+                uint32_t xx = x, slab = gs.slab, wb = gs.wave_bytes, rpw = gs.rpw;
+                void *args[] = {(void *)&Dd, (void *)&Bd, &xx, &slab, &wb, &rpw};
+                const hipError_t le =
+                    hipModuleLaunchKernel(d->jit[x], (unsigned)blocks, 1, 1, TB, 1, 1, (unsigned)lds, st, args, nullptr);
+                if (le != hipSuccess) {
+                    note_hip_error(le);
                     return SPEC_E_HIP;
+                }
             } else {
                 hipLaunchKernelGGL(tree_group_kernel, dim3((unsigned)blocks), dim3(TB), lds, st, Dd, Bd, x, gs.slab,
-                                   gs.wave_bytes);
+                                   gs.wave_bytes, gs.rpw);
             }
         }
         // every list owned in the group: one batched scan

@@ -24,10 +24,13 @@ struct TreeLds {
     lds_u8 *lds;
     long long off;
     int size;
+    // 32-bit window offset (the stream is < 4 GiB): a position below the window wraps to a huge
+    // value and, like one past it, is clamped to the window's last n bytes (only reads the
+    // decoders mask out go outside [lo - 64, hi + 16))
     __device__ __forceinline__ int at(long long p, int n) const {
-        long long i = p - off;
-        i = i < 0 ? 0 : i;
-        return (int)(i > size - n ? size - n : i);
+        const uint32_t i = (uint32_t)p - (uint32_t)off;
+        const uint32_t lim = (uint32_t)(size - n);
+        return (int)(i < lim ? i : lim);
     }
     __device__ __forceinline__ uint32_t u8(long long p) const { return lds[at(p, 1)]; }
     __device__ __forceinline__ uint64_t d64(long long p) const {
@@ -57,18 +60,20 @@ __device__ __forceinline__ uint64_t dec_rows(const TreeDesc &D, const TreeBufs &
 // lds_body(src, row, lo, hi, panic) with src = the staged bytes (TreeLds), or glob_body(...) with
 // src = HBM (GlobalSrc) when the rows fit neither staging.  Each body has one call site, so a
 // specialised row body is inlined once.
+// rpw = rows per wave, 64 or 32: with 32 the wave's lanes 32..63 idle and its slab holds half
+// the span, so twice the waves share a CU's LDS (rows too large for 64 per slab at good occupancy).
 template <class LdsBody, class GlobBody>
 __device__ __forceinline__ void tree_rows(const TreeBufs &B, uint32_t x, uint64_t rows, uint32_t slab_bytes,
-                                          uint32_t wave_bytes, LdsBody lds_body, GlobBody glob_body) {
+                                          uint32_t wave_bytes, uint32_t rpw, LdsBody lds_body, GlobBody glob_body) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint8_t *slab = smem + wave * wave_bytes;
     const __amdgpu_buffer_rsrc_t rsrc = stream_rsrc(B);
-    const GlobalSrc gs{rsrc, B.stream_len};
-    const uint64_t wstride = (uint64_t)gridDim.x * (TB / 64) * 64;
-    for (uint64_t base = ((uint64_t)blockIdx.x * (TB / 64) + wave) * 64; base < rows; base += wstride) {
+    const GlobalSrc gs{B.stream, B.stream_len};
+    const uint64_t wstride = (uint64_t)gridDim.x * (TB / 64) * rpw;
+    for (uint64_t base = ((uint64_t)blockIdx.x * (TB / 64) + wave) * rpw; base < rows; base += wstride) {
         const uint64_t row = base + lane;
-        const bool valid = row < rows;
+        const bool valid = row < rows && (uint32_t)lane < rpw;
         long long lo = 0, hi = 0;
         bool panic = false;
         if (valid) row_range(B, x, row, lo, hi, panic);
@@ -329,14 +334,22 @@ __device__ __forceinline__ long long tree_end(const Src &s, const TOpen &o) {
 }
 
 // m.<Kind>(tag) of a field of constant kind K into its column (nullable); returns !err
+// The value's window is read for the type a Writer emits for K (decode_core.hpp load_win<K, true>:
+// 8 bytes for the narrow kinds, the payload qwords for the fixed-width ones); a value of another
+// accepted type (an int of another width, float32 <-> float64) takes the general decode.  For
+// kinds that accept one type only the narrow window holds everything a valid value needs, and a
+// value of another type fails on its type byte either way.
 template <uint32_t K, class Src>
 __device__ __forceinline__ bool tree_field_k(const Src &s, long long ds, long long end, void *col, uint64_t row) {
+    using pos_t = typename Src::pos_t;
     Val v = {0, 0, 0, 0};
     bool ok = true;
     if (end > 0) {
-        const long long e = ds + end;
-        v = decode_tail_k<K>(load_win<K>(s, (typename Src::pos_t)e), (typename Src::pos_t)ds, (typename Src::pos_t)e, 0,
-                             &ok);
+        const pos_t e = (pos_t)(ds + end), lo = (pos_t)ds;
+        constexpr uint32_t NT = cross_kind_type(K);
+        const Win w = load_win<K, true>(s, e);
+        if (NT == 0 || ((uint32_t)w.t.q0 & 0xff) == NT) v = decode_tail_k<K, true>(w, lo, e, 0, &ok);
+        else v = decode_tail_k<K>(load_win<K>(s, e), lo, e, 0, &ok);
     }
     if (col) store_value_k<K>(col, row, v);
     return ok;

@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void parse_kernel(DecodeArgs a, uint32_t *size
     const bool valid = r < a.n;
     uint8_t *slab = smem + wave * a.slab;
     __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)a.stream, (short)0, (int)(uint32_t)a.stream_len, 0x00020000);
+        uniform_rsrc(a.stream, a.stream_len);
     uint64_t lo, hi;
     load_group_ends(a, base, lane, lo, hi);
     const Group gr = make_group(a, base, lane, lo, hi, a.slab);
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void parse_kernel(DecodeArgs a, uint32_t *size
                           SLAB_GUARD + (long long)(gr.rec_hi - gr.aligned_lo), size);
     } else {
         if (!valid) return;
-        GlobalSrc s{rsrc, a.stream_len};
+        GlobalSrc s{a.stream, a.stream_len};
         st = parse_record(s, (long long)gr.rec_lo, (long long)gr.rec_hi, size);
     }
     a.f.status[r] = (uint8_t)st;

@@ -143,6 +143,10 @@ class NestedEncoder:
                cuda_stream=None):
         """outer_cols: one tensor per outer field (None for the list field); item_begin: int32/uint32
         [n+1]; writes out/ends when given, always self.total."""
+        ws = _lib.lib().spec_encode_nested_workspace_size_items(self.n, nitems)
+        if ws > self.ws_bytes:  # room for the size pass's item prefixes (the write pass reuses them)
+            self.workspace = torch.empty((ws + 7) // 8, dtype=torch.int64, device=self.workspace.device)
+            self.ws_bytes = ws
         ohp, ohl = self._heaps(self.schema.outer.fields, outer_heaps)
         ihp, ihl = self._heaps(self.schema.item.fields, item_heaps)
         rc = _lib.lib().spec_encode_nested(

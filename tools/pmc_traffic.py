@@ -11,6 +11,10 @@ out, records = sys.argv[1], int(sys.argv[2])
 dst = sys.argv[3] if len(sys.argv) > 3 else os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                           "profiles", "pmc_traffic.json")
 summ = json.load(open(os.path.join(out, "summary.json")))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import source_rev  # noqa: E402
+
+rev = source_rev()
 res = json.load(open(dst)) if os.path.exists(dst) else {}
 for k, d in summ.items():
     if "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
@@ -19,6 +23,6 @@ for k, d in summ.items():
     rd = 2 * d["FETCH_SIZE"] * 1024
     wr = d["WRITE_SIZE"] * 1024
     res[name] = {"records": records, "fetch_size_kib": d["FETCH_SIZE"], "write_size_kib": d["WRITE_SIZE"],
-                 "read_bytes": rd, "write_bytes": wr, "hbm_bytes_per_launch": rd + wr}
+                 "read_bytes": rd, "write_bytes": wr, "hbm_bytes_per_launch": rd + wr, "source_rev": rev}
 json.dump(res, open(dst, "w"), indent=1)
 print(json.dumps(res, indent=1))
