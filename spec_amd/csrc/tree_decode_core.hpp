@@ -307,10 +307,25 @@ __device__ __forceinline__ TOpen tree_open(const Src &s, long long lo, long long
     bool ok = !tr.big && nent <= (uint32_t)N;
     uint32_t prev = 0;
     uint64_t P = 0;
+    if constexpr (N == 0) {
+        o.fast = ok;
+        return o;
+    } else {
+    // the table's first 3N bytes, re-aligned into qwords (as decode_core.hpp fast_prepare): tag i
+    // is byte 3i, a compile-time position
+    constexpr int NC = (3 * N + 7) / 8, NQ = NC + 1;
+    const long long base = tr.tstart & ~7ll;
+    const uint32_t sh = 8u * (uint32_t)(tr.tstart & 7);
+    uint64_t q[NQ];
+#pragma unroll
+    for (int j = 0; j < NQ; j++) q[j] = s.d64(base + 8 * j);
+    uint64_t c[NC];
+#pragma unroll
+    for (int j = 0; j < NC; j++) c[j] = (q[j] >> sh) | ((q[j + 1] << 1) << (63 - sh));
 #pragma unroll
     for (int i = 0; i < N; i++) {
         const bool use = (uint32_t)i < nent;
-        const uint32_t t = s.u8(tr.tstart + 3 * i);
+        const uint32_t t = (uint32_t)(c[(3 * i) >> 3] >> (8 * ((3 * i) & 7))) & 0xff;
         bool in;
         const uint32_t r = tag_rank<M0, M1, M2, M3>(t, in);
         ok = ok & (!use | (in & (i == 0 || t > prev)));
@@ -320,6 +335,7 @@ __device__ __forceinline__ TOpen tree_open(const Src &s, long long lo, long long
     o.fast = ok;
     o.P = P;
     return o;
+    }
 }
 
 // m.field(tag) of the field of rank R: its end offset (data-relative), or -1 (absent or

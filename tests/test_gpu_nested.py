@@ -229,6 +229,38 @@ def test_nested_encode_bitexact(dev, kernel, n):
     assert np.array_equal(out.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("n", [1, 100, 5000])
+def test_nested_encode_workspace_sizes(dev, kernel, n):
+    """The same bytes with the minimal workspace (spec_encode_nested_workspace_size: the write pass
+    recomputes the item prefixes) and the larger one (..._size_items: it reads the size pass's)."""
+    import ctypes as C
+
+    import torch
+
+    from spec_amd import _lib
+
+    w = workload.nested(n, seed=n + 11, count=(0, 12))
+    want, want_ends = O.encode_nested_batch(w)
+    oc, oh, ib, ic, ih = nested_device_inputs(w, dev)
+    m = int(ic[0].shape[0])
+    L = _lib.lib()
+    for ws in (L.spec_encode_nested_workspace_size(n), L.spec_encode_nested_workspace_size_items(n, m)):
+        enc = spec_amd.NestedEncoder(NESTED, n, dev)
+        enc.workspace = torch.empty((ws + 7) // 8, dtype=torch.int64, device=dev)
+        enc.ws_bytes = ws
+        out = torch.empty(len(want), dtype=torch.uint8, device=dev)
+        ends = torch.empty(n, dtype=torch.int64, device=dev)
+        rc = L.spec_encode_nested(
+            C.byref(NESTED.c), enc._ptrs(oc), *enc._heaps(NESTED.outer.fields, oh), C.c_void_p(ib.data_ptr()),
+            enc._ptrs(ic), *enc._heaps(NESTED.item.fields, ih), m, n, C.c_void_p(out.data_ptr()), out.numel(),
+            C.c_void_p(ends.data_ptr()), C.c_void_p(enc.workspace.data_ptr()), ws, C.c_void_p(enc.total.data_ptr()),
+            None)
+        assert rc == 0
+        torch.cuda.synchronize()
+        assert np.array_equal(ends.cpu().numpy().view(np.uint64), want_ends), ws
+        assert np.array_equal(out.cpu().numpy(), want), ws
+
+
 def test_nested_encode_big_lists_and_empty(dev, kernel):
     """Lists of 0 and > 255 items (IsBigList by count), long labels (big items / big lists by
     offset), in one batch."""
