@@ -672,6 +672,17 @@ std::string generate_tree(const TreeDesc &D, bool *has) {
           << "            [&](const GlobalSrc &s, uint64_t row, long long lo, long long hi, bool panic) {\n"
           << "              gen_row_" << x << "(s, D, B, row, lo, hi, panic, gr);\n"
           << "            });\n"
+          << "}\n"
+          << "extern \"C\" __global__ __launch_bounds__(256) void spec_tree_group_" << x
+          << "g(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x, uint32_t slab, uint32_t wave_bytes, uint32_t rpw) {\n"
+          << "  const TreeDesc &D = *Dp;\n"
+          << "  const TreeBufs &B = *Bp;\n"
+          << "  const uint64_t rows = dec_rows(D, B, x);\n"
+          << "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+          << "  uint2 *gr = (uint2 *)(smem + (threadIdx.x >> 6) * wave_bytes + slab) + (threadIdx.x & 63);\n"
+          << "  tree_rows_global(B, x, rows, [&](const GlobalSrc &s, uint64_t row, long long lo, long long hi, bool panic) {\n"
+          << "    gen_row_" << x << "(s, D, B, row, lo, hi, panic, gr);\n"
+          << "  });\n"
           << "}\n";
     }
     return o.str();
@@ -679,7 +690,7 @@ std::string generate_tree(const TreeDesc &D, bool *has) {
 
 struct TreeEntry {
     hipModule_t mod = nullptr;
-    hipFunction_t fn[spec::TREE_MAX_T] = {};
+    hipFunction_t fn[2 * spec::TREE_MAX_T] = {}; // [x]: staged rows, [TREE_MAX_T + x]: rows from HBM
     bool failed = false;
 };
 std::unordered_map<std::string, TreeEntry> g_tree_cache;
@@ -697,7 +708,8 @@ long long jit_compile_only_tree(const TreeDesc &D) {
 }
 
 // The schema-specialised group kernels of a tree: fn[x] for each group root x that has one
-// (nullptr where the run-time kernel runs); nullptr when the JIT is off or failed.
+// (nullptr where the run-time kernel runs), fn[TREE_MAX_T + x] its variant without staging;
+// nullptr when the JIT is off or failed.
 const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
     if (!enabled()) return nullptr;
     int dev = 0;
@@ -714,7 +726,8 @@ const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
         for (uint32_t x = 0; ok && x < D.ntables; x++) {
             if (!has[x]) continue;
             const std::string name = "spec_tree_group_" + std::to_string(x);
-            ok = hipModuleGetFunction(&e.fn[x], e.mod, name.c_str()) == hipSuccess;
+            ok = hipModuleGetFunction(&e.fn[x], e.mod, name.c_str()) == hipSuccess &&
+                 hipModuleGetFunction(&e.fn[TREE_MAX_T + x], e.mod, (name + "g").c_str()) == hipSuccess;
         }
         if (!ok) {
             (void)hipGetLastError();

@@ -376,8 +376,11 @@ int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, 
             if (d->jit && d->jit[x] && all_cols) {
                 uint32_t xx = x, slab = gs.slab, wb = gs.wave_bytes, rpw = gs.rpw;
                 void *args[] = {(void *)&Dd, (void *)&Bd, &xx, &slab, &wb, &rpw};
+                // rows from HBM: the kernel without staging code (fewer registers, more waves)
+                const hipFunction_t fn = gs.slab == 0 && d->jit[TREE_MAX_T + x] ? d->jit[TREE_MAX_T + x] : d->jit[x];
+                const unsigned grid = gs.slab == 0 ? row_grid(cap) : (unsigned)blocks;
                 const hipError_t le =
-                    hipModuleLaunchKernel(d->jit[x], (unsigned)blocks, 1, 1, TB, 1, 1, (unsigned)lds, st, args, nullptr);
+                    hipModuleLaunchKernel(fn, grid, 1, 1, TB, 1, 1, (unsigned)lds, st, args, nullptr);
                 if (le != hipSuccess) {
                     note_hip_error(le);
                     return SPEC_E_HIP;

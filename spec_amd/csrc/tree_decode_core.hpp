@@ -139,6 +139,20 @@ __device__ __forceinline__ void tree_rows(const TreeBufs &B, uint32_t x, uint64_
     }
 }
 
+// tree_rows without staging (slab 0): every row parsed from HBM.  A kernel of its own, so its
+// register budget is the row code's alone (the staging paths' 16-chunk lane windows would
+// otherwise set it) and the CU holds as many waves as the latency of the reads needs.
+template <class GlobBody>
+__device__ __forceinline__ void tree_rows_global(const TreeBufs &B, uint32_t x, uint64_t rows, GlobBody glob_body) {
+    const GlobalSrc gs{B.stream, B.stream_len};
+    for (uint64_t row = (uint64_t)blockIdx.x * TB + threadIdx.x; row < rows; row += (uint64_t)gridDim.x * TB) {
+        long long lo = 0, hi = 0;
+        bool panic = false;
+        row_range(B, x, row, lo, hi, panic);
+        glob_body(gs, row, lo, hi, panic);
+    }
+}
+
 // ---- the run-time-schema row code ------------------------------------------------------------
 
 template <class Src>
