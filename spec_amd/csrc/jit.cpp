@@ -621,7 +621,7 @@ void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, con
     }
     o << "      if (errp) errp[row] = errs;\n"
       << "    } else {\n"
-      << "      st = tree_message_row(s, D, B, " << t << "u, row, tlo, thi, gr);\n"
+      << "      st = tree_message_fallback(s, D, B, " << t << "u, row, tlo, thi, gr);\n"
       << "    }\n"
       << "    store_u8(" << col_expr(T.status_col) << ", row, " << (root ? "panic ? (uint32_t)ST_PANIC : st" : "st")
       << ");\n"

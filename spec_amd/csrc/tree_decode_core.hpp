@@ -173,8 +173,8 @@ __device__ __forceinline__ bool tree_scalar(const Src &s, uint32_t kind, long lo
 // copy per call site overflowed the instruction cache (98K instructions: the waves of one
 // kernel executing different fields' code missed it constantly).
 template <class Src>
-__device__ __noinline__ uint32_t tree_message_row(const Src &s, const TreeDesc &D, const TreeBufs &B, uint32_t t,
-                                                  uint64_t row, long long lo, long long hi, uint2 *gr) {
+__device__ __forceinline__ uint32_t tree_message_row_inl(const Src &s, const TreeDesc &D, const TreeBufs &B, uint32_t t,
+                                                         uint64_t row, long long lo, long long hi, uint2 *gr) {
     const TTable &T = D.t[t];
     const RecInfo ri = rec_open(s, lo, hi); // empty (or panicked) range => empty message
     uint32_t st = ri.tr.st;
@@ -246,6 +246,26 @@ __device__ __noinline__ uint32_t tree_message_row(const Src &s, const TreeDesc &
     }
     if (errp) errp[row] = errs;
     return st;
+}
+
+template <class Src>
+__device__ __noinline__ uint32_t tree_message_row(const Src &s, const TreeDesc &D, const TreeBufs &B, uint32_t t,
+                                                  uint64_t row, long long lo, long long hi, uint2 *gr) {
+    return tree_message_row_inl(s, D, B, t, row, lo, hi, gr);
+}
+
+// The schema-specialised rows' fallback for a table the fast path rejects: out of line when the
+// row is parsed from LDS (the kernel's register budget is set by its staging code anyway), inline
+// when it is parsed from HBM (a call's register saves would set the no-staging kernel's budget).
+__device__ __forceinline__ uint32_t tree_message_fallback(const TreeLds &s, const TreeDesc &D, const TreeBufs &B,
+                                                          uint32_t t, uint64_t row, long long lo, long long hi,
+                                                          uint2 *gr) {
+    return tree_message_row(s, D, B, t, row, lo, hi, gr);
+}
+__device__ __forceinline__ uint32_t tree_message_fallback(const GlobalSrc &s, const TreeDesc &D, const TreeBufs &B,
+                                                          uint32_t t, uint64_t row, long long lo, long long hi,
+                                                          uint2 *gr) {
+    return tree_message_row_inl(s, D, B, t, row, lo, hi, gr);
 }
 
 // One row of group root x (run-time schema): the root table's row, then the group's
