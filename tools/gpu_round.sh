@@ -29,4 +29,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 find $OUT/prof -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats.csv \;
 cut -d, -f1-4 $OUT/kernel_stats.csv | head -n 14
 f=$(find $OUT/prof -name '*kernel_trace.csv' | head -n 1)
-python3 tools/trace_stats.py $f spec_decode_flat_jit 1048576 --json $OUT/decode_flat_1M_trace.json | head -n 2
+python3 tools/trace_stats.py $f spec_decode_flat_jit 1048576 --json $OUT/decode_flat_1M_trace.json > $OUT/decode_flat_1M_trace.txt && head -n 2 $OUT/decode_flat_1M_trace.txt
