@@ -934,7 +934,8 @@ __device__ __forceinline__ void encode_size_body(const EncodeArgs &a) {
     __syncthreads();
     const uint64_t r = (uint64_t)blockIdx.x * ENC_BLOCK + threadIdx.x;
     const bool valid = r < a.n;
-    const typename P::Rec rec = P::load(a.f, valid ? r : a.n - 1);
+    typename P::Rec rec; // sizes need the columns only (string/bytes: their spans), not heap bytes
+    P::load_cols(a.f, valid ? r : a.n - 1, rec);
     bool err = false;
     const RecSize rs = P::size(a.f, rec, r, a.check_heaps, err);
     if (valid & err) errs = 1;

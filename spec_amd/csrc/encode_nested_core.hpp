@@ -223,7 +223,7 @@ __device__ __forceinline__ bool wave_item_prefix(const NestedEncodeArgs &a, uint
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const uint32_t k = c0 + 64 * j + lane;
-            rec[j] = IP::load(a.item, I0 + (k < cnt ? k : cnt - 1));
+            IP::load_cols(a.item, I0 + (k < cnt ? k : cnt - 1), rec[j]); // sizes: columns only
         }
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -315,7 +315,8 @@ __device__ __forceinline__ void nested_enc_size_body(const NestedEncodeArgs &a, 
             for (uint32_t k = lane; k < L.cnt; k += 64) a.item_pre[L.I0 + k] = pre[k + 1];
         }
     }
-    const typename OP::Rec orec = OP::load(a.outer, L.valid ? L.r : a.n - 1);
+    typename OP::Rec orec; // sizes: columns only
+    OP::load_cols(a.outer, L.valid ? L.r : a.n - 1, orec);
     ListSize ls;
     const RecSize rs = lane_record_size<OP>(a, L, orec, pre, a.check_heaps, err, ls);
     if (L.valid & err) *errs = 1;

@@ -572,6 +572,13 @@ struct BEmit {
             for (uint64_t q = base > lo ? base : lo; q < end; q++) out[q] = (uint8_t)(w >> (8 * (q - base)));
         }
     }
+    __device__ __forceinline__ void store_word(uint64_t base, uint64_t end, uint32_t v) { // bytes [base, end) of v
+        if (base >= lo && end == base + 4) {
+            *(uint32_t *)(out + base) = v;
+        } else {
+            for (uint64_t q = base > lo ? base : lo; q < end; q++) out[q] = (uint8_t)(v >> (8 * (q - base)));
+        }
+    }
     __device__ __forceinline__ void put1(uint32_t b) {
         w |= (b & 0xffu) << (8 * (pos & 3));
         pos++;
@@ -579,6 +586,21 @@ struct BEmit {
             store_pending(pos - 4, pos);
             w = 0;
         }
+    }
+    // nb (<= 8) bytes of v, lowest first, merged with the pending bytes: the full dwords stored
+    __device__ __forceinline__ void put_n(uint64_t v, uint32_t nb) {
+        const uint32_t ph = (uint32_t)(pos & 3), sh = 8 * ph;
+        const uint64_t lo64 = (uint64_t)w | (v << sh);
+        const uint32_t hi32 = sh ? (uint32_t)(v >> (64 - sh)) : 0u;
+        const uint32_t total = ph + nb;
+        const uint64_t d = pos & ~3ull;
+        if (total >= 4) store_word(d, d + 4, (uint32_t)lo64);
+        if (total >= 8) store_word(d + 4, d + 8, (uint32_t)(lo64 >> 32));
+        const uint32_t full = total >> 2;
+        const uint32_t rest = full == 0 ? (uint32_t)lo64 : (full == 1 ? (uint32_t)(lo64 >> 32) : hi32);
+        const uint32_t keep = total & 3;
+        w = keep ? (rest & (0xffffffffu >> (32 - 8 * keep))) : 0u;
+        pos += nb;
     }
     __device__ __forceinline__ void skip(uint64_t n) {
         if (!n) return;
@@ -593,18 +615,27 @@ struct BEmit {
         if (pos & 3) store_pending(pos & ~3ull, pos);
         w = 0;
     }
-    __device__ __forceinline__ void rvarint(uint64_t v) { // oracle/compactint.c so_put_reverse_*
+    // reverse varint (oracle/compactint.c so_put_reverse_*): top group first, MSB clear, the
+    // following groups with 0x80; up to 8 bytes (values < 2^56) built in a register at once
+    __device__ __forceinline__ void rvarint(uint64_t v) {
         const uint32_t L = vlen64(v);
+        if (L <= 8) {
+            uint64_t x = v & 0x00ffffffffffffffull; // 7-bit groups -> bytes
+            x = (x & 0x000000000fffffffull) | ((x << 4) & 0x0fffffff00000000ull);
+            x = (x & 0x00003fff00003fffull) | ((x << 2) & 0x3fff00003fff0000ull);
+            x = (x & 0x007f007f007f007full) | ((x << 1) & 0x7f007f007f007f00ull);
+            const uint32_t drop = 8 * (8 - L);
+            put_n((__builtin_bswap64(x) >> drop) | ((0x8080808080808080ull >> drop) & ~0xffull), L);
+            return;
+        }
         for (uint32_t i = 0; i < L; i++) put1(((uint32_t)(v >> (7 * (L - 1 - i))) & 0x7f) | (i ? 0x80 : 0));
     }
-    __device__ __forceinline__ void be(uint64_t v, int nb) {
-        for (int i = nb - 1; i >= 0; i--) put1((uint32_t)(v >> (8 * i)) & 0xff);
+    __device__ __forceinline__ void be(uint64_t v, int nb) { // the low nb bytes of v, big-endian
+        put_n(__builtin_bswap64(v) >> (8 * (8 - nb)), (uint32_t)nb);
     }
-    __device__ __forceinline__ void le(uint64_t v, int nb) {
-        for (int i = 0; i < nb; i++) put1((uint32_t)(v >> (8 * i)) & 0xff);
-    }
-    // heap bytes [off, off + len): 16 at a time from four dword loads issued together
-    // (range-checked: bytes past the heap read as 0 and are never used)
+    __device__ __forceinline__ void le(uint64_t v, int nb) { put_n(v, (uint32_t)nb); }
+    // heap bytes [off, off + len): 16 at a time from four dword loads issued together, appended
+    // 8 at a time (range-checked: bytes past the heap read as 0 and are never used)
     __device__ __forceinline__ void heap(const uint8_t *h, uint64_t hlen, uint32_t off, uint32_t len) {
         const __amdgpu_buffer_rsrc_t r = uniform_rsrc(h, hlen);
         uint32_t i = 0;
@@ -612,8 +643,15 @@ struct BEmit {
             const uint32_t a = (off + i) & ~3u;
             const uint64_t lo = (uint64_t)buf_ld32(r, a, hlen) | ((uint64_t)buf_ld32(r, a + 4, hlen) << 32);
             const uint64_t hi = (uint64_t)buf_ld32(r, a + 8, hlen) | ((uint64_t)buf_ld32(r, a + 12, hlen) << 32);
-            for (uint32_t q = off + i - a; q < 16 && i < len; q++, i++)
-                put1((uint32_t)((q < 8 ? lo >> (8 * q) : hi >> (8 * (q - 8))) & 0xff));
+            const uint32_t q = off + i - a; // 0..3: bytes [q, 16) of (lo, hi) are heap bytes
+            const uint32_t n1 = min(8u, len - i);
+            put_n((lo >> (8 * q)) | (q ? hi << (64 - 8 * q) : 0ull), n1);
+            i += n1;
+            if (i < len) {
+                const uint32_t n2 = min(8u - q, len - i); // the rest of the 16 loaded bytes
+                put_n(hi >> (8 * q), n2);
+                i += n2;
+            }
         }
     }
 };
