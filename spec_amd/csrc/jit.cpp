@@ -628,9 +628,95 @@ void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, con
       << "  }\n";
 }
 
+// The generated Write() of a message table (internal/lang/generator/message.go:319-439,
+// internal/writer/writer.go:376-553) for one row at start: every column read issued before the
+// first byte is written, then the fields in write order (constant kinds, heaps and tags), the
+// table in the Writer's tie-sorted order over the present fields, the trailer.  Sub-messages and
+// list elements are children written by their tables' later launches into the gaps skipped here.
+void gen_write_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
+    const TTable &T = D.t[t];
+    o << "__device__ __forceinline__ void gen_wrow_" << t
+      << "(BEmit &em, const TreeDesc &D, const TreeBufs &B, uint64_t row, uint64_t start) {\n";
+    for (uint32_t k = 0; k < T.nd; k++) {
+        const TField &F = D.f[D.direct[T.d0 + k]];
+        if ((F.kind >= spec::K_BOOL && F.kind <= spec::K_BYTES) || F.kind == spec::K_ANY)
+            o << "  uint64_t a" << k << "[4];\n  load_value_k<" << (int)F.kind << ">(" << col_expr(F.col) << ", row, a" << k
+              << ");\n";
+        else if (F.kind == spec::K_MESSAGE || F.kind == spec::K_LIST)
+            o << "  const uint32_t pr" << k << " = ((const uint8_t *)" << col_expr(F.present) << ")[row];\n";
+        if (F.kind == spec::K_MESSAGE) o << "  const uint32_t sz" << k << " = B.size[" << F.table << "][row];\n";
+    }
+    o << "  uint32_t nf = 0;\n  bool bigtag = false;\n";
+    for (uint32_t k = 0; k < T.nd; k++) {
+        const uint32_t fi = D.direct[T.d0 + k];
+        const TField &F = D.f[fi];
+        const std::string mark = "    e" + std::to_string(k) + " = (uint32_t)(em.pos - start);\n    nf++;\n" +
+                                 (F.tag > 255 ? "    bigtag = true;\n" : "");
+        o << "  uint32_t e" << k << " = 0xffffffffu; // field " << fi << " tag " << F.tag << "\n";
+        if (F.kind >= spec::K_BOOL && F.kind <= spec::K_BYTES) {
+            const bool heap = F.kind == spec::K_STRING || F.kind == spec::K_BYTES;
+            o << "  {\n    emit_value_k<" << (int)F.kind << ">(em, a" << k << ", "
+              << (heap ? "B.heaps[" + std::to_string(F.col) + "], B.heap_lens[" + std::to_string(F.col) + "]" : "nullptr, 0")
+              << ");\n" << mark << "  }\n";
+        } else if (F.kind == spec::K_ANY) {
+            o << "  if ((uint32_t)(a" << k << "[0] >> 32)) {\n    emit_value_k<" << (int)F.kind << ">(em, a" << k
+              << ", B.heaps[" << F.col << "], B.heap_lens[" << F.col << "]);\n" << mark << "  }\n";
+        } else if (F.kind == spec::K_STRUCT) {
+            o << "  {\n    emit_struct(em, B, D, " << fi << "u, row);\n" << mark << "  }\n";
+        } else if (F.kind == spec::K_MESSAGE) {
+            o << "  if (pr" << k << ") {\n    B.pos[" << F.table << "][row] = em.pos;\n    em.skip(sz" << k << ");\n" << mark
+              << "  }\n";
+        } else if (F.kind == spec::K_LIST) {
+            const int y = F.table;
+            o << "  if (pr" << k << ") {\n"
+              << "    bool lerr = false;\n    uint32_t j0, j1;\n"
+              << "    list_span(B, D, " << y << "u, row, j0, j1, lerr);\n"
+              << "    const TreeListSize L = list_size(B, D, " << y << "u, row, lerr);\n"
+              << "    for (uint32_t j = j0; j < j1; j++) {\n      B.pos[" << y << "][j] = em.pos;\n      em.skip(B.size[" << y
+              << "][j]);\n    }\n"
+              << "    uint64_t off = 0;\n"
+              << "    for (uint32_t j = j0; j < j1; j++) {\n      off += B.size[" << y << "][j];\n      em.be(off, L.big ? 4 : 2);\n    }\n"
+              << "    em.rvarint(L.data);\n    em.rvarint((uint64_t)L.count * (L.big ? 4 : 2));\n"
+              << "    em.put1(L.big ? T_BIG_LIST : T_LIST);\n"
+              << mark << "  }\n";
+        }
+    }
+    // IsBigMessage (internal/format/msg.go:43-61), the table (encode/msg.go:58-72), the trailer
+    o << "  const uint64_t data = em.pos - start;\n"
+      << "  const bool big = bigtag || (nf > 0 && data > 65535);\n"
+      << "  if (!big) {\n";
+    for (uint32_t j = 0; j < T.nd; j++) {
+        const uint32_t fi = D.sorted[T.d0 + j], slot = D.sslot[T.d0 + j];
+        if (D.f[fi].tag > 255) continue; // a present one makes the table big
+        o << "    if (e" << slot << " != 0xffffffffu) em.put_n(" << D.f[fi].tag << "u | ((uint64_t)__builtin_bswap16((uint16_t)e"
+          << slot << ") << 8), 3);\n";
+    }
+    o << "  } else {\n";
+    for (uint32_t j = 0; j < T.nd; j++) {
+        const uint32_t fi = D.sorted[T.d0 + j], slot = D.sslot[T.d0 + j];
+        o << "    if (e" << slot << " != 0xffffffffu) { em.be(" << D.f[fi].tag << "u, 2); em.be(e" << slot << ", 4); }\n";
+    }
+    o << "  }\n"
+      << "  em.rvarint(data);\n  em.rvarint((uint64_t)nf * (big ? 6 : 3));\n"
+      << "  em.put1(big ? T_BIG_MESSAGE : T_MESSAGE);\n  em.finish();\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void spec_tree_write_" << t
+      << "(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x, uint64_t rows) {\n"
+      << "  const TreeDesc &D = *Dp;\n  const TreeBufs &B = *Bp;\n"
+      << "  if (!B.out || *B.err || *B.total > B.out_cap) return;\n"
+      << "  for (uint64_t row = grid_first(); row < rows; row += grid_stride()) {\n"
+      << "    const uint64_t start = x == 0 ? B.offsets[row] : B.pos[x][row];\n"
+      << "    if (start == ~0ull) continue; // a row no written owner placed\n"
+      << "    if (x == 0 && B.ends_out) B.ends_out[row] = start + B.size[0][row];\n"
+      << "    BEmit em{B.out, start, start};\n"
+      << "    gen_wrow_" << t << "(em, D, B, row, start);\n"
+      << "  }\n}\n";
+}
+
 std::string generate_tree(const TreeDesc &D, bool *has) {
     std::ostringstream o;
     o << "#include \"tree_decode_core.hpp\"\nusing namespace spec;\n";
+    for (uint32_t t = 0; t < D.ntables; t++)
+        if (D.t[t].shape == spec::SHAPE_MESSAGE) gen_write_table(o, D, t);
     for (uint32_t x = 0; x < D.ntables; x++) {
         const TTable &T = D.t[x];
         has[x] = false;
@@ -690,7 +776,8 @@ std::string generate_tree(const TreeDesc &D, bool *has) {
 
 struct TreeEntry {
     hipModule_t mod = nullptr;
-    hipFunction_t fn[2 * spec::TREE_MAX_T] = {}; // [x]: staged rows, [TREE_MAX_T + x]: rows from HBM
+    // [x]: decode, staged rows; [TREE_MAX_T + x]: decode, rows from HBM; [2 TREE_MAX_T + t]: write
+    hipFunction_t fn[3 * spec::TREE_MAX_T] = {};
     bool failed = false;
 };
 std::unordered_map<std::string, TreeEntry> g_tree_cache;
@@ -708,8 +795,8 @@ long long jit_compile_only_tree(const TreeDesc &D) {
 }
 
 // The schema-specialised group kernels of a tree: fn[x] for each group root x that has one
-// (nullptr where the run-time kernel runs), fn[TREE_MAX_T + x] its variant without staging;
-// nullptr when the JIT is off or failed.
+// (nullptr where the run-time kernel runs), fn[TREE_MAX_T + x] its variant without staging,
+// fn[2 TREE_MAX_T + t] the writer of message table t; nullptr when the JIT is off or failed.
 const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
     if (!enabled()) return nullptr;
     int dev = 0;
@@ -723,6 +810,10 @@ const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
         TreeEntry e;
         const std::vector<char> code = compile_source(src, TREE);
         bool ok = !code.empty() && hipModuleLoadData(&e.mod, code.data()) == hipSuccess;
+        for (uint32_t t = 0; ok && t < D.ntables; t++)
+            if (D.t[t].shape == SHAPE_MESSAGE)
+                ok = hipModuleGetFunction(&e.fn[2 * TREE_MAX_T + t], e.mod,
+                                          ("spec_tree_write_" + std::to_string(t)).c_str()) == hipSuccess;
         for (uint32_t x = 0; ok && x < D.ntables; x++) {
             if (!has[x]) continue;
             const std::string name = "spec_tree_group_" + std::to_string(x);

@@ -623,9 +623,23 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
             hipLaunchKernelGGL(tree_pos_fill_kernel, dim3(gx, L.nt - 1), dim3(256), 0, st, pf);
         }
     }
+    // the generated writers (jit.cpp) for message tables, else the run-time row kernel
+    const hipFunction_t *jit = out ? jit_tree_kernels(L.desc) : nullptr;
     for (uint32_t x = 0; ok && out && x < L.nt; x++)
         if (rows[x]) {
             const TTable &T = L.desc.t[x];
+            if (jit && jit[2 * TREE_MAX_T + x]) {
+                uint32_t xx = x;
+                uint64_t r = rows[x];
+                void *args[] = {(void *)&Dd, (void *)&Bd, &xx, &r};
+                const hipError_t le = hipModuleLaunchKernel(jit[2 * TREE_MAX_T + x], row_grid(rows[x]), 1, 1, TB, 1, 1, 0,
+                                                            st, args, nullptr);
+                if (le != hipSuccess) {
+                    note_hip_error(le);
+                    ok = false;
+                }
+                continue;
+            }
             const size_t lds = T.shape == SHAPE_MESSAGE ? (size_t)(TB / 64) * T.nd * 64 * sizeof(uint32_t) : 0;
             hipLaunchKernelGGL(tree_write_kernel, dim3(row_grid(rows[x])), dim3(TB), lds, st, Dd, Bd, x, rows[x]);
         }

@@ -656,6 +656,61 @@ struct BEmit {
     }
 };
 
+// ---- schema-specialised writer pieces (jit.cpp generate_tree: spec_tree_write_<t>) ---------
+
+// A scalar column element of constant kind K as raw bits (v[0..3]; string/bytes/any: the span)
+template <uint32_t K>
+__device__ __forceinline__ void load_value_k(const void *col, uint64_t row, uint64_t (&v)[4]) {
+    const uint8_t *c = (const uint8_t *)col;
+    v[1] = v[2] = v[3] = 0;
+    if constexpr (K == K_BOOL || K == K_BYTE) v[0] = c[row];
+    else if constexpr (K == K_INT16 || K == K_UINT16) v[0] = ((const uint16_t *)c)[row];
+    else if constexpr (K == K_INT32 || K == K_UINT32 || K == K_FLOAT32) v[0] = ((const uint32_t *)c)[row];
+    else if constexpr (K == K_BIN128) {
+        const ulonglong2 q = ((const ulonglong2 *)c)[row];
+        v[0] = q.x;
+        v[1] = q.y;
+    } else if constexpr (K == K_BIN256) {
+        const ulonglong2 q0 = ((const ulonglong2 *)c)[2 * row], q1 = ((const ulonglong2 *)c)[2 * row + 1];
+        v[0] = q0.x;
+        v[1] = q0.y;
+        v[2] = q1.x;
+        v[3] = q1.y;
+    } else v[0] = ((const uint64_t *)c)[row]; // 64-bit kinds, string/bytes/any spans
+}
+
+// The element through its encoder (internal/encode/...), as emit_value; string/bytes from heap h
+template <uint32_t K>
+__device__ __forceinline__ void emit_value_k(BEmit &em, const uint64_t (&v)[4], const uint8_t *h, uint64_t hlen) {
+    if constexpr (K == K_BOOL) em.put1(v[0] ? T_TRUE : T_FALSE);
+    else if constexpr (K == K_BYTE) em.put_n(v[0] | ((uint64_t)T_BYTE << 8), 2);
+    else if constexpr (K == K_INT16) { em.rvarint(zigzag32((int16_t)v[0])); em.put1(T_INT16); }
+    else if constexpr (K == K_INT32) { em.rvarint(zigzag32((int32_t)v[0])); em.put1(T_INT32); }
+    else if constexpr (K == K_INT64) { em.rvarint(zigzag64((int64_t)v[0])); em.put1(T_INT64); }
+    else if constexpr (K == K_UINT16 || K == K_UINT32 || K == K_UINT64) {
+        em.rvarint(v[0]);
+        em.put1(K == K_UINT16 ? T_UINT16 : K == K_UINT32 ? T_UINT32 : T_UINT64);
+    } else if constexpr (K == K_FLOAT32) em.put_n(bswap32((uint32_t)v[0]) | ((uint64_t)T_FLOAT32 << 32), 5);
+    else if constexpr (K == K_FLOAT64) { em.be(v[0], 8); em.put1(T_FLOAT64); }
+    else if constexpr (K == K_BIN64) { em.le(v[0], 8); em.put1(T_BIN64); }
+    else if constexpr (K == K_BIN128) { em.le(v[0], 8); em.le(v[1], 8); em.put1(T_BIN128); }
+    else if constexpr (K == K_BIN256) {
+        em.le(v[0], 8);
+        em.le(v[1], 8);
+        em.le(v[2], 8);
+        em.le(v[3], 8);
+        em.put1(T_BIN256);
+    } else if constexpr (K == K_STRING || K == K_BYTES) {
+        const uint32_t off = (uint32_t)v[0], len = (uint32_t)(v[0] >> 32);
+        em.heap(h, hlen, off, len);
+        if constexpr (K == K_STRING) em.put1(0);
+        em.rvarint(len);
+        em.put1(K == K_STRING ? T_STRING : T_BYTES);
+    } else if constexpr (K == K_ANY) {
+        em.heap(h, hlen, (uint32_t)v[0], (uint32_t)(v[0] >> 32));
+    }
+}
+
 // One column element through its encoder (internal/encode/...)
 __device__ __forceinline__ void emit_value(BEmit &em, const TreeBufs &B, const TreeDesc &D, int c, uint32_t kind,
                                            uint64_t row) {
