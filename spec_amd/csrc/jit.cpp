@@ -712,11 +712,84 @@ void gen_write_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
       << "  }\n}\n";
 }
 
+// The generated writer's size pass for a message table (tree.hip tree_size_kernel with constant
+// kinds, columns and tags): every column read first, then the encoded sizes, IsBigMessage.
+void gen_size_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
+    const TTable &T = D.t[t];
+    o << "extern \"C\" __global__ __launch_bounds__(256) void spec_tree_size_" << t
+      << "(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x, uint64_t rows) {\n"
+      << "  const TreeDesc &D = *Dp;\n  const TreeBufs &B = *Bp;\n  bool err = false;\n"
+      << "  for (uint64_t row = grid_first(); row < rows; row += grid_stride()) {\n";
+    for (uint32_t k = 0; k < T.nd; k++) {
+        const TField &F = D.f[D.direct[T.d0 + k]];
+        if ((F.kind >= spec::K_BOOL && F.kind <= spec::K_BYTES) || F.kind == spec::K_ANY)
+            o << "    uint64_t a" << k << "[4];\n    load_value_k<" << (int)F.kind << ">(" << col_expr(F.col) << ", row, a" << k
+              << ");\n";
+        else if (F.kind == spec::K_MESSAGE || F.kind == spec::K_LIST)
+            o << "    const uint32_t pr" << k << " = ((const uint8_t *)" << col_expr(F.present) << ")[row];\n";
+    }
+    o << "    uint64_t data = 0;\n    uint32_t nf = 0;\n    bool bigtag = false;\n";
+    for (uint32_t k = 0; k < T.nd; k++) {
+        const uint32_t fi = D.direct[T.d0 + k];
+        const TField &F = D.f[fi];
+        const std::string tg = F.tag > 255 ? " bigtag = true;" : "";
+        switch (F.kind) {
+        case spec::K_MESSAGE:
+            o << "    if (pr" << k << ") { data += B.size[" << F.table << "][row]; nf++;" << tg << " }\n";
+            break;
+        case spec::K_LIST:
+            o << "    if (pr" << k << ") { data += list_size(B, D, " << F.table << "u, row, err).total; nf++;" << tg << " }\n";
+            break;
+        case spec::K_STRUCT:
+            o << "    data += struct_size(B, D, " << fi << "u, row, err); nf++;" << tg << "\n";
+            break;
+        case spec::K_ANY:
+            o << "    { const uint32_t off = (uint32_t)a" << k << "[0], len = (uint32_t)(a" << k << "[0] >> 32);\n"
+              << "      if ((uint64_t)len > MAX_SIZE || (uint64_t)off + len > B.heap_lens[" << F.col << "]) err = true;\n"
+              << "      if (len) { data += len; nf++;" << tg << " } }\n";
+            break;
+        case spec::K_STRING:
+        case spec::K_BYTES:
+            o << "    { const uint32_t off = (uint32_t)a" << k << "[0], len = (uint32_t)(a" << k << "[0] >> 32);\n"
+              << "      if ((uint64_t)len > MAX_SIZE || (uint64_t)off + len > B.heap_lens[" << F.col << "]) err = true;\n"
+              << "      data += (uint64_t)len + vlen32(len) + " << (F.kind == spec::K_STRING ? 2 : 1) << "; nf++;" << tg << " }\n";
+            break;
+        default: {
+            const int K = F.kind;
+            std::string sz;
+            if (K == spec::K_BOOL) sz = "1";
+            else if (K == spec::K_BYTE) sz = "2";
+            else if (K == spec::K_INT16) sz = "vlen32(zigzag32((int16_t)a" + std::to_string(k) + "[0])) + 1";
+            else if (K == spec::K_INT32) sz = "vlen32(zigzag32((int32_t)a" + std::to_string(k) + "[0])) + 1";
+            else if (K == spec::K_INT64) sz = "vlen64(zigzag64((int64_t)a" + std::to_string(k) + "[0])) + 1";
+            else if (K == spec::K_UINT16 || K == spec::K_UINT32 || K == spec::K_UINT64)
+                sz = "vlen64(a" + std::to_string(k) + "[0]) + 1";
+            else if (K == spec::K_FLOAT32) sz = "5";
+            else if (K == spec::K_FLOAT64 || K == spec::K_BIN64) sz = "9";
+            else if (K == spec::K_BIN128) sz = "17";
+            else sz = "33";
+            o << "    data += " << sz << "; nf++;" << tg << "\n";
+        }
+        }
+    }
+    // IsBigMessage (internal/format/msg.go:43-61), encodeMessageTable sizes
+    o << "    const bool big = bigtag || (nf > 0 && data > 65535);\n"
+      << "    const uint64_t tsize = (uint64_t)nf * (big ? 6 : 3);\n"
+      << "    if (data > MAX_SIZE) err = true;\n"
+      << "    const uint64_t total = data + tsize + vlen64(data) + vlen64(tsize) + 1;\n"
+      << "    if (total > 0xffffffffull) err = true;\n"
+      << "    B.size[x][row] = (uint32_t)total;\n"
+      << "  }\n  if (err) *B.err = 1;\n}\n";
+}
+
 std::string generate_tree(const TreeDesc &D, bool *has) {
     std::ostringstream o;
     o << "#include \"tree_decode_core.hpp\"\nusing namespace spec;\n";
     for (uint32_t t = 0; t < D.ntables; t++)
-        if (D.t[t].shape == spec::SHAPE_MESSAGE) gen_write_table(o, D, t);
+        if (D.t[t].shape == spec::SHAPE_MESSAGE) {
+            gen_write_table(o, D, t);
+            gen_size_table(o, D, t);
+        }
     for (uint32_t x = 0; x < D.ntables; x++) {
         const TTable &T = D.t[x];
         has[x] = false;
@@ -776,8 +849,9 @@ std::string generate_tree(const TreeDesc &D, bool *has) {
 
 struct TreeEntry {
     hipModule_t mod = nullptr;
-    // [x]: decode, staged rows; [TREE_MAX_T + x]: decode, rows from HBM; [2 TREE_MAX_T + t]: write
-    hipFunction_t fn[3 * spec::TREE_MAX_T] = {};
+    // [x]: decode, staged rows; [TREE_MAX_T + x]: decode, rows from HBM; [2 TREE_MAX_T + t]: write;
+    // [3 TREE_MAX_T + t]: size
+    hipFunction_t fn[4 * spec::TREE_MAX_T] = {};
     bool failed = false;
 };
 std::unordered_map<std::string, TreeEntry> g_tree_cache;
@@ -796,11 +870,25 @@ long long jit_compile_only_tree(const TreeDesc &D) {
 
 // The schema-specialised group kernels of a tree: fn[x] for each group root x that has one
 // (nullptr where the run-time kernel runs), fn[TREE_MAX_T + x] its variant without staging,
-// fn[2 TREE_MAX_T + t] the writer of message table t; nullptr when the JIT is off or failed.
+// fn[2 TREE_MAX_T + t] / fn[3 TREE_MAX_T + t] the writer / size pass of message table t; nullptr
+// when the JIT is off or failed.
 const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
     if (!enabled()) return nullptr;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    // a repeated tree is found by its descriptor's bytes, without regenerating the source (every
+    // spec_encode_tree call looks its kernels up)
+    struct Known {
+        int dev;
+        TreeDesc desc;
+        const hipFunction_t *fn;
+    };
+    static std::vector<Known *> known;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        for (const Known *k : known)
+            if (k->dev == dev && memcmp(&k->desc, &D, sizeof(TreeDesc)) == 0) return k->fn;
+    }
     bool has[TREE_MAX_T];
     const std::string src = generate_tree(D, has);
     const std::string key = "tree:" + std::to_string(dev) + ":" + src;
@@ -813,7 +901,9 @@ const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
         for (uint32_t t = 0; ok && t < D.ntables; t++)
             if (D.t[t].shape == SHAPE_MESSAGE)
                 ok = hipModuleGetFunction(&e.fn[2 * TREE_MAX_T + t], e.mod,
-                                          ("spec_tree_write_" + std::to_string(t)).c_str()) == hipSuccess;
+                                          ("spec_tree_write_" + std::to_string(t)).c_str()) == hipSuccess &&
+                     hipModuleGetFunction(&e.fn[3 * TREE_MAX_T + t], e.mod,
+                                          ("spec_tree_size_" + std::to_string(t)).c_str()) == hipSuccess;
         for (uint32_t x = 0; ok && x < D.ntables; x++) {
             if (!has[x]) continue;
             const std::string name = "spec_tree_group_" + std::to_string(x);
@@ -827,7 +917,13 @@ const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
         }
         it = g_tree_cache.emplace(key, e).first;
     }
-    return it->second.failed ? nullptr : it->second.fn;
+    const hipFunction_t *fn = it->second.failed ? nullptr : it->second.fn;
+    Known *k = new Known;
+    k->dev = dev;
+    memcpy(&k->desc, &D, sizeof(TreeDesc));
+    k->fn = fn;
+    known.push_back(k);
+    return fn;
 }
 
 long long jit_compile_only(const spec_schema *schema, double) {

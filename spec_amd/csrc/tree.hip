@@ -596,9 +596,25 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
     bool ok = hipMemcpyAsync(ws + w.desc, &L.desc, sizeof(TreeDesc), hipMemcpyHostToDevice, st) == hipSuccess &&
               hipMemcpyAsync(Bd, B, sizeof(TreeBufs), hipMemcpyHostToDevice, st) == hipSuccess &&
               hipMemsetAsync(B->err, 0, sizeof(uint32_t), st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
+    // the generated writers and size passes (jit.cpp) for message tables, else the run-time row kernels
+    const hipFunction_t *jit = jit_tree_kernels(L.desc);
     // sizes bottom-up (children before their owners: table order is pre-order)
-    for (int x = (int)L.nt - 1; ok && x >= 0; x--)
-        if (rows[x]) hipLaunchKernelGGL(tree_size_kernel, dim3(row_grid(rows[x])), dim3(TB), 0, st, Dd, Bd, (uint32_t)x, rows[x]);
+    for (int x = (int)L.nt - 1; ok && x >= 0; x--) {
+        if (!rows[x]) continue;
+        if (jit && jit[3 * TREE_MAX_T + x]) {
+            uint32_t xx = (uint32_t)x;
+            uint64_t r = rows[x];
+            void *args[] = {(void *)&Dd, (void *)&Bd, &xx, &r};
+            const hipError_t le =
+                hipModuleLaunchKernel(jit[3 * TREE_MAX_T + x], row_grid(rows[x]), 1, 1, TB, 1, 1, 0, st, args, nullptr);
+            if (le != hipSuccess) {
+                note_hip_error(le);
+                ok = false;
+            }
+            continue;
+        }
+        hipLaunchKernelGGL(tree_size_kernel, dim3(row_grid(rows[x])), dim3(TB), 0, st, Dd, Bd, (uint32_t)x, rows[x]);
+    }
     // record offsets, ends, total
     if (ok) {
         if (n) {
@@ -623,8 +639,6 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
             hipLaunchKernelGGL(tree_pos_fill_kernel, dim3(gx, L.nt - 1), dim3(256), 0, st, pf);
         }
     }
-    // the generated writers (jit.cpp) for message tables, else the run-time row kernel
-    const hipFunction_t *jit = out ? jit_tree_kernels(L.desc) : nullptr;
     for (uint32_t x = 0; ok && out && x < L.nt; x++)
         if (rows[x]) {
             const TTable &T = L.desc.t[x];
