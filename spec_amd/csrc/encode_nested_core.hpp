@@ -395,11 +395,17 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
     const int lst = le.lstart;
     const bool fix = L.valid && ls.count > 0 && (lst & 3);
     const uint32_t saved = fix ? *(const uint32_t *)(slab + (lst & ~3)) : 0u;
+    // the prefix has been read (list tables): each record turns its items' entries into their
+    // slab positions, so an item lane reads its position instead of searching for its owner
+    if (L.valid && ls.count > 0) {
+        const uint32_t k0 = L.b - L.I0, k1 = L.e - L.I0;
+        const int delta = lst - (int)pre[k0];
+        for (uint32_t q = k0; q < k1; q++) pre[q] = (uint32_t)((int)pre[q] + delta);
+    }
     wave_sync();
     // B: items, last chunk first, three chunks in flight: the column loads of chunk c-128 and
     // the heap loads of chunk c-64 (addressed by the spans its column loads brought one
     // iteration earlier) are issued before chunk c is emitted
-    const int lbase = lst - (int)pre[L.b - L.I0];
     int c = ((int)L.cnt - 1) & ~63;
     typename IP::Rec cur, nxt, nn;
     if (c >= 0) {
@@ -413,10 +419,7 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
         const uint32_t kk = (uint32_t)c + lane;
         const bool iv = kk < L.cnt;
         const uint32_t i = L.I0 + (iv ? kk : 0u);
-        int o = 0; // owner lane: the last lane whose first item is <= i
-        for (int st = 32; st > 0; st >>= 1)
-            if (__shfl(L.b, o + st) <= i) o += st;
-        const int pos = __shfl(lbase, o) + (int)pre[iv ? kk : 0u];
+        const int pos = (int)pre[iv ? kk : 0u];
         if (iv) {
             bool e2 = false;
             const RecSize irs = IP::size(a.item, cur, i, false, e2);
