@@ -953,16 +953,30 @@ __device__ __forceinline__ void encode_size_body(const EncodeArgs &a) {
 // Copy slab [head, lim) -> gbase[head, lim) (gbase 16-B aligned), one 16-B store per lane.
 __device__ __forceinline__ void copy_slab_out(const uint8_t *slab, uint8_t *gbase, uint64_t head, uint64_t lim,
                                               int lane) {
-    for (uint64_t c = 0; c < lim; c += 1024) {
-        const uint64_t p = c + (uint64_t)lane * 16;
-        if (p >= lim) break;
-        if (p >= head && p + 16 <= lim) {
-            *(uint4 *)(gbase + p) = *(const uint4 *)(slab + p);
-        } else {
-            for (int i = 0; i < 16; i++)
-                if (p + i >= head && p + i < lim) gbase[p + i] = slab[p + i];
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) const v4u lds_v4;
+    typedef __attribute__((address_space(3))) const uint8_t lds_b;
+    lds_v4 *s4 = (lds_v4 *)(lds_b *)slab; // ds_read_b128 (a generic pointer would be a flat load)
+    lds_b *sb = (lds_b *)slab;
+    v4u *g4 = (v4u *)gbase;
+    // the whole 16-byte chunks [h16, l16): four per lane per round, every LDS read before the stores
+    const uint64_t h16 = (head + 15) >> 4, l16 = lim >> 4;
+    for (uint64_t q = h16 + lane; q < l16; q += 256) {
+        v4u v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint64_t qq = q + 64 * u;
+            v[u] = s4[qq < l16 ? qq : q]; // q < l16: in range
         }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (q + 64 * u < l16) g4[q + 64 * u] = v[u];
     }
+    // the partial chunks at either end, a byte per lane
+    const uint64_t hend = (h16 << 4) < lim ? (h16 << 4) : lim;
+    const uint64_t tb = (l16 << 4) > hend ? (l16 << 4) : hend;
+    if (lane < 16 && head + lane < hend) gbase[head + lane] = sb[head + lane];
+    if (lane >= 16 && lane < 32 && tb + (lane - 16) < lim) gbase[tb + (lane - 16)] = sb[tb + (lane - 16)];
 }
 
 // Pass 3: block scan of the recomputed sizes -> record offsets; each lane emits its record
