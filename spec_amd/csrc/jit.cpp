@@ -699,7 +699,7 @@ void gen_write_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
     o << "  }\n"
       << "  em.rvarint(data);\n  em.rvarint((uint64_t)nf * (big ? 6 : 3));\n"
       << "  em.put1(big ? T_BIG_MESSAGE : T_MESSAGE);\n  em.finish();\n}\n"
-      << "extern \"C\" __global__ __launch_bounds__(256) void spec_tree_write_" << t
+      << "extern \"C\" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void spec_tree_write_" << t
       << "(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x, uint64_t rows) {\n"
       << "  const TreeDesc &D = *Dp;\n  const TreeBufs &B = *Bp;\n"
       << "  if (!B.out || *B.err || *B.total > B.out_cap) return;\n"
