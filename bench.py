@@ -59,6 +59,7 @@ def parse(argv=None):
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="collective backend for N>1 (gloo: rehearsal, every rank on the same GPU)")
     p.add_argument("--no-jit", action="store_true", help="generic decode kernel (no schema specialisation)")
+    p.add_argument("--no-native", action="store_true", help="skip the native one-process multi-device leg")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="PMC traffic per kernel (tools/pmc_traffic.py) used for roofline.traffic")
@@ -472,18 +473,26 @@ def shard_leg(args, dist, rank, world, dev):
         for d in decs:
             d()
 
-    reps = max(3, args.steps // 10)
+    reps = max(10, args.steps // 5)
     decode_all()
     barrier(dist)
     t0 = time.perf_counter()
     for _ in range(reps):
         decode_all()
     barrier(dist)
-    dec_s = max_over_ranks(dist, (time.perf_counter() - t0) / reps)
+    wall_s = max_over_ranks(dist, (time.perf_counter() - t0) / reps)
+    # HIP events on the launch stream around back-to-back steps (the rank's blocks), and each
+    # block alone: the per-launch kernel times the 1M headline is compared with
+    ev_ms, _ = kernel_time_events(decode_all, reps, lead=2)
+    block_ms = [round(kernel_time_events(d_, 10, lead=2)[0], 4) for d_ in decs]
+    dec_s = max_over_ranks(dist, ev_ms * 1e-3)
     bytes_all = sum_over_ranks(dist, float(stream_bytes))
     out = {"records_total": nblocks * bsz, "blocks": nblocks, "block_records": bsz, "ranks": world,
            "decode_ms": round(dec_s * 1e3, 3), "decode_mmsg_s": round(nblocks * bsz / dec_s / 1e6, 1),
            "decode_gb_s": round((bytes_all + nblocks * bsz * (8 + row)) / dec_s / 1e9, 1),
+           "decode_wall_ms": round(wall_s * 1e3, 3), "block_kernel_ms": block_ms,
+           "timing": "HIP events on the launch stream around back-to-back steps (max over ranks); "
+                     "decode_wall_ms: perf_counter around the same steps incl. Python dispatch",
            "status_ok": bool(int(pc.status.ne(0).sum()) == 0)}
     if dist is None:
         out["gather"] = "n/a (one rank: the columns are already on rank 0)"
@@ -519,6 +528,162 @@ def shard_leg(args, dist, rank, world, dev):
         ok = all(np.array_equal(last.cols[f][r0:r0 + m].numpy(), want[f]) for f in range(16))
         out["gathered_sample_vs_oracle"] = bool(ok and np.array_equal(last.status[r0:r0 + m].numpy(), wst))
     return out
+
+
+def native_shard_leg(args, world, devices_distinct):
+    """The native multi-device path a cgo host drives (include/spec_amd.h spec_shard_*): ONE
+    process, one stream + RCCL communicator per device, N = --gpus devices (weak scaling: 1M
+    Flat16 records per device, the headline's per-GPU batch).  Per step, timed by the wall clock
+    around `reps` back-to-back steps between spec_shard_sync calls (the devices run
+    concurrently), plus HIP events on every device's shard stream:
+      encode  spec_shard_encode: size passes, one host scan of the shard totals, write passes;
+      decode  spec_shard_decode of every device's encoded shard into its packed buffer;
+      gather  spec_shard_gather of every packed buffer to device 0 (grouped ncclSend/ncclRecv
+              over xGMI; with one device the communicator is forced and the part is a send to
+              itself, so the RCCL path executes);
+      host    spec_shard_host_decode: the pinned host batch -> H2D / decode / D2H on every
+              device at once (PCIe-inclusive, never the headline).
+    On a box with fewer GPUs than N (a gloo rehearsal) the N shards share the visible GPUs
+    (SPEC_SHARD_SHARED, no communicator) and `rehearsal` says so."""
+    import ctypes as C
+
+    from spec_amd import _lib
+    from spec_amd.shard import NativeShard, PackedColumns
+
+    visible = torch.cuda.device_count()
+    n = args.records
+    if visible >= world and devices_distinct >= world:
+        devs, mode = list(range(world)), ("rccl" if world > 1 else "rccl-self")
+        sh = NativeShard(devs, force_comm=True)
+    else:
+        devs, mode = [k % visible for k in range(world)], "shared-rehearsal"
+        sh = NativeShard(devs, shared=True)
+    L = _lib.lib()
+    shards = []
+    for k, d in enumerate(devs):
+        cols, heaps = workload.flat16(n, args.seed + 0x200 + k)
+        dv = torch.device("cuda", d)
+        shards.append(([torch.from_numpy(c).to(dv) for c in cols], {f: torch.from_numpy(h).to(dv) for f, h in heaps.items()}, n))
+        del cols, heaps
+    outs, ends, totals, bases = sh.encode(FLAT16, shards)
+    sh.sync()
+    reps = max(20, args.steps)
+
+    def timed(step, nrep):
+        step()
+        sh.sync()
+        evs = []
+        for k, d in enumerate(devs):
+            with torch.cuda.device(d):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(sh.stream(k))
+                evs.append((a, b))
+        t0 = time.perf_counter()
+        for _ in range(nrep):
+            step()
+        for k, (a, b) in enumerate(evs):
+            b.record(sh.stream(k))
+        sh.sync()
+        wall = (time.perf_counter() - t0) / nrep
+        dev_ms = max(a.elapsed_time(b) for a, b in evs) / nrep
+        return wall, dev_ms
+
+    enc_wall, enc_dev = timed(lambda: sh.encode(FLAT16, shards, outs=outs, ends=ends), reps)
+    # decode: every device's shard, ends relative to its own stream (prepared ctypes arguments,
+    # so the timed loop is the C ABI calls alone, as a cgo caller issues them)
+    rel = [(e - b).contiguous() for e, b in zip(ends, bases)]
+    packs = [PackedColumns(FLAT16, n, torch.device("cuda", d)) for d in devs]
+    k_ = len(devs)
+    sp = (C.c_void_p * k_)(*[o.data_ptr() for o in outs])
+    lens = (C.c_uint64 * k_)(*totals)
+    ep = (C.c_void_p * k_)(*[e.data_ptr() for e in rel])
+    ns = (C.c_uint64 * k_)(*[n] * k_)
+    pp = (C.c_void_p * k_)(*[p.buf.data_ptr() for p in packs])
+    for d in sorted(set(devs)):  # rel / packs come from torch's streams: complete before the shard streams use them
+        torch.cuda.synchronize(d)
+
+    def decode():
+        _lib.check(L.spec_shard_decode(sh._h, C.byref(FLAT16.c), sp, lens, ep, ns, pp), "spec_shard_decode")
+
+    dec_wall, dec_dev = timed(decode, reps)
+    sizes = [p.nbytes for p in packs]
+    gathered = torch.empty(sum(sizes), dtype=torch.uint8, device=torch.device("cuda", devs[0]))
+    nb = (C.c_uint64 * k_)(*sizes)
+
+    def gather():
+        _lib.check(L.spec_shard_gather(sh._h, nb, pp, 0, C.c_void_p(gathered.data_ptr())), "spec_shard_gather")
+
+    gat_wall, gat_dev = timed(gather, reps)
+
+    def dec_gather():
+        decode()
+        gather()
+
+    dg_wall, _ = timed(dec_gather, reps)
+    # checks: every device's decoded fixed-width columns == its input columns, string lengths
+    # equal; the gathered buffer == the packed buffers back to back; a 20k-record sample of the
+    # last shard: the oracle Writer's bytes == the encoded shard, the oracle decode == its columns
+    ok = int(sum(int(p.status.ne(0).sum()) for p in packs)) == 0
+    for k, (p, s) in enumerate(zip(packs, shards)):
+        for f in (0, 3, 4, 9, 12, 15):
+            ok = ok and torch.equal(p.cols[f], s[0][f])
+        ok = ok and torch.equal(p.cols[13][:, 4:], s[0][13][:, 4:])
+    g = gathered.cpu()
+    off = 0
+    for p in packs:
+        ok = ok and torch.equal(g[off:off + p.nbytes], p.buf[: p.nbytes].cpu())
+        off += p.nbytes
+    sample_ok = None
+    if not args.no_verify:
+        from oracle import oracle as O
+
+        m = min(20_000, n)
+        cols, heaps = workload.flat16(n, args.seed + 0x200 + k_ - 1)
+        st, en = O.encode_flat_batch(FLAT16.tags, FLAT16.kinds, [c[:m] for c in cols], [heaps.get(f) for f in range(16)], m)
+        want, wst = O.decode_flat_batch(FLAT16.tags, FLAT16.kinds, st, en, FLAT16.widths, host_cores())
+        last = packs[-1]
+        sample_ok = bool(np.array_equal(outs[-1][: st.size].cpu().numpy(), st)
+                         and np.array_equal(rel[-1][:m].cpu().numpy(), en.view(np.int64))
+                         and all(np.array_equal(last.cols[f][:m].cpu().numpy(), want[f]) for f in range(16))
+                         and np.array_equal(last.status[:m].cpu().numpy(), wst))
+    res = {"devices": devs, "mode": mode, "rccl_version": NativeShard.rccl_version(), "has_comm": sh.has_comm,
+           "records_per_device": n, "records_total": n * k_, "stream_bytes_total": int(sum(totals)),
+           "encode_ms": round(enc_wall * 1e3, 4), "encode_mmsg_s": round(n * k_ / enc_wall / 1e6, 1),
+           "encode_device_ms_max": round(enc_dev, 4),
+           "decode_ms": round(dec_wall * 1e3, 4), "decode_mmsg_s": round(n * k_ / dec_wall / 1e6, 1),
+           "decode_device_ms_max": round(dec_dev, 4),
+           "decode_device_mmsg_s": round(n * k_ / (dec_dev * 1e-3) / 1e6, 1),
+           "gather_ms": round(gat_wall * 1e3, 4), "gather_bytes": int(sum(sizes)),
+           "gather_gb_s": round(sum(sizes) / gat_wall / 1e9, 1),
+           "decode_gather_ms": round(dg_wall * 1e3, 4), "decode_gather_mmsg_s": round(n * k_ / dg_wall / 1e6, 1),
+           "columns_ok": bool(ok), "oracle_sample_ok": sample_ok}
+    # host batch in, host columns out, every device at once (pinned, chunked)
+    try:
+        whole = torch.empty(int(sum(totals)), dtype=torch.uint8).pin_memory()
+        off = 0
+        for o, t in zip(outs, totals):
+            whole[off:off + t].copy_(o[:t].cpu())
+            off += t
+        gends = torch.cat([e.cpu() for e in ends]).pin_memory()
+        sh.host_prepare(FLAT16, n, max(totals), chunks=8)
+        hout = [torch.empty(sh.host_out_bytes(k, n), dtype=torch.uint8).pin_memory() for k in range(k_)]
+        sh.host_decode(whole, gends, hout)
+        t0 = time.perf_counter()
+        hreps = 3
+        for _ in range(hreps):
+            sh.host_decode(whole, gends, hout)
+        host_s = (time.perf_counter() - t0) / hreps
+        r0, r1, co, so = sh.host_chunk(k_ - 1, n, 0)
+        h_ok = bool(np.array_equal(hout[-1].numpy()[co[4]: co[4] + (r1 - r0) * 8],
+                                   packs[-1].cols[4][r0:r1].cpu().numpy().reshape(-1)))
+        res.update({"host_e2e_ms": round(host_s * 1e3, 3), "host_e2e_mmsg_s": round(n * k_ / host_s / 1e6, 1),
+                    "host_e2e_ok": h_ok,
+                    "host_note": "pinned host batch -> per device 8 chunks H2D/decode/D2H on 3 streams, devices "
+                                 "on their own host threads (spec_shard_host_decode); PCIe-bound"})
+    except Exception as e:  # the PCIe leg never hides the device-resident numbers
+        res["host_e2e_error"] = repr(e)[:300]
+    del sh
+    return res
 
 
 def generic_leg(stream, ends, want_cols, want_status, avg_jit_ms):
@@ -616,9 +781,10 @@ def tree_leg(dev, n=1 << 18, seed=7):
     d.index(out, ends)
     dcols = d.alloc(dev)
     rows_out = torch.empty(len(tree.tables), dtype=torch.int64, device=dev)
+    col_rows = d.column_capacity(dcols)
 
     def decode():  # one asynchronous pass: every group kernel + list scans, no host sync
-        d.run(out, ends, dcols, rows_out)
+        d.run(out, ends, dcols, rows_out, col_rows=col_rows)
 
     res = {}
     fn = encode
@@ -686,12 +852,12 @@ def main(argv=None):
         launch_ranks(args, argv if argv is not None else sys.argv[1:])
         return
     global _RESULT_OUT
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        # the collective libraries print to fd 1 (gloo: "[Gloo] Rank k is connected ..."): send
-        # everything but the result line to stderr, so stdout carries exactly one JSON line
-        sys.stdout.flush()
-        _RESULT_OUT = os.fdopen(os.dup(1), "w")
-        os.dup2(2, 1)
+    # the collective libraries print to fd 1 (gloo: "[Gloo] Rank k is connected ...", RCCL its
+    # version banner at the first communicator): send everything but the result line to stderr,
+    # so stdout carries exactly one JSON line
+    sys.stdout.flush()
+    _RESULT_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     run(args, env)
 
 
@@ -817,6 +983,24 @@ def run(args, env):
                          f"per thread count on {threads} host threads (all cores this process may use) and on 1; "
                          f"C restatement of OpenMessageErr + 16 getters",
                "single_core_value": round(res[1], 2)}
+
+    # the native one-process multi-device leg (spec_shard_*): rank 0 drives every device while the
+    # other ranks wait on the rendezvous store (no GPU work of theirs runs meanwhile)
+    if not args.no_native and not args.no_extras:
+        if rank == 0:
+            try:
+                extras["native_shard"] = native_shard_leg(args, world, devices)
+                checks["native_shard_columns"] = extras["native_shard"]["columns_ok"]
+            except Exception as e:
+                extras["native_shard"] = {"error": repr(e)[:300]}
+        if dist is not None:
+            import datetime
+
+            store = dist.distributed_c10d._get_default_store()
+            if rank == 0:
+                store.set("spec_native_done", "1")
+            else:
+                store.wait(["spec_native_done"], datetime.timedelta(minutes=15))
 
     if rank == 0:
         line = {

@@ -85,6 +85,7 @@ typedef enum spec_rc {
     SPEC_E_CAPACITY = -4,  /* output buffer smaller than the encoded batch */
     SPEC_E_WORKSPACE = -5, /* workspace smaller than *_workspace_size() */
     SPEC_E_CORRUPT = -6,   /* corrupt LZ4 frame (magic, version, header/block checksum, block size) */
+    SPEC_E_ENCODE = -7,    /* an encoder error in some shard (a span outside its heap, a value > MaxSize) */
 } spec_rc;
 
 typedef struct spec_span {
@@ -215,8 +216,15 @@ int spec_tree_layout(const spec_tree *tree, spec_tree_table *tables, uint32_t *n
  *     rows; NULL skips a column), asynchronous; the batch must be the one indexed;
  *   spec_tree_decoder_run: the pass over a new batch with columns, asynchronous, no host
  *     synchronisation: rows_out (device, ntables uint64) receives the row counts, ~0 for a list
- *     table that outgrew the decoder's capacity for it (its rows beyond capacity are not
- *     decoded: index a batch of that shape first, or spec_tree_decoder_reserve);
+ *     table that outgrew the decoder's capacity for it or the caller's columns, and for every
+ *     table below such a list (their rows beyond capacity are not decoded: index a batch of that
+ *     shape first, or spec_tree_decoder_reserve).  col_rows (host, ntables; may be NULL) = the
+ *     rows the caller's columns of each table hold (a BEGIN column holds its owner table's rows
+ *     + 1 entries): rows are clamped to them, nothing is written past them (SPEC_E_CAPACITY if
+ *     a record table's columns hold fewer than n rows).  With NULL, every list table's columns
+ *     must hold spec_tree_decoder_capacity rows;
+ *   spec_tree_decoder_capacity: the decoder's row capacity per list table (host; 0 for tables
+ *     with a row per record);
  *   spec_tree_decoder_reserve: list-table capacities of at least rows[t] (host). */
 typedef struct spec_tree_decoder spec_tree_decoder;
 int spec_tree_decoder_create(const spec_tree *tree, spec_tree_decoder **out);
@@ -225,7 +233,9 @@ int spec_tree_decoder_index(spec_tree_decoder *d, const uint8_t *stream_bytes, u
                             const uint64_t *ends, uint64_t n, uint64_t *rows, void *stream);
 int spec_tree_decoder_decode(spec_tree_decoder *d, void *const *columns, void *stream);
 int spec_tree_decoder_run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, const uint64_t *ends,
-                          uint64_t n, void *const *columns, uint64_t *rows_out, void *stream);
+                          uint64_t n, void *const *columns, const uint64_t *col_rows, uint64_t *rows_out,
+                          void *stream);
+int spec_tree_decoder_capacity(const spec_tree_decoder *d, uint64_t *rows);
 int spec_tree_decoder_reserve(spec_tree_decoder *d, const uint64_t *rows);
 /* spec_tree_jit_compile: compile (hiprtc, no GPU needed) the decoder's schema-specialised group
  * kernels for this tree into the code-object cache (a decoder compiles them on first use
@@ -259,30 +269,58 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
 
 /* ---- several devices in one process (the reference has no multi-device code) ----
  * Records are independent, so a batch splits into contiguous record shards, one per device.  A
- * spec_shard holds one stream and one RCCL communicator per device (ncclCommInitAll: one rank
- * per GPU, no duplicates; librccl is loaded on first use).  Per device, a shard decodes into ONE
- * packed buffer: the schema's columns back to back, each starting on a 256-byte boundary, then
- * the status bytes (spec_packed_layout; what spec_amd.shard.PackedColumns lays out), so the
- * gather to the root device is one grouped RCCL send/recv per device over xGMI.  String/bytes
- * spans stay shard-relative (a 16M-record batch is > 4 GiB): the shard's byte base travels
- * alongside (spec_shard_decode_host reports it).
+ * spec_shard holds per device a stream and, with more than one device (or SPEC_SHARD_FORCE_COMM),
+ * an RCCL communicator rank (ncclCommInitAll over the listed devices, no duplicates; librccl is
+ * loaded on first use).  Per device, a shard decodes into ONE packed buffer: the schema's
+ * columns back to back, each starting on a 256-byte boundary, then the status bytes
+ * (spec_packed_layout; what spec_amd.shard.PackedColumns lays out), so the gather to the root
+ * device is one grouped RCCL send/recv per device over xGMI.  String/bytes spans stay
+ * shard-relative (a 16M-record batch is > 4 GiB): the shard's byte base travels alongside.
+ * Every call replaces the per-record loop of decode.go:9-40 / internal/types/msg.go:43-55
+ * (decode) or internal/writer/writer.go:520-553 -> internal/encode/msg.go:15-77 (encode) over
+ * the shard, exactly as spec_decode_flat / spec_encode_flat do on one device.
  *   spec_packed_layout: column offsets / status offset of n records; returns the bytes;
  *   spec_shard_bounds: shard k's records [r0, r1) of n (sizes differ by at most one);
+ *   spec_shard_create_ex: flags SPEC_SHARD_FORCE_COMM = build the communicator even for one
+ *     device; the gather then moves every part, the root's own too, through RCCL;
+ *     SPEC_SHARD_SHARED = devices may repeat (several shards on one GPU, no communicator, the
+ *     gather is device copies): the multi-shard flow on a machine with fewer GPUs;
+ *   spec_shard_has_comm: 1 when the communicator exists; spec_shard_rccl_version: ncclGetVersion
+ *     of the RCCL in use (< 0 if none loads);
  *   spec_shard_decode: device i decodes its device-resident shard (streams[i], ends[i] relative
  *     to streams[i], ns[i] records) into packed[i] (on device i), asynchronously on its stream;
- *   spec_shard_decode_host: a host batch (pinned memory for overlap) split by spec_shard_bounds:
- *     each shard copied to its device (ends rebased there), then spec_shard_decode;
- *     byte_bases[i] (optional) = shard i's first byte in the batch;
+ *   spec_shard_decode_host: a host batch split by spec_shard_bounds; per device, on its own host
+ *     thread, the shard is copied in spec_shard_set_chunks record chunks (default 8; through
+ *     pinned staging slots when the batch is pageable) and every chunk decoded once it has
+ *     landed (ends rebased on the device); byte_bases[i] (optional) = shard i's first byte.
+ *     Returns once every copy is issued; a pinned batch must stay valid until spec_shard_sync;
  *   spec_shard_gather: every device's packed buffer (nbytes[i]) to `gathered` on device `root`,
  *     part i at the sum of the earlier parts' sizes, ordered after the decodes on each stream;
- *   spec_shard_stream: device k's stream; spec_shard_sync: wait for every device's stream. */
+ *   spec_shard_encode: device i encodes its ns[i] records from columns[i] (heaps[i], heap_lens[i]
+ *     as spec_encode_flat) into outs[i] (out_caps[i] bytes) with ends[i][r] = the record's end
+ *     in the WHOLE batch: every device's size and write passes (the write pass needs no base: a
+ *     record's bytes do not depend on its offset), one host wait for the size passes alone, the
+ *     exclusive scan of the shard totals (byte_bases, host) while the writes run, then each
+ *     shard's ends moved by its base.  totals[i] (host) = shard i's bytes (all-ones on an
+ *     encoder error).  outs[0..ndev) back to back (e.g. through spec_shard_gather with nbytes =
+ *     totals) are exactly one spec_encode_flat of the batch.  Each shard behaves as its own
+ *     spec_encode_flat: one whose total exceeds its capacity or errs writes nothing; the call
+ *     then returns SPEC_E_CAPACITY / SPEC_E_ENCODE and moves no ends to the whole batch (the
+ *     shards that fit hold shard-relative ends).  Asynchronous after the size passes;
+ *   spec_shard_stream: device k's stream; spec_shard_sync: wait for every device's streams. */
 #define SPEC_SHARD_MAX_DEVICES 16
+#define SPEC_SHARD_FORCE_COMM 1u
+#define SPEC_SHARD_SHARED 2u
 typedef struct spec_shard spec_shard;
 uint64_t spec_packed_layout(const spec_schema *schema, uint64_t n, uint64_t *col_offsets, uint64_t *status_offset);
 void spec_shard_bounds(uint64_t n, int nshards, int k, uint64_t *r0, uint64_t *r1);
 int spec_shard_create(const int *devices, int ndev, spec_shard **out);
+int spec_shard_create_ex(const int *devices, int ndev, uint32_t flags, spec_shard **out);
 void spec_shard_destroy(spec_shard *c);
 int spec_shard_ndev(const spec_shard *c);
+int spec_shard_has_comm(const spec_shard *c);
+int spec_shard_rccl_version(void);
+int spec_shard_set_chunks(spec_shard *c, uint32_t chunks);
 void *spec_shard_stream(const spec_shard *c, int k);
 int spec_shard_decode(spec_shard *c, const spec_schema *schema, const uint8_t *const *streams,
                       const uint64_t *stream_lens, const uint64_t *const *ends, const uint64_t *ns,
@@ -290,6 +328,10 @@ int spec_shard_decode(spec_shard *c, const spec_schema *schema, const uint8_t *c
 int spec_shard_decode_host(spec_shard *c, const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
                            const uint64_t *ends, uint64_t n, uint8_t *const *packed, uint64_t *byte_bases);
 int spec_shard_gather(spec_shard *c, const uint64_t *nbytes, uint8_t *const *packed, int root, uint8_t *gathered);
+int spec_shard_encode(spec_shard *c, const spec_schema *schema, const void *const *const *columns,
+                      const uint8_t *const *const *heaps, const uint64_t *const *heap_lens, const uint64_t *ns,
+                      uint8_t *const *outs, const uint64_t *out_caps, uint64_t *const *ends, uint64_t *totals,
+                      uint64_t *byte_bases);
 int spec_shard_sync(spec_shard *c);
 
 /* ---- introspection ---- */
@@ -420,6 +462,18 @@ int spec_host_decoder_chunk(const spec_host_decoder *d, uint64_t n, uint32_t k, 
                             uint64_t *col_offsets, uint64_t *status_offset);
 int spec_host_decoder_run(spec_host_decoder *d, const uint8_t *stream_host, uint64_t stream_len,
                           const uint64_t *ends_host, uint64_t n, uint8_t *out_host);
+
+/* The host pipeline on every device of a spec_shard at once (host batch in, host columns out,
+ * one host thread per device): spec_shard_host_prepare creates a spec_host_decoder per device
+ * (n_cap / stream_cap per SHARD); spec_shard_host_decode splits the batch by spec_shard_bounds
+ * and runs device i's decoder over shard i into out_host[i] (that decoder's chunk-major layout:
+ * spec_host_decoder_out_bytes / _chunk on spec_shard_host_decoder(c, i)), spans shard-relative,
+ * byte_bases[i] (optional) = shard i's first byte.  Synchronous. */
+int spec_shard_host_prepare(spec_shard *c, const spec_schema *schema, uint64_t n_cap, uint64_t stream_cap,
+                            uint32_t chunks);
+spec_host_decoder *spec_shard_host_decoder(const spec_shard *c, int k);
+int spec_shard_host_decode(spec_shard *c, const uint8_t *stream_host, uint64_t stream_len, const uint64_t *ends_host,
+                           uint64_t n, uint8_t *const *out_host, uint64_t *byte_bases);
 
 /* ---- recursive validation ----
  * spec_parse_messages: for every record, spec.ParseMessage (msg.go:29-32 ->

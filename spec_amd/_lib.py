@@ -170,7 +170,19 @@ def _declare(L):
                                          C.POINTER(C.c_uint64)]
     L.spec_shard_gather.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(vp), C.c_int, vp]
     L.spec_shard_sync.argtypes = [vp]
-    L.spec_tree_decoder_run.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.POINTER(vp), vp, vp]
+    L.spec_shard_create_ex.argtypes = [C.POINTER(C.c_int), C.c_int, C.c_uint32, C.POINTER(vp)]
+    L.spec_shard_has_comm.argtypes = [vp]
+    L.spec_shard_rccl_version.argtypes = []
+    L.spec_shard_set_chunks.argtypes = [vp, C.c_uint32]
+    L.spec_shard_encode.argtypes = [vp, C.POINTER(SpecSchema), C.POINTER(vp), C.POINTER(vp), C.POINTER(vp),
+                                    C.POINTER(C.c_uint64), C.POINTER(vp), C.POINTER(C.c_uint64), C.POINTER(vp),
+                                    C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    L.spec_shard_host_prepare.argtypes = [vp, C.POINTER(SpecSchema), C.c_uint64, C.c_uint64, C.c_uint32]
+    L.spec_shard_host_decoder.argtypes = [vp, C.c_int]
+    L.spec_shard_host_decoder.restype = vp
+    L.spec_shard_host_decode.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.POINTER(vp), C.POINTER(C.c_uint64)]
+    L.spec_tree_decoder_run.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64, C.POINTER(vp), vp, vp, vp]
+    L.spec_tree_decoder_capacity.argtypes = [vp, C.POINTER(C.c_uint64)]
     L.spec_tree_decoder_reserve.argtypes = [vp, C.POINTER(C.c_uint64)]
     L.spec_encode_nested_workspace_size_items.argtypes = [C.c_uint64, C.c_uint64]
     L.spec_encode_nested_workspace_size_items.restype = C.c_size_t

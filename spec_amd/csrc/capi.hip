@@ -113,6 +113,36 @@ namespace spec {
 void note_hip_error(hipError_t e) {
     if (e != hipSuccess) g_last_hip_error = (int)e;
 }
+
+int encode_flat_passes(const spec_schema *schema, const void *const *columns, const uint8_t *const *heaps,
+                       const uint64_t *heap_lens, uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *ends,
+                       uint64_t ends_base, void *workspace, size_t workspace_size, uint64_t *total, int passes,
+                       hipStream_t stream) {
+    int rc = check_schema(schema);
+    if (rc) return rc;
+    if (!columns || !workspace || (n && (!ends || !out))) return SPEC_E_INVALID_ARGUMENT;
+    if (workspace_size < spec_encode_flat_workspace_size(n)) return SPEC_E_WORKSPACE;
+    EncodeArgs a{};
+    fill_encode_args(a, schema, columns, n);
+    for (uint32_t f = 0; f < schema->nfields; f++) {
+        int k = schema->fields[f].kind;
+        if (k == SPEC_KIND_STRING || k == SPEC_KIND_BYTES) {
+            if (!heaps || !heap_lens || (!heaps[f] && heap_lens[f])) return SPEC_E_INVALID_ARGUMENT;
+            a.f.heaps[f] = heaps[f];
+            a.f.heap_lens[f] = heap_lens[f];
+        }
+    }
+    a.check_heaps = 1;
+    a.out = out;
+    a.out_cap = out_cap;
+    a.ends = ends;
+    a.ends_base = ends_base;
+    a.block_sums = (uint64_t *)workspace;
+    a.total = total;
+    if ((passes & ENC_PASS_SIZE) && launch_encode_size(schema, a, stream)) return hip_rc(hipGetLastError());
+    if ((passes & ENC_PASS_WRITE) && launch_encode_write(schema, a, stream)) return hip_rc(hipGetLastError());
+    return SPEC_OK;
+}
 } // namespace spec
 
 extern "C" {
@@ -132,6 +162,7 @@ const char *spec_strerror(int rc) {
     case SPEC_E_CAPACITY: return "output capacity too small";
     case SPEC_E_WORKSPACE: return "workspace too small";
     case SPEC_E_CORRUPT: return "corrupt LZ4 frame";
+    case SPEC_E_ENCODE: return "encoder error (a span outside its heap or a value > format.MaxSize)";
     }
     return "unknown error";
 }
@@ -488,29 +519,9 @@ int spec_encode_flat(const spec_schema *schema, const void *const *columns,
                      const uint8_t *const *heaps, const uint64_t *heap_lens, uint64_t n,
                      uint8_t *out, uint64_t out_cap, uint64_t *ends, void *workspace,
                      size_t workspace_size, uint64_t *total, void *stream) {
-    int rc = check_schema(schema);
-    if (rc) return rc;
-    if (!columns || !workspace || (n && (!ends || !out))) return SPEC_E_INVALID_ARGUMENT;
-    if (workspace_size < spec_encode_flat_workspace_size(n)) return SPEC_E_WORKSPACE;
-    spec::EncodeArgs a{};
-    fill_encode_args(a, schema, columns, n);
-    for (uint32_t f = 0; f < schema->nfields; f++) {
-        int k = schema->fields[f].kind;
-        if (k == SPEC_KIND_STRING || k == SPEC_KIND_BYTES) {
-            if (!heaps || !heap_lens || (!heaps[f] && heap_lens[f])) return SPEC_E_INVALID_ARGUMENT;
-            a.f.heaps[f] = heaps[f];
-            a.f.heap_lens[f] = heap_lens[f];
-        }
-    }
-    a.check_heaps = 1;
-    a.out = out;
-    a.out_cap = out_cap;
-    a.ends = ends;
-    a.block_sums = (uint64_t *)workspace;
-    a.total = total;
-    if (spec::launch_encode_size(schema, a, (hipStream_t)stream)) return hip_rc(hipGetLastError());
-    if (spec::launch_encode_write(schema, a, (hipStream_t)stream)) return hip_rc(hipGetLastError());
-    return SPEC_OK;
+    return spec::encode_flat_passes(schema, columns, heaps, heap_lens, n, out, out_cap, ends, 0, workspace,
+                                    workspace_size, total, spec::ENC_PASS_SIZE | spec::ENC_PASS_WRITE,
+                                    (hipStream_t)stream);
 }
 
 } // extern "C"

@@ -35,6 +35,7 @@ struct EncodeArgs {
     uint8_t *out;
     uint64_t out_cap;
     uint64_t *ends;
+    uint64_t ends_base;    // added to every end offset (a shard's first byte in the whole batch)
     uint64_t *block_sums;  // workspace: per-block encoded bytes, then exclusive offsets
     uint64_t nblocks;
     uint64_t *total;
@@ -1008,7 +1009,7 @@ __device__ __forceinline__ void encode_write_body(const EncodeArgs &a, uint8_t *
     uint64_t pre = a.block_sums[blockIdx.x];
     for (int w = 0; w < wave; w++) pre += wsum[w];
     const uint64_t start = pre + x - rs.total;
-    if (valid) a.ends[r] = start + rs.total;
+    if (valid) a.ends[r] = a.ends_base + start + rs.total;
 
     // wave output span [S, E)
     const uint64_t wbase = (uint64_t)blockIdx.x * ENC_BLOCK + wave * 64;

@@ -64,6 +64,18 @@ int hip_fail(hipError_t e) {
 
 } // namespace
 
+namespace spec {
+// shard.hip: ends[0, n) -= base on `stream`
+int launch_rebase_ends(uint64_t *ends, uint64_t n, uint64_t base, hipStream_t stream);
+
+// spec_host_decoder_run over a batch whose end offsets are all `ends_base` too large: a shard of
+// a larger host batch (stream_host = the shard's first byte, ends_host = the shard's ends as
+// they are in the whole batch).  The device copy of `ends` is rebased chunk by chunk after its
+// H2D, so spans come out shard-relative.  spec_shard_host_decode runs one per device.
+int host_decoder_run_based(spec_host_decoder *d, const uint8_t *stream_host, uint64_t stream_len,
+                           const uint64_t *ends_host, uint64_t n, uint64_t ends_base, uint8_t *out_host);
+} // namespace spec
+
 extern "C" {
 
 uint64_t spec_host_decoder_out_bytes(const spec_host_decoder *d, uint64_t n) {
@@ -150,10 +162,17 @@ int spec_host_decoder_create(const spec_schema *schema, uint64_t n_cap, uint64_t
 
 int spec_host_decoder_run(spec_host_decoder *d, const uint8_t *stream_host, uint64_t stream_len,
                           const uint64_t *ends_host, uint64_t n, uint8_t *out_host) {
+    return spec::host_decoder_run_based(d, stream_host, stream_len, ends_host, n, 0, out_host);
+}
+
+} // extern "C"
+
+int spec::host_decoder_run_based(spec_host_decoder *d, const uint8_t *stream_host, uint64_t stream_len,
+                                 const uint64_t *ends_host, uint64_t n, uint64_t ends_base, uint8_t *out_host) {
     if (!d || n > d->n_cap || stream_len > d->stream_cap) return SPEC_E_INVALID_ARGUMENT;
     if (n == 0) return SPEC_OK;
     if (!stream_host || !ends_host || !out_host) return SPEC_E_INVALID_ARGUMENT;
-    if (ends_host[n - 1] > stream_len) return SPEC_E_INVALID_ARGUMENT;
+    if (ends_host[n - 1] < ends_base || ends_host[n - 1] - ends_base > stream_len) return SPEC_E_INVALID_ARGUMENT;
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (prev != d->device) (void)hipSetDevice(d->device);
@@ -165,16 +184,24 @@ int spec_host_decoder_run(spec_host_decoder *d, const uint8_t *stream_host, uint
         uint64_t r0 = 0, r1 = 0;
         const uint64_t end = chunk_layout(d, n, k, &r0, &r1, col_off, &status_off);
         if (r1 > r0) {
-            const uint64_t b0 = r0 ? ends_host[r0 - 1] : 0, b1 = ends_host[r1 - 1];
-            if (b1 < b0) {
+            const uint64_t a0 = r0 ? ends_host[r0 - 1] : ends_base, a1 = ends_host[r1 - 1];
+            if (a1 < a0 || a0 < ends_base) {
                 rc = SPEC_E_INVALID_ARGUMENT;
                 break;
             }
+            const uint64_t b0 = a0 - ends_base, b1 = a1 - ends_base;
             if ((e = hipMemcpyAsync(d->d_ends + r0, ends_host + r0, (r1 - r0) * 8, hipMemcpyHostToDevice,
                                     d->s_in)) != hipSuccess ||
                 (b1 > b0 && (e = hipMemcpyAsync(d->d_stream + b0, stream_host + b0, b1 - b0, hipMemcpyHostToDevice,
-                                                d->s_in)) != hipSuccess) ||
-                (e = hipEventRecord(d->ev_in[k], d->s_in)) != hipSuccess ||
+                                                d->s_in)) != hipSuccess)) {
+                rc = hip_fail(e);
+                break;
+            }
+            if (ends_base && spec::launch_rebase_ends(d->d_ends + r0, r1 - r0, ends_base, d->s_in)) {
+                rc = SPEC_E_HIP;
+                break;
+            }
+            if ((e = hipEventRecord(d->ev_in[k], d->s_in)) != hipSuccess ||
                 (e = hipStreamWaitEvent(d->s_dec, d->ev_in[k], 0)) != hipSuccess) {
                 rc = hip_fail(e);
                 break;
@@ -202,5 +229,3 @@ int spec_host_decoder_run(spec_host_decoder *d, const uint8_t *stream_host, uint
     if (prev != d->device) (void)hipSetDevice(prev);
     return rc;
 }
-
-} // extern "C"

@@ -59,6 +59,14 @@ void jit_set_enabled(int on);
 long long jit_compile_only(const spec_schema *schema, double avg_record);
 long long jit_compile_only_encode(const spec_schema *schema);
 int launch_encode_size(const spec_schema *schema, const EncodeArgs &a, hipStream_t stream);
+// capi.hip: spec_encode_flat's passes (ENC_PASS_SIZE: sizes + scan into the workspace, heaps
+// checked; ENC_PASS_WRITE: the write pass over a workspace the size pass filled), every end
+// offset + ends_base (shard.hip: a shard's first byte in the whole batch).
+enum { ENC_PASS_SIZE = 1, ENC_PASS_WRITE = 2 };
+int encode_flat_passes(const spec_schema *schema, const void *const *columns, const uint8_t *const *heaps,
+                       const uint64_t *heap_lens, uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *ends,
+                       uint64_t ends_base, void *workspace, size_t workspace_size, uint64_t *total, int passes,
+                       hipStream_t stream);
 int launch_encode_write(const spec_schema *schema, const EncodeArgs &a, hipStream_t stream);
 // jit.cpp: schema-specialised encode pass 1 (write=false) or 3; 1 launched, 0 use the
 // precompiled kernel, <0 HIP error.

@@ -204,14 +204,18 @@ __global__ __launch_bounds__(256) void values_kernel(const uint8_t *stream, uint
     }
 }
 
-// rows_out[t] = rows of table t, or ~0 where a list table overflowed its capacity
+// rows_out[t] = rows of table t, or ~0 where its group or any group above it (the list tables
+// it hangs under) overflowed the capacity: a table under a truncated list is incomplete too
 __global__ void rows_out_kernel(const TreeDesc *Dp, const TreeBufs *Bp, uint64_t *out) {
     const TreeDesc &D = *Dp;
     const TreeBufs &B = *Bp;
     const uint32_t t = threadIdx.x;
     if (t >= D.ntables) return;
     const uint32_t g = D.t[t].groot;
-    out[t] = g == 0 ? B.n : (B.rowsd[g] > B.caps[g] ? ~0ull : B.rowsd[g]);
+    bool ovf = false;
+    for (uint32_t x = g; x != 0; x = D.t[D.t[x].parent].groot) // x: a list group root
+        ovf = ovf || B.rowsd[x] > B.caps[x];
+    out[t] = g == 0 ? B.n : (ovf ? ~0ull : B.rowsd[g]);
 }
 
 } // namespace
@@ -330,8 +334,11 @@ int upload(spec_tree_decoder *d, hipStream_t st) {
 }
 
 // The whole decode of a batch, asynchronous on st: every group's kernel, then its lists' scans.
+// col_rows (optional, host, per table): rows the caller's columns hold; every group's rows are
+// clamped to them (its tables' columns, and the BEGIN columns of the lists it owns: owner rows +
+// 1 entries), so nothing is written past a column; a clamped list reports ~0 in rows_out.
 int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, const uint64_t *ends,
-        const uint2 *spans, uint64_t n, void *const *columns, hipStream_t st) {
+        const uint2 *spans, uint64_t n, void *const *columns, const uint64_t *col_rows, hipStream_t st) {
     if (stream_len >= (1ull << 32)) return SPEC_E_TOO_LARGE;
     if (n && (!stream_bytes || (!ends && !spans))) return SPEC_E_INVALID_ARGUMENT;
     Layout &L = d->L;
@@ -339,6 +346,18 @@ int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, 
     const TreeDesc &D = L.desc;
     int rc = prepare(d, n);
     if (rc) return rc;
+    if (col_rows) {
+        for (uint32_t x = 0; x < L.nt; x++) {
+            const uint32_t g = D.t[x].groot;
+            if (g == 0) {
+                if (col_rows[x] < n) return SPEC_E_CAPACITY; // a row per record: no clamp possible
+            } else {
+                B.caps[g] = std::min(B.caps[g], col_rows[x]);
+            }
+        }
+        for (uint32_t x = 1; x < L.nt; x++) B.caps[x] = B.caps[D.t[x].groot == 0 ? 0 : D.t[x].groot];
+        B.caps[0] = n;
+    }
     B.stream = stream_bytes;
     B.stream_len = stream_len;
     B.ends = ends;
@@ -353,9 +372,11 @@ int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, 
     }
     if ((rc = upload(d, st))) return rc;
     if (hipMemsetAsync(B.ovf, 0, sizeof(uint32_t), st) != hipSuccess) return SPEC_E_HIP;
-    if (n == 0) {
-        if (hipMemsetAsync(B.rowsd, 0, TREE_MAX_T * sizeof(uint64_t), st) != hipSuccess) return SPEC_E_HIP;
-    }
+    // a group with no capacity yet is skipped, and with it the scans of the lists it owns: their
+    // row counts must read 0, not a previous batch's (and n == 0 skips every scan)
+    bool skipped = n == 0;
+    for (uint32_t x = 1; x < L.nt; x++) skipped = skipped || (D.t[x].groot == x && d->caps[x] == 0);
+    if (skipped && hipMemsetAsync(B.rowsd, 0, TREE_MAX_T * sizeof(uint64_t), st) != hipSuccess) return SPEC_E_HIP;
     if (!d->jit_looked) { // compiled (or read from the code-object cache) on first use
         d->jit = jit_tree_kernels(D);
         d->jit_looked = true;
@@ -420,8 +441,10 @@ int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, 
 int index(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, const uint64_t *ends,
           const uint2 *spans, uint64_t n, uint64_t *rows, hipStream_t st) {
     Layout &L = d->L;
-    for (int attempt = 0; attempt < 8; attempt++) {
-        int rc = run(d, stream_bytes, stream_len, ends, spans, n, nullptr, st);
+    // an inner list's count is exact only once its owner list fits: at most one growth per level
+    // of list nesting (bounded by the table count)
+    for (uint32_t attempt = 0; attempt <= L.nt; attempt++) {
+        int rc = run(d, stream_bytes, stream_len, ends, spans, n, nullptr, nullptr, st);
         if (rc) return rc;
         uint64_t got[TREE_MAX_T];
         if (hipMemcpyAsync(got, d->B.rowsd, sizeof(uint64_t) * TREE_MAX_T, hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -446,7 +469,7 @@ int index(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len
         d->indexed = true;
         return SPEC_OK;
     }
-    return SPEC_E_HIP;
+    return SPEC_E_TOO_LARGE; // the capacities did not settle (cannot happen for a finite tree)
 }
 
 } // namespace
@@ -467,7 +490,8 @@ int spec_tree_decoder_create(const spec_tree *tree, spec_tree_decoder **out) {
     bool ok = hipGetDevice(&d->device) == hipSuccess && !d->desc.reserve(sizeof(TreeDesc)) &&
               !d->bufs.reserve(sizeof(TreeBufs)) && !d->misc.reserve(TREE_MAX_T * sizeof(uint64_t) + 256) &&
               hipHostMalloc((void **)&d->pinned, 4 * sizeof(TreeBufs), hipHostMallocDefault) == hipSuccess &&
-              hipMemcpy(d->desc.p, &d->L.desc, sizeof(TreeDesc), hipMemcpyHostToDevice) == hipSuccess;
+              hipMemcpy(d->desc.p, &d->L.desc, sizeof(TreeDesc), hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemset(d->misc.p, 0, TREE_MAX_T * sizeof(uint64_t) + 256) == hipSuccess;
     for (hipEvent_t &e : d->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         note_hip_error(hipGetLastError());
@@ -495,17 +519,27 @@ int spec_tree_decoder_index_spans(spec_tree_decoder *d, const uint8_t *stream_by
 int spec_tree_decoder_decode(spec_tree_decoder *d, void *const *columns, void *stream) {
     if (!d || !d->indexed || !columns) return SPEC_E_INVALID_ARGUMENT;
     const TreeBufs &B = d->B;
-    return run(d, B.stream, B.stream_len, B.ends, B.spans, B.n, columns, (hipStream_t)stream);
+    return run(d, B.stream, B.stream_len, B.ends, B.spans, B.n, columns, nullptr, (hipStream_t)stream);
 }
 
 int spec_tree_decoder_run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, const uint64_t *ends,
-                          uint64_t n, void *const *columns, uint64_t *rows_out, void *stream) {
+                          uint64_t n, void *const *columns, const uint64_t *col_rows, uint64_t *rows_out,
+                          void *stream) {
     if (!d || !columns) return SPEC_E_INVALID_ARGUMENT;
-    const int rc = run(d, stream_bytes, stream_len, ends, nullptr, n, columns, (hipStream_t)stream);
+    const int rc = run(d, stream_bytes, stream_len, ends, nullptr, n, columns, col_rows, (hipStream_t)stream);
     if (rc || !rows_out) return rc;
     hipLaunchKernelGGL(rows_out_kernel, dim3(1), dim3(TREE_MAX_T), 0, (hipStream_t)stream,
                        (const TreeDesc *)d->desc.p, (const TreeBufs *)d->bufs.p, rows_out);
     return hipGetLastError() == hipSuccess ? SPEC_OK : SPEC_E_HIP;
+}
+
+int spec_tree_decoder_capacity(const spec_tree_decoder *d, uint64_t *rows) {
+    if (!d || !rows) return SPEC_E_INVALID_ARGUMENT;
+    for (uint32_t x = 0; x < d->L.nt; x++) {
+        const uint32_t g = d->L.desc.t[x].groot;
+        rows[x] = g == 0 ? 0 : d->caps[g];
+    }
+    return SPEC_OK;
 }
 
 int spec_tree_decoder_reserve(spec_tree_decoder *d, const uint64_t *rows) {

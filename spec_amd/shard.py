@@ -132,61 +132,231 @@ class NativeShard:
     """One process driving several devices through the C ABI (include/spec_amd.h spec_shard_*):
     a stream and an RCCL communicator per device, shards decoded into packed buffers
     (PackedColumns' layout, spec_packed_layout), one grouped RCCL send/recv gather to a root
-    device.  What a cgo caller of INTEGRATION.md drives, without torch.distributed."""
+    device, sharded encode with one host scan of the shard totals, and the pinned host pipeline
+    on every device at once.  What a cgo caller of INTEGRATION.md drives, without
+    torch.distributed.
 
-    def __init__(self, devices):
+    `force_comm` builds the RCCL communicator even for one device (SPEC_SHARD_FORCE_COMM): the
+    gather then moves every part through ncclSend/ncclRecv, the root's own as a send to itself.
+    `shared` lets devices repeat (SPEC_SHARD_SHARED: several shards per GPU, no communicator),
+    so the N-shard flow runs on a one-GPU box.
+
+    The shard's work runs on its own per-device streams.  Every call below first makes each shard
+    stream wait for the device's current torch stream (inputs torch just produced are complete),
+    and afterwards makes the current torch stream wait for the shard stream, so torch code after
+    the call sees finished data; the tensors a call touched are referenced until sync() (or the
+    object's end, which synchronises first), so the caching allocator cannot hand their memory
+    out while the shard still reads or writes it.  (No record_stream: the shard's streams may
+    end before the tensors do.)"""
+
+    def __init__(self, devices, force_comm: bool = False, shared: bool = False):
         from . import _lib
 
         self._lib = _lib
         self.devices = list(devices)
         arr = (C.c_int * len(self.devices))(*self.devices)
         self._h = C.c_void_p()
-        _lib.check(_lib.lib().spec_shard_create(arr, len(self.devices), C.byref(self._h)), "spec_shard_create")
+        flags = (1 if force_comm else 0) | (2 if shared else 0)  # SPEC_SHARD_FORCE_COMM, SPEC_SHARD_SHARED
+        _lib.check(_lib.lib().spec_shard_create_ex(arr, len(self.devices), flags, C.byref(self._h)),
+                   "spec_shard_create_ex")
+        self._ext = [torch.cuda.ExternalStream(self._lib.lib().spec_shard_stream(self._h, k),
+                                               device=torch.device("cuda", d))
+                     for k, d in enumerate(self.devices)]
+        self._inflight = []
+        self._host = None  # (schema, per-device host decoders) after host_prepare
 
     def __del__(self):
         h, self._h = getattr(self, "_h", None), None
         if h and h.value:
             try:
-                self._lib.lib().spec_shard_destroy(h)
+                self._lib.lib().spec_shard_destroy(h)  # drains every stream first
             except Exception:
                 pass
+        self._inflight = []
 
     @property
     def ndev(self) -> int:
         return len(self.devices)
+
+    @property
+    def has_comm(self) -> bool:
+        return bool(self._lib.lib().spec_shard_has_comm(self._h))
+
+    @staticmethod
+    def rccl_version() -> int:
+        from . import _lib
+
+        return int(_lib.lib().spec_shard_rccl_version())
+
+    def stream(self, k: int) -> torch.cuda.ExternalStream:
+        return self._ext[k]
+
+    def set_chunks(self, chunks: int):
+        self._lib.check(self._lib.lib().spec_shard_set_chunks(self._h, chunks), "spec_shard_set_chunks")
 
     def bounds(self, n: int, k: int):
         r0, r1 = C.c_uint64(), C.c_uint64()
         self._lib.lib().spec_shard_bounds(n, self.ndev, k, C.byref(r0), C.byref(r1))
         return r0.value, r1.value
 
-    def decode_host(self, schema: Schema, stream: np.ndarray, ends: np.ndarray):
-        """Split a host batch over the devices, decode each shard on its device: -> (packed
-        buffers [PackedColumns per device], byte bases)."""
-        stream = np.ascontiguousarray(stream, dtype=np.uint8)
-        ends = np.ascontiguousarray(ends, dtype=np.uint64)
-        n = len(ends)
-        packs = []
+    def _enter(self):
+        """Order every shard stream after its device's current torch stream."""
         for k, d in enumerate(self.devices):
-            r0, r1 = self.bounds(n, k)
-            packs.append(PackedColumns(schema, r1 - r0, torch.device("cuda", d)))
+            self._ext[k].wait_stream(torch.cuda.current_stream(torch.device("cuda", d)))
+
+    def _join(self, tensors_per_dev):
+        """Order torch's current stream of every device after the shard streams; keep the
+        tensors referenced until sync()."""
+        for k, d in enumerate(self.devices):
+            torch.cuda.current_stream(torch.device("cuda", d)).wait_stream(self._ext[k])
+        self._inflight.append(tensors_per_dev)
+
+    def decode_host(self, schema: Schema, stream: np.ndarray | torch.Tensor, ends: np.ndarray | torch.Tensor,
+                    packs=None):
+        """Split a host batch over the devices, decode each shard on its device: -> (packed
+        buffers [PackedColumns per device], byte bases).  `stream`/`ends` may be numpy arrays or
+        (pinned) CPU tensors; they are kept alive until sync()."""
+        if isinstance(stream, torch.Tensor):
+            sp, slen = stream.data_ptr(), stream.numel()
+        else:
+            stream = np.ascontiguousarray(stream, dtype=np.uint8)
+            sp, slen = stream.ctypes.data, stream.size
+        if isinstance(ends, torch.Tensor):
+            ep, n = ends.data_ptr(), ends.numel()
+        else:
+            ends = np.ascontiguousarray(ends, dtype=np.uint64)
+            ep, n = ends.ctypes.data, len(ends)
+        if packs is None:
+            packs = []
+            for k, d in enumerate(self.devices):
+                r0, r1 = self.bounds(n, k)
+                packs.append(PackedColumns(schema, r1 - r0, torch.device("cuda", d)))
         ptrs = (C.c_void_p * self.ndev)(*[p.buf.data_ptr() for p in packs])
         bases = (C.c_uint64 * self.ndev)()
-        rc = self._lib.lib().spec_shard_decode_host(self._h, C.byref(schema.c), stream.ctypes.data, stream.size,
-                                                    ends.ctypes.data, n, ptrs, bases)
+        self._enter()
+        rc = self._lib.lib().spec_shard_decode_host(self._h, C.byref(schema.c), sp, slen, ep, n, ptrs, bases)
         self._lib.check(rc, "spec_shard_decode_host")
-        self._keep = (stream, ends)
+        self._join([[p.buf] for p in packs])
+        self._inflight.append((stream, ends))
         return packs, list(bases)
 
-    def gather(self, packs, root: int = 0) -> torch.Tensor:
-        """Every device's packed buffer to one buffer on device `root` (parts back to back)."""
-        sizes = [p.nbytes for p in packs]
-        out = torch.empty(max(sum(sizes), 1), dtype=torch.uint8, device=torch.device("cuda", self.devices[root]))
-        ptrs = (C.c_void_p * self.ndev)(*[p.buf.data_ptr() for p in packs])
+    def decode(self, schema: Schema, streams, ends, packs):
+        """Device-resident shards: device k decodes (streams[k], ends[k]) (ends relative to its
+        stream) into packs[k] (PackedColumns on device k)."""
+        k_ = self.ndev
+        sp = (C.c_void_p * k_)(*[s.data_ptr() for s in streams])
+        lens = (C.c_uint64 * k_)(*[s.numel() for s in streams])
+        ep = (C.c_void_p * k_)(*[e.data_ptr() for e in ends])
+        ns = (C.c_uint64 * k_)(*[e.numel() for e in ends])
+        pp = (C.c_void_p * k_)(*[p.buf.data_ptr() for p in packs])
+        self._enter()
+        self._lib.check(self._lib.lib().spec_shard_decode(self._h, C.byref(schema.c), sp, lens, ep, ns, pp),
+                        "spec_shard_decode")
+        self._join([[s, e, p.buf] for s, e, p in zip(streams, ends, packs)])
+
+    def gather(self, packs, root: int = 0, out: torch.Tensor | None = None, sizes=None) -> torch.Tensor:
+        """Every device's packed buffer (or any uint8 device buffers, `sizes` bytes each) to one
+        buffer on device `root` (parts back to back)."""
+        bufs = [p.buf if isinstance(p, PackedColumns) else p for p in packs]
+        if sizes is None:
+            sizes = [p.nbytes if isinstance(p, PackedColumns) else p.numel() for p in packs]
+        if out is None:
+            out = torch.empty(max(sum(sizes), 1), dtype=torch.uint8, device=torch.device("cuda", self.devices[root]))
+        ptrs = (C.c_void_p * self.ndev)(*[b.data_ptr() for b in bufs])
         nb = (C.c_uint64 * self.ndev)(*sizes)
+        self._enter()
         self._lib.check(self._lib.lib().spec_shard_gather(self._h, nb, ptrs, root, C.c_void_p(out.data_ptr())),
                         "spec_shard_gather")
+        self._join([list(bufs[k:k + 1]) + ([out] if k == root else []) for k in range(self.ndev)])
         return out
+
+    def encode(self, schema: Schema, shards, outs=None, ends=None):
+        """Sharded encode: shards[k] = (columns, heaps, n) on device k (as spec_amd.encode_flat
+        takes them).  -> (outs, ends, totals, byte_bases): device k's bytes outs[k][:totals[k]]
+        and ends[k] = its records' ends in the WHOLE batch; the outs back to back are exactly
+        one encode of the batch.  Without `outs`, the totals are found first (a call with no
+        capacity) and the buffers allocated."""
+        k_ = self.ndev
+        if len(shards) != k_:
+            raise ValueError("one shard per device")
+        nf = max(1, len(schema))
+        cols, hp, hl = [], [], []
+        for k, (cs, heaps, n) in enumerate(shards):
+            if len(cs) != len(schema):
+                raise ValueError("one column per schema field")
+            for f, c in enumerate(cs):
+                if not c.is_cuda or c.device.index != self.devices[k]:
+                    raise ValueError(f"shard {k} column {f} is not on device {self.devices[k]}")
+                if c.numel() * c.element_size() < int(n) * schema.fields[f].width:
+                    raise ValueError(f"shard {k} column {f} too small")
+            cols.append((C.c_void_p * nf)(*[c.data_ptr() for c in cs]))
+            h, l_ = (C.c_void_p * nf)(), (C.c_uint64 * nf)()
+            for f, fld in enumerate(schema.fields):
+                if f in (heaps or {}):
+                    h[f], l_[f] = heaps[f].data_ptr(), heaps[f].numel()
+            hp.append(h)
+            hl.append(l_)
+        ns = (C.c_uint64 * k_)(*[int(s[2]) for s in shards])
+        colsp = (C.c_void_p * k_)(*[C.cast(c, C.c_void_p) for c in cols])
+        hpp = (C.c_void_p * k_)(*[C.cast(h, C.c_void_p) for h in hp])
+        hlp = (C.c_void_p * k_)(*[C.cast(h, C.c_void_p) for h in hl])
+        totals = (C.c_uint64 * k_)()
+        bases = (C.c_uint64 * k_)()
+        devs = [torch.device("cuda", d) for d in self.devices]
+        if ends is None:
+            ends = [torch.empty(max(int(s[2]), 1), dtype=torch.int64, device=dv) for s, dv in zip(shards, devs)]
+        L = self._lib.lib()
+
+        def call(bufs, caps):
+            op = (C.c_void_p * k_)(*[b.data_ptr() for b in bufs])
+            cp = (C.c_uint64 * k_)(*caps)
+            ep = (C.c_void_p * k_)(*[e.data_ptr() for e in ends])
+            return L.spec_shard_encode(self._h, C.byref(schema.c), colsp, hpp, hlp, ns, op, cp, ep, totals, bases)
+
+        self._enter()
+        if outs is None:
+            probe = [torch.empty(1, dtype=torch.uint8, device=dv) for dv in devs]
+            rc = call(probe, [0] * k_)
+            if rc not in (0, -4):  # SPEC_E_CAPACITY: the totals are known
+                self._lib.check(rc, "spec_shard_encode")
+            outs = [torch.empty(max(int(t), 1), dtype=torch.uint8, device=dv) for t, dv in zip(totals, devs)]
+        self._lib.check(call(outs, [o.numel() for o in outs]), "spec_shard_encode")
+        keep = [list(s[0]) + list(s[1].values()) if isinstance(s[1], dict) else list(s[0]) for s in shards]
+        self._join([[o, e] + [t for t in kk if isinstance(t, torch.Tensor)] for o, e, kk in zip(outs, ends, keep)])
+        self._inflight.append((cols, hp, hl))
+        return outs, ends, list(totals), list(bases)
+
+    def host_prepare(self, schema: Schema, shard_records: int, shard_bytes: int, chunks: int = 8):
+        """A spec_host_decoder per device for shards of up to shard_records / shard_bytes."""
+        self._lib.check(self._lib.lib().spec_shard_host_prepare(self._h, C.byref(schema.c), shard_records,
+                                                                shard_bytes, chunks), "spec_shard_host_prepare")
+        self._host = schema
+
+    def host_out_bytes(self, k: int, n: int) -> int:
+        L = self._lib.lib()
+        return int(L.spec_host_decoder_out_bytes(L.spec_shard_host_decoder(self._h, k), n))
+
+    def host_chunk(self, k: int, n: int, j: int):
+        """Chunk j of device k's host output for an n-record shard: (r0, r1, column offsets, status offset)."""
+        L = self._lib.lib()
+        nf = len(self._host)
+        r0, r1, so = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        co = (C.c_uint64 * nf)()
+        self._lib.check(L.spec_host_decoder_chunk(L.spec_shard_host_decoder(self._h, k), n, j, C.byref(r0),
+                                                  C.byref(r1), co, C.byref(so)), "spec_host_decoder_chunk")
+        return r0.value, r1.value, list(co), so.value
+
+    def host_decode(self, stream: torch.Tensor, ends: torch.Tensor, outs):
+        """Pinned host batch -> every device's host output buffer (outs[k], pinned uint8 tensors
+        of host_out_bytes(k, n_k)), all devices at once.  Synchronous.  -> byte bases."""
+        n = ends.numel()
+        op = (C.c_void_p * self.ndev)(*[o.data_ptr() for o in outs])
+        bases = (C.c_uint64 * self.ndev)()
+        self._lib.check(self._lib.lib().spec_shard_host_decode(self._h, stream.data_ptr(), stream.numel(),
+                                                               ends.data_ptr(), n, op, bases),
+                        "spec_shard_host_decode")
+        return list(bases)
 
     def sync(self):
         self._lib.check(self._lib.lib().spec_shard_sync(self._h), "spec_shard_sync")
+        self._inflight = []

@@ -307,11 +307,32 @@ class TreeDecoder:
         return [torch.empty((max(self.tree.column_rows(c, self.rows), 1), c.width), dtype=torch.uint8, device=device)
                 for c in self.tree.columns]
 
+    def column_capacity(self, cols: list) -> list:
+        """Rows each table's columns hold (the smallest of its columns; a BEGIN column of n + 1
+        entries holds n rows of the owner table); None entries do not limit."""
+        cap = [None] * len(self.tree.tables)
+        for c, tc in zip(cols, self.tree.columns):
+            if c is None:
+                continue
+            entries = c.numel() * c.element_size() // tc.width
+            t, k = (self.tree.tables[tc.table].parent, entries - 1) if tc.role == ROLE_BEGIN else (tc.table, entries)
+            cap[t] = k if cap[t] is None else min(cap[t], k)
+        return [(1 << 64) - 1 if k is None else max(k, 0) for k in cap]
+
+    def capacity(self) -> list:
+        """The decoder's list-table row capacities (spec_tree_decoder_capacity)."""
+        r = (C.c_uint64 * len(self.tree.tables))()
+        _lib.check(_lib.lib().spec_tree_decoder_capacity(self._h, r), "spec_tree_decoder_capacity")
+        return [int(x) for x in r]
+
     def run(self, stream: torch.Tensor, ends: torch.Tensor, cols: list, rows_out: torch.Tensor | None = None,
-            cuda_stream=None) -> torch.Tensor:
+            cuda_stream=None, col_rows=None) -> torch.Tensor:
         """Decode a new batch into `cols` in one asynchronous pass (spec_tree_decoder_run): no
         host synchronisation; returns the device row counts (int64 [ntables], -1 where a list
-        table outgrew the decoder's capacity: index() a batch of that shape first)."""
+        table outgrew the decoder's capacity or its columns, and below such a list: index() a
+        batch of that shape first).  Rows are clamped to what `cols` hold: nothing is written
+        past a column (`col_rows`: column_capacity(cols), precomputed by a caller that runs
+        the same columns repeatedly)."""
         if not (stream.is_cuda and ends.is_cuda and stream.dtype == torch.uint8 and ends.dtype == torch.int64):
             raise ValueError("stream uint8 and ends int64 device tensors")
         if len(cols) != len(self.tree.columns):
@@ -320,8 +341,9 @@ class TreeDecoder:
             rows_out = torch.empty(len(self.tree.tables), dtype=torch.int64, device=stream.device)
         self._keep = (stream, ends)
         ptrs = (C.c_void_p * len(cols))(*[c.data_ptr() if c is not None else 0 for c in cols])
+        caps = (C.c_uint64 * len(self.tree.tables))(*(col_rows if col_rows is not None else self.column_capacity(cols)))
         rc = _lib.lib().spec_tree_decoder_run(self._h, C.c_void_p(stream.data_ptr()), stream.numel(),
-                                               C.c_void_p(ends.data_ptr()), ends.numel(), ptrs,
+                                               C.c_void_p(ends.data_ptr()), ends.numel(), ptrs, caps,
                                                C.c_void_p(rows_out.data_ptr()), _stream_handle(cuda_stream))
         _lib.check(rc, "spec_tree_decoder_run")
         return rows_out

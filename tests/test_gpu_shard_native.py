@@ -1,9 +1,15 @@
 """The native multi-device path (include/spec_amd.h spec_shard_*, spec_amd.shard.NativeShard):
-one process, one stream + RCCL communicator per visible device, a host batch split into
-contiguous shards, every shard decoded on its device into a packed buffer, one gather to the
-root device — against the oracle's decode of the whole batch (spans rebased by the shards'
-byte bases).  On a one-GPU box the flow runs with one device (the gather is the root's own
-copy); with more devices the gather goes through RCCL send/recv."""
+one process, one stream + RCCL communicator per device.  Against the oracle:
+  * decode: a host batch split into contiguous shards, every shard decoded on its device into a
+    packed buffer (chunked copies, pinned or pageable sources), one gather to the root device —
+    the oracle's decode of the whole batch, spans rebased by the shards' byte bases;
+  * the gather through RCCL: with force_comm the communicator exists on a one-GPU box and every
+    part (the root's own) goes through ncclSend/ncclRecv;
+  * encode: the shards' bytes back to back == the oracle Writer's bytes for the whole batch, ends
+    global (internal/writer/writer.go:520-553 -> internal/encode/msg.go:15-77 per record);
+  * the host pipeline on every device at once.
+`shared=True` puts several shards on one GPU (SPEC_SHARD_SHARED), so the N-shard code paths
+(threads, bases, cross-stream ordering of the gather) run on a one-GPU box."""
 from __future__ import annotations
 
 import numpy as np
@@ -11,26 +17,24 @@ import pytest
 import torch
 
 from oracle import oracle as O
-from spec_amd import FLAT16, workload
+from spec_amd import FLAT16, SpecError, workload
 from spec_amd.shard import NativeShard, PackedColumns
 from tests.test_shard_gloo import rebase_spans
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n", [1, 4099, 300_001])
-def test_native_shard_decode_gather(dev, n):
+def _devices(shared_shards: int):
     ndev = torch.cuda.device_count()
-    sh = NativeShard(list(range(ndev)))
-    cols, heaps = workload.flat16(n, seed=n % 97)
-    stream, ends = O.encode_flat_batch(FLAT16.tags, FLAT16.kinds, cols, [heaps.get(f) for f in range(16)], n)
-    packs, bases = sh.decode_host(FLAT16, stream, ends)
-    gathered = sh.gather(packs, root=0)
-    sh.sync()
-    want, wst = O.decode_flat_batch(FLAT16.tags, FLAT16.kinds, stream, ends, FLAT16.widths, 8)
+    if shared_shards:
+        return [k % ndev for k in range(shared_shards)], True
+    return list(range(ndev)), False
+
+
+def _check_gathered(sh, gathered, n, ends, bases, want, wst):
     g = gathered.cpu()
     views, off = [], 0
-    for k in range(ndev):
+    for k in range(sh.ndev):
         r0, r1 = sh.bounds(n, k)
         nb = PackedColumns.nbytes_for(FLAT16, r1 - r0)
         views.append(PackedColumns(FLAT16, r1 - r0, "cpu", buf=g[off: off + nb]))
@@ -42,8 +46,207 @@ def test_native_shard_decode_gather(dev, n):
     assert np.array_equal(np.concatenate([v.status.numpy() for v in views]), wst)
 
 
-def test_native_shard_rejects_duplicate_devices():
-    from spec_amd import SpecError
+@pytest.mark.parametrize("mode", ["plain", "force_comm", "shared3"])
+@pytest.mark.parametrize("n", [1, 4099, 300_001])
+def test_native_shard_decode_gather(dev, n, mode):
+    if mode == "shared3":
+        devs, shared = _devices(3)
+        sh = NativeShard(devs, shared=True)
+    else:
+        devs, _ = _devices(0)
+        sh = NativeShard(devs, force_comm=mode == "force_comm")
+        assert sh.has_comm == (mode == "force_comm" or len(devs) > 1)
+    cols, heaps = workload.flat16(n, seed=n % 97)
+    stream, ends = O.encode_flat_batch(FLAT16.tags, FLAT16.kinds, cols, [heaps.get(f) for f in range(16)], n)
+    packs, bases = sh.decode_host(FLAT16, stream, ends)
+    gathered = sh.gather(packs, root=0)
+    sh.sync()
+    want, wst = O.decode_flat_batch(FLAT16.tags, FLAT16.kinds, stream, ends, FLAT16.widths, 8)
+    _check_gathered(sh, gathered, n, ends, bases, want, wst)
 
+
+@pytest.mark.parametrize("chunks", [1, 3, 64])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_native_shard_decode_host_chunks(dev, chunks, pinned):
+    """Chunked host->device copies: pageable sources go through the pinned staging slots,
+    pinned ones are copied directly; every chunk's decode ordered after its copy."""
+    n = 70_001
+    devs, _ = _devices(2)
+    sh = NativeShard(devs, shared=True)
+    sh.set_chunks(chunks)
+    cols, heaps = workload.flat16(n, seed=chunks)
+    stream, ends = O.encode_flat_batch(FLAT16.tags, FLAT16.kinds, cols, [heaps.get(f) for f in range(16)], n)
+    s_in, e_in = stream, ends
+    if pinned:
+        s_in = torch.from_numpy(stream).pin_memory()
+        e_in = torch.from_numpy(ends.view(np.int64)).pin_memory()
+    want, wst = O.decode_flat_batch(FLAT16.tags, FLAT16.kinds, stream, ends, FLAT16.widths, 8)
+    for _ in range(2):  # the second call reuses the staging and device buffers
+        packs, bases = sh.decode_host(FLAT16, s_in, e_in)
+        gathered = sh.gather(packs, root=1)
+        sh.sync()
+        _check_gathered(sh, gathered, n, ends, bases, want, wst)
+
+
+def test_native_shard_rccl_gather_is_rccl(dev):
+    """The communicator exists on one GPU with force_comm; the gather (a send to itself through
+    RCCL) moves arbitrary buffers byte for byte, zero-size parts included."""
+    sh = NativeShard([0], force_comm=True)
+    assert sh.has_comm and NativeShard.rccl_version() > 0
+    g = torch.Generator().manual_seed(3)
+    for size in (0, 1, 255, 1 << 20, (1 << 26) + 7):
+        src = torch.randint(0, 256, (max(size, 1),), dtype=torch.uint8, generator=g).to(dev)
+        out = sh.gather([src], sizes=[size])
+        sh.sync()
+        assert torch.equal(out[:size].cpu(), src[:size].cpu())
+
+
+def _device_shards(sh, nshard, seed0, nrec):
+    """Per shard k: Flat16 columns seeded seed0 + k on shard k's device -> (shards, host cols, heaps)."""
+    shards, host = [], []
+    for k in range(nshard):
+        cols, heaps = workload.flat16(nrec[k], seed0 + k)
+        d = torch.device("cuda", sh.devices[k])
+        shards.append(([torch.from_numpy(c).to(d) for c in cols], {f: torch.from_numpy(h).to(d) for f, h in heaps.items()},
+                       nrec[k]))
+        host.append((cols, heaps))
+    return shards, host
+
+
+def _check_encode(sh, shards, host, outs, ends, totals, bases):
+    off = 0
+    for k, (cols, heaps) in enumerate(host):
+        n = shards[k][2]
+        want, wends = O.encode_flat_batch(FLAT16.tags, FLAT16.kinds, cols, [heaps.get(f) for f in range(16)], n)
+        assert totals[k] == want.size and bases[k] == off
+        assert np.array_equal(outs[k][: totals[k]].cpu().numpy(), want)
+        assert np.array_equal(ends[k][:n].cpu().numpy(), wends.view(np.int64) + off)
+        off += want.size
+
+
+@pytest.mark.parametrize("nshard,n", [(1, 1_048_576), (4, 1_048_576), (5, 1), (3, 0), (4, 4099)])
+def test_native_shard_encode(dev, nshard, n):
+    """Sharded encode: every shard's bytes == the oracle Writer's bytes for its records, the
+    shard bases = the exclusive scan of the earlier shards' totals, ends global; the shards
+    gathered back to back == one batch (the oracle's bytes of all records in order)."""
+    devs, _ = _devices(nshard)
+    sh = NativeShard(devs, shared=True)
+    nrec = [sh.bounds(n, k)[1] - sh.bounds(n, k)[0] for k in range(nshard)]
+    shards, host = _device_shards(sh, nshard, 11, nrec)
+    outs, ends, totals, bases = sh.encode(FLAT16, shards)
+    whole = sh.gather(outs, root=0, sizes=totals)
+    sh.sync()
+    _check_encode(sh, shards, host, outs, ends, totals, bases)
+    # the gathered stream decodes to the shards' columns (device decode of the whole batch)
+    if n:
+        all_ends = torch.cat([e[:m].to(dev) for e, m in zip(ends, nrec)])
+        from spec_amd import decode_flat
+
+        got = decode_flat(FLAT16, whole[: sum(totals)], all_ends)
+        torch.cuda.synchronize()
+        assert int(got.status.ne(0).sum()) == 0
+        for f in (0, 4, 7, 15):
+            want = np.concatenate([c[0][f] for c in host])
+            assert np.array_equal(got.cols[f].cpu().numpy(), want), f
+    # again into the same buffers (the bench's steady state)
+    outs2, ends2, totals2, bases2 = sh.encode(FLAT16, shards, outs=outs, ends=ends)
+    sh.sync()
+    assert totals2 == totals and bases2 == bases
+
+
+def test_native_shard_encode_errors(dev):
+    """An encoder error in one shard (a span outside its heap) and a too-small output: that
+    shard writes nothing, the totals tell which shard, no ends are moved to the whole batch."""
+    devs, _ = _devices(3)
+    sh = NativeShard(devs, shared=True)
+    shards, host = _device_shards(sh, 3, 5, [1000, 1000, 1000])
+    shards[1][0][13][7].view(torch.int32)[0] = 1 << 30  # string span offset far outside its heap
+    sentinel = [torch.full((1 << 20,), 0xAB, dtype=torch.uint8, device=dev) for _ in range(3)]
+    ends = [torch.zeros(1000, dtype=torch.int64, device=dev) for _ in range(3)]
+    with pytest.raises(SpecError) as ei:
+        sh.encode(FLAT16, shards, outs=sentinel, ends=ends)
+    assert ei.value.rc == -7  # SPEC_E_ENCODE
+    sh.sync()
+    assert int(sentinel[1].ne(0xAB).sum()) == 0 and int(ends[1].ne(0).sum()) == 0
+    for k in (0, 2):  # the shards that encoded: their bytes, shard-relative ends
+        cols, heaps = host[k]
+        want, wends = O.encode_flat_batch(FLAT16.tags, FLAT16.kinds, cols, [heaps.get(f) for f in range(16)], 1000)
+        assert np.array_equal(sentinel[k][: want.size].cpu().numpy(), want)
+        assert np.array_equal(ends[k].cpu().numpy(), wends.view(np.int64))
+    shards, host = _device_shards(sh, 3, 5, [1000, 1000, 1000])
+    small = [torch.empty(1 << 20, dtype=torch.uint8, device=dev), torch.full((10,), 7, dtype=torch.uint8, device=dev),
+             torch.empty(1 << 20, dtype=torch.uint8, device=dev)]
+    ends = [torch.zeros(1000, dtype=torch.int64, device=dev) for _ in range(3)]
+    with pytest.raises(SpecError) as ei:
+        sh.encode(FLAT16, shards, outs=small, ends=ends)
+    assert ei.value.rc == -4  # SPEC_E_CAPACITY
+    sh.sync()
+    assert int(small[1].ne(7).sum()) == 0 and int(ends[1].ne(0).sum()) == 0
+    assert int(ends[2][-1]) == int(ends[2][-1]) and int(ends[2][0]) < int(ends[2][-1]) < (1 << 20)
+
+
+def test_native_shard_encode_config5(dev):
+    """BASELINE config 5's batch (16M records = 8 shards of 2M) encoded as 8 shards: each
+    shard's bytes == the oracle Writer's, bases chained, ends global (4.28 GB in total)."""
+    devs, _ = _devices(8)
+    sh = NativeShard(devs, shared=True)
+    nrec = [1 << 21] * 8
+    total_bytes, prev = 0, None
+    shards, _ = _device_shards(sh, 8, 0x100, nrec)
+    outs, ends, totals, bases = sh.encode(FLAT16, shards)
+    sh.sync()
+    assert sum(totals) > 4_000_000_000  # ends past 32 bits of a 4 GB batch
+    for k in range(8):
+        assert bases[k] == total_bytes
+        total_bytes += totals[k]
+        assert int(ends[k][-1]) == total_bytes
+        if prev is not None:
+            assert int(ends[k][0]) > prev
+        prev = int(ends[k][-1])
+    # oracle bytes for a sample of every shard: its first and last 20k records
+    for k in (0, 3, 7):
+        cols, heaps = workload.flat16(nrec[k], 0x100 + k)
+        m = 20_000
+        want, wends = O.encode_flat_batch(FLAT16.tags, FLAT16.kinds, [c[:m] for c in cols],
+                                          [heaps.get(f) for f in range(16)], m)
+        assert np.array_equal(outs[k][: want.size].cpu().numpy(), want)
+        assert np.array_equal(ends[k][:m].cpu().numpy(), wends.view(np.int64) + bases[k])
+
+
+@pytest.mark.parametrize("nshard", [1, 3])
+def test_native_shard_host_decode(dev, nshard):
+    """The host pipeline on every shard's device at once: host batch in, each shard's
+    chunk-major host output == the oracle's decode of its records (spans shard-relative)."""
+    n = 200_003
+    devs, _ = _devices(nshard)
+    sh = NativeShard(devs, shared=True)
+    cols, heaps = workload.flat16(n, seed=21)
+    stream, ends = O.encode_flat_batch(FLAT16.tags, FLAT16.kinds, cols, [heaps.get(f) for f in range(16)], n)
+    want, wst = O.decode_flat_batch(FLAT16.tags, FLAT16.kinds, stream, ends, FLAT16.widths, 8)
+    sh.host_prepare(FLAT16, n // nshard + 1, stream.size, chunks=4)
+    s_in = torch.from_numpy(stream).pin_memory()
+    e_in = torch.from_numpy(ends.view(np.int64)).pin_memory()
+    nk = [sh.bounds(n, k)[1] - sh.bounds(n, k)[0] for k in range(nshard)]
+    outs = [torch.empty(sh.host_out_bytes(k, nk[k]), dtype=torch.uint8).pin_memory() for k in range(nshard)]
+    bases = sh.host_decode(s_in, e_in, outs)
+    for k in range(nshard):
+        R0 = sh.bounds(n, k)[0]
+        assert bases[k] == (int(ends[R0 - 1]) if R0 else 0)
+        o = outs[k].numpy()
+        for j in range(4):
+            r0, r1, co, so = sh.host_chunk(k, nk[k], j)
+            for f, fld in enumerate(FLAT16.fields):
+                w = fld.width
+                got = o[co[f]: co[f] + (r1 - r0) * w].reshape(r1 - r0, w)
+                exp = want[f][R0 + r0: R0 + r1]
+                if fld.kind.name in ("STRING", "BYTES"):
+                    exp = rebase_spans([exp], [-bases[k] % (1 << 32)], True)
+                assert np.array_equal(got, exp), (k, j, fld)
+            assert np.array_equal(o[so: so + r1 - r0], wst[R0 + r0: R0 + r1])
+
+
+def test_native_shard_rejects_duplicate_devices():
     with pytest.raises(SpecError):
         NativeShard([0, 0])
+    with pytest.raises(SpecError):
+        NativeShard([0], force_comm=True, shared=True)

@@ -315,3 +315,71 @@ def test_run_async_and_capacity(dev):
     assert list(got_rows) == want_rows
     got = [c[: tree.column_rows(tc, want_rows)].cpu().numpy() for c, tc in zip(out, tree.columns)]
     assert mismatches(tree, got, want) == []
+
+
+def test_run_columns_sized_by_indexed_batch(dev):
+    """columns allocated from an indexed batch's rows, then a batch with more
+    list elements run into them — within the decoder's internal capacity (index grows it by 1/8
+    + 64), beyond the columns.  Nothing may be written past a column: each column sits between
+    guard bytes that must stay intact; lists that do not fit (and tables under them) report -1,
+    every other table decodes exactly."""
+    tree = spec_amd.pkg1_tree()
+    cols_a, heaps_a, _ = workload.tree_batch(tree, 400, 81, count=(3, 4))
+    s1, e1 = oracle_encode(tree, cols_a, heaps_a, 400)
+    cols_b, heaps_b, _ = workload.tree_batch(tree, 400, 82, count=(4, 4))
+    s2, e2 = oracle_encode(tree, cols_b, heaps_b, 400)
+    want_rows, want = oracle_decode(tree, s2, e2)
+    d = spec_amd.TreeDecoder(tree)
+    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    rows_a = d.index(to(s1), to(e1.view(np.int64)))
+    caps = d.capacity()
+    lists = [t.index for t in tree.tables if t.rel == 2]
+    assert any(rows_a[t] < want_rows[t] <= caps[t] for t in lists)  # the case the advice describes
+    guard = 4096
+    bufs, out = [], []
+    for c in tree.columns:
+        nbytes = max(tree.column_rows(c, rows_a), 1) * c.width
+        b = torch.full((nbytes + 2 * guard,), 0xA5, dtype=torch.uint8, device=dev)
+        bufs.append((b, nbytes))
+        out.append(b[guard: guard + nbytes].view(-1, c.width))
+    got_rows = d.run(to(s2), to(e2.view(np.int64)), out).cpu().numpy()
+    torch.cuda.synchronize()
+    for (b, nbytes), c in zip(bufs, tree.columns):
+        h = b.cpu().numpy()
+        assert (h[:guard] == 0xA5).all() and (h[guard + nbytes:] == 0xA5).all(), c.name
+
+    over = {t for t in lists if want_rows[t] > rows_a[t]}
+
+    def under(t):  # t is, or hangs under, a list that did not fit
+        while t > 0:
+            if t in over:
+                return True
+            t = tree.tables[t].parent
+        return False
+
+    assert over
+    for t in range(len(tree.tables)):
+        assert got_rows[t] == (-1 if under(t) else want_rows[t]), t
+    for i, c in enumerate(tree.columns):
+        if not under(c.table):
+            g = out[i][: tree.column_rows(c, want_rows)].cpu().numpy()
+            assert np.array_equal(g, want[i]), c.name
+
+
+def test_rows_out_first_run_without_index(dev):
+    """run() on a fresh decoder (no index, list capacities 0) reports -1 for
+    every list table (none fits), never uninitialised counts."""
+    tree = spec_amd.pkg1_tree()
+    cols, heaps, _ = workload.tree_batch(tree, 300, 83)
+    s, e = oracle_encode(tree, cols, heaps, 300)
+    want_rows, _ = oracle_decode(tree, s, e)
+    d = spec_amd.TreeDecoder(tree)
+    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    out = [torch.zeros((max(tree.column_rows(c, want_rows), 1), c.width), dtype=torch.uint8, device=dev)
+           for c in tree.columns]
+    got = d.run(to(s), to(e.view(np.int64)), out).cpu().numpy()
+    for t, tb in enumerate(tree.tables):
+        if tb.rel == 2 or (t and got[tb.parent] == -1):
+            assert got[t] == -1 or want_rows[t] == 0, (t, got[t], want_rows[t])
+        elif t and tree.tables[t].parent == 0:
+            assert got[t] == 300
