@@ -588,7 +588,9 @@ def native_shard_leg(args, world, devices_distinct):
         dev_ms = max(a.elapsed_time(b) for a, b in evs) / nrep
         return wall, dev_ms
 
-    enc_wall, enc_dev = timed(lambda: sh.encode(FLAT16, shards, outs=outs, ends=ends), reps)
+    for d in sorted(set(devs)):
+        torch.cuda.synchronize(d)
+    enc_wall, enc_dev = timed(sh.encode_call(FLAT16, shards, outs, ends), reps)
     # decode: every device's shard, ends relative to its own stream (prepared ctypes arguments,
     # so the timed loop is the C ABI calls alone, as a cgo caller issues them)
     rel = [(e - b).contiguous() for e, b in zip(ends, bases)]

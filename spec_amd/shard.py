@@ -270,12 +270,7 @@ class NativeShard:
         self._join([list(bufs[k:k + 1]) + ([out] if k == root else []) for k in range(self.ndev)])
         return out
 
-    def encode(self, schema: Schema, shards, outs=None, ends=None):
-        """Sharded encode: shards[k] = (columns, heaps, n) on device k (as spec_amd.encode_flat
-        takes them).  -> (outs, ends, totals, byte_bases): device k's bytes outs[k][:totals[k]]
-        and ends[k] = its records' ends in the WHOLE batch; the outs back to back are exactly
-        one encode of the batch.  Without `outs`, the totals are found first (a call with no
-        capacity) and the buffers allocated."""
+    def _encode_args(self, schema: Schema, shards):
         k_ = self.ndev
         if len(shards) != k_:
             raise ValueError("one shard per device")
@@ -300,6 +295,16 @@ class NativeShard:
         colsp = (C.c_void_p * k_)(*[C.cast(c, C.c_void_p) for c in cols])
         hpp = (C.c_void_p * k_)(*[C.cast(h, C.c_void_p) for h in hp])
         hlp = (C.c_void_p * k_)(*[C.cast(h, C.c_void_p) for h in hl])
+        return (cols, hp, hl), ns, colsp, hpp, hlp
+
+    def encode(self, schema: Schema, shards, outs=None, ends=None):
+        """Sharded encode: shards[k] = (columns, heaps, n) on device k (as spec_amd.encode_flat
+        takes them).  -> (outs, ends, totals, byte_bases): device k's bytes outs[k][:totals[k]]
+        and ends[k] = its records' ends in the WHOLE batch; the outs back to back are exactly
+        one encode of the batch.  Without `outs`, the totals are found first (a call with no
+        capacity) and the buffers allocated."""
+        k_ = self.ndev
+        keepalive, ns, colsp, hpp, hlp = self._encode_args(schema, shards)
         totals = (C.c_uint64 * k_)()
         bases = (C.c_uint64 * k_)()
         devs = [torch.device("cuda", d) for d in self.devices]
@@ -323,8 +328,26 @@ class NativeShard:
         self._lib.check(call(outs, [o.numel() for o in outs]), "spec_shard_encode")
         keep = [list(s[0]) + list(s[1].values()) if isinstance(s[1], dict) else list(s[0]) for s in shards]
         self._join([[o, e] + [t for t in kk if isinstance(t, torch.Tensor)] for o, e, kk in zip(outs, ends, keep)])
-        self._inflight.append((cols, hp, hl))
+        self._inflight.append(keepalive)
         return outs, ends, list(totals), list(bases)
+
+    def encode_call(self, schema: Schema, shards, outs, ends):
+        """A prepared spec_shard_encode over fixed buffers: -> fn() that issues it (the C ABI call
+        alone, as a cgo caller issues it; no torch stream ordering: synchronise the inputs first)."""
+        k_ = self.ndev
+        keepalive, ns, colsp, hpp, hlp = self._encode_args(schema, shards)
+        totals, bases = (C.c_uint64 * k_)(), (C.c_uint64 * k_)()
+        op = (C.c_void_p * k_)(*[b.data_ptr() for b in outs])
+        cp = (C.c_uint64 * k_)(*[b.numel() for b in outs])
+        ep = (C.c_void_p * k_)(*[e.data_ptr() for e in ends])
+        L, h, sc = self._lib.lib(), self._h, C.byref(schema.c)
+        self._inflight.append((keepalive, shards, outs, ends))
+
+        def fn():
+            self._lib.check(L.spec_shard_encode(h, sc, colsp, hpp, hlp, ns, op, cp, ep, totals, bases),
+                            "spec_shard_encode")
+
+        return fn
 
     def host_prepare(self, schema: Schema, shard_records: int, shard_bytes: int, chunks: int = 8):
         """A spec_host_decoder per device for shards of up to shard_records / shard_bytes."""
