@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(TB) void tree_write_kernel(const TreeDesc *Dp, cons
         const uint64_t start = x == 0 ? B.offsets[row] : B.pos[x][row];
         if (start == ~0ull) continue; // a row no written owner placed (absent message / list)
         if (x == 0 && B.ends_out) B.ends_out[row] = start + B.size[0][row];
-        BEmit em{B.out, start, start};
+        BEmit em{{B.out}, start, start};
         if (T.shape == SHAPE_VALUE) {
             const TField &F = D.f[T.field];
             emit_value(em, B, D, F.col, F.elem, row);
@@ -521,6 +522,46 @@ size_t enc_plan(const Layout &L, const uint64_t *rows, EncWs &w) {
 }
 } // namespace
 
+namespace {
+// Pinned staging for the descriptor + buffer block each spec_encode_tree call uploads: a ring of
+// slots per device, a slot reused once the copy out of it has run (its event), so the call
+// never synchronises with the device.
+struct UploadRing {
+    static constexpr int SLOTS = 16;
+    struct Slot {
+        uint8_t *p = nullptr;
+        hipEvent_t ev = nullptr;
+    } slot[SLOTS];
+    int next = 0;
+};
+std::mutex g_ring_mu;
+UploadRing g_rings[64];
+
+// copies [desc | bufs] to the device workspace on st from a pinned slot; false on a HIP error
+bool upload_block(const TreeDesc &desc, const TreeBufs &bufs, void *ddesc, void *dbufs, hipStream_t st) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    std::lock_guard<std::mutex> lk(g_ring_mu);
+    UploadRing &R = g_rings[dev];
+    UploadRing::Slot &S = R.slot[R.next];
+    R.next = (R.next + 1) % UploadRing::SLOTS;
+    if (!S.p) {
+        if (hipHostMalloc((void **)&S.p, sizeof(TreeDesc) + sizeof(TreeBufs), hipHostMallocDefault) != hipSuccess ||
+            hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess) {
+            S.p = nullptr;
+            return false;
+        }
+    } else if (hipEventSynchronize(S.ev) != hipSuccess) { // the slot's previous copy has run
+        return false;
+    }
+    memcpy(S.p, &desc, sizeof(TreeDesc));
+    memcpy(S.p + sizeof(TreeDesc), &bufs, sizeof(TreeBufs));
+    return hipMemcpyAsync(ddesc, S.p, sizeof(TreeDesc), hipMemcpyHostToDevice, st) == hipSuccess &&
+           hipMemcpyAsync(dbufs, S.p + sizeof(TreeDesc), sizeof(TreeBufs), hipMemcpyHostToDevice, st) == hipSuccess &&
+           hipEventRecord(S.ev, st) == hipSuccess;
+}
+} // namespace
+
 size_t spec_encode_tree_workspace_size(const spec_tree *tree, const uint64_t *rows) {
     Layout *L = new (std::nothrow) Layout();
     if (!L || !rows || !build_layout(tree, *L)) {
@@ -593,9 +634,8 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
     B->err = (uint32_t *)(ws + w.err);
     const TreeDesc *Dd = (const TreeDesc *)(ws + w.desc);
     TreeBufs *Bd = (TreeBufs *)(ws + w.bufs);
-    bool ok = hipMemcpyAsync(ws + w.desc, &L.desc, sizeof(TreeDesc), hipMemcpyHostToDevice, st) == hipSuccess &&
-              hipMemcpyAsync(Bd, B, sizeof(TreeBufs), hipMemcpyHostToDevice, st) == hipSuccess &&
-              hipMemsetAsync(B->err, 0, sizeof(uint32_t), st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
+    bool ok = upload_block(L.desc, *B, ws + w.desc, Bd, st) &&
+              hipMemsetAsync(B->err, 0, sizeof(uint32_t), st) == hipSuccess;
     // the generated writers and size passes (jit.cpp) for message tables, else the run-time row kernels
     const hipFunction_t *jit = jit_tree_kernels(L.desc);
     // sizes bottom-up (children before their owners: table order is pre-order)
