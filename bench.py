@@ -688,6 +688,55 @@ def native_shard_leg(args, world, devices_distinct):
     return res
 
 
+def wide_leg(dev, n=1 << 20, seed=11):
+    """Schemas outside the register-resident fast path (decode_core.hpp fast_wide): a 40-field
+    schema (every kind, write order permuted) and a 16-field schema whose tags > 255 make every
+    table big (6-byte entries, internal/format/msg.go:43-61, 138-186).  n records each, encoded
+    on the GPU; the schema-specialised kernel and the generic kernel timed with HIP events; their
+    columns must match each other, and a 20k-record sample the oracle."""
+    from oracle import oracle as O
+
+    schemas = workload.bench_wide_schemas()
+    res = {}
+    for name, sc in schemas.items():
+        cols, heaps = workload.gen_columns(sc, n, seed, str_len=(0, 24))
+        d_cols = [torch.from_numpy(c).to(dev) for c in cols]
+        d_heaps = {f: torch.from_numpy(h).to(dev) for f, h in heaps.items()}
+        stream, ends = spec_amd.encode_flat(sc, d_cols, d_heaps, n)
+        del d_cols, d_heaps
+        torch.cuda.synchronize()
+        out = {}
+        got = {}
+        for jit in (True, False):
+            spec_amd.set_jit(jit)
+            try:
+                dec = spec_amd.Decoder(sc, stream, ends)
+                gpu_prewarm(dec, 0.1)
+                ms, _ = kernel_time_events(dec, 20)
+                torch.cuda.synchronize()
+                got[jit] = dec
+            finally:
+                spec_amd.set_jit(True)
+            col_bytes = sum(f.width for f in sc.fields)
+            alg = stream.numel() + n * (8 + col_bytes + 1)
+            out["jit" if jit else "generic"] = {"ms": round(ms, 4), "mmsg_s": round(n / (ms * 1e-3) / 1e6, 1),
+                                                "gb_s": round(alg / (ms * 1e-3) / 1e9, 1),
+                                                "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        same = torch.equal(got[True].status, got[False].status) and all(
+            torch.equal(a, b) for a, b in zip(got[True].cols, got[False].cols))
+        m = 20_000
+        st, en = O.encode_flat_batch(sc.tags, sc.kinds, [c[:m] for c in cols], [heaps.get(f) for f in range(len(sc))], m)
+        want, wst = O.decode_flat_batch(sc.tags, sc.kinds, st, en, sc.widths, host_cores())
+        ok = bool(np.array_equal(got[True].status[:m].cpu().numpy(), wst) and all(
+            np.array_equal(got[True].cols[f][:m].cpu().numpy(), want[f]) for f in range(len(sc))))
+        out.update({"fields": len(sc), "mean_record_bytes": round(stream.numel() / n, 1),
+                    "alg_bytes": int(stream.numel() + n * (8 + sum(f.width for f in sc.fields) + 1)),
+                    "jit_vs_generic_same": bool(same), "oracle_sample_ok": ok})
+        res[name] = out
+        del got, stream, ends
+    return res
+
+
 def generic_leg(stream, ends, want_cols, want_status, avg_jit_ms):
     """The precompiled generic decode kernel (no schema specialisation: what schemas without a
     fast path run) on the headline batch; its columns must equal the specialised kernel's."""
@@ -949,6 +998,12 @@ def run(args, env):
             except Exception as e:
                 extras["config5_sharded"] = {"error": repr(e)[:300]}
         if rank == 0 and world == 1:
+            try:
+                extras["decode_wide"] = wide_leg(dev)
+                checks["wide_parity"] = all(v["jit_vs_generic_same"] and v["oracle_sample_ok"]
+                                            for v in extras["decode_wide"].values())
+            except Exception as e:
+                extras["decode_wide"] = {"error": repr(e)[:300]}
             try:
                 extras["nested"] = nested_leg(n, args.seed, dev)
             except Exception as e:

@@ -528,9 +528,9 @@ int spec_decode_nested(const spec_nested_schema *schema, const uint8_t *stream_b
                        uint32_t *item_begin, void *const *item_columns, uint8_t *item_status, uint64_t item_cap,
                        void *workspace, size_t workspace_size, void *stream);
 /* spec_decode_nested_onepass: the same outputs from ONE call, with no host round trip for the
- * item total: the index kernels and the decode kernel back to back on the stream (default), or
- * (environment SPEC_AMD_LOOKBACK=1) a single kernel in which each 64-record group publishes its
- * item count and finds its first item by looking back over the groups before it.
+ * item total: the index kernels and the decode kernel back to back on the stream (a library
+ * built with -DSPEC_AB_LOOKBACK=1 runs one kernel instead, in which each 64-record group
+ * publishes its item count and finds its first item by looking back over the groups before it).
  * Writes *total_items (device uint64); items at index >= item_cap are not
  * written — if *total_items > item_cap, call again with item columns of that size (the stream
  * bytes bound it: every item has a list-table entry of at least 2 bytes, so stream_len / 2

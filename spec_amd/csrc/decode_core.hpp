@@ -580,12 +580,17 @@ __device__ __forceinline__ void decode_record_generic(const Src &s, typename Src
 // A run-time schema has no fast path.
 struct RuntimeSpec {
     static constexpr int N = 0;
+    static constexpr bool big = false;
 };
 
 // Spec (generated by jit.cpp) provides:
-//   N              number of fields (1..FAST_MAX_FIELDS)
+//   N              number of fields (1..SPEC_MAX_FIELDS; the register-resident fast path below
+//                  takes up to FAST_MAX_FIELDS small-table fields, fast_wide the rest)
 //   kind[f], rank[f]  per schema field
-//   stag[k]        k-th tag of the table a Writer emits (strictly increasing, all <= 255)
+//   stag[k]        k-th tag of the table a Writer emits (strictly increasing)
+//   order[k]       the schema field of table entry k (rank's inverse)
+//   big            the Writer's tables are big for every record (a tag > 255: IsBigMessage,
+//                  internal/format/msg.go:43-61)
 constexpr int FAST_MAX_FIELDS = 24;
 
 // Unrolled at compile time: field F's kind and table index are constants, so every field
@@ -742,6 +747,123 @@ __device__ __forceinline__ void fast_finish(const FastRec<Spec> &fr, uint64_t r,
     FieldStore<Spec, 0, ERR>::run(fr, to_stream, fs, r, errs);
     if (fs.status) fs.status[r] = ST_OK;
     if constexpr (ERR) fs.errmask[r] = errs;
+}
+
+// ---- fast path for wide schemas and big tables --------------------------------------------
+// Schemas with more than FAST_MAX_FIELDS fields, or whose tags make every table big (u16 tag |
+// u32 end entries, internal/format/msg.go:138-186).  The trailer is checked as by fast_prepare;
+// then the table is walked in batches of FAST_BATCH entries: the batch's entries read with a few
+// wide LDS reads and checked against the Writer's tags (strictly increasing, so the reference's
+// binary search lands on entry k for the k-th tag), its fields' windows read, their types checked
+// (the type a Writer emits for the kind), decoded and stored.  A record rejected after some
+// batches were stored runs the generic path, which rewrites every column and the status, so the
+// result never depends on where the fast path gave up.
+constexpr int FAST_BATCH = 8;
+
+template <class Spec, int J0, int K, int NB>
+struct WideField {
+    static __device__ __forceinline__ void load(Win (&w)[NB], int (&e)[NB], int (&lo)[NB], const LdsSrc &s, int ds,
+                                                const uint32_t (&ends)[NB], uint32_t dsize) {
+        if constexpr (K < NB) {
+            constexpr uint32_t KD = Spec::kind[Spec::order[J0 + K]];
+            const bool has = (ends[K] <= dsize) & (ends[K] > 0);
+            e[K] = has ? ds + (int)ends[K] : SLAB_GUARD;
+            lo[K] = has ? ds : SLAB_GUARD;
+            w[K] = load_win<KD, true>(s, e[K]);
+            WideField<Spec, J0, K + 1, NB>::load(w, e, lo, s, ds, ends, dsize);
+        }
+    }
+    static __device__ __forceinline__ bool nat(const Win (&w)[NB], const int (&e)[NB], const int (&lo)[NB]) {
+        if constexpr (K >= NB) {
+            return true;
+        } else {
+            constexpr uint32_t NT = cross_kind_type(Spec::kind[Spec::order[J0 + K]]);
+            bool good = true;
+            if constexpr (NT != 0) good = (e[K] <= lo[K]) | (((uint32_t)w[K].t.q0 & 0xff) == NT);
+            return good & WideField<Spec, J0, K + 1, NB>::nat(w, e, lo);
+        }
+    }
+    template <bool ERR>
+    static __device__ __forceinline__ void store(const Win (&w)[NB], const int (&e)[NB], const int (&lo)[NB],
+                                                 long long to_stream, const FieldSet &fs, uint64_t r, uint64_t &errs) {
+        if constexpr (K < NB) {
+            constexpr int F = Spec::order[J0 + K];
+            constexpr uint32_t KD = Spec::kind[F];
+            bool ok = true;
+            const Val v = decode_tail_k<KD, true>(w[K], lo[K], e[K], to_stream, ERR ? &ok : nullptr);
+            store_value_k<KD>(fs.cols[F], r, v);
+            if constexpr (ERR && F < 64) errs |= (!ok & (e[K] > lo[K])) ? (1ull << F) : 0ull;
+            WideField<Spec, J0, K + 1, NB>::template store<ERR>(w, e, lo, to_stream, fs, r, errs);
+        }
+    }
+};
+
+// table entries [J0, J1): false when the record needs the generic path
+template <class Spec, int J0, int J1, bool ERR>
+__device__ __forceinline__ bool wide_batch(const LdsSrc &s, int ts, int ds, uint32_t dsize, uint64_t r,
+                                           const FieldSet &fs, long long to_stream, uint64_t &errs) {
+    constexpr int NB = J1 - J0;
+    constexpr int ESZ = Spec::big ? 6 : 3;
+    constexpr int NC = (ESZ * NB + 7) / 8, NQ = NC + 1;
+    const int p0 = ts + ESZ * J0;
+    const int base = p0 & ~7;
+    const uint32_t sh = 8u * (uint32_t)(p0 & 7);
+    uint64_t q[NQ];
+#pragma unroll
+    for (int j = 0; j < NQ; j++) q[j] = s.d64(base + 8 * j);
+    uint64_t c[NC];
+#pragma unroll
+    for (int j = 0; j < NC; j++) c[j] = (q[j] >> sh) | ((q[j + 1] << 1) << (63 - sh));
+    auto byte_at = [&](int j) -> uint32_t { return (uint32_t)(c[j >> 3] >> (8 * (j & 7))) & 0xff; };
+    bool hit = true;
+    uint32_t ends[NB];
+#pragma unroll
+    for (int k = 0; k < NB; k++) {
+        if constexpr (Spec::big) {
+            hit = hit & (((byte_at(6 * k) << 8) | byte_at(6 * k + 1)) == Spec::stag[J0 + k]);
+            ends[k] = (byte_at(6 * k + 2) << 24) | (byte_at(6 * k + 3) << 16) | (byte_at(6 * k + 4) << 8) |
+                      byte_at(6 * k + 5);
+        } else {
+            hit = hit & (byte_at(3 * k) == Spec::stag[J0 + k]);
+            ends[k] = (byte_at(3 * k + 1) << 8) | byte_at(3 * k + 2);
+        }
+    }
+    if (!hit) return false;
+    Win w[NB];
+    int e[NB], lo[NB];
+    WideField<Spec, J0, 0, NB>::load(w, e, lo, s, ds, ends, dsize);
+    if (!WideField<Spec, J0, 0, NB>::nat(w, e, lo)) return false;
+    WideField<Spec, J0, 0, NB>::template store<ERR>(w, e, lo, to_stream, fs, r, errs);
+    return true;
+}
+
+template <class Spec, int J0, bool ERR>
+struct WideBatches {
+    static __device__ __forceinline__ bool run(const LdsSrc &s, int ts, int ds, uint32_t dsize, uint64_t r,
+                                               const FieldSet &fs, long long to_stream, uint64_t &errs) {
+        if constexpr (J0 >= Spec::N) {
+            return true;
+        } else {
+            constexpr int J1 = J0 + FAST_BATCH < Spec::N ? J0 + FAST_BATCH : Spec::N;
+            if (!wide_batch<Spec, J0, J1, ERR>(s, ts, ds, dsize, r, fs, to_stream, errs)) return false;
+            return WideBatches<Spec, J1, ERR>::run(s, ts, ds, dsize, r, fs, to_stream, errs);
+        }
+    }
+};
+
+// The whole record (columns, status, errmask); false: nothing final written, run the generic path.
+template <class Spec, bool ERR = false>
+__device__ __forceinline__ bool fast_wide(const LdsSrc &s, int rs, int re, uint64_t r, const FieldSet &fs,
+                                          long long to_stream) {
+    if (re <= rs) return false;
+    const Trailer tr = parse_trailer(s, rs, re);
+    if ((tr.st != ST_OK) | (tr.big != Spec::big) | (tr.tsize != (Spec::big ? 6u : 3u) * (uint32_t)Spec::N)) return false;
+    uint64_t errs = 0;
+    if (!WideBatches<Spec, 0, ERR>::run(s, (int)tr.tstart, (int)tr.dstart, tr.dsize, r, fs, to_stream, errs))
+        return false;
+    if (fs.status) fs.status[r] = ST_OK;
+    if constexpr (ERR) fs.errmask[r] = errs;
+    return true;
 }
 
 // ---- kernel body -------------------------------------------------------------------------
@@ -920,10 +1042,14 @@ __device__ __forceinline__ void decode_flat_once(const DecodeArgs &a) {
         const int re = SLAB_GUARD + (int)(cur.rec_hi - cur.aligned_lo);
         const long long to_stream = (long long)cur.aligned_lo - SLAB_GUARD;
         if constexpr (Spec::N > 0) {
-            FastRec<Spec> fr;
-            if (fast_prepare<Spec>(s, rs, re, fr)) {
-                fast_finish<Spec, ERR>(fr, r, a.f, to_stream);
-                return;
+            if constexpr (Spec::N <= FAST_MAX_FIELDS && !Spec::big) {
+                FastRec<Spec> fr;
+                if (fast_prepare<Spec>(s, rs, re, fr)) {
+                    fast_finish<Spec, ERR>(fr, r, a.f, to_stream);
+                    return;
+                }
+            } else {
+                if (fast_wide<Spec, ERR>(s, rs, re, r, a.f, to_stream)) return;
             }
         }
         decode_record_generic(s, rs, re, r, a.f, to_stream);
@@ -943,7 +1069,7 @@ __device__ __forceinline__ void decode_flat_entry(const DecodeArgs &a) {
         decode_flat_once<Spec, ERR>(a);
 }
 
-bool xcd_swizzle_decode(); // XCD-aware block order, default on; SPEC_AMD_XCD=0 off (decode_flat.hip)
+bool xcd_swizzle_decode(); // XCD-aware block order, default on; build-time SPEC_AB_NOXCD off (decode_flat.hip)
 
 // Launch shape of the flat decode: per-wave slab, waves per block, grid.
 struct DecodeLaunch {

@@ -2,7 +2,6 @@
 // The device code lives in decode_core.hpp; schema-specialised variants of the same body
 // are compiled at run time by jit.cpp.
 #include <hip/hip_runtime.h>
-#include <stdlib.h>
 
 #include "decode_core.hpp"
 #include "spec_internal.hpp"
@@ -15,32 +14,24 @@ __global__ __launch_bounds__(256) void decode_flat_kernel_persistent(DecodeArgs 
     decode_flat_entry<true, RuntimeSpec>(a);
 }
 
-bool persistent_decode() {
-    static int v = [] {
-        const char *e = getenv("SPEC_AMD_PERSIST");
-        return (e && e[0] == '1') ? 1 : 0;
-    }();
-    return v == 1;
-}
-
-// XCD-aware block order (consecutive groups on one XCD's L2) is the default: 1.3 % faster on the
-// 1M Flat16 decode (tools/ab.py, 6 interleaved rounds, r02); SPEC_AMD_XCD=0 turns it off
-bool xcd_swizzle_decode() {
-    static int v = [] {
-        const char *e = getenv("SPEC_AMD_XCD");
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    return v == 1;
-}
-
-unsigned decode_wpb() {
-    static unsigned v = [] {
-        const char *e = getenv("SPEC_AMD_WPB");
-        int w = e ? atoi(e) : 1;
-        return (unsigned)(w >= 1 && w <= 4 ? w : 1);
-    }();
-    return v;
-}
+// Launch variants measured in rounds 1-3 and not kept as defaults are chosen when the library
+// is BUILT (make HIPFLAGS+="-DSPEC_AB_PERSIST=1 ..."), never by a process's environment:
+//   SPEC_AB_PERSIST=1  persistent, software-pipelined decode (no faster on MI355X);
+//   SPEC_AB_NOXCD=1    blocks in launch order instead of XCD-aware contiguous shares (1.3 %
+//                      slower on the 1M Flat16 decode, tools/ab.py, 6 interleaved rounds, r02);
+//   SPEC_AB_WPB=k      k waves per block (1 packs the most slabs per CU: LDS is the limit).
+#ifndef SPEC_AB_PERSIST
+#define SPEC_AB_PERSIST 0
+#endif
+#ifndef SPEC_AB_NOXCD
+#define SPEC_AB_NOXCD 0
+#endif
+#ifndef SPEC_AB_WPB
+#define SPEC_AB_WPB 1
+#endif
+bool persistent_decode() { return SPEC_AB_PERSIST != 0; }
+bool xcd_swizzle_decode() { return SPEC_AB_NOXCD == 0; }
+unsigned decode_wpb() { return SPEC_AB_WPB >= 1 && SPEC_AB_WPB <= 4 ? SPEC_AB_WPB : 1; }
 
 int device_cus() {
     static int cus[64] = {0};

@@ -77,7 +77,25 @@ void writer_order(const spec_schema *s, uint8_t *order, uint16_t *sorted) {
     }
 }
 
-// A fast path exists when the Writer's table is strictly increasing in tags <= 255.
+// The flat decoder's fast path (decode_core.hpp fast_prepare / fast_wide) exists when the
+// Writer's table is strictly increasing: any field count, tags <= 255 (small tables) or with a
+// tag > 255 (every table big).
+bool has_flat_fast_path(const spec_schema *s) {
+    if (s->nfields == 0 || s->nfields > SPEC_MAX_FIELDS) return false;
+    for (uint32_t f = 0; f < s->nfields; f++)
+        if (s->fields[f].kind == SPEC_KIND_LIST) return false;
+    uint8_t order[SPEC_MAX_FIELDS];
+    uint16_t sorted[SPEC_MAX_FIELDS];
+    writer_order(s, order, sorted);
+    for (uint32_t k = 0; k < s->nfields; k++) {
+        if (sorted[k] == 0) return false;
+        if (k && sorted[k] <= sorted[k - 1]) return false;
+    }
+    return true;
+}
+
+// The nested decoder's fast path (register-resident): strictly increasing tags <= 255, at most
+// FAST_MAX_FIELDS fields.
 bool has_fast_path(const spec_schema *s) {
     if (s->nfields == 0 || s->nfields > (uint32_t)spec::FAST_MAX_FIELDS) return false;
     uint8_t order[SPEC_MAX_FIELDS];
@@ -122,7 +140,11 @@ void emit_spec(std::ostringstream &o, const char *name, const spec_schema *s) {
     for (uint32_t f = 0; f < s->nfields; f++) o << (f ? "," : "") << (int)rank[f];
     o << "};\n  static constexpr uint32_t stag[N] = {";
     for (uint32_t k = 0; k < s->nfields; k++) o << (k ? "," : "") << sorted[k];
-    o << "};\n};\n";
+    o << "};\n  static constexpr int order[N] = {";
+    for (uint32_t k = 0; k < s->nfields; k++) o << (k ? "," : "") << (int)order[k];
+    bool big = false;
+    for (uint32_t k = 0; k < s->nfields; k++) big = big || sorted[k] > 255;
+    o << "};\n  static constexpr bool big = " << (big ? "true" : "false") << ";\n};\n";
 }
 
 std::string generate_decode(const spec_schema *s) {
@@ -384,7 +406,7 @@ const Entry *lookup_key(const std::string &k, Prog p, Make make) {
 }
 
 const Entry *lookup(const spec_schema *s, Prog p) {
-    if (!enabled() || !(p == ENCODE ? has_encoder(s) : has_fast_path(s))) return nullptr;
+    if (!enabled() || !(p == ENCODE ? has_encoder(s) : has_flat_fast_path(s))) return nullptr;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     return lookup_key(key_of(s, dev, p), p, [&] { return compile_code(s, p); });
@@ -927,7 +949,7 @@ const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
 }
 
 long long jit_compile_only(const spec_schema *schema, double) {
-    if (!has_fast_path(schema)) return 0;
+    if (!has_flat_fast_path(schema)) return 0;
     return (long long)compile_code(schema, DECODE).size();
 }
 

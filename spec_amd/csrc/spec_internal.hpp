@@ -33,8 +33,8 @@ int launch_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends,
                                uint64_t *consumed, int32_t *status, void *ws, hipStream_t stream);
 int device_cus(); // CUs of the current device (cached)
 void note_hip_error(hipError_t e); // capi.hip: remembered for spec_last_hip_error()
-bool persistent_decode(); // SPEC_AMD_PERSIST=1
-unsigned decode_wpb();     // SPEC_AMD_WPB (waves per block, default 1)
+bool persistent_decode(); // build-time A/B variants (decode_flat.hip): SPEC_AB_PERSIST
+unsigned decode_wpb();     // SPEC_AB_WPB (waves per block, default 1)
 int launch_parse(DecodeArgs a, uint32_t *sizes, double avg_record, hipStream_t stream);
 int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream);
 int launch_nested_decode(const spec_nested_schema *schema, NestedArgs a, double avg_record, hipStream_t stream);
@@ -49,7 +49,7 @@ int launch_nested_onepass(const spec_nested_schema *schema, NestedArgs a, double
 // TAILCOUNT with an XCD-aware block order for the decode pass: the default)
 enum { NESTED_ONEPASS = 0, NESTED_GROUPS = 1, NESTED_RANGES = 2, NESTED_HALVES = 3, NESTED_TAILCOUNT = 4, NESTED_XCD = 5 };
 int jit_launch_nested(const spec_nested_schema *schema, const NestedArgs &a, int mode, hipStream_t stream);
-bool nested_lookback(); // SPEC_AMD_LOOKBACK=1: spec_decode_nested_onepass runs the look-back kernel
+bool nested_lookback(); // build-time SPEC_AB_LOOKBACK: spec_decode_nested_onepass runs the look-back kernel
 long long jit_compile_only_nested(const spec_nested_schema *schema);
 // jit.cpp: schema-specialised decode kernel (hiprtc); returns 1 if launched, 0 if the caller
 // should launch the generic kernel, <0 on a HIP error.

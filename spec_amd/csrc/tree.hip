@@ -85,7 +85,7 @@ __global__ __launch_bounds__(TB) void tree_write_kernel(const TreeDesc *Dp, cons
         const uint64_t start = x == 0 ? B.offsets[row] : B.pos[x][row];
         if (start == ~0ull) continue; // a row no written owner placed (absent message / list)
         if (x == 0 && B.ends_out) B.ends_out[row] = start + B.size[0][row];
-        BEmit em{{B.out}, start, start};
+        BEmit em{B.out, start, start};
         if (T.shape == SHAPE_VALUE) {
             const TField &F = D.f[T.field];
             emit_value(em, B, D, F.col, F.elem, row);

@@ -224,3 +224,15 @@ def tree_batch(tree, n: int, seed: int = SEED, count=(0, 4), present: float = 0.
                 if h is not None:
                     heaps[c.name] = h if h.size else np.zeros(1, np.uint8)
     return cols, heaps, rows
+
+
+def bench_wide_schemas():
+    """The bench's schemas outside the register-resident fast path (bench.py wide_leg): a
+    40-field schema cycling through every kind with its write order permuted, and a 16-field
+    schema whose tags > 255 make every table big (internal/format/msg.go:43-61)."""
+    from .schema import Kind, Schema
+
+    kinds = [Kind(k) for k in range(1, 16)]
+    tags40 = [int(t) for t in np.random.default_rng(3).permutation(np.arange(1, 41))]
+    return {"wide40": Schema([(t, kinds[i % 15]) for i, t in enumerate(tags40)]),
+            "big16": Schema([(256 + 37 * i, kinds[i % 15]) for i in range(16)])}
