@@ -812,7 +812,7 @@ def tree_leg(dev, n=1 << 18, seed=7):
     (both synchronise with the host once per list table); encode bytes and every decoded column
     checked against the oracle outside the timed region."""
     from oracle import oracle as O  # noqa: F401  (checker only)
-    from tests.tree_helpers import mismatches, oracle_decode, oracle_encode
+    from oracle.tree_oracle import mismatches, oracle_decode, oracle_encode
 
     tree = spec_amd.pkg1_tree()
     cols, heaps, rows = workload.tree_batch(tree, n, seed)

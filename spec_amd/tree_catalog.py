@@ -1,0 +1,65 @@
+"""Schema trees the engine precompiles (build(): their schema-specialised kernels go into the
+code-object cache that travels with the library) — the bench's pkg1.spec Message at depths 1-3
+and the shapes the GPU tests exercise.  No oracle here: this is product code."""
+from __future__ import annotations
+
+import json
+
+from .schema import Kind
+from .tree import ListOf, Message, Struct, Tree, pkg1_tree
+
+
+# ---- trees used by the tests --------------------------------------------------------------
+
+def shapes_tree() -> Tree:
+    """Lists inside list items, big tags (big message tables), value lists of every width, a
+    struct with string members (pkg1.spec ComplexStruct), any."""
+    complex_s = Struct("ComplexStruct", [("bin64", Kind.BIN64), ("bin128", Kind.BIN128), ("bin256", Kind.BIN256),
+                                         ("string", Kind.STRING)])
+    leaf = Message("Leaf", [("u", 1, Kind.UINT64), ("vals", 2, ListOf(Kind.INT16)), ("c", 3, complex_s)])
+    item = Message("Item", [("name", 1, Kind.STRING), ("leaves", 2, ListOf(leaf)), ("f", 3, Kind.FLOAT32),
+                            ("bytes", 4, ListOf(Kind.BYTES))])
+    big = Message("Big", [("a", 300, Kind.INT32), ("b", 7, Kind.BOOL), ("any", 1000, Kind.ANY)])
+    root = Message("Root", [
+        ("id", 1, Kind.BIN128), ("items", 2, ListOf(item)), ("big", 3, big), ("u16s", 4, ListOf(Kind.UINT16)),
+        ("f64s", 5, ListOf(Kind.FLOAT64)), ("bools", 6, ListOf(Kind.BOOL)), ("cs", 7, ListOf(complex_s)),
+        ("seq", 65535, Kind.INT64),
+    ])
+    return Tree(root)
+
+
+def nested_struct_tree() -> Tree:
+    """Structs inside structs (internal/lang/model/struct_field.go:57-70): a struct field of a
+    message, a list of such structs, a sub-message holding one, and three levels of nesting."""
+    inner = Struct("Inner", [("x", Kind.INT32), ("y", Kind.STRING)])
+    mid = Struct("Mid", [("i", inner), ("f", Kind.FLOAT64), ("j", inner)])
+    outer = Struct("Outer", [("a", Kind.INT32), ("in", inner), ("s", Kind.STRING)])
+    deep = Struct("Deep", [("m", mid), ("b", Kind.BIN64), ("o", outer)])
+    sub = Message("Sub", [("o", 1, outer), ("n", 2, Kind.UINT16)])
+    root = Message("Root", [
+        ("id", 1, Kind.INT64), ("outer", 2, outer), ("outers", 3, ListOf(outer)), ("sub", 4, sub),
+        ("deep", 5, deep), ("deeps", 6, ListOf(deep)), ("tail", 7, Kind.STRING),
+    ])
+    return Tree(root)
+
+
+def precompiled_trees(spec_trees_json: str | None = None) -> list:
+    """Every tree the GPU tests and the bench decode and encode: build() compiles their
+    schema-specialised kernels into the code-object cache that travels with the library.
+    spec_trees_json: the trees spec_amd.specfile derived from the reference's .spec files
+    (tests/golden/spec_trees.json, a data fixture), added when given."""
+    trees = [pkg1_tree(k) for k in (1, 2, 3)] + [shapes_tree(), nested_struct_tree()]
+    if spec_trees_json:
+        d = json.load(open(spec_trees_json))
+        trees += [Tree.from_fields(d[k]) for k in ("pkg1.Message", "pmpx.Message", "prpc.Message", "pmpx.ChannelOpen")]
+    base = pkg1_tree()
+    for shift in (1, 4, 9):  # test_errmask_cross_kind's readers
+        fields = []
+        for p, tag, k, e, par in base.to_fields():
+            if 1 <= k <= 15:
+                k = (k - 1 + shift) % 15 + 1
+            fields.append((p, tag, k, e, par))
+        trees.append(Tree.from_fields(fields))
+    trees.append(Tree(Message("message1", [("f1", 1, Kind.INT32), ("f2", 2, Kind.INT32),
+                                                    ("f3", 3, Kind.INT32), ("l", 4, ListOf(Kind.STRING))])))
+    return trees

@@ -1,63 +1,12 @@
-"""The trees the GPU tests and the bench decode.  No oracle import: build() uses jit_trees() to
-compile their schema-specialised group kernels into the code-object cache."""
+"""The trees the GPU tests decode (spec_amd.tree_catalog) and the reference-derived ones."""
 from __future__ import annotations
 
-import json
 import os
 
-import spec_amd
-from spec_amd.schema import Kind
-from spec_amd.tree import ListOf, Message, Struct, Tree
+from spec_amd.tree_catalog import nested_struct_tree, precompiled_trees, shapes_tree  # noqa: F401
 
-
-# ---- trees used by the tests --------------------------------------------------------------
-
-def shapes_tree() -> Tree:
-    """Lists inside list items, big tags (big message tables), value lists of every width, a
-    struct with string members (pkg1.spec ComplexStruct), any."""
-    complex_s = Struct("ComplexStruct", [("bin64", Kind.BIN64), ("bin128", Kind.BIN128), ("bin256", Kind.BIN256),
-                                         ("string", Kind.STRING)])
-    leaf = Message("Leaf", [("u", 1, Kind.UINT64), ("vals", 2, ListOf(Kind.INT16)), ("c", 3, complex_s)])
-    item = Message("Item", [("name", 1, Kind.STRING), ("leaves", 2, ListOf(leaf)), ("f", 3, Kind.FLOAT32),
-                            ("bytes", 4, ListOf(Kind.BYTES))])
-    big = Message("Big", [("a", 300, Kind.INT32), ("b", 7, Kind.BOOL), ("any", 1000, Kind.ANY)])
-    root = Message("Root", [
-        ("id", 1, Kind.BIN128), ("items", 2, ListOf(item)), ("big", 3, big), ("u16s", 4, ListOf(Kind.UINT16)),
-        ("f64s", 5, ListOf(Kind.FLOAT64)), ("bools", 6, ListOf(Kind.BOOL)), ("cs", 7, ListOf(complex_s)),
-        ("seq", 65535, Kind.INT64),
-    ])
-    return Tree(root)
-
-
-def nested_struct_tree() -> Tree:
-    """Structs inside structs (internal/lang/model/struct_field.go:57-70): a struct field of a
-    message, a list of such structs, a sub-message holding one, and three levels of nesting."""
-    inner = Struct("Inner", [("x", Kind.INT32), ("y", Kind.STRING)])
-    mid = Struct("Mid", [("i", inner), ("f", Kind.FLOAT64), ("j", inner)])
-    outer = Struct("Outer", [("a", Kind.INT32), ("in", inner), ("s", Kind.STRING)])
-    deep = Struct("Deep", [("m", mid), ("b", Kind.BIN64), ("o", outer)])
-    sub = Message("Sub", [("o", 1, outer), ("n", 2, Kind.UINT16)])
-    root = Message("Root", [
-        ("id", 1, Kind.INT64), ("outer", 2, outer), ("outers", 3, ListOf(outer)), ("sub", 4, sub),
-        ("deep", 5, deep), ("deeps", 6, ListOf(deep)), ("tail", 7, Kind.STRING),
-    ])
-    return Tree(root)
+SPEC_TREES_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "spec_trees.json")
 
 
 def jit_trees() -> list:
-    """Every tree the GPU tests and the bench decode: build() compiles their schema-specialised
-    group kernels into the code-object cache that travels with the library."""
-    d = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "spec_trees.json")))
-    trees = [spec_amd.pkg1_tree(k) for k in (1, 2, 3)] + [shapes_tree(), nested_struct_tree()]
-    trees += [Tree.from_fields(d[k]) for k in ("pkg1.Message", "pmpx.Message", "prpc.Message", "pmpx.ChannelOpen")]
-    base = spec_amd.pkg1_tree()
-    for shift in (1, 4, 9):  # test_errmask_cross_kind's readers
-        fields = []
-        for p, tag, k, e, par in base.to_fields():
-            if 1 <= k <= 15:
-                k = (k - 1 + shift) % 15 + 1
-            fields.append((p, tag, k, e, par))
-        trees.append(Tree.from_fields(fields))
-    trees.append(spec_amd.Tree(Message("message1", [("f1", 1, Kind.INT32), ("f2", 2, Kind.INT32),
-                                                    ("f3", 3, Kind.INT32), ("l", 4, ListOf(Kind.STRING))])))
-    return trees
+    return precompiled_trees(SPEC_TREES_JSON)

@@ -92,11 +92,14 @@ def test_jit_source_compiles_for_gfx950():
     L = spec_amd.lib()
     s = spec_amd.FLAT16.c
     assert L.spec_decode_flat_jit_compile(C.byref(s), 256 << 20, 1 << 20) > 1000
-    # no fast path: repeated tags / tags > 255 / too many fields => generic kernel, nothing compiled
+    # no fast path: repeated tags => generic kernel, nothing compiled
     dup = spec_amd.Schema([(5, spec_amd.Kind.INT32), (5, spec_amd.Kind.INT64)])
     assert L.spec_decode_flat_jit_compile(C.byref(dup.c), 1000, 10) == 0
+    # big tables (a tag > 255) and wide schemas (> 24 fields) have one (decode_core.hpp fast_wide)
     big = spec_amd.Schema([(300, spec_amd.Kind.INT32)])
-    assert L.spec_decode_flat_jit_compile(C.byref(big.c), 1000, 10) == 0
+    assert L.spec_decode_flat_jit_compile(C.byref(big.c), 1000, 10) > 1000
+    wide = spec_amd.Schema([(i + 1, spec_amd.Kind.INT64) for i in range(64)])
+    assert L.spec_decode_flat_jit_compile(C.byref(wide.c), 1000, 10) > 1000
 
 
 def test_encode_jit_source_compiles_for_gfx950():

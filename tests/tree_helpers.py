@@ -4,28 +4,13 @@ from __future__ import annotations
 
 import numpy as np
 
-from oracle import oracle as O
+from oracle import oracle as O  # noqa: F401
+from oracle.tree_oracle import as_list, mismatches, oracle_decode, oracle_encode, oracle_fields  # noqa: F401
 from spec_amd.schema import Kind
 from spec_amd.tree import (ROLE_BEGIN, ROLE_ERRMASK, ROLE_PRESENT, ROLE_STATUS, ROLE_TYPE, ROLE_VALUE, ListOf, Message,
                            Struct, Tree)
 
 SPAN_KINDS = (Kind.STRING, Kind.BYTES, Kind.ANY)
-
-
-def oracle_fields(tree: Tree) -> np.ndarray:
-    return O.tree_fields([(f.tag, int(f.kind), int(f.elem), f.parent) for f in tree.fields])
-
-
-def as_list(tree: Tree, d: dict, fill=None):
-    return [d.get(c.name, fill) for c in tree.columns]
-
-
-def oracle_encode(tree: Tree, cols: dict, heaps: dict, n: int):
-    return O.encode_tree_batch(oracle_fields(tree), as_list(tree, cols), as_list(tree, heaps), n)
-
-
-def oracle_decode(tree: Tree, stream, ends):
-    return O.decode_tree_batch(oracle_fields(tree), stream, ends)
 
 
 def span_bytes(col: np.ndarray, buf: np.ndarray):
@@ -58,13 +43,6 @@ def roundtrip_mismatches(tree: Tree, inputs: dict, heaps: dict, got: list, strea
     return bad
 
 
-def mismatches(tree: Tree, got: list, want: list):
-    bad = []
-    for c, g, w in zip(tree.columns, got, want):
-        g = np.asarray(g)
-        if g.shape != w.shape or not np.array_equal(g, w):
-            bad.append(c.name)
-    return bad
 
 
-from tests.jit_trees import nested_struct_tree, shapes_tree  # noqa: E402,F401  (trees used by the tests)
+from spec_amd.tree_catalog import nested_struct_tree, shapes_tree  # noqa: E402,F401  (trees used by the tests)
