@@ -250,3 +250,25 @@ def test_native_shard_rejects_duplicate_devices():
         NativeShard([0, 0])
     with pytest.raises(SpecError):
         NativeShard([0], force_comm=True, shared=True)
+
+
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,
+                    reason="needs two GPUs (the RCCL gather across devices; the one-GPU pool cannot run it)")
+def test_native_shard_two_devices_rccl(dev):
+    """Two real devices, one RCCL communicator: decode from host + gather across xGMI and the
+    sharded encode, against the oracle."""
+    n = 200_001
+    sh = NativeShard([0, 1])
+    assert sh.has_comm
+    cols, heaps = workload.flat16(n, seed=44)
+    stream, ends = O.encode_flat_batch(FLAT16.tags, FLAT16.kinds, cols, [heaps.get(f) for f in range(16)], n)
+    packs, bases = sh.decode_host(FLAT16, stream, ends)
+    gathered = sh.gather(packs, root=1)
+    sh.sync()
+    want, wst = O.decode_flat_batch(FLAT16.tags, FLAT16.kinds, stream, ends, FLAT16.widths, 8)
+    _check_gathered(sh, gathered, n, ends, bases, want, wst)
+    nrec = [sh.bounds(n, k)[1] - sh.bounds(n, k)[0] for k in range(2)]
+    shards, host = _device_shards(sh, 2, 31, nrec)
+    outs, e2, totals, b2 = sh.encode(FLAT16, shards)
+    sh.sync()
+    _check_encode(sh, shards, host, outs, e2, totals, b2)

@@ -9,4 +9,7 @@ echo "== nested prof"
 bash tools/prof_nested.sh gpurun_out/$TAG/nested > gpurun_out/$TAG/nested.log 2>&1 || { tail -n 20 gpurun_out/$TAG/nested.log; exit 1; }
 echo "== tree prof"
 bash tools/prof_tree.sh gpurun_out/$TAG/tree > gpurun_out/$TAG/tree.log 2>&1 || { tail -n 20 gpurun_out/$TAG/tree.log; exit 1; }
+echo "== tree encode/decode trace"
+bash tools/gpu_tree_enc.sh $TAG/tree_trace > gpurun_out/$TAG/tree_trace.log 2>&1 || { tail -n 20 gpurun_out/$TAG/tree_trace.log; exit 1; }
+tail -n 3 gpurun_out/$TAG/tree_trace/enc_trace.txt
 echo done
