@@ -687,9 +687,13 @@ void gen_write_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
             o << "  {\n    emit_struct(em, B, D, " << fi << "u, row);\n" << mark << "  }\n";
         } else if (F.kind == spec::K_MESSAGE) {
             o << "  if (pr" << k << ") {\n    B.pos[" << F.table << "][row] = em.pos;\n    em.skip(sz" << k << ");\n" << mark
-              << "  }\n";
+              << "  } else {\n    B.pos[" << F.table << "][row] = ~0ull; // absent: its row is not written\n  }\n";
         } else if (F.kind == spec::K_LIST) {
             const int y = F.table;
+            o << "  if (!pr" << k << ") { // absent: rows in its range (if any) are not written\n"
+              << "    bool lerr = false;\n    uint32_t j0, j1;\n"
+              << "    list_span(B, D, " << y << "u, row, j0, j1, lerr);\n"
+              << "    for (uint32_t j = j0; j < j1; j++) B.pos[" << y << "][j] = ~0ull;\n  }\n";
             o << "  if (pr" << k << ") {\n"
               << "    bool lerr = false;\n    uint32_t j0, j1;\n"
               << "    list_span(B, D, " << y << "u, row, j0, j1, lerr);\n"
@@ -720,28 +724,28 @@ void gen_write_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
     }
     o << "  }\n"
       << "  em.rvarint(data);\n  em.rvarint((uint64_t)nf * (big ? 6 : 3));\n"
-      << "  em.put1(big ? T_BIG_MESSAGE : T_MESSAGE);\n  em.finish();\n}\n"
-      << "extern \"C\" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void spec_tree_write_" << t
-      << "(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x, uint64_t rows) {\n"
-      << "  const TreeDesc &D = *Dp;\n  const TreeBufs &B = *Bp;\n"
-      << "  if (!B.out || *B.err || *B.total > B.out_cap) return;\n"
-      << "  for (uint64_t row = grid_first(); row < rows; row += grid_stride()) {\n"
-      << "    const uint64_t start = x == 0 ? B.offsets[row] : B.pos[x][row];\n"
-      << "    if (start == ~0ull) continue; // a row no written owner placed\n"
-      << "    if (x == 0 && B.ends_out) B.ends_out[row] = start + B.size[0][row];\n"
-      << "    BEmit em{B.out, start, start};\n"
-      << "    gen_wrow_" << t << "(em, D, B, row, start);\n"
-      << "  }\n}\n";
+      << "  em.put1(big ? T_BIG_MESSAGE : T_MESSAGE);\n  em.finish();\n}\n";
+    // a row no owner placed (its own owner absent or unplaced): its children are not written either
+    o << "__device__ __forceinline__ void gen_unplace_" << t << "(const TreeDesc &D, const TreeBufs &B, uint64_t row) {\n";
+    for (uint32_t k = 0; k < T.nd; k++) {
+        const TField &F = D.f[D.direct[T.d0 + k]];
+        if (F.kind == spec::K_MESSAGE) {
+            o << "  B.pos[" << F.table << "][row] = ~0ull;\n";
+        } else if (F.kind == spec::K_LIST) {
+            o << "  { bool lerr = false; uint32_t j0, j1; list_span(B, D, " << F.table << "u, row, j0, j1, lerr);\n"
+              << "    for (uint32_t j = j0; j < j1; j++) B.pos[" << F.table << "][j] = ~0ull; }\n";
+        }
+    }
+    o << "}\n";
 }
 
 // The generated writer's size pass for a message table (tree.hip tree_size_kernel with constant
 // kinds, columns and tags): every column read first, then the encoded sizes, IsBigMessage.
 void gen_size_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
     const TTable &T = D.t[t];
-    o << "extern \"C\" __global__ __launch_bounds__(256) void spec_tree_size_" << t
-      << "(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x, uint64_t rows) {\n"
-      << "  const TreeDesc &D = *Dp;\n  const TreeBufs &B = *Bp;\n  bool err = false;\n"
-      << "  for (uint64_t row = grid_first(); row < rows; row += grid_stride()) {\n";
+    o << "__device__ __forceinline__ void gen_srow_" << t
+      << "(const TreeDesc &D, const TreeBufs &B, uint32_t x, uint64_t row, bool &err) {\n"
+      << "  {\n";
     for (uint32_t k = 0; k < T.nd; k++) {
         const TField &F = D.f[D.direct[T.d0 + k]];
         if ((F.kind >= spec::K_BOOL && F.kind <= spec::K_BYTES) || F.kind == spec::K_ANY)
@@ -801,7 +805,7 @@ void gen_size_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
       << "    const uint64_t total = data + tsize + vlen64(data) + vlen64(tsize) + 1;\n"
       << "    if (total > 0xffffffffull) err = true;\n"
       << "    B.size[x][row] = (uint32_t)total;\n"
-      << "  }\n  if (err) *B.err = 1;\n}\n";
+      << "  }\n}\n";
 }
 
 std::string generate_tree(const TreeDesc &D, bool *has) {
@@ -812,6 +816,42 @@ std::string generate_tree(const TreeDesc &D, bool *has) {
             gen_write_table(o, D, t);
             gen_size_table(o, D, t);
         }
+    // level-fused launches (tree_core.hpp TableSet): blockIdx.y = the set's table
+    o << "extern \"C\" __global__ __launch_bounds__(256) void spec_tree_size_set(const TreeDesc *Dp, const TreeBufs *Bp, "
+         "TableSet s) {\n"
+      << "  const TreeDesc &D = *Dp;\n  const TreeBufs &B = *Bp;\n  bool err = false;\n"
+      << "  const uint32_t x = s.t[blockIdx.y];\n  const uint64_t rows = B.rows[x];\n"
+      << "  switch (x) {\n";
+    for (uint32_t t = 0; t < D.ntables; t++)
+        if (D.t[t].shape == spec::SHAPE_MESSAGE)
+            o << "  case " << t << ": for (uint64_t row = grid_first(); row < rows; row += grid_stride()) gen_srow_" << t
+              << "(D, B, x, row, err); break;\n";
+    o << "  default:\n"
+      << "    for (uint64_t row = grid_first(); row < rows; row += grid_stride()) {\n"
+      << "      const uint64_t total = size_row_shaped(D, B, x, row, err);\n"
+      << "      if (total > 0xffffffffull) err = true;\n"
+      << "      B.size[x][row] = (uint32_t)total;\n"
+      << "    }\n  }\n  if (err) *B.err = 1;\n}\n";
+    o << "extern \"C\" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void spec_tree_write_set("
+         "const TreeDesc *Dp, const TreeBufs *Bp, TableSet s) {\n"
+      << "  const TreeDesc &D = *Dp;\n  const TreeBufs &B = *Bp;\n"
+      << "  if (!B.out || *B.err || *B.total > B.out_cap) return;\n"
+      << "  const uint32_t x = s.t[blockIdx.y];\n  const uint64_t rows = B.rows[x];\n"
+      << "  switch (x) {\n";
+    for (uint32_t t = 0; t < D.ntables; t++)
+        if (D.t[t].shape == spec::SHAPE_MESSAGE)
+            o << "  case " << t << ":\n"
+              << "    for (uint64_t row = grid_first(); row < rows; row += grid_stride()) {\n"
+              << (D.t[t].rel == spec::REL_MANY ? "      if (!list_row_covered(D, B, x, row)) continue;\n" : "")
+              << "      const uint64_t start = x == 0 ? B.offsets[row] : B.pos[x][row];\n"
+              << "      if (start == ~0ull) { gen_unplace_" << t << "(D, B, row); continue; }\n"
+              << "      if (x == 0 && B.ends_out) B.ends_out[row] = start + B.size[0][row];\n"
+              << "      BEmit em{B.out, start, start};\n"
+              << "      gen_wrow_" << t << "(em, D, B, row, start);\n"
+              << "    }\n    break;\n";
+    o << "  default:\n"
+      << "    for (uint64_t row = grid_first(); row < rows; row += grid_stride()) write_row_shaped(D, B, x, row);\n"
+      << "  }\n}\n";
     for (uint32_t x = 0; x < D.ntables; x++) {
         const TTable &T = D.t[x];
         has[x] = false;
@@ -871,9 +911,9 @@ std::string generate_tree(const TreeDesc &D, bool *has) {
 
 struct TreeEntry {
     hipModule_t mod = nullptr;
-    // [x]: decode, staged rows; [TREE_MAX_T + x]: decode, rows from HBM; [2 TREE_MAX_T + t]: write;
-    // [3 TREE_MAX_T + t]: size
-    hipFunction_t fn[4 * spec::TREE_MAX_T] = {};
+    // [x]: decode, staged rows; [TREE_MAX_T + x]: decode, rows from HBM; [4 TREE_MAX_T], [+1]: the
+    // level-fused encode size / write kernels
+    hipFunction_t fn[4 * spec::TREE_MAX_T + 2] = {};
     bool failed = false;
 };
 std::unordered_map<std::string, TreeEntry> g_tree_cache;
@@ -892,7 +932,7 @@ long long jit_compile_only_tree(const TreeDesc &D) {
 
 // The schema-specialised group kernels of a tree: fn[x] for each group root x that has one
 // (nullptr where the run-time kernel runs), fn[TREE_MAX_T + x] its variant without staging,
-// fn[2 TREE_MAX_T + t] / fn[3 TREE_MAX_T + t] the writer / size pass of message table t; nullptr
+// fn[4 TREE_MAX_T] / fn[4 TREE_MAX_T + 1] the level-fused size / write kernels of the encoder; nullptr
 // when the JIT is off or failed.
 const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
     if (!enabled()) return nullptr;
@@ -920,12 +960,9 @@ const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
         TreeEntry e;
         const std::vector<char> code = compile_source(src, TREE);
         bool ok = !code.empty() && hipModuleLoadData(&e.mod, code.data()) == hipSuccess;
-        for (uint32_t t = 0; ok && t < D.ntables; t++)
-            if (D.t[t].shape == SHAPE_MESSAGE)
-                ok = hipModuleGetFunction(&e.fn[2 * TREE_MAX_T + t], e.mod,
-                                          ("spec_tree_write_" + std::to_string(t)).c_str()) == hipSuccess &&
-                     hipModuleGetFunction(&e.fn[3 * TREE_MAX_T + t], e.mod,
-                                          ("spec_tree_size_" + std::to_string(t)).c_str()) == hipSuccess;
+        if (ok)
+            ok = hipModuleGetFunction(&e.fn[4 * TREE_MAX_T], e.mod, "spec_tree_size_set") == hipSuccess &&
+                 hipModuleGetFunction(&e.fn[4 * TREE_MAX_T + 1], e.mod, "spec_tree_write_set") == hipSuccess;
         for (uint32_t x = 0; ok && x < D.ntables; x++) {
             if (!has[x]) continue;
             const std::string name = "spec_tree_group_" + std::to_string(x);

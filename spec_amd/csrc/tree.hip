@@ -202,7 +202,8 @@ __global__ __launch_bounds__(SCAN_T) void scan_tiles_kernel(const uint32_t *in, 
 }
 
 // pass 2: exclusive scan of the tile sums (one workgroup), total
-__global__ __launch_bounds__(SCAN_T) void scan_top_kernel(uint64_t *tile_sums, uint64_t ntiles, uint64_t *total) {
+__global__ __launch_bounds__(SCAN_T) void scan_top_kernel(uint64_t *tile_sums, uint64_t ntiles, uint64_t *total,
+                                                          const uint32_t *err) {
     __shared__ uint64_t sh[17];
     uint64_t carry = 0;
     for (uint64_t b = 0; b < ntiles; b += SCAN_T) {
@@ -213,7 +214,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_top_kernel(uint64_t *tile_sums, u
         if (i < ntiles) tile_sums[i] = carry + e;
         carry += tot;
     }
-    if (threadIdx.x == 0) *total = carry;
+    if (threadIdx.x == 0) *total = err && *err ? ~0ull : carry; // an encoder error: all-ones
 }
 
 // pass 3: per tile, the exclusive prefix of every element: into out32 (u32, + out32[n] = total)
@@ -253,18 +254,15 @@ __global__ __launch_bounds__(256) void tree_pos_fill_kernel(PosFill f) {
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) p[i] = ~0ull;
 }
 
-__global__ void tree_err_kernel(const uint32_t *err, uint64_t *total) {
-    if (*err) *total = ~0ull;
-}
-
 size_t scan_ws_bytes(uint64_t n) { return ((n + SCAN_TILE - 1) / SCAN_TILE + 1) * sizeof(uint64_t); }
 
-// exclusive scan of in[0, n) (in place allowed for out32); *total (device) = the sum
+// exclusive scan of in[0, n) (in place allowed for out32); *total (device) = the sum, or all-ones
+// when *err (optional) is set
 int launch_scan(const uint32_t *in, uint64_t n, uint32_t *out32, uint64_t *out64, uint64_t *ends64, uint64_t *ws,
-                uint64_t *total, hipStream_t st) {
+                uint64_t *total, const uint32_t *err, hipStream_t st) {
     const uint64_t tiles = std::max<uint64_t>(1, (n + SCAN_TILE - 1) / SCAN_TILE);
     hipLaunchKernelGGL(scan_tiles_kernel, dim3((unsigned)tiles), dim3(SCAN_T), 0, st, in, n, ws);
-    hipLaunchKernelGGL(scan_top_kernel, dim3(1), dim3(SCAN_T), 0, st, ws, tiles, total);
+    hipLaunchKernelGGL(scan_top_kernel, dim3(1), dim3(SCAN_T), 0, st, ws, tiles, total, err);
     hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)tiles), dim3(SCAN_T), 0, st, in, n, ws, total, out32, out64,
                        ends64);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -498,12 +496,19 @@ struct EncWs {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// [desc | bufs | err] first and contiguous: ONE upload (from a pinned slot) sets all three, the
+// error word to zero
+constexpr size_t ENC_HEAD_DESC = 0;
+constexpr size_t ENC_HEAD_BUFS = (sizeof(TreeDesc) + 255) & ~(size_t)255;
+constexpr size_t ENC_HEAD_ERR = ENC_HEAD_BUFS + ((sizeof(TreeBufs) + 255) & ~(size_t)255);
+constexpr size_t ENC_HEAD = ENC_HEAD_ERR + 256;
+
 size_t enc_plan(const Layout &L, const uint64_t *rows, EncWs &w) {
     size_t o = 0;
-    w.desc = o;
-    o += align256(sizeof(TreeDesc));
-    w.bufs = o;
-    o += align256(sizeof(TreeBufs));
+    w.desc = ENC_HEAD_DESC;
+    w.bufs = ENC_HEAD_BUFS;
+    w.err = ENC_HEAD_ERR;
+    o = ENC_HEAD;
     for (uint32_t x = 0; x < L.nt; x++) {
         w.size[x] = o;
         o += align256(std::max<uint64_t>(rows[x], 1) * sizeof(uint32_t));
@@ -514,8 +519,6 @@ size_t enc_plan(const Layout &L, const uint64_t *rows, EncWs &w) {
     o += align256(std::max<uint64_t>(rows[0], 1) * sizeof(uint64_t));
     w.scan = o;
     o += align256(scan_ws_bytes(rows[0]));
-    w.err = o;
-    o += 256;
     w.total = o;
     o += 256;
     return o;
@@ -537,8 +540,9 @@ struct UploadRing {
 std::mutex g_ring_mu;
 UploadRing g_rings[64];
 
-// copies [desc | bufs] to the device workspace on st from a pinned slot; false on a HIP error
-bool upload_block(const TreeDesc &desc, const TreeBufs &bufs, void *ddesc, void *dbufs, hipStream_t st) {
+// copies the workspace head [desc | bufs | err = 0] (ENC_HEAD bytes) to the device on st from a
+// pinned slot; false on a HIP error
+bool upload_head(const TreeDesc &desc, const TreeBufs &bufs, void *dhead, hipStream_t st) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
     std::lock_guard<std::mutex> lk(g_ring_mu);
@@ -546,7 +550,7 @@ bool upload_block(const TreeDesc &desc, const TreeBufs &bufs, void *ddesc, void 
     UploadRing::Slot &S = R.slot[R.next];
     R.next = (R.next + 1) % UploadRing::SLOTS;
     if (!S.p) {
-        if (hipHostMalloc((void **)&S.p, sizeof(TreeDesc) + sizeof(TreeBufs), hipHostMallocDefault) != hipSuccess ||
+        if (hipHostMalloc((void **)&S.p, ENC_HEAD, hipHostMallocDefault) != hipSuccess ||
             hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess) {
             S.p = nullptr;
             return false;
@@ -554,10 +558,10 @@ bool upload_block(const TreeDesc &desc, const TreeBufs &bufs, void *ddesc, void 
     } else if (hipEventSynchronize(S.ev) != hipSuccess) { // the slot's previous copy has run
         return false;
     }
-    memcpy(S.p, &desc, sizeof(TreeDesc));
-    memcpy(S.p + sizeof(TreeDesc), &bufs, sizeof(TreeBufs));
-    return hipMemcpyAsync(ddesc, S.p, sizeof(TreeDesc), hipMemcpyHostToDevice, st) == hipSuccess &&
-           hipMemcpyAsync(dbufs, S.p + sizeof(TreeDesc), sizeof(TreeBufs), hipMemcpyHostToDevice, st) == hipSuccess &&
+    memset(S.p, 0, ENC_HEAD);
+    memcpy(S.p + ENC_HEAD_DESC, &desc, sizeof(TreeDesc));
+    memcpy(S.p + ENC_HEAD_BUFS, &bufs, sizeof(TreeBufs));
+    return hipMemcpyAsync(dhead, S.p, ENC_HEAD, hipMemcpyHostToDevice, st) == hipSuccess &&
            hipEventRecord(S.ev, st) == hipSuccess;
 }
 } // namespace
@@ -634,39 +638,56 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
     B->err = (uint32_t *)(ws + w.err);
     const TreeDesc *Dd = (const TreeDesc *)(ws + w.desc);
     TreeBufs *Bd = (TreeBufs *)(ws + w.bufs);
-    bool ok = upload_block(L.desc, *B, ws + w.desc, Bd, st) &&
-              hipMemsetAsync(B->err, 0, sizeof(uint32_t), st) == hipSuccess;
+    bool ok = upload_head(L.desc, *B, ws, st);
     // the generated writers and size passes (jit.cpp) for message tables, else the run-time row kernels
     const hipFunction_t *jit = jit_tree_kernels(L.desc);
-    // sizes bottom-up (children before their owners: table order is pre-order)
-    for (int x = (int)L.nt - 1; ok && x >= 0; x--) {
-        if (!rows[x]) continue;
-        if (jit && jit[3 * TREE_MAX_T + x]) {
-            uint32_t xx = (uint32_t)x;
-            uint64_t r = rows[x];
-            void *args[] = {(void *)&Dd, (void *)&Bd, &xx, &r};
-            const hipError_t le =
-                hipModuleLaunchKernel(jit[3 * TREE_MAX_T + x], row_grid(rows[x]), 1, 1, TB, 1, 1, 0, st, args, nullptr);
-            if (le != hipSuccess) {
-                note_hip_error(le);
-                ok = false;
-            }
-            continue;
-        }
-        hipLaunchKernelGGL(tree_size_kernel, dim3(row_grid(rows[x])), dim3(TB), 0, st, Dd, Bd, (uint32_t)x, rows[x]);
+    // level-fused launches (tree_core.hpp TableSet) when the generated module has them: the
+    // tables of one height sized together (children have smaller heights), the tables of one
+    // depth written together (owners have smaller depths)
+    const bool sets = jit && jit[4 * TREE_MAX_T] && jit[4 * TREE_MAX_T + 1];
+    int height[TREE_MAX_T] = {0}, depth[TREE_MAX_T] = {0}, maxh = 0, maxd = 0;
+    for (uint32_t x = 1; x < L.nt; x++) depth[x] = depth[L.desc.t[x].parent] + 1;
+    for (int x = (int)L.nt - 1; x > 0; x--) {
+        const int par = L.desc.t[x].parent;
+        height[par] = std::max(height[par], height[x] + 1);
     }
-    // record offsets, ends, total
+    for (uint32_t x = 0; x < L.nt; x++) {
+        maxh = std::max(maxh, height[x]);
+        maxd = std::max(maxd, depth[x]);
+    }
+    auto launch_set = [&](hipFunction_t fn, const int *level, int lv) -> bool {
+        TableSet ts;
+        ts.n = 0;
+        uint64_t most = 0;
+        for (uint32_t x = 0; x < L.nt; x++)
+            if (level[x] == lv && rows[x]) {
+                ts.t[ts.n++] = x;
+                most = std::max(most, rows[x]);
+            }
+        if (!ts.n) return true;
+        void *args[] = {(void *)&Dd, (void *)&Bd, &ts};
+        const hipError_t le = hipModuleLaunchKernel(fn, row_grid(most), ts.n, 1, TB, 1, 1, 0, st, args, nullptr);
+        if (le != hipSuccess) note_hip_error(le);
+        return le == hipSuccess;
+    };
+    for (int h = 0; sets && ok && h <= maxh; h++) ok = launch_set(jit[4 * TREE_MAX_T], height, h);
+    // (no generated module: the run-time row kernels) sizes bottom-up (children before their
+    // owners: table order is pre-order)
+    for (int x = (int)L.nt - 1; !sets && ok && x >= 0; x--)
+        if (rows[x])
+            hipLaunchKernelGGL(tree_size_kernel, dim3(row_grid(rows[x])), dim3(TB), 0, st, Dd, Bd, (uint32_t)x, rows[x]);
+    // record offsets, total (all-ones on an encoder error)
     if (ok) {
         if (n) {
-            ok = launch_scan(B->size[0], n, nullptr, B->offsets, nullptr, (uint64_t *)(ws + w.scan), total, st) == 0;
+            ok = launch_scan(B->size[0], n, nullptr, B->offsets, nullptr, (uint64_t *)(ws + w.scan), total, B->err,
+                             st) == 0;
         } else {
             ok = hipMemsetAsync(total, 0, sizeof(uint64_t), st) == hipSuccess;
         }
     }
-    // an encoder error: total = all-ones
-    if (ok) hipLaunchKernelGGL(tree_err_kernel, dim3(1), dim3(1), 0, st, (const uint32_t *)B->err, total);
-    // child rows start unplaced: only rows their owner writes get a position
-    if (ok && out && L.nt > 1) {
+    // child rows start unplaced: only rows their owner writes get a position (the generated
+    // writers mark the rows under an absent or unplaced owner themselves)
+    if (!sets && ok && out && L.nt > 1) {
         PosFill pf;
         uint64_t most = 0;
         for (uint32_t x = 1; x < L.nt; x++) {
@@ -679,21 +700,10 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
             hipLaunchKernelGGL(tree_pos_fill_kernel, dim3(gx, L.nt - 1), dim3(256), 0, st, pf);
         }
     }
-    for (uint32_t x = 0; ok && out && x < L.nt; x++)
+    for (int d = 0; sets && ok && out && d <= maxd; d++) ok = launch_set(jit[4 * TREE_MAX_T + 1], depth, d);
+    for (uint32_t x = 0; !sets && ok && out && x < L.nt; x++)
         if (rows[x]) {
             const TTable &T = L.desc.t[x];
-            if (jit && jit[2 * TREE_MAX_T + x]) {
-                uint32_t xx = x;
-                uint64_t r = rows[x];
-                void *args[] = {(void *)&Dd, (void *)&Bd, &xx, &r};
-                const hipError_t le = hipModuleLaunchKernel(jit[2 * TREE_MAX_T + x], row_grid(rows[x]), 1, 1, TB, 1, 1, 0,
-                                                            st, args, nullptr);
-                if (le != hipSuccess) {
-                    note_hip_error(le);
-                    ok = false;
-                }
-                continue;
-            }
             const size_t lds = T.shape == SHAPE_MESSAGE ? (size_t)(TB / 64) * T.nd * 64 * sizeof(uint32_t) : 0;
             hipLaunchKernelGGL(tree_write_kernel, dim3(row_grid(rows[x])), dim3(TB), lds, st, Dd, Bd, x, rows[x]);
         }

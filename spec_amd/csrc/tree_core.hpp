@@ -793,4 +793,50 @@ __device__ __forceinline__ void emit_struct(BEmit &em, const TreeBufs &B, const 
     }
 }
 
+// ---- level-fused encode launches (jit.cpp spec_tree_size_set / spec_tree_write_set) ---------
+// Tables with no size dependency between them (the same height: every child sized first) are
+// sized in ONE launch, tables at the same depth (every owner written first) written in one:
+// blockIdx.y picks the table of the set, the blocks stride over its rows.
+struct TableSet {
+    uint32_t n;
+    uint32_t t[TREE_MAX_T];
+};
+
+// the size of row `row` of a VALUE or STRUCT table (tree.hip tree_size_kernel's run-time rules)
+__device__ __forceinline__ uint64_t size_row_shaped(const TreeDesc &D, const TreeBufs &B, uint32_t x, uint64_t row,
+                                                    bool &err) {
+    const TTable &T = D.t[x];
+    if (T.shape == SHAPE_VALUE) {
+        const TField &F = D.f[T.field];
+        return value_size(B, D, F.col, F.elem, row, err);
+    }
+    return struct_size(B, D, T.field, row, err);
+}
+
+// A list table's rows its owners' BEGIN ranges cover: [begin[0], begin[owner rows]) (the writers
+// check BEGIN is monotonic: an encoder error otherwise).  Rows outside belong to no owner and are
+// not written; every row inside gets its position (or ~0: an absent / unplaced owner) from its
+// owner's write, so the level-fused writers need no position fill first.
+__device__ __forceinline__ bool list_row_covered(const TreeDesc &D, const TreeBufs &B, uint32_t y, uint64_t row) {
+    const uint32_t *b = (const uint32_t *)B.cols[D.t[y].begin_col];
+    return row >= b[0] && row < b[B.rows[D.t[y].parent]];
+}
+
+// the bytes of row `row` of a VALUE or STRUCT table (list elements) at its position
+// (tree_write_kernel's rules)
+__device__ __forceinline__ void write_row_shaped(const TreeDesc &D, const TreeBufs &B, uint32_t x, uint64_t row) {
+    const TTable &T = D.t[x];
+    if (!list_row_covered(D, B, x, row)) return;
+    const uint64_t start = B.pos[x][row];
+    if (start == ~0ull) return; // a row no written owner placed
+    BEmit em{B.out, start, start};
+    if (T.shape == SHAPE_VALUE) {
+        const TField &F = D.f[T.field];
+        emit_value(em, B, D, F.col, F.elem, row);
+    } else {
+        emit_struct(em, B, D, T.field, row);
+    }
+    em.finish();
+}
+
 } // namespace spec

@@ -14,7 +14,7 @@ def short(name):
     return name.split("(")[0].split("::")[-1]
 
 
-ENC = ("tree_size", "scan_tiles", "scan_top", "scan_apply", "tree_err", "tree_pos_fill", "tree_write", "copyBuffer",
+ENC = ("tree_size", "spec_tree_size_set", "scan_tiles", "scan_top", "scan_apply", "tree_err", "tree_pos_fill", "tree_write", "copyBuffer",
        "fillBuffer")
 
 
