@@ -21,17 +21,16 @@ ENC = ("tree_size", "spec_tree_size_set", "scan_tiles", "scan_top", "scan_apply"
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    fills = [i for i, r in enumerate(rows) if "tree_pos_fill" in r["Kernel_Name"]]
-    if not fills:
-        print("no tree_pos_fill dispatch")
+    writes = [i for i, r in enumerate(rows) if "tree_write" in r["Kernel_Name"]]
+    if not writes:
+        print("no tree writer dispatch")
         return
-    f = fills[-1]
-    s = f
-    while s > 0 and any(k in rows[s - 1]["Kernel_Name"] for k in ENC) and "tree_write" not in rows[s - 1]["Kernel_Name"]:
+    e = writes[-1]
+    s = e
+    while s > 0 and any(k in rows[s - 1]["Kernel_Name"] for k in ENC):
         s -= 1
-    e = f
-    while e + 1 < len(rows) and "tree_write" in rows[e + 1]["Kernel_Name"]:
-        e += 1
+        if "tree_size" in rows[s]["Kernel_Name"] and s > 0 and "tree_write" in rows[s - 1]["Kernel_Name"]:
+            break  # the previous encode's writers end here
     total, prev = 0.0, None
     for r in rows[s:e + 1]:
         a, b = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
