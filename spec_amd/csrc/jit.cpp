@@ -152,9 +152,13 @@ std::string generate_decode(const spec_schema *s) {
     o << "#include \"decode_core.hpp\"\n";
     emit_spec(o, "GenSpec", s);
     const char *pers = spec::persistent_decode() ? "true" : "false";
-    o << "extern \"C\" __global__ __launch_bounds__(256) void spec_decode_flat_jit(spec::DecodeArgs a) {\n"
+    // schemas on decode_core.hpp fast_wide get kernels of their own names (traces tell them apart)
+    bool big = false;
+    for (uint32_t f = 0; f < s->nfields; f++) big = big || s->fields[f].tag > 255;
+    const char *w = (s->nfields > (uint32_t)spec::FAST_MAX_FIELDS || big) ? "_wide" : "";
+    o << "extern \"C\" __global__ __launch_bounds__(256) void spec_decode_flat" << w << "_jit(spec::DecodeArgs a) {\n"
       << "  spec::decode_flat_entry<" << pers << ", GenSpec>(a);\n}\n"
-      << "extern \"C\" __global__ __launch_bounds__(256) void spec_decode_flat_err_jit(spec::DecodeArgs a) {\n"
+      << "extern \"C\" __global__ __launch_bounds__(256) void spec_decode_flat" << w << "_err_jit(spec::DecodeArgs a) {\n"
       << "  spec::decode_flat_entry<" << pers << ", GenSpec, true>(a);\n}\n";
     return o.str();
 }
@@ -382,6 +386,11 @@ Entry load(const std::vector<char> &code, Prog p) {
                                {"spec_decode_nested_jit", "spec_decode_nested2_jit", "spec_decode_nested3_jit", nullptr},
                                {"spec_encode_nested_size_jit", "spec_encode_nested_write_jit", nullptr, nullptr}};
     bool ok = hipModuleLoadData(&e.mod, code.data()) == hipSuccess;
+    if (ok && p == DECODE && hipModuleGetFunction(&e.fn[0], e.mod, names[p][0]) != hipSuccess) {
+        (void)hipGetLastError(); // a wide / big-table schema (generate_decode): its own kernel names
+        names[p][0] = "spec_decode_flat_wide_jit";
+        names[p][1] = "spec_decode_flat_wide_err_jit";
+    }
     for (int i = 0; ok && i < 4; i++)
         if (names[p][i]) ok = hipModuleGetFunction(&e.fn[i], e.mod, names[p][i]) == hipSuccess;
     if (!ok) {
