@@ -737,6 +737,37 @@ def wide_leg(dev, n=1 << 20, seed=11):
     return res
 
 
+def _native_child(args, world, devices, q):
+    try:
+        res = native_shard_leg(args, world, devices)
+    except Exception as e:  # reported in the result line, never fatal
+        res = {"error": repr(e)[:300]}
+    q.put(res)
+
+
+def native_leg_isolated(args, world, devices, timeout=300.0):
+    """native_shard_leg in a fresh child process (spawned: its own HIP contexts and RCCL
+    communicator), so a failure or a hang there (e.g. a communicator that never forms on some
+    machine) cannot take the headline measurement with it: after `timeout` seconds the child is
+    killed and the leg reports an error."""
+    import multiprocessing as mp
+    import queue
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_native_child, args=(args, world, devices, q))
+    p.start()
+    try:
+        res = q.get(timeout=timeout)
+    except queue.Empty:
+        res = {"error": f"native leg did not finish in {timeout:.0f} s (child killed)"}
+    p.join(timeout=60)
+    if p.is_alive():
+        p.kill()
+        p.join()
+    return res
+
+
 def generic_leg(stream, ends, want_cols, want_status, avg_jit_ms):
     """The precompiled generic decode kernel (no schema specialisation: what schemas without a
     fast path run) on the headline batch; its columns must equal the specialised kernel's."""
@@ -1048,15 +1079,13 @@ def run(args, env):
                          f"C restatement of OpenMessageErr + 16 getters",
                "single_core_value": round(res[1], 2)}
 
-    # the native one-process multi-device leg (spec_shard_*): rank 0 drives every device while the
-    # other ranks wait on the rendezvous store (no GPU work of theirs runs meanwhile)
+    # the native one-process multi-device leg (spec_shard_*): a child of rank 0 drives every device
+    # while the ranks wait (the others on the rendezvous store: no GPU work of theirs runs meanwhile)
     if not args.no_native and not args.no_extras:
         if rank == 0:
-            try:
-                extras["native_shard"] = native_shard_leg(args, world, devices)
+            extras["native_shard"] = native_leg_isolated(args, world, devices)
+            if "columns_ok" in extras["native_shard"]:
                 checks["native_shard_columns"] = extras["native_shard"]["columns_ok"]
-            except Exception as e:
-                extras["native_shard"] = {"error": repr(e)[:300]}
         if dist is not None:
             import datetime
 
