@@ -307,7 +307,8 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
  *     spec_encode_flat: one whose total exceeds its capacity or errs writes nothing; the call
  *     then returns SPEC_E_CAPACITY / SPEC_E_ENCODE and moves no ends to the whole batch (the
  *     shards that fit hold shard-relative ends).  Asynchronous after the size passes;
- *   spec_shard_stream: device k's stream; spec_shard_sync: wait for every device's streams. */
+ *   spec_shard_stream: device k's stream; spec_shard_sync: wait for every device's streams.
+ * A spec_shard is driven by one host thread at a time (it starts its own per-device threads). */
 #define SPEC_SHARD_MAX_DEVICES 16
 #define SPEC_SHARD_FORCE_COMM 1u
 #define SPEC_SHARD_SHARED 2u

@@ -272,3 +272,25 @@ def test_native_shard_two_devices_rccl(dev):
     outs, e2, totals, b2 = sh.encode(FLAT16, shards)
     sh.sync()
     _check_encode(sh, shards, host, outs, e2, totals, b2)
+
+
+@pytest.mark.parametrize("nshard", [1, 3])
+def test_native_shard_decode_device_resident(dev, nshard):
+    """spec_shard_decode: device-resident shards (what spec_shard_encode leaves, ends made
+    shard-relative) decoded into packed buffers == the input columns and the oracle's decode."""
+    devs, _ = _devices(nshard)
+    sh = NativeShard(devs, shared=True)
+    nrec = [5000 + 37 * k for k in range(nshard)]
+    shards, host = _device_shards(sh, nshard, 77, nrec)
+    outs, ends, totals, bases = sh.encode(FLAT16, shards)
+    streams = [o[:t] for o, t in zip(outs, totals)]
+    rel = [(e[:m] - b).contiguous() for e, m, b in zip(ends, nrec, bases)]
+    packs = [PackedColumns(FLAT16, m, torch.device("cuda", d)) for m, d in zip(nrec, devs)]
+    sh.decode(FLAT16, streams, rel, packs)
+    sh.sync()
+    for k, (cols, heaps) in enumerate(host):
+        st, en = O.encode_flat_batch(FLAT16.tags, FLAT16.kinds, cols, [heaps.get(f) for f in range(16)], nrec[k])
+        want, wst = O.decode_flat_batch(FLAT16.tags, FLAT16.kinds, st, en, FLAT16.widths, 8)
+        assert np.array_equal(packs[k].status.cpu().numpy(), wst)
+        for f in range(16):
+            assert np.array_equal(packs[k].cols[f].cpu().numpy(), want[f]), (k, f)
