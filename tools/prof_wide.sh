@@ -1,0 +1,12 @@
+#!/bin/bash
+# Wide / big-tag flat decode kernels: rocprofv3 kernel stats + PMC passes of tools/bench_wide.py.
+# Usage (GPU box): bash tools/prof_wide.sh OUTDIR
+set -o pipefail
+OUT=${1:-gpurun_out/wide}
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 tools/bench_wide.py > $OUT/prof.log 2>&1 || { tail -n 20 $OUT/prof.log; exit 1; }
+find $OUT/prof -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats.csv \;
+cut -d, -f1-4 $OUT/kernel_stats.csv | head -n 8
+bash tools/pmc.sh $OUT/pmc "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY" -- python3 tools/bench_wide.py > $OUT/pmc.log 2>&1 || { tail -n 20 $OUT/pmc.log; exit 1; }
+tail -n 80 $OUT/pmc.log
