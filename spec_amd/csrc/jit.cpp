@@ -941,14 +941,37 @@ std::string generate_tree(const TreeDesc &D, bool *has) {
           << "  });\n"
           << "}\n";
     }
+    // level-fused list groups: the groups one decode level holds (lists owned by the previous
+    // level's groups, rows from HBM) in ONE launch, blockIdx.y picking the group — each group is
+    // a chain of dependent loads per row, so side by side their latencies overlap
+    // (one launch for all of them: split by register budget — lists of values / structs at ~40
+    // VGPRs, lists of messages at ~120 — the two launches ran back to back, 75.5 vs 70.5 us for
+    // pkg1; amdgpu_waves_per_eu 6 or 8 spills: 86-87 us)
+    {
+        o << "extern \"C\" __global__ __launch_bounds__(256) void spec_tree_group_set"
+          << "(const TreeDesc *Dp, const TreeBufs *Bp, TableSet ts, uint32_t wave_bytes) {\n"
+          << "  const TreeDesc &D = *Dp;\n  const TreeBufs &B = *Bp;\n"
+          << "  const uint32_t x = ts.t[blockIdx.y];\n  const uint64_t rows = dec_rows(D, B, x);\n"
+          << "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+          << "  uint2 *gr = (uint2 *)(smem + (threadIdx.x >> 6) * wave_bytes) + (threadIdx.x & 63);\n"
+          << "  switch (x) {\n";
+        for (uint32_t x = 1; x < D.ntables; x++)
+            if (has[x])
+                o << "  case " << x << ":\n"
+                  << "    tree_rows_global(B, x, rows, [&](const GlobalSrc &s, uint64_t row, long long lo, long long hi, "
+                     "bool panic) {\n"
+                  << "      gen_row_" << x << "(s, D, B, row, lo, hi, panic, gr);\n"
+                  << "    });\n    break;\n";
+        o << "  default: break;\n  }\n}\n";
+    }
     return o.str();
 }
 
 struct TreeEntry {
     hipModule_t mod = nullptr;
     // [x]: decode, staged rows; [TREE_MAX_T + x]: decode, rows from HBM; [4 TREE_MAX_T], [+1]: the
-    // level-fused encode size / write kernels
-    hipFunction_t fn[4 * spec::TREE_MAX_T + 2] = {};
+    // level-fused encode size / write kernels; [+2]: the level-fused list-group decode kernel
+    hipFunction_t fn[4 * spec::TREE_MAX_T + 3] = {};
     bool failed = false;
 };
 std::unordered_map<std::string, TreeEntry> g_tree_cache;
@@ -967,8 +990,8 @@ long long jit_compile_only_tree(const TreeDesc &D) {
 
 // The schema-specialised group kernels of a tree: fn[x] for each group root x that has one
 // (nullptr where the run-time kernel runs), fn[TREE_MAX_T + x] its variant without staging,
-// fn[4 TREE_MAX_T] / fn[4 TREE_MAX_T + 1] the level-fused size / write kernels of the encoder; nullptr
-// when the JIT is off or failed.
+// fn[4 TREE_MAX_T] / fn[4 TREE_MAX_T + 1] the level-fused size / write kernels of the encoder,
+// fn[4 TREE_MAX_T + 2] the level-fused list-group decode kernel; nullptr when the JIT is off or failed.
 const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
     if (!enabled()) return nullptr;
     int dev = 0;
@@ -997,7 +1020,8 @@ const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
         bool ok = !code.empty() && hipModuleLoadData(&e.mod, code.data()) == hipSuccess;
         if (ok)
             ok = hipModuleGetFunction(&e.fn[4 * TREE_MAX_T], e.mod, "spec_tree_size_set") == hipSuccess &&
-                 hipModuleGetFunction(&e.fn[4 * TREE_MAX_T + 1], e.mod, "spec_tree_write_set") == hipSuccess;
+                 hipModuleGetFunction(&e.fn[4 * TREE_MAX_T + 1], e.mod, "spec_tree_write_set") == hipSuccess &&
+                 hipModuleGetFunction(&e.fn[4 * TREE_MAX_T + 2], e.mod, "spec_tree_group_set") == hipSuccess;
         for (uint32_t x = 0; ok && x < D.ntables; x++) {
             if (!has[x]) continue;
             const std::string name = "spec_tree_group_" + std::to_string(x);
