@@ -231,13 +231,14 @@ def time_decode(dec, steps, warmup, dist):
     return time.perf_counter() - t0
 
 
-def kernel_time_events(fn, reps, lead=None):
+def kernel_time_events(fn, reps, lead=None, spread=False):
     """Average per-launch duration from HIP events on the launch stream: one event pair around
     `reps` back-to-back launches (an event between every launch adds ~10 us of marker/flush to
     each interval, which the kernel trace does not see), plus the median of per-launch pairs.
     `lead` untimed launches go first: the GPU is busy (and at its working clock) on them while
     the host enqueues the timed ones, so the interval measures the GPU, not host submission.
-    (A spin kernel in front instead lets the chip drop its clock during the spin.)"""
+    (A spin kernel in front instead lets the chip drop its clock during the spin.)
+    spread=True also returns the 10th / 90th percentiles of the per-launch pairs."""
     s = torch.cuda.current_stream()
     for _ in range(reps if lead is None else lead):
         fn()
@@ -253,6 +254,8 @@ def kernel_time_events(fn, reps, lead=None):
         y.record(s)
     torch.cuda.synchronize()
     ms = sorted(x.elapsed_time(y) for x, y in evs)
+    if spread:
+        return a.elapsed_time(b) / reps, ms[len(ms) // 2], ms[len(ms) // 10], ms[(9 * len(ms)) // 10]
     return a.elapsed_time(b) / reps, ms[len(ms) // 2]
 
 
@@ -971,7 +974,7 @@ def run(args, env):
     ms_per_step = elapsed / args.steps * 1e3
 
     # per-launch kernel time on the launch stream (HIP events)
-    avg_ms, med_ms = kernel_time_events(dec, max(20, args.steps))
+    avg_ms, med_ms, p10_ms, p90_ms = kernel_time_events(dec, max(20, args.steps), spread=True)
     alg_bytes = stream_bytes + n * (8 + COLUMN_BYTES + 1)
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9
     read_only = (stream_bytes + 8 * n) / (avg_ms * 1e-3) / 1e9
@@ -1119,7 +1122,8 @@ def run(args, env):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": kname, "kernel_ms_avg": round(avg_ms, 5),
-                         "kernel_ms_median": round(med_ms, 5), "alg_bytes_per_launch": alg_bytes,
+                         "kernel_ms_median": round(med_ms, 5), "kernel_ms_p10": round(p10_ms, 5),
+                         "kernel_ms_p90": round(p90_ms, 5), "alg_bytes_per_launch": alg_bytes,
                          "read_only_gb_s": round(read_only, 1), "source_rev": rev, "traffic_rev": traffic_rev},
             "cpu_baseline": cpu,
             "correct": bool(all(checks.values())),
