@@ -566,16 +566,19 @@ __device__ __forceinline__ void nested_count_body(const NestedArgs &a) {
 // The count pass needs, per record, only OpenMessage's trailer and table, the list field's
 // table entry and the list's own trailer.  A Writer emits the table and trailer last and, for a
 // record whose list is its last field, the list's trailer right below the table: all within the
-// record's last few dozen bytes.  So instead of staging the whole span, each lane loads the 64
-// bytes [a, a + 64) (a = (end - 48) & ~15: at least the last 48 bytes) into its own LDS window
-// and parses from there; a read outside the window (big tables, a list followed by other fields,
-// malformed records) goes to HBM through the same range-checked loads GlobalSrc uses, so the
-// count is the same whatever the record looks like.  One 64-byte window per record touches one
-// or two 128-byte lines of the ~210-byte config-4 records instead of all of them.
-constexpr int TAIL_WIN = 64;
-// Windows sit TAIL_STRIDE = 17 dwords apart: lane i's byte k is in bank (17 i + k / 4) mod 32,
-// so the 32 lanes of a ds_write_b32 / ds_read group never share a bank at equal k (a 16-dword
-// stride put every other lane on the same 4 banks: 10.4 conflict cycles per LDS instruction).
+// record's last few dozen bytes.  So instead of staging the whole span, each lane loads the 40
+// bytes [a, a + 40) (a = (end - 32) & ~7: at least the last 32 bytes, 8-byte aligned so the
+// parse's qword reads stay in the window) into its own LDS window and parses from there; a read
+// outside the window (big tables, a list followed by other fields, malformed records) goes to HBM
+// through the same range-checked loads GlobalSrc uses, so the count is the same whatever the
+// record looks like.  The count is bound by the 128-byte lines the windows touch: 1 + 39/128 per
+// record on average (round 3's 64-byte window at a 16-byte boundary: 1 + 63/128).
+constexpr int TAIL_WIN = 40;
+constexpr int TAIL_BACK = 32; // bytes below the record end the window always holds
+// Windows sit TAIL_STRIDE = 11 dwords apart: lane i's byte k is in bank (11 i + k / 4) mod 32,
+// so the 32 lanes of a ds_write_b32 / ds_read group never share a bank at equal k (an even
+// stride of 16 dwords put every other lane on the same 4 banks: 10.4 conflict cycles per LDS
+// instruction, r02h).
 constexpr int TAIL_STRIDE = TAIL_WIN + 4;
 
 struct WinSrc {
@@ -627,19 +630,31 @@ __device__ __forceinline__ void nested_count_tail_body(const NestedArgs &a, uint
     if (hi < lo) hi = lo; // malformed ends: an empty record (make_group)
     uint32_t cnt = 0;
     if (base + lane < a.n) {
-        const uint64_t w0 = hi >= 48 ? (hi - 48) & ~15ull : 0;
+        const uint64_t w0 = hi >= TAIL_BACK ? (hi - TAIL_BACK) & ~7ull : 0;
         uint8_t *win = wins + threadIdx.x * TAIL_STRIDE;
-        uint4 v[TAIL_WIN / 16];
-#pragma unroll
-        for (int k = 0; k < TAIL_WIN / 16; k++) v[k] = win_piece(rsrc, w0 + 16 * k, a.stream_len);
-#pragma unroll
-        for (int k = 0; k < TAIL_WIN / 16; k++) {
-            uint32_t *d = (uint32_t *)(win + 16 * k);
-            d[0] = v[k].x;
-            d[1] = v[k].y;
-            d[2] = v[k].z;
-            d[3] = v[k].w;
+        static_assert(TAIL_WIN == 40, "two 16-byte pieces and one 8-byte piece");
+        const uint4 v0 = win_piece(rsrc, w0, a.stream_len), v1 = win_piece(rsrc, w0 + 16, a.stream_len);
+        const uint32_t o2 = (uint32_t)(w0 + 32);
+        uint32_t v2x, v2y;
+        if ((uint64_t)o2 + 8 <= a.stream_len) {
+            const auto q = __builtin_amdgcn_raw_buffer_load_b64(rsrc, o2, 0, 0);
+            v2x = q[0];
+            v2y = q[1];
+        } else {
+            v2x = buf_ld32(rsrc, o2, a.stream_len);
+            v2y = buf_ld32(rsrc, o2 + 4, a.stream_len);
         }
+        uint32_t *d = (uint32_t *)win;
+        d[0] = v0.x;
+        d[1] = v0.y;
+        d[2] = v0.z;
+        d[3] = v0.w;
+        d[4] = v1.x;
+        d[5] = v1.y;
+        d[6] = v1.z;
+        d[7] = v1.w;
+        d[8] = v2x;
+        d[9] = v2y;
         WinSrc s{(lds_u8 *)win, (long long)w0, GlobalSrc{a.stream, a.stream_len}};
         cnt = record_count(s, (long long)lo, (long long)hi, a);
     }
