@@ -50,6 +50,15 @@ __global__ __launch_bounds__(TB) void tree_group_kernel(const TreeDesc *Dp, cons
 // one owner row per thread: the apply pass's per-row element loads are the latency to hide
 constexpr int SCAN_T = 1024, SCAN_PER = 1, SCAN_TILE = SCAN_T * SCAN_PER;
 
+// A workgroup barrier that orders LDS only: the waves' global loads stay in flight across it
+// (__syncthreads' fence also covers global memory, so it waits for every outstanding load).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Exclusive block scan through LDS (lds_barrier: a caller's loads issued before it overlap it).
 __device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t *sh, uint64_t &block_total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint64_t incl = v;
@@ -59,7 +68,7 @@ __device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t *sh, uint64_
         if (lane >= d) incl += t;
     }
     if (lane == 63) sh[wave] = incl;
-    __syncthreads();
+    lds_barrier();
     if (threadIdx.x == 0) {
         uint64_t acc = 0;
         for (int w = 0; w < (int)(blockDim.x >> 6); w++) {
@@ -69,10 +78,10 @@ __device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t *sh, uint64_
         }
         sh[16] = acc;
     }
-    __syncthreads();
+    lds_barrier();
     const uint64_t r = sh[wave] + incl - v;
     block_total = sh[16];
-    __syncthreads();
+    lds_barrier();
     return r;
 }
 
@@ -146,7 +155,7 @@ __global__ __launch_bounds__(SCAN_T) void list_apply_kernel(const TreeDesc *Dp, 
     // scan (they do not depend on it): only the element ranges' positions wait for it
     const uint64_t r = base;
     const uint32_t v0 = r < rows ? cnt[r] : 0;
-    const uint4 h = v0 ? lh[r] : make_uint4(0, 0, 0, 0);
+    const uint4 h = r < rows ? lh[r] : make_uint4(0, 0, 0, 0); // with cnt, not after it
     const uint64_t t0 = v0 ? load_le64(gs, (long long)h.x) : 0, t1 = v0 ? load_le64(gs, (long long)h.x + 8) : 0;
     uint64_t tot;
     uint64_t p = m.ws[blockIdx.y][blockIdx.x] + block_scan(v0, sh, tot);

@@ -10,7 +10,7 @@ python3 - $f <<'PY'
 import csv, sys, collections
 d = collections.defaultdict(list)
 for r in csv.DictReader(open(sys.argv[1])):
-    n = r["Kernel_Name"].split("(")[0].split("::")[-1]
+    n = r["Kernel_Name"].replace("(anonymous namespace)", "anon").split("(")[0].split("::")[-1]
     if "tree" in n or "list_" in n or "scan" in n or "rows_out" in n:
         d[n].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 for n, v in sorted(d.items()):
