@@ -988,14 +988,15 @@ template <class P>
 __device__ __forceinline__ void encode_write_body(const EncodeArgs &a, uint8_t *smem) {
     uint64_t *wsum = (uint64_t *)smem;
     uint8_t *inv_order = smem + 8 * (ENC_BLOCK / 64);
-    const uint64_t total = a.block_sums[a.nblocks];
-    if (total > a.out_cap) return; // capacity error or encoder error (total == ~0)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (threadIdx.x < a.f.nfields) inv_order[a.f.order[threadIdx.x]] = (uint8_t)threadIdx.x;
-
     const uint64_t r = (uint64_t)blockIdx.x * ENC_BLOCK + threadIdx.x;
     const bool valid = r < a.n;
+    // the record's loads, the total and this block's offset all in flight together (the check
+    // that nothing is written after an error or a capacity overflow waits for the total only now)
     const typename P::Rec rec = P::load(a.f, valid ? r : a.n - 1);
+    const uint64_t total = a.block_sums[a.nblocks], blk_pre = a.block_sums[blockIdx.x];
+    if (total > a.out_cap) return; // capacity error or encoder error (total == ~0)
+    if (threadIdx.x < a.f.nfields) inv_order[a.f.order[threadIdx.x]] = (uint8_t)threadIdx.x;
     bool err = false;
     RecSize rs = P::size(a.f, rec, r, false, err);
     if (!valid) rs.total = 0;
@@ -1005,8 +1006,8 @@ __device__ __forceinline__ void encode_write_body(const EncodeArgs &a, uint8_t *
         if (lane >= o) x += y;
     }
     if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    uint64_t pre = a.block_sums[blockIdx.x];
+    lds_barrier(); // (heap loads still in flight)
+    uint64_t pre = blk_pre;
     for (int w = 0; w < wave; w++) pre += wsum[w];
     const uint64_t start = pre + x - rs.total;
     if (valid) a.ends[r] = a.ends_base + start + rs.total;

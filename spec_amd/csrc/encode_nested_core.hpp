@@ -336,14 +336,13 @@ template <class OP, class IP>
 __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a, uint8_t *smem) {
     uint64_t *wsum = (uint64_t *)smem;
     uint8_t *inv_outer = smem + 32, *inv_item = smem + 96;
-    const uint64_t total = a.block_sums[a.nblocks];
-    if (total > a.out_cap) return; // capacity error or encoder error (total == ~0)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     // blocks dealt to the 8 XCDs in contiguous shares (xcd = 1): neighbouring blocks, whose
     // outputs share a cache line at each boundary, write through one L2
     uint64_t blk = blockIdx.x;
     if (a.xcd) blk = (blockIdx.x & 7) * ((gridDim.x + 7) / 8) + (blockIdx.x >> 3);
     if (blk >= a.nblocks) return;
+    const uint64_t total = a.block_sums[a.nblocks], blk_pre = a.block_sums[blk];
     if (threadIdx.x < a.outer.nfields) inv_outer[a.outer.order[threadIdx.x]] = (uint8_t)threadIdx.x;
     if (threadIdx.x < a.item.nfields) inv_item[a.item.order[threadIdx.x]] = (uint8_t)threadIdx.x;
     uint32_t *pre = (uint32_t *)(smem + NENC_HEAD + wave * NENC_WAVE_LDS);
@@ -354,6 +353,8 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
     const uint64_t r0 = blk * NENC_BLOCK + threadIdx.x;
     const typename OP::Rec orec = OP::load(a.outer, r0 < a.n ? r0 : a.n - 1);
     const LaneRecord L = lane_record<IP>(a, pre, lane, false, err, blk, a.item_pre != nullptr);
+    // (checked once the loads above are in flight: nothing is written before this point)
+    if (total > a.out_cap) return; // capacity error or encoder error (total == ~0)
     wave_sync(); // the prefix (from the cache) is in LDS
     ListSize ls;
     RecSize rs = lane_record_size<OP>(a, L, orec, pre, false, err, ls);
@@ -364,8 +365,8 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
         if (lane >= o) x += y;
     }
     if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    uint64_t pre_b = a.block_sums[blk];
+    lds_barrier();
+    uint64_t pre_b = blk_pre;
     for (int w = 0; w < wave; w++) pre_b += wsum[w];
     const uint64_t start = pre_b + x - rs.total;
     if (L.valid) a.ends[L.r] = start + rs.total;

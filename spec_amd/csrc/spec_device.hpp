@@ -90,6 +90,14 @@ struct LdsSrc {
     __device__ __forceinline__ uint32_t d32(int p) const { return *(lds_u32 *)(lds + p); }
 };
 
+// A workgroup barrier that orders LDS only: the waves' global loads stay in flight across it
+// (__syncthreads' fence also covers global memory, so it waits for every outstanding load).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // A buffer load that straddles num_records returns 0 for the WHOLE access (not just the
 // bytes past the end), so the last partial word of a buffer is read bytewise.
 __device__ __forceinline__ uint32_t buf_ld32(__amdgpu_buffer_rsrc_t r, uint32_t off, uint64_t len) {

@@ -50,15 +50,8 @@ __global__ __launch_bounds__(TB) void tree_group_kernel(const TreeDesc *Dp, cons
 // one owner row per thread: the apply pass's per-row element loads are the latency to hide
 constexpr int SCAN_T = 1024, SCAN_PER = 1, SCAN_TILE = SCAN_T * SCAN_PER;
 
-// A workgroup barrier that orders LDS only: the waves' global loads stay in flight across it
-// (__syncthreads' fence also covers global memory, so it waits for every outstanding load).
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-// Exclusive block scan through LDS (lds_barrier: a caller's loads issued before it overlap it).
+// Exclusive block scan through LDS (lds_barrier, spec_device.hpp: a caller's loads issued before it
+// overlap it).
 __device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t *sh, uint64_t &block_total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint64_t incl = v;
