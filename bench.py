@@ -350,7 +350,7 @@ def nested_leg(n, seed, dev):
             "decode_gb_s": round(dec_alg / (dec_ms * 1e-3) / 1e9, 1),
             "decode_frac": round(dec_alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3),
             "decode_alg_bytes": int(dec_alg),
-            "decode_note": "spec_decode_nested_onepass: count (per record from its last 64 bytes) + scan + decode "
+            "decode_note": "spec_decode_nested_onepass: count (per record from a 40-byte window at its end) + scan + decode "
                            "launched back to back, no host sync",
             "decode_twopass_ms": round(two_ms, 4),
             "encode_mmsg_s": round(n / (enc_ms * 1e-3) / 1e6, 1), "encode_ms": round(enc_ms, 4),
