@@ -79,7 +79,6 @@ struct TreeBufs {
     uint4 *lh[TREE_MAX_T];      // decode: LIST tables: per owner row (table start, data start, data size, count | big << 31)
     uint64_t caps[TREE_MAX_T];  // decode: row capacity per table (a list table's buffers)
     uint64_t *rowsd;            // decode: device row counts of the list tables
-    uint32_t *ovf;              // decode: set when a list outgrew its capacity
     uint32_t *size[TREE_MAX_T]; // encode: encoded bytes per row
     uint64_t *pos[TREE_MAX_T];  // encode: start of each row in out (tables 1..)
     uint64_t rows[TREE_MAX_T];

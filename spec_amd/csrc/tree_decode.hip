@@ -104,7 +104,7 @@ __global__ __launch_bounds__(SCAN_T) void list_tiles_kernel(const TreeDesc *Dp, 
 }
 
 // pass 2: per list j (blockIdx.x), exclusive offsets of the tile totals; the list's row count
-// (and a capacity overflow flag)
+// (rows_out_kernel compares it with the capacity)
 __global__ __launch_bounds__(SCAN_T) void list_top_kernel(const TreeDesc *Dp, const TreeBufs *Bp, ListSet m) {
     __shared__ uint64_t sh[17];
     const TreeDesc &D = *Dp;
@@ -124,7 +124,6 @@ __global__ __launch_bounds__(SCAN_T) void list_top_kernel(const TreeDesc *Dp, co
     if (threadIdx.x == 0) {
         const uint32_t y = m.y[blockIdx.x];
         B.rowsd[y] = carry;
-        if (carry > B.caps[y] || carry > 0xffffffffull) *B.ovf = 1;
     }
 }
 
@@ -366,14 +365,12 @@ int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, 
     B.spans = spans;
     B.n = n;
     B.rowsd = (uint64_t *)d->misc.p;
-    B.ovf = (uint32_t *)((uint8_t *)d->misc.p + TREE_MAX_T * sizeof(uint64_t));
     bool all_cols = columns != nullptr; // the schema-specialised kernels store every column unconditionally
     for (uint32_t c = 0; c < L.nc; c++) {
         B.cols[c] = columns ? columns[c] : nullptr;
         all_cols = all_cols && B.cols[c];
     }
     if ((rc = upload(d, st))) return rc;
-    if (hipMemsetAsync(B.ovf, 0, sizeof(uint32_t), st) != hipSuccess) return SPEC_E_HIP;
     // a group with no capacity yet is skipped, and with it the scans of the lists it owns: their
     // row counts must read 0, not a previous batch's (and n == 0 skips every scan)
     bool skipped = n == 0;
