@@ -103,31 +103,11 @@ __global__ __launch_bounds__(SCAN_T) void list_tiles_kernel(const TreeDesc *Dp, 
     if (threadIdx.x == 0) m.ws[blockIdx.y][blockIdx.x] = tot;
 }
 
-// pass 2: per list j (blockIdx.x), exclusive offsets of the tile totals; the list's row count
-// (rows_out_kernel compares it with the capacity)
-__global__ __launch_bounds__(SCAN_T) void list_top_kernel(const TreeDesc *Dp, const TreeBufs *Bp, ListSet m) {
-    __shared__ uint64_t sh[17];
-    const TreeDesc &D = *Dp;
-    const TreeBufs &B = *Bp;
-    const uint64_t rows = dec_rows(D, B, m.owner);
-    const uint64_t ntiles = (rows + SCAN_TILE - 1) / SCAN_TILE;
-    uint64_t *ws = m.ws[blockIdx.x];
-    uint64_t carry = 0;
-    for (uint64_t b = 0; b < ntiles; b += SCAN_T) {
-        const uint64_t i = b + threadIdx.x;
-        const uint64_t v = i < ntiles ? ws[i] : 0;
-        uint64_t tot;
-        const uint64_t e = block_scan(v, sh, tot);
-        if (i < ntiles) ws[i] = carry + e;
-        carry += tot;
-    }
-    if (threadIdx.x == 0) {
-        const uint32_t y = m.y[blockIdx.x];
-        B.rowsd[y] = carry;
-    }
-}
-
-// pass 3: per tile, every owner row's begin (BEGIN column) and its elements' byte ranges
+// pass 2: per tile, every owner row's begin (BEGIN column) and its elements' byte ranges.  The
+// tile's element offset is the sum of the earlier tiles' totals (list_tiles_kernel), summed by
+// the block itself (<= 16 per thread for 16M owner rows) instead of a separate top-level scan
+// launch; block 0 sums every tile: the list's row count (rowsd, for rows_out and the next level's
+// groups) and the BEGIN column's closing entry.
 __global__ __launch_bounds__(SCAN_T) void list_apply_kernel(const TreeDesc *Dp, const TreeBufs *Bp, ListSet m) {
     __shared__ uint64_t sh[17];
     const TreeDesc &D = *Dp;
@@ -148,9 +128,15 @@ __global__ __launch_bounds__(SCAN_T) void list_apply_kernel(const TreeDesc *Dp, 
     const uint64_t r = base;
     const uint32_t v0 = r < rows ? cnt[r] : 0;
     const uint4 h = r < rows ? lh[r] : make_uint4(0, 0, 0, 0); // with cnt, not after it
+    const uint64_t *tiles = m.ws[blockIdx.y];
+    const uint64_t ntiles = (rows + SCAN_TILE - 1) / SCAN_TILE;
+    const uint64_t lim = blockIdx.x ? (uint64_t)blockIdx.x : ntiles;
+    uint64_t part = 0;
+    for (uint64_t i = threadIdx.x; i < lim; i += SCAN_T) part += tiles[i];
     const uint64_t t0 = v0 ? load_le64(gs, (long long)h.x) : 0, t1 = v0 ? load_le64(gs, (long long)h.x + 8) : 0;
-    uint64_t tot;
-    uint64_t p = m.ws[blockIdx.y][blockIdx.x] + block_scan(v0, sh, tot);
+    uint64_t sum, tot;
+    (void)block_scan(part, sh, sum); // sum: earlier tiles (block 0: every tile)
+    uint64_t p = (blockIdx.x ? sum : 0) + block_scan(v0, sh, tot);
     const uint32_t v[1] = {v0};
     for (int k = 0; k < SCAN_PER; k++) {
         if (r >= rows) break;
@@ -181,9 +167,9 @@ __global__ __launch_bounds__(SCAN_T) void list_apply_kernel(const TreeDesc *Dp, 
         }
         p += v[k];
     }
-    if (beg && blockIdx.x == 0 && threadIdx.x == 0) {
-        const uint64_t tr = B.rowsd[y];
-        beg[rows] = (uint32_t)tr; // the closing entry: the list's row count
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        B.rowsd[y] = sum; // the list's row count
+        if (beg) beg[rows] = (uint32_t)sum; // the closing entry
     }
 }
 
@@ -465,7 +451,6 @@ int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, 
             const ListSet &m = ms[x];
             const uint64_t tiles = std::max<uint64_t>(1, (cap + SCAN_TILE - 1) / SCAN_TILE);
             hipLaunchKernelGGL(list_tiles_kernel, dim3((unsigned)tiles, m.n), dim3(SCAN_T), 0, st, Dd, Bd, m);
-            hipLaunchKernelGGL(list_top_kernel, dim3(m.n), dim3(SCAN_T), 0, st, Dd, Bd, m);
             hipLaunchKernelGGL(list_apply_kernel, dim3((unsigned)tiles, m.n), dim3(SCAN_T), 0, st, Dd, Bd, m);
         }
     }
