@@ -82,6 +82,7 @@ __device__ __forceinline__ uint64_t block_scan(uint64_t v, uint64_t *sh, uint64_
 struct ListSet {
     uint32_t n;                 // lists
     uint32_t owner;             // the group root (its rows are the lists' owner rows)
+    uint32_t top;               // 1: list_top_kernel turned the tile sums into offsets (many tiles)
     uint32_t y[TREE_MAX_T];     // the list tables
     uint64_t *ws[TREE_MAX_T];   // per list: tile sums, then their exclusive offsets
 };
@@ -103,11 +104,33 @@ __global__ __launch_bounds__(SCAN_T) void list_tiles_kernel(const TreeDesc *Dp, 
     if (threadIdx.x == 0) m.ws[blockIdx.y][blockIdx.x] = tot;
 }
 
-// pass 2: per tile, every owner row's begin (BEGIN column) and its elements' byte ranges.  The
-// tile's element offset is the sum of the earlier tiles' totals (list_tiles_kernel), summed by
-// the block itself (<= 16 per thread for 16M owner rows) instead of a separate top-level scan
-// launch; block 0 sums every tile: the list's row count (rowsd, for rows_out and the next level's
-// groups) and the BEGIN column's closing entry.
+// Many tiles (owner rows > FOLD_TILES tiles): per list j (blockIdx.x), exclusive offsets of the
+// tile totals in place, and the list's row count (rows_out_kernel compares it with the capacity).
+constexpr uint64_t FOLD_TILES = 1024;
+__global__ __launch_bounds__(SCAN_T) void list_top_kernel(const TreeDesc *Dp, const TreeBufs *Bp, ListSet m) {
+    __shared__ uint64_t sh[17];
+    const TreeDesc &D = *Dp;
+    const TreeBufs &B = *Bp;
+    const uint64_t rows = dec_rows(D, B, m.owner);
+    const uint64_t ntiles = (rows + SCAN_TILE - 1) / SCAN_TILE;
+    uint64_t *ws = m.ws[blockIdx.x];
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < ntiles; b += SCAN_T) {
+        const uint64_t i = b + threadIdx.x;
+        const uint64_t v = i < ntiles ? ws[i] : 0;
+        uint64_t tot;
+        const uint64_t e = block_scan(v, sh, tot);
+        if (i < ntiles) ws[i] = carry + e;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) B.rowsd[m.y[blockIdx.x]] = carry;
+}
+
+// per tile, every owner row's begin (BEGIN column) and its elements' byte ranges.  Up to
+// FOLD_TILES tiles the tile's element offset is the sum of the earlier tiles' totals
+// (list_tiles_kernel), summed by the block itself (one load per thread) instead of a top-level
+// scan launch, and block 0 sums every tile: the list's row count (rowsd, for rows_out and the next
+// level's groups); beyond, list_top_kernel ran first (m.top) and left the offsets in place.
 __global__ __launch_bounds__(SCAN_T) void list_apply_kernel(const TreeDesc *Dp, const TreeBufs *Bp, ListSet m) {
     __shared__ uint64_t sh[17];
     const TreeDesc &D = *Dp;
@@ -130,13 +153,13 @@ __global__ __launch_bounds__(SCAN_T) void list_apply_kernel(const TreeDesc *Dp, 
     const uint4 h = r < rows ? lh[r] : make_uint4(0, 0, 0, 0); // with cnt, not after it
     const uint64_t *tiles = m.ws[blockIdx.y];
     const uint64_t ntiles = (rows + SCAN_TILE - 1) / SCAN_TILE;
-    const uint64_t lim = blockIdx.x ? (uint64_t)blockIdx.x : ntiles;
+    const uint64_t lim = m.top ? 0 : (blockIdx.x ? (uint64_t)blockIdx.x : ntiles);
     uint64_t part = 0;
     for (uint64_t i = threadIdx.x; i < lim; i += SCAN_T) part += tiles[i];
     const uint64_t t0 = v0 ? load_le64(gs, (long long)h.x) : 0, t1 = v0 ? load_le64(gs, (long long)h.x + 8) : 0;
-    uint64_t sum, tot;
-    (void)block_scan(part, sh, sum); // sum: earlier tiles (block 0: every tile)
-    uint64_t p = (blockIdx.x ? sum : 0) + block_scan(v0, sh, tot);
+    uint64_t sum = 0, tot;
+    if (!m.top) (void)block_scan(part, sh, sum); // sum: earlier tiles (block 0: every tile)
+    uint64_t p = (m.top ? tiles[blockIdx.x] : (blockIdx.x ? sum : 0)) + block_scan(v0, sh, tot);
     const uint32_t v[1] = {v0};
     for (int k = 0; k < SCAN_PER; k++) {
         if (r >= rows) break;
@@ -168,8 +191,8 @@ __global__ __launch_bounds__(SCAN_T) void list_apply_kernel(const TreeDesc *Dp, 
         p += v[k];
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        B.rowsd[y] = sum; // the list's row count
-        if (beg) beg[rows] = (uint32_t)sum; // the closing entry
+        if (!m.top) B.rowsd[y] = sum; // the list's row count
+        if (beg) beg[rows] = (uint32_t)(m.top ? B.rowsd[y] : sum); // the closing entry
     }
 }
 
@@ -383,6 +406,7 @@ int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, 
         ListSet &m = ms[x];
         m.n = 0;
         m.owner = x;
+        m.top = (cap + SCAN_TILE - 1) / SCAN_TILE > FOLD_TILES ? 1u : 0u;
         for (uint32_t y = x + 1; y < L.nt; y++) {
             if (D.t[y].rel != REL_MANY || D.t[D.t[y].parent].groot != x) continue;
             m.y[m.n] = y;
@@ -451,6 +475,7 @@ int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, 
             const ListSet &m = ms[x];
             const uint64_t tiles = std::max<uint64_t>(1, (cap + SCAN_TILE - 1) / SCAN_TILE);
             hipLaunchKernelGGL(list_tiles_kernel, dim3((unsigned)tiles, m.n), dim3(SCAN_T), 0, st, Dd, Bd, m);
+            if (m.top) hipLaunchKernelGGL(list_top_kernel, dim3(m.n), dim3(SCAN_T), 0, st, Dd, Bd, m);
             hipLaunchKernelGGL(list_apply_kernel, dim3((unsigned)tiles, m.n), dim3(SCAN_T), 0, st, Dd, Bd, m);
         }
     }

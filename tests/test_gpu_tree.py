@@ -383,3 +383,17 @@ def test_rows_out_first_run_without_index(dev):
             assert got[t] == -1 or want_rows[t] == 0, (t, got[t], want_rows[t])
         elif t and tree.tables[t].parent == 0:
             assert got[t] == 300
+
+
+def test_list_scan_many_tiles(dev):
+    """Owner rows over 1,024 scan tiles (1,100,000 records): the list scans take the top-level
+    offset launch (list_top_kernel, m.top) instead of per-block sums of the earlier tiles; both
+    paths give the oracle's BEGIN columns and element rows."""
+    from spec_amd.schema import Kind
+    from spec_amd.tree import ListOf, Message, Tree
+
+    tree = Tree(Message("message1", [("f1", 1, Kind.INT32), ("f2", 2, Kind.INT32), ("f3", 3, Kind.INT32),
+                                     ("l", 4, ListOf(Kind.STRING))]))  # tree_catalog's last tree (precompiled)
+    n = 1_100_000
+    cols, heaps, rows = workload.tree_batch(tree, n, 21, count=(0, 3), str_len=(0, 6))
+    check_encode_decode(tree, cols, heaps, rows, dev, n)
