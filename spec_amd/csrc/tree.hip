@@ -172,7 +172,7 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *sh, ui
         if (lane >= d) incl += t;
     }
     if (lane == 63) sh[wave] = incl;
-    __syncthreads();
+    lds_barrier();
     if (threadIdx.x == 0) {
         uint64_t acc = 0;
         for (int w = 0; w < (int)(blockDim.x >> 6); w++) {
@@ -182,10 +182,10 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *sh, ui
         }
         sh[16] = acc;
     }
-    __syncthreads();
+    lds_barrier();
     const uint64_t r = sh[wave] + incl - v;
     block_total = sh[16];
-    __syncthreads();
+    lds_barrier();
     return r;
 }
 
@@ -218,10 +218,13 @@ __global__ __launch_bounds__(SCAN_T) void scan_top_kernel(uint64_t *tile_sums, u
 }
 
 // pass 3: per tile, the exclusive prefix of every element: into out32 (u32, + out32[n] = total)
-// or out64 (u64); ends64 (optional) = prefix + element
+// or out64 (u64); ends64 (optional) = prefix + element.  fold (up to FOLD_TILES tiles, no pass 2):
+// the tile's offset is the sum of the earlier tiles' totals, summed by the block itself (one load
+// per thread), and block 0 sums every tile into *total (all-ones when *err).
+constexpr uint64_t FOLD_TILES = 1024;
 __global__ __launch_bounds__(SCAN_T) void scan_apply_kernel(const uint32_t *in, uint64_t n, const uint64_t *tile_sums,
-                                                            const uint64_t *total, uint32_t *out32, uint64_t *out64,
-                                                            uint64_t *ends64) {
+                                                            uint64_t *total, uint32_t *out32, uint64_t *out64,
+                                                            uint64_t *ends64, uint32_t fold, const uint32_t *err) {
     __shared__ uint64_t sh[17];
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_PER;
     uint32_t v[SCAN_PER];
@@ -230,8 +233,19 @@ __global__ __launch_bounds__(SCAN_T) void scan_apply_kernel(const uint32_t *in, 
         v[k] = base + k < n ? in[base + k] : 0;
         sum += v[k];
     }
-    uint64_t tot;
-    uint64_t p = tile_sums[blockIdx.x] + block_excl_scan(sum, sh, tot);
+    uint64_t tot, off = 0, grand = 0;
+    if (fold) {
+        const uint64_t ntiles = gridDim.x, lim = blockIdx.x ? (uint64_t)blockIdx.x : ntiles;
+        uint64_t part = 0;
+        for (uint64_t i = threadIdx.x; i < lim; i += SCAN_T) part += tile_sums[i];
+        (void)block_excl_scan(part, sh, grand); // earlier tiles (block 0: every tile)
+        off = blockIdx.x ? grand : 0;
+        if (blockIdx.x == 0) grand = err && *err ? ~0ull : grand; // an encoder error: all-ones
+        if (blockIdx.x == 0 && threadIdx.x == 0) *total = grand;
+    } else {
+        off = tile_sums[blockIdx.x];
+    }
+    uint64_t p = off + block_excl_scan(sum, sh, tot);
     for (int k = 0; k < SCAN_PER; k++) {
         if (base + k < n) {
             if (out32) out32[base + k] = (uint32_t)p;
@@ -240,7 +254,7 @@ __global__ __launch_bounds__(SCAN_T) void scan_apply_kernel(const uint32_t *in, 
         }
         p += v[k];
     }
-    if (out32 && blockIdx.x == 0 && threadIdx.x == 0) out32[n] = (uint32_t)*total;
+    if (out32 && blockIdx.x == 0 && threadIdx.x == 0) out32[n] = (uint32_t)(fold ? grand : *total);
 }
 
 // Every child table's row positions to ~0 (unplaced) in one launch: table blockIdx.y
@@ -261,10 +275,11 @@ size_t scan_ws_bytes(uint64_t n) { return ((n + SCAN_TILE - 1) / SCAN_TILE + 1) 
 int launch_scan(const uint32_t *in, uint64_t n, uint32_t *out32, uint64_t *out64, uint64_t *ends64, uint64_t *ws,
                 uint64_t *total, const uint32_t *err, hipStream_t st) {
     const uint64_t tiles = std::max<uint64_t>(1, (n + SCAN_TILE - 1) / SCAN_TILE);
+    const uint32_t fold = tiles <= FOLD_TILES ? 1u : 0u;
     hipLaunchKernelGGL(scan_tiles_kernel, dim3((unsigned)tiles), dim3(SCAN_T), 0, st, in, n, ws);
-    hipLaunchKernelGGL(scan_top_kernel, dim3(1), dim3(SCAN_T), 0, st, ws, tiles, total, err);
+    if (!fold) hipLaunchKernelGGL(scan_top_kernel, dim3(1), dim3(SCAN_T), 0, st, ws, tiles, total, err);
     hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)tiles), dim3(SCAN_T), 0, st, in, n, ws, total, out32, out64,
-                       ends64);
+                       ends64, fold, err);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
