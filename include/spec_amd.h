@@ -281,6 +281,15 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
  * the shard, exactly as spec_decode_flat / spec_encode_flat do on one device.
  *   spec_packed_layout: column offsets / status offset of n records; returns the bytes;
  *   spec_shard_bounds: shard k's records [r0, r1) of n (sizes differ by at most one);
+ *   spec_shard_bounds_bytes: shard k's records [r0, r1) of n such that the shards' BYTES are
+ *     near-equal: `ends` is any non-decreasing cumulative byte count per record (a batch's end
+ *     offsets; for encode, e.g. a prefix sum of the records' heap bytes), split point k the
+ *     record boundary nearest to ends[n-1] * k / nshards (binary search).  Records are
+ *     variable-length (internal/encode/bytes.go:14-26, string.go:14-26), so with skewed sizes
+ *     a record split leaves the slowest device with most of the bytes;
+ *   spec_shard_set_split: how spec_shard_decode_host and spec_shard_host_decode split a host
+ *     batch: SPEC_SHARD_SPLIT_RECORDS (default, spec_shard_bounds) or SPEC_SHARD_SPLIT_BYTES
+ *     (spec_shard_bounds_bytes over the batch's ends);
  *   spec_shard_create_ex: flags SPEC_SHARD_FORCE_COMM = build the communicator even for one
  *     device; the gather then moves every part, the root's own too, through RCCL;
  *     SPEC_SHARD_SHARED = devices may repeat (several shards on one GPU, no communicator, the
@@ -289,11 +298,13 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
  *     of the RCCL in use (< 0 if none loads);
  *   spec_shard_decode: device i decodes its device-resident shard (streams[i], ends[i] relative
  *     to streams[i], ns[i] records) into packed[i] (on device i), asynchronously on its stream;
- *   spec_shard_decode_host: a host batch split by spec_shard_bounds; per device, on its own host
+ *   spec_shard_decode_host: a host batch split by the shard's split mode; per device, on its own host
  *     thread, the shard is copied in spec_shard_set_chunks record chunks (default 8; through
  *     pinned staging slots when the batch is pageable) and every chunk decoded once it has
  *     landed (ends rebased on the device); byte_bases[i] (optional) = shard i's first byte.
- *     Returns once every copy is issued; a pinned batch must stay valid until spec_shard_sync;
+ *     Returns once every copy is issued; a pinned batch must stay valid until spec_shard_sync.
+ *     Calls may follow each other without spec_shard_sync: a call's copies into the device's
+ *     staging buffer are ordered after the previous call's decodes that read it;
  *   spec_shard_gather: every device's packed buffer (nbytes[i]) to `gathered` on device `root`,
  *     part i at the sum of the earlier parts' sizes, ordered after the decodes on each stream;
  *   spec_shard_encode: device i encodes its ns[i] records from columns[i] (heaps[i], heap_lens[i]
@@ -312,9 +323,13 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
 #define SPEC_SHARD_MAX_DEVICES 16
 #define SPEC_SHARD_FORCE_COMM 1u
 #define SPEC_SHARD_SHARED 2u
+#define SPEC_SHARD_SPLIT_RECORDS 0u
+#define SPEC_SHARD_SPLIT_BYTES 1u
 typedef struct spec_shard spec_shard;
 uint64_t spec_packed_layout(const spec_schema *schema, uint64_t n, uint64_t *col_offsets, uint64_t *status_offset);
 void spec_shard_bounds(uint64_t n, int nshards, int k, uint64_t *r0, uint64_t *r1);
+void spec_shard_bounds_bytes(const uint64_t *ends, uint64_t n, int nshards, int k, uint64_t *r0, uint64_t *r1);
+int spec_shard_set_split(spec_shard *c, uint32_t split);
 int spec_shard_create(const int *devices, int ndev, spec_shard **out);
 int spec_shard_create_ex(const int *devices, int ndev, uint32_t flags, spec_shard **out);
 void spec_shard_destroy(spec_shard *c);
@@ -466,7 +481,7 @@ int spec_host_decoder_run(spec_host_decoder *d, const uint8_t *stream_host, uint
 
 /* The host pipeline on every device of a spec_shard at once (host batch in, host columns out,
  * one host thread per device): spec_shard_host_prepare creates a spec_host_decoder per device
- * (n_cap / stream_cap per SHARD); spec_shard_host_decode splits the batch by spec_shard_bounds
+ * (n_cap / stream_cap per SHARD); spec_shard_host_decode splits the batch by the split mode
  * and runs device i's decoder over shard i into out_host[i] (that decoder's chunk-major layout:
  * spec_host_decoder_out_bytes / _chunk on spec_shard_host_decoder(c, i)), spans shard-relative,
  * byte_bases[i] (optional) = shard i's first byte.  Synchronous. */

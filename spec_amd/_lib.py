@@ -80,6 +80,8 @@ def _declare(L):
     L.spec_strerror.restype = C.c_char_p
     L.spec_strerror.argtypes = [C.c_int]
     L.spec_last_hip_error.restype = C.c_int
+    L.spec_last_hip_error.argtypes = []
+    L.spec_abi_version.argtypes = []
     L.spec_decode_flat.argtypes = [C.POINTER(SpecSchema), vp, C.c_uint64, vp, C.c_uint64,
                                    C.POINTER(vp), vp, vp]
     L.spec_decode_flat_range.argtypes = [C.POINTER(SpecSchema), vp, C.c_uint64, vp, C.c_uint64, C.c_uint64,
@@ -158,6 +160,10 @@ def _declare(L):
     L.spec_packed_layout.restype = C.c_uint64
     L.spec_shard_bounds.argtypes = [C.c_uint64, C.c_int, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
     L.spec_shard_bounds.restype = None
+    L.spec_shard_bounds_bytes.argtypes = [vp, C.c_uint64, C.c_int, C.c_int, C.POINTER(C.c_uint64),
+                                          C.POINTER(C.c_uint64)]
+    L.spec_shard_bounds_bytes.restype = None
+    L.spec_shard_set_split.argtypes = [vp, C.c_uint32]
     L.spec_shard_create.argtypes = [C.POINTER(C.c_int), C.c_int, C.POINTER(vp)]
     L.spec_shard_destroy.argtypes = [vp]
     L.spec_shard_destroy.restype = None

@@ -877,7 +877,13 @@ std::string generate_tree(const TreeDesc &D, bool *has) {
         if (D.t[t].shape == spec::SHAPE_MESSAGE)
             o << "  case " << t << ":\n"
               << "    for (uint64_t row = grid_first(); row < rows; row += grid_stride()) {\n"
-              << (D.t[t].rel == spec::REL_MANY ? "      if (!list_row_covered(D, B, x, row)) continue;\n" : "")
+              // a row outside its owners' BEGIN ranges is not written, and neither is anything
+              // under it: its children's positions are marked unplaced (they may hold stale
+              // workspace bytes otherwise, and the next depth's writer would emit at them)
+              << (D.t[t].rel == spec::REL_MANY
+                      ? "      if (!list_row_covered(D, B, x, row)) { gen_unplace_" + std::to_string(t) +
+                            "(D, B, row); continue; }\n"
+                      : std::string())
               << "      const uint64_t start = x == 0 ? B.offsets[row] : B.pos[x][row];\n"
               << "      if (start == ~0ull) { gen_unplace_" << t << "(D, B, row); continue; }\n"
               << "      if (x == 0 && B.ends_out) B.ends_out[row] = start + B.size[0][row];\n"

@@ -122,6 +122,7 @@ struct Dev {
     size_t pin_cap = 0;
     hipEvent_t ev_in[MAX_CHUNKS] = {};
     hipEvent_t ev_done = nullptr; // gather without a communicator: the part is ready
+    hipEvent_t ev_drained = nullptr; // decode_host: the previous call's decodes (readers of buf)
     void *ws = nullptr;         // encode workspace (block sums), then the total
     size_t ws_cap = 0;
     spec_host_decoder *hd = nullptr;
@@ -142,6 +143,7 @@ struct spec_shard {
     int ndev = 0;
     uint32_t flags = 0;
     uint32_t chunks = 8;
+    uint32_t split = SPEC_SHARD_SPLIT_RECORDS;
     Dev d[SPEC_SHARD_MAX_DEVICES];
     uint64_t *host_totals = nullptr; // pinned: the encode size passes' totals
 };
@@ -208,6 +210,11 @@ int decode_host_dev(spec_shard *c, int i, const spec_schema *schema, const uint8
         }
         if ((rc = ensure_pin(D, slot))) return rc;
     }
+    // this call's copies overwrite buf, which the previous call's decodes (on st) may still
+    // read: order them after those decodes (no host wait: back-to-back
+    // calls need no spec_shard_sync between them)
+    if ((e = hipEventRecord(D.ev_drained, D.st)) != hipSuccess || (e = hipStreamWaitEvent(D.s_in, D.ev_drained, 0)) != hipSuccess)
+        return hip_err(e);
     for (uint32_t k = 0; k < nch; k++) {
         const uint64_t r0 = ns * k / nch, r1 = ns * (k + 1) / nch;
         if (r1 == r0) continue;
@@ -237,6 +244,12 @@ int decode_host_dev(spec_shard *c, int i, const spec_schema *schema, const uint8
         if (rc) return rc;
     }
     return SPEC_OK;
+}
+
+// Shard i's first record under the shard's split mode (i == ndev: n).
+void shard_split(const spec_shard *c, const uint64_t *ends, uint64_t n, int i, uint64_t *r0) {
+    if (c->split == SPEC_SHARD_SPLIT_BYTES) spec_shard_bounds_bytes(ends, n, c->ndev, i, r0, nullptr);
+    else spec_shard_bounds(n, c->ndev, i, r0, nullptr);
 }
 
 // Run fn(i) for every device, each on its own host thread (inline for one device); returns the
@@ -276,6 +289,28 @@ void spec_shard_bounds(uint64_t n, int nshards, int k, uint64_t *r0, uint64_t *r
     if (r1) *r1 = (uint64_t)(N * (unsigned)(k + 1) / (unsigned)nshards);
 }
 
+void spec_shard_bounds_bytes(const uint64_t *ends, uint64_t n, int nshards, int k, uint64_t *r0, uint64_t *r1) {
+    if (nshards < 1) nshards = 1;
+    // split point j: the record boundary nearest to byte quantile total * j / nshards
+    auto split = [&](int j) -> uint64_t {
+        if (j <= 0 || !n || !ends) return 0;
+        if (j >= nshards) return n;
+        const uint64_t q = (uint64_t)((unsigned __int128)ends[n - 1] * (unsigned)j / (unsigned)nshards);
+        const uint64_t i = (uint64_t)(std::lower_bound(ends, ends + n, q) - ends); // first end >= q
+        if (i >= n) return n;
+        const uint64_t below = i ? ends[i - 1] : 0; // records [0, i) end at or below q
+        return ends[i] - q <= q - below ? i + 1 : i;
+    };
+    if (r0) *r0 = split(k);
+    if (r1) *r1 = split(k + 1);
+}
+
+int spec_shard_set_split(spec_shard *c, uint32_t split) {
+    if (!c || split > SPEC_SHARD_SPLIT_BYTES) return SPEC_E_INVALID_ARGUMENT;
+    c->split = split;
+    return SPEC_OK;
+}
+
 int spec_shard_create_ex(const int *devices, int ndev, uint32_t flags, spec_shard **out) {
     if (!out || !devices || ndev < 1 || ndev > SPEC_SHARD_MAX_DEVICES) return SPEC_E_INVALID_ARGUMENT;
     if (flags & ~(uint32_t)(SPEC_SHARD_FORCE_COMM | SPEC_SHARD_SHARED)) return SPEC_E_INVALID_ARGUMENT;
@@ -297,7 +332,8 @@ int spec_shard_create_ex(const int *devices, int ndev, uint32_t flags, spec_shar
         if ((e = hipSetDevice(devices[i])) != hipSuccess ||
             (e = hipStreamCreateWithFlags(&D.st, hipStreamNonBlocking)) != hipSuccess ||
             (e = hipStreamCreateWithFlags(&D.s_in, hipStreamNonBlocking)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&D.ev_done, hipEventDisableTiming)) != hipSuccess) {
+            (e = hipEventCreateWithFlags(&D.ev_done, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&D.ev_drained, hipEventDisableTiming)) != hipSuccess) {
             spec_shard_destroy(c);
             return hip_err(e);
         }
@@ -345,6 +381,7 @@ void spec_shard_destroy(spec_shard *c) {
         for (hipEvent_t &ev : D.ev_in)
             if (ev) (void)hipEventDestroy(ev);
         if (D.ev_done) (void)hipEventDestroy(D.ev_done);
+        if (D.ev_drained) (void)hipEventDestroy(D.ev_drained);
         for (void *p : D.pin)
             if (p) (void)hipHostFree(p);
         if (D.buf) (void)hipFree(D.buf);
@@ -402,9 +439,9 @@ int spec_shard_decode_host(spec_shard *c, const spec_schema *schema, const uint8
     if (schema->nfields == 0 || schema->nfields > SPEC_MAX_FIELDS) return SPEC_E_INVALID_ARGUMENT;
     uint64_t R[SPEC_SHARD_MAX_DEVICES + 1], B[SPEC_SHARD_MAX_DEVICES + 1];
     for (int i = 0; i <= c->ndev; i++) {
-        spec_shard_bounds(n, c->ndev, i, &R[i], nullptr);
+        shard_split(c, ends, n, i, &R[i]);
         B[i] = R[i] ? ends[R[i] - 1] : 0;
-        if ((i && B[i] < B[i - 1]) || B[i] > stream_len) return SPEC_E_INVALID_ARGUMENT;
+        if ((i && (R[i] < R[i - 1] || B[i] < B[i - 1])) || B[i] > stream_len) return SPEC_E_INVALID_ARGUMENT;
         if (byte_bases && i < c->ndev) byte_bases[i] = B[i];
     }
     for (int i = 0; i < c->ndev; i++)
@@ -511,7 +548,9 @@ int spec_shard_encode(spec_shard *c, const spec_schema *schema, const void *cons
         else if (t > out_caps[i] && rc == SPEC_OK) rc = SPEC_E_CAPACITY;
         o += t == ~0ull ? 0 : t;
     }
-    if (rc) return rc; // no write pass wrote anything
+    // a shard over its capacity or in error wrote nothing (its write pass checks its own total);
+    // the shards that fit hold their bytes, with shard-relative ends
+    if (rc) return rc;
     // 3. every shard's ends moved to the whole batch, after its write pass
     for (int i = 0; i < c->ndev; i++) {
         if (!base[i] || !ns[i]) continue;
@@ -547,9 +586,9 @@ int spec_shard_host_decode(spec_shard *c, const uint8_t *stream_host, uint64_t s
     uint64_t R[SPEC_SHARD_MAX_DEVICES + 1], B[SPEC_SHARD_MAX_DEVICES + 1];
     for (int i = 0; i <= c->ndev; i++) {
         if (i < c->ndev && !c->d[i].hd) return SPEC_E_INVALID_ARGUMENT; // spec_shard_host_prepare first
-        spec_shard_bounds(n, c->ndev, i, &R[i], nullptr);
+        shard_split(c, ends_host, n, i, &R[i]);
         B[i] = R[i] ? ends_host[R[i] - 1] : 0;
-        if ((i && B[i] < B[i - 1]) || B[i] > stream_len) return SPEC_E_INVALID_ARGUMENT;
+        if ((i && (R[i] < R[i - 1] || B[i] < B[i - 1])) || B[i] > stream_len) return SPEC_E_INVALID_ARGUMENT;
         if (byte_bases && i < c->ndev) byte_bases[i] = B[i];
     }
     DeviceGuard g;

@@ -814,8 +814,9 @@ __device__ __forceinline__ uint64_t size_row_shaped(const TreeDesc &D, const Tre
 
 // A list table's rows its owners' BEGIN ranges cover: [begin[0], begin[owner rows]) (the writers
 // check BEGIN is monotonic: an encoder error otherwise).  Rows outside belong to no owner and are
-// not written; every row inside gets its position (or ~0: an absent / unplaced owner) from its
-// owner's write, so the level-fused writers need no position fill first.
+// not written (a message row outside marks its own children unplaced, jit.cpp gen_unplace_*);
+// every row inside gets its position (or ~0: an absent / unplaced owner) from its owner's write,
+// so the level-fused writers need no position fill first.
 __device__ __forceinline__ bool list_row_covered(const TreeDesc &D, const TreeBufs &B, uint32_t y, uint64_t row) {
     const uint32_t *b = (const uint32_t *)B.cols[D.t[y].begin_col];
     return row >= b[0] && row < b[B.rows[D.t[y].parent]];

@@ -194,9 +194,22 @@ class NativeShard:
     def set_chunks(self, chunks: int):
         self._lib.check(self._lib.lib().spec_shard_set_chunks(self._h, chunks), "spec_shard_set_chunks")
 
-    def bounds(self, n: int, k: int):
+    def set_split(self, by_bytes: bool):
+        """How decode_host / host_decode split a host batch: near-equal record counts (default)
+        or near-equal bytes (spec_shard_bounds_bytes over the batch's ends)."""
+        self._lib.check(self._lib.lib().spec_shard_set_split(self._h, 1 if by_bytes else 0), "spec_shard_set_split")
+        self._by_bytes = bool(by_bytes)
+
+    def bounds(self, n: int, k: int, ends=None):
+        """Shard k's records [r0, r1) of n.  With the byte split, pass the batch's ends (host)."""
         r0, r1 = C.c_uint64(), C.c_uint64()
-        self._lib.lib().spec_shard_bounds(n, self.ndev, k, C.byref(r0), C.byref(r1))
+        if getattr(self, "_by_bytes", False):
+            if ends is None:
+                raise ValueError("byte-balanced bounds need the batch's ends")
+            e = np.ascontiguousarray(ends.numpy() if isinstance(ends, torch.Tensor) else ends).view(np.uint64)
+            self._lib.lib().spec_shard_bounds_bytes(e.ctypes.data, n, self.ndev, k, C.byref(r0), C.byref(r1))
+        else:
+            self._lib.lib().spec_shard_bounds(n, self.ndev, k, C.byref(r0), C.byref(r1))
         return r0.value, r1.value
 
     def _enter(self):
@@ -229,7 +242,7 @@ class NativeShard:
         if packs is None:
             packs = []
             for k, d in enumerate(self.devices):
-                r0, r1 = self.bounds(n, k)
+                r0, r1 = self.bounds(n, k, ends)
                 packs.append(PackedColumns(schema, r1 - r0, torch.device("cuda", d)))
         ptrs = (C.c_void_p * self.ndev)(*[p.buf.data_ptr() for p in packs])
         bases = (C.c_uint64 * self.ndev)()

@@ -4,6 +4,7 @@ and the shapes the GPU tests exercise.  No oracle here: this is product code."""
 from __future__ import annotations
 
 import json
+import os
 
 from .schema import Kind
 from .tree import ListOf, Message, Struct, Tree, pkg1_tree
@@ -43,15 +44,24 @@ def nested_struct_tree() -> Tree:
     return Tree(root)
 
 
-def precompiled_trees(spec_trees_json: str | None = None) -> list:
+# the trees spec_amd.specfile derives from the reference's own .spec files (pkg1.spec,
+# proto/pmpx/mpx.spec, proto/prpc/rpc.spec), as flattened descriptors (path, tag, kind, elem,
+# parent) — package data written by tests/golden/make_spec_trees.py with the test fixture
+REFERENCE_TREES_JSON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "reference_trees.json")
+REFERENCE_TREE_NAMES = ("pkg1.Message", "pmpx.Message", "prpc.Message", "pmpx.ChannelOpen")
+
+
+def reference_trees() -> dict:
+    """{name: Tree} of the reference-derived trees the engine precompiles."""
+    d = json.load(open(REFERENCE_TREES_JSON))
+    return {k: Tree.from_fields(d[k]) for k in REFERENCE_TREE_NAMES}
+
+
+def precompiled_trees() -> list:
     """Every tree the GPU tests and the bench decode and encode: build() compiles their
-    schema-specialised kernels into the code-object cache that travels with the library.
-    spec_trees_json: the trees spec_amd.specfile derived from the reference's .spec files
-    (tests/golden/spec_trees.json, a data fixture), added when given."""
+    schema-specialised kernels into the code-object cache that travels with the library."""
     trees = [pkg1_tree(k) for k in (1, 2, 3)] + [shapes_tree(), nested_struct_tree()]
-    if spec_trees_json:
-        d = json.load(open(spec_trees_json))
-        trees += [Tree.from_fields(d[k]) for k in ("pkg1.Message", "pmpx.Message", "prpc.Message", "pmpx.ChannelOpen")]
+    trees += list(reference_trees().values())
     base = pkg1_tree()
     for shift in (1, 4, 9):  # test_errmask_cross_kind's readers
         fields = []

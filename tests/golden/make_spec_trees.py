@@ -1,4 +1,5 @@
-"""Writes tests/golden/spec_trees.json: the schema trees spec_amd.specfile derives from the
+"""Writes tests/golden/spec_trees.json (and spec_amd/data/reference_trees.json, the package's
+copy of the four trees the engine precompiles): the schema trees spec_amd.specfile derives from the
 reference's own .spec files (run here, where /root/reference exists; the GPU box has only the
 JSON).  Each entry is the flattened tree [(path, tag, kind, elem, parent), ...] of one message —
 derived descriptors (tags, kinds, nesting), not the schema text.
@@ -38,5 +39,11 @@ def trees(ref):
 
 if __name__ == "__main__":
     dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), "spec_trees.json")
-    json.dump(trees(REF), open(dst, "w"), indent=0)
+    t = trees(REF)
+    json.dump(t, open(dst, "w"), indent=0)
     print(dst)
+    # the package's copy of the trees the engine precompiles (spec_amd.tree_catalog)
+    from spec_amd.tree_catalog import REFERENCE_TREE_NAMES, REFERENCE_TREES_JSON
+
+    json.dump({k: t[k] for k in REFERENCE_TREE_NAMES}, open(REFERENCE_TREES_JSON, "w"), indent=0)
+    print(REFERENCE_TREES_JSON)

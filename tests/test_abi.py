@@ -123,3 +123,50 @@ def test_nested_encode_jit_source_compiles_for_gfx950():
         [(1, spec_amd.Kind.INT64), (2, spec_amd.Kind.LIST)],
         [(i + 1, spec_amd.Kind.INT32) for i in range(40)])
     assert L.spec_encode_nested_jit_compile(C.byref(wide.c)) > 1000
+
+
+def _header_prototypes():
+    """(return type, name) of every function include/spec_amd.h declares."""
+    import re
+
+    src = open(_lib.HEADER_PATH).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    out = []
+    for m in re.finditer(r"(?:^|;|\})\s*((?:const\s+)?[A-Za-z_][\w ]*?[\s\*]+)(spec_[a-z0-9_]+)\s*\(", src):
+        out.append((" ".join(m.group(1).split()), m.group(2)))
+    return out
+
+
+def test_ctypes_declarations_match_header():
+    """Every entry point the Python host calls is declared to ctypes with argtypes, and every one
+    returning a pointer or a 64-bit value has a matching restype.  ctypes' default (int argument,
+    int result) truncates a 64-bit pointer: a stream or decoder handle returned as int, or a
+    device pointer passed as int, is the host-side segfault class of the round-4 `nat1` crash
+    (test_native_shard_decode_gather[1-plain])."""
+    protos = _header_prototypes()
+    names = {n for _, n in protos}
+    assert set(_lib.header_symbols()) == names, set(_lib.header_symbols()) ^ names
+    L = spec_amd.lib()
+    wide = ("uint64_t", "size_t", "long long", "int64_t")
+    bad = []
+    for ret, name in protos:
+        fn = getattr(L, name)
+        if "*" in ret:
+            if fn.restype not in (C.c_void_p, C.c_char_p) and "char" not in ret:
+                bad.append((name, ret, fn.restype))
+            if "char" in ret and fn.restype is not C.c_char_p:
+                bad.append((name, ret, fn.restype))
+        elif any(w in ret for w in wide):
+            if fn.restype not in (C.c_uint64, C.c_size_t, C.c_longlong, C.c_int64, C.c_ulonglong):
+                bad.append((name, ret, fn.restype))
+    assert not bad, bad
+    # every function the package calls has its argument types declared
+    import pathlib
+    import re
+
+    used = set()
+    for p in pathlib.Path(_lib.__file__).parent.glob("*.py"):
+        used |= set(re.findall(r"\.(spec_[a-z0-9_]+)\(", p.read_text()))
+    undeclared = sorted(n for n in used & names if getattr(L, n).argtypes is None)
+    assert not undeclared, undeclared

@@ -397,3 +397,73 @@ def test_list_scan_many_tiles(dev):
     n = 1_100_000
     cols, heaps, rows = workload.tree_batch(tree, n, 21, count=(0, 3), str_len=(0, 6))
     check_encode_decode(tree, cols, heaps, rows, dev, n)
+
+
+def pad_list_rows(tree, cols, rows, x, front, back, per=2):
+    """The batch (cols, rows) with list table x given `front` rows before and `back` rows after
+    the range its owners' BEGIN cover (begin[0] > 0, rows past begin[owner rows]).  Every table
+    under x gets matching junk rows: a REL_ONE child one per junk owner row, a list `per`
+    elements per junk owner row (covered by that list's own BEGIN range, owned by a junk row).
+    Junk rows copy row 0's values (valid spans: the size pass checks every row).  The batch
+    encodes to the same bytes as the original: nothing under an uncovered row is written."""
+    from spec_amd.tree import REL_ONE, ROLE_BEGIN, INPUT_ROLES
+
+    cols, rows = dict(cols), list(rows)
+    pad = {x: (front, back)}
+    bname = f"{tree.fields[tree.tables[x].field].path}#begin"
+    cols[bname] = (cols[bname].reshape(-1).view(np.uint32) + np.uint32(front)).view(np.uint8).reshape(-1, 4)
+    for t in tree.tables[x + 1:]:  # pre-order: owners first
+        if t.parent not in pad:
+            continue
+        F, K = pad[t.parent]
+        if t.rel == REL_ONE:
+            pad[t.index] = (F, K)
+            continue
+        bn = f"{tree.fields[t.field].path}#begin"
+        b = cols[bn].reshape(-1).view(np.uint32).astype(np.int64)
+        Fc = F * per
+        nb = np.concatenate([np.arange(0, Fc, per), b + Fc, b[-1] + Fc + per * np.arange(1, K + 1)])
+        cols[bn] = nb.astype(np.uint32).view(np.uint8).reshape(-1, 4)
+        pad[t.index] = (Fc, K * per)
+    for t, (F, K) in pad.items():
+        for c in tree.tables[t].columns:
+            if c.role == ROLE_BEGIN or c.role not in INPUT_ROLES or c.name not in cols:
+                continue
+            a = cols[c.name].reshape(rows[t], c.width)
+            tmpl = a[:1] if rows[t] else np.zeros((1, c.width), np.uint8)
+            cols[c.name] = np.ascontiguousarray(np.concatenate([np.repeat(tmpl, F, 0), a, np.repeat(tmpl, K, 0)]))
+        rows[t] += F + K
+    return cols, rows
+
+
+@pytest.mark.parametrize("which", ["pkg1_3", "shapes"])
+def test_encode_list_rows_outside_owner_ranges(dev, which):
+    """list rows outside their owners' BEGIN ranges (begin[0] > 0, trailing
+    rows) are skipped by the level-fused writers, and so is everything under them — their
+    sub-message rows and nested list rows get no position.  The workspace is zero-filled before
+    the call (a stale position 0 would write over the first record), and bytes past the output
+    capacity stay intact: the output == the oracle Writer's bytes of the unpadded batch."""
+    from spec_amd.tree import REL_MANY, SHAPE_MESSAGE
+
+    tree = spec_amd.pkg1_tree(3) if which == "pkg1_3" else shapes_tree()
+    n = 400
+    cols, heaps, rows = workload.tree_batch(tree, n, 1234, count=(1, 3), present=0.9)
+    want_stream, want_ends = oracle_encode(tree, cols, heaps, n)
+    lists = [t.index for t in tree.tables if t.rel == REL_MANY and t.shape == SHAPE_MESSAGE and t.parent == 0]
+    assert lists
+    for x in lists:
+        pcols, prows = pad_list_rows(tree, cols, rows, x, 3, 5)
+        enc = spec_amd.TreeEncoder(tree, prows, dev)
+        enc.workspace.zero_()
+        total = int(enc.encode(to_dev(pcols, dev), to_dev(heaps, dev), None, None).item())
+        assert total == want_stream.size, x
+        guard = 4096
+        buf = torch.full((total + guard,), 0xA5, dtype=torch.uint8, device=dev)
+        ends = torch.zeros(n, dtype=torch.int64, device=dev)
+        enc.workspace.zero_()
+        enc.encode(to_dev(pcols, dev), to_dev(heaps, dev), buf[:total], ends)
+        torch.cuda.synchronize()
+        b = buf.cpu().numpy()
+        assert (b[total:] == 0xA5).all(), x
+        assert np.array_equal(b[:total], want_stream), x
+        assert np.array_equal(ends.cpu().numpy().view(np.uint64), want_ends), x

@@ -138,3 +138,64 @@ def test_packed_layout_matches_c_abi():
                 r0, r1 = C.c_uint64(), C.c_uint64()
                 L.spec_shard_bounds(n, world, k, C.byref(r0), C.byref(r1))
                 assert (r0.value, r1.value) == shard_bounds(n, world, k)
+
+
+def _bytes_split_ref(ends, world):
+    """spec_shard_bounds_bytes restated: split point j = the record boundary nearest to byte
+    quantile total * j / world (ties to the later boundary's lower side: fewer bytes before)."""
+    n = len(ends)
+    cuts = [0]
+    for j in range(1, world):
+        q = int(ends[-1]) * j // world if n else 0
+        i = int(np.searchsorted(ends, q, side="left")) if n else 0
+        if i >= n:
+            cuts.append(n)
+            continue
+        below = int(ends[i - 1]) if i else 0
+        cuts.append(i + 1 if int(ends[i]) - q <= q - below else i)
+    cuts.append(n)
+    return cuts
+
+
+def test_shard_bounds_bytes():
+    """spec_shard_bounds_bytes (C ABI, host code): contiguous, covering, monotonic shards whose
+    bytes differ from total/world by at most one record's size; equal to the restatement above;
+    a skewed batch (10x record sizes, the long ones first) balances where the record split does
+    not; degenerate inputs (no records, one record, more shards than records, zero-size
+    records)."""
+    import ctypes as C
+
+    import spec_amd
+
+    L = spec_amd.lib()
+    rng = np.random.default_rng(9)
+    sizes_long = rng.integers(2000, 2600, 20_000)
+    sizes_short = rng.integers(200, 260, 180_000)
+    cases = [np.cumsum(np.concatenate([sizes_long, sizes_short])).astype(np.uint64),
+             np.cumsum(rng.integers(0, 300, 10_001)).astype(np.uint64),
+             np.zeros(0, np.uint64), np.array([5], np.uint64), np.array([0, 0, 0], np.uint64),
+             np.cumsum(np.full(5, 10)).astype(np.uint64)]
+    for ends in cases:
+        ends = np.ascontiguousarray(ends)
+        n = len(ends)
+        for world in (1, 2, 3, 8, 16):
+            got = []
+            for k in range(world):
+                r0, r1 = C.c_uint64(), C.c_uint64()
+                L.spec_shard_bounds_bytes(ends.ctypes.data if n else None, n, world, k, C.byref(r0), C.byref(r1))
+                got.append((r0.value, r1.value))
+            cuts = _bytes_split_ref(ends, world)
+            assert got == list(zip(cuts[:-1], cuts[1:])), (n, world)
+            assert got[0][0] == 0 and got[-1][1] == n
+            assert all(a[1] == b[0] and a[0] <= a[1] for a, b in zip(got, got[1:] + [(n, n)]))
+            if n > 100:
+                sz = np.diff(np.concatenate([[0], ends.astype(np.int64)]))
+                tot = int(ends[-1])
+                for r0, r1 in got:
+                    b = (int(ends[r1 - 1]) if r1 else 0) - (int(ends[r0 - 1]) if r0 else 0)
+                    assert abs(b - tot / world) <= sz.max(), (world, b, tot / world)
+    skew = cases[0]
+    r1 = C.c_uint64()
+    L.spec_shard_bounds_bytes(skew.ctypes.data, len(skew), 3, 0, None, C.byref(r1))
+    assert abs(int(skew[r1.value - 1]) - int(skew[-1]) / 3) < 0.01 * int(skew[-1]) / 3
+    assert int(skew[len(skew) // 3 - 1]) > 0.6 * int(skew[-1])  # the record split

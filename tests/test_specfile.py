@@ -172,3 +172,19 @@ def test_fixture_trees_shapes():
     assert mpx["code"][2] == int(Kind.INT32) and mpx["channel_open.id"][2] == int(Kind.BIN128)
     assert mpx["batch.list"][2:4] == [int(Kind.LIST), int(Kind.MESSAGE)]
     assert mpx["connect_request.versions"][2:4] == [int(Kind.LIST), int(Kind.INT32)]
+
+
+def test_package_reference_trees_match_fixture():
+    """build() precompiles the reference-derived trees from the package's own copy
+    (spec_amd/data/reference_trees.json, no test-tree reads); it equals the golden fixture."""
+    import json
+
+    from spec_amd.tree_catalog import REFERENCE_TREE_NAMES, REFERENCE_TREES_JSON, reference_trees
+
+    pkg = json.load(open(REFERENCE_TREES_JSON))
+    gold = json.load(open(GOLDEN))
+    assert sorted(pkg) == sorted(REFERENCE_TREE_NAMES)
+    for k in REFERENCE_TREE_NAMES:
+        assert pkg[k] == gold[k], k
+    assert [t.to_fields() for t in reference_trees().values()] == \
+        [[tuple(f) for f in gold[k]] for k in REFERENCE_TREE_NAMES]
