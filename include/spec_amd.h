@@ -34,7 +34,12 @@ extern "C" {
 #endif
 
 #define SPEC_AMD_ABI_VERSION 1
-#define SPEC_MAX_FIELDS 64
+/* Fields of a flat schema.  Schemas of up to 64 fields run the schema-specialised kernels; wider
+ * ones decode in chunks of 64 fields (the generic kernel once per chunk, each getter against the
+ * record's whole table) and encode through the wide kernels, whose field set the call writes into
+ * the workspace.  A nested schema's outer and item halves hold at most 64 fields each. */
+#define SPEC_MAX_FIELDS 1024
+#define SPEC_NESTED_MAX_FIELDS 64
 
 /* Column kinds: one per typed getter / FieldWriter method
  * (internal/types/msg.go:219-421, internal/writer/msg.go:99-211). */
@@ -386,7 +391,9 @@ int spec_decode_flat(const spec_schema *schema, const uint8_t *stream_bytes, uin
 /* spec_decode_flat_errors: spec_decode_flat plus, per record, which getters' *Err variants
  * return an error (internal/types/msg.go:233-459: Int32Err, StringErr, ...): errmask[i] bit f
  * is set when field f is present and Decode<Kind> fails on it (an absent field is no error;
- * the record-level OpenMessageErr class is in status).  Fields >= 64 are not reported.
+ * the record-level OpenMessageErr class is in status).  A schema of more than 64 fields has
+ * ceil(nfields / 64) mask words per record, word-major: errmask[c * n + i] bit f is field
+ * 64 c + f of record i.
  * Runs the schema-specialised kernel's errmask variant where the schema has one (else the
  * generic kernel): the same columns and status as spec_decode_flat. */
 int spec_decode_flat_errors(const spec_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,

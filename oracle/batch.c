@@ -93,7 +93,8 @@ typedef struct {
 
 static void *decode_range(void *arg) {
     decode_job *j = (decode_job *)arg;
-    int widths[256];
+    int widths[1024];
+    if (j->nfields > 1024) return NULL;
     for (int f = 0; f < j->nfields; f++) widths[f] = so_kind_width(j->kinds[f]);
     for (uint64_t r = j->lo; r < j->hi; r++) {
         uint64_t s = rec_start(j->ends, r);
@@ -111,7 +112,7 @@ static void *decode_range(void *arg) {
 int so_decode_flat_batch(int nfields, const uint16_t *tags, const uint8_t *kinds,
                          const uint8_t *stream, const uint64_t *ends, uint64_t n,
                          void *const *columns, uint8_t *status, int nthreads) {
-    if (nfields > 256) return -1;
+    if (nfields > 1024) return -1;
     if (nthreads < 1) nthreads = 1;
     if ((uint64_t)nthreads > n) nthreads = n ? (int)n : 1;
     decode_job jobs[256];
@@ -165,8 +166,8 @@ int so_encode_flat_batch(int nfields, const uint16_t *tags, const uint8_t *kinds
     so_buf buf;
     so_buf_init_fixed(&buf, out, (size_t)out_cap);
     so_writer *w = so_writer_new(&buf);
-    int widths[256];
-    if (nfields > 256) return -1;
+    int widths[1024];
+    if (nfields > 1024) return -1;
     for (int f = 0; f < nfields; f++) widths[f] = so_kind_width(kinds[f]);
     int rc = 0;
     for (uint64_t r = 0; r < n; r++) {
@@ -333,7 +334,9 @@ long long so_frames_read(const uint8_t *buf, uint64_t len, uint64_t *ends, uint6
 
 /* The *Err getters (internal/types/msg.go:233-459) of every field of every record:
  * errmask[r] bit f = m.<Kind>Err(tag_f) returns an error (decode.Decode<Kind>(m.field(tag)):
- * an absent field is nil and decodes without error).  Fields >= 64 are not reported. */
+ * an absent field is nil and decodes without error).  More than 64 fields: ceil(nfields / 64)
+ * words per record, word-major (errmask[c * n + r] bit f = field 64 c + f), as
+ * spec_decode_flat_errors lays them out. */
 int so_decode_flat_errors(int nfields, const uint16_t *tags, const uint8_t *kinds, const uint8_t *stream,
                           const uint64_t *ends, uint64_t n, uint64_t *errmask) {
     for (uint64_t r = 0; r < n; r++) {
@@ -341,7 +344,11 @@ int so_decode_flat_errors(int nfields, const uint16_t *tags, const uint8_t *kind
         so_message m;
         if (so_open_message_err(stream + s, (size_t)(ends[r] - s), &m)) memset(&m, 0, sizeof(m));
         uint64_t bits = 0;
-        for (int f = 0; f < nfields && f < 64; f++) {
+        for (int f = 0; f < nfields; f++) {
+            if (f && (f & 63) == 0) { /* the next word */
+                errmask[(uint64_t)(f / 64 - 1) * n + r] = bits;
+                bits = 0;
+            }
             size_t len;
             const uint8_t *b = so_message_field_raw(&m, tags[f], &len);
             int k;
@@ -368,9 +375,9 @@ int so_decode_flat_errors(int nfields, const uint16_t *tags, const uint8_t *kind
             case SO_KIND_STRING: e = so_decode_string(b, len, &off, &vlen, &k); break;
             case SO_KIND_BYTES: e = so_decode_bytes(b, len, &off, &vlen, &k); break;
             }
-            if (e) bits |= 1ull << f;
+            if (e) bits |= 1ull << (f & 63);
         }
-        errmask[r] = bits;
+        errmask[(uint64_t)(nfields > 0 ? (nfields - 1) / 64 : 0) * n + r] = bits;
     }
     return 0;
 }

@@ -556,16 +556,18 @@ def decode_flat_batch(tags, kinds, stream: np.ndarray, ends: np.ndarray, widths,
 
 
 def decode_flat_errors(tags, kinds, stream: np.ndarray, ends: np.ndarray) -> np.ndarray:
-    """Per record the *Err getters' error bits (bit f = field f's getter errs) -> uint64 [n]."""
+    """Per record the *Err getters' error bits (bit f = field f's getter errs) -> uint64 [n]; more
+    than 64 fields: uint64 [ceil(nfields / 64), n] (row c: fields 64c..64c+63)."""
     n = len(ends)
-    em = np.zeros(max(n, 1), np.uint64)
+    words = max(1, (len(tags) + 63) // 64)
+    em = np.zeros((words, max(n, 1)), np.uint64)
     tags_a = np.asarray(tags, dtype=np.uint16)
     kinds_a = np.asarray(kinds, dtype=np.uint8)
     stream = np.ascontiguousarray(stream, dtype=np.uint8)
     ends = np.ascontiguousarray(ends, dtype=np.uint64)
     lib().so_decode_flat_errors(len(tags), _ptr(tags_a), _ptr(kinds_a), _ptr(stream) if stream.size else None,
                                 _ptr(ends) if n else None, n, _ptr(em))
-    return em[:n]
+    return em[0, :n] if words == 1 else em[:, :n]
 
 
 def encode_flat_batch(tags, kinds, columns, heaps, n, cap=None):
@@ -578,7 +580,9 @@ def encode_flat_batch(tags, kinds, columns, heaps, n, cap=None):
           for h in heaps]
     heapptrs = (C.c_void_p * len(hs))(*[h.ctypes.data for h in hs])
     if cap is None:
-        cap = 64 + n * 1024 + sum(int(h.size) for h in hs) * 2
+        # per record: <= 45 bytes per fixed field (bin256 + type + a 6-byte big-table entry) + string
+        # headers; string/bytes payloads from the heaps
+        cap = 64 + n * (64 + 48 * len(tags)) + sum(int(h.size) for h in hs) * 2
     out = np.zeros(cap, dtype=np.uint8)
     ends = np.zeros(n, dtype=np.uint64)
     rc = lib().so_encode_flat_batch(len(tags), _ptr(tags_a), _ptr(kinds_a), colptrs, heapptrs, n,

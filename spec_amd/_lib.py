@@ -14,7 +14,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libspec_amd.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "spec_amd.h")
 
-SPEC_MAX_FIELDS = 64
+SPEC_MAX_FIELDS = 1024  # include/spec_amd.h (schemas over 64 fields: chunked decode, wide encode)
+SPEC_NESTED_MAX_FIELDS = 64
 
 
 class SpecField(C.Structure):

@@ -92,18 +92,20 @@ def decode_flat(schema: Schema, stream: torch.Tensor, ends: torch.Tensor, *, col
 
 def decode_flat_errors(schema: Schema, stream: torch.Tensor, ends: torch.Tensor, cuda_stream=None):
     """spec_decode_flat_errors: decode_flat plus the per-record field error mask (bit f: field f's
-    <Kind>Err getter errs, internal/types/msg.go:233-459) -> (Columns, errmask int64 [n])."""
+    <Kind>Err getter errs, internal/types/msg.go:233-459) -> (Columns, errmask int64 [n]); a schema
+    of more than 64 fields gets errmask int64 [ceil(nfields / 64), n] (row c: fields 64c..64c+63)."""
     _check_dev(stream, "stream", torch.uint8)
     _check_dev(ends, "ends", torch.int64)
     n = ends.numel()
     cols = alloc_columns(schema, n, stream.device)
     st = torch.empty(n, dtype=torch.uint8, device=stream.device)
-    em = torch.empty(max(n, 1), dtype=torch.int64, device=stream.device)
+    words = max(1, (len(schema) + 63) // 64)
+    em = torch.empty((words, max(n, 1)), dtype=torch.int64, device=stream.device)
     ptrs = (C.c_void_p * max(1, len(cols)))(*[c.data_ptr() for c in cols])
     rc = _lib.lib().spec_decode_flat_errors(C.byref(schema.c), _ptr(stream), stream.numel(), _ptr(ends), n, ptrs,
                                              _ptr(st), _ptr(em), _stream_handle(cuda_stream))
     _lib.check(rc, "spec_decode_flat_errors")
-    return Columns(schema, cols, st), em[:n]
+    return Columns(schema, cols, st), (em[0, :n] if words == 1 else em[:, :n])
 
 
 class Decoder:

@@ -3,6 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <mutex>
+#include <vector>
+
 #include "../../include/spec_amd.h"
 #include "spec_internal.hpp"
 
@@ -26,23 +29,24 @@ int kind_width(int kind) {
 // Table order a Writer produces for this schema: messageStack.insert over the tags in write
 // order, insertion sort where an equal tag written later moves before the earlier one
 // (internal/writer/stack_msg.go:37-61).  order[j] = schema index of the j-th table entry.
-void table_order(const spec_schema *s, uint8_t *order) {
+template <class T>
+void table_order(const spec_schema *s, T *order) {
     uint16_t tags[SPEC_MAX_FIELDS];
-    uint8_t idx[SPEC_MAX_FIELDS];
+    uint16_t idx[SPEC_MAX_FIELDS];
     for (uint32_t f = 0; f < s->nfields; f++) {
         tags[f] = s->fields[f].tag;
-        idx[f] = (uint8_t)f;
+        idx[f] = (uint16_t)f;
         for (int i = (int)f; i > 0; i--) {
             if (tags[i - 1] < tags[i]) break;
             uint16_t t = tags[i - 1];
             tags[i - 1] = tags[i];
             tags[i] = t;
-            uint8_t x = idx[i - 1];
+            uint16_t x = idx[i - 1];
             idx[i - 1] = idx[i];
             idx[i] = x;
         }
     }
-    memcpy(order, idx, s->nfields);
+    for (uint32_t j = 0; j < s->nfields; j++) order[j] = (T)idx[j];
 }
 
 int check_schema(const spec_schema *s) {
@@ -54,7 +58,8 @@ int check_schema(const spec_schema *s) {
 
 // outer schema of a nested decode: flat kinds plus exactly one SPEC_KIND_LIST; *list_f = its index
 int check_nested(const spec_nested_schema *s, uint32_t *list_f) {
-    if (!s || s->outer.nfields > SPEC_MAX_FIELDS || check_schema(&s->item)) return SPEC_E_INVALID_ARGUMENT;
+    if (!s || s->outer.nfields > SPEC_KFIELDS || check_schema(&s->item) || s->item.nfields > SPEC_KFIELDS)
+        return SPEC_E_INVALID_ARGUMENT; // the nested kernels take both field sets as kernel arguments
     int lists = 0;
     for (uint32_t f = 0; f < s->outer.nfields; f++) {
         if (s->outer.fields[f].kind == SPEC_KIND_LIST) {
@@ -67,24 +72,68 @@ int check_nested(const spec_nested_schema *s, uint32_t *list_f) {
     return lists == 1 ? SPEC_OK : SPEC_E_INVALID_ARGUMENT;
 }
 
+// ---- pinned uploads: per-call kernel data too large for the kernel arguments (the field set of a
+// wide schema) goes to the device from a ring of pinned slots per device, a slot reused once the
+// copy out of it has run (its event), so a call never synchronises with the device
+struct UploadRing {
+    static constexpr int SLOTS = 8;
+    struct Slot {
+        uint8_t *p = nullptr;
+        size_t cap = 0;
+        hipEvent_t ev = nullptr;
+    } slot[SLOTS];
+    int next = 0;
+};
+std::mutex g_upload_mu;
+UploadRing g_upload[64];
+
+hipError_t upload_async(void *dst, const void *src, size_t bytes, hipStream_t st) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> lk(g_upload_mu);
+    UploadRing &R = g_upload[dev];
+    UploadRing::Slot &S = R.slot[R.next];
+    R.next = (R.next + 1) % UploadRing::SLOTS;
+    if (S.ev && (e = hipEventSynchronize(S.ev)) != hipSuccess) return e; // its previous copy has run
+    if (!S.ev && (e = hipEventCreateWithFlags(&S.ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if (S.cap < bytes) {
+        if (S.p) (void)hipHostFree(S.p);
+        S.p = nullptr;
+        S.cap = 0;
+        if ((e = hipHostMalloc((void **)&S.p, bytes, hipHostMallocDefault)) != hipSuccess) return e;
+        S.cap = bytes;
+    }
+    memcpy(S.p, src, bytes);
+    if ((e = hipMemcpyAsync(dst, S.p, bytes, hipMemcpyHostToDevice, st)) != hipSuccess) return e;
+    return hipEventRecord(S.ev, st);
+}
+
 int hip_rc(hipError_t e) {
     if (e == hipSuccess) return SPEC_OK;
     g_last_hip_error = (int)e;
     return SPEC_E_HIP;
 }
 
-void fill_field_set(spec::FieldSet &fs, const spec_schema *schema, void *const *columns, uint8_t *status) {
+// Fields [f0, f1) (at most SPEC_KFIELDS) of the schema as one kernel field set; rank = the
+// field's index in the table a Writer emits for the WHOLE schema (a chunk of a wide schema is
+// looked up in the full table).
+void fill_field_set(spec::FieldSet &fs, const spec_schema *schema, void *const *columns, uint8_t *status,
+                    uint32_t f0 = 0, uint32_t f1 = ~0u) {
     memset(&fs, 0, sizeof(fs));
+    if (f1 > schema->nfields) f1 = schema->nfields;
     fs.status = status;
     fs.errmask = nullptr;
-    fs.nfields = schema->nfields;
-    uint8_t order[SPEC_MAX_FIELDS];
+    fs.nfields = f1 - f0;
+    uint16_t order[SPEC_MAX_FIELDS], rank[SPEC_MAX_FIELDS];
     table_order(schema, order);
-    for (uint32_t j = 0; j < schema->nfields; j++) fs.rank[order[j]] = (uint8_t)j;
-    for (uint32_t f = 0; f < schema->nfields; f++) {
-        fs.tags[f] = schema->fields[f].tag;
-        fs.kinds[f] = schema->fields[f].kind;
-        fs.cols[f] = columns ? columns[f] : nullptr;
+    for (uint32_t j = 0; j < schema->nfields; j++) rank[order[j]] = (uint16_t)j;
+    for (uint32_t f = f0; f < f1; f++) {
+        fs.tags[f - f0] = schema->fields[f].tag;
+        fs.kinds[f - f0] = schema->fields[f].kind;
+        fs.rank[f - f0] = rank[f];
+        fs.cols[f - f0] = columns ? columns[f] : nullptr;
     }
 }
 
@@ -107,6 +156,55 @@ void fill_encode_args(spec::EncodeArgs &a, const spec_schema *schema, const void
     a.nblocks = (n + spec::ENC_BLOCK - 1) / spec::ENC_BLOCK;
 }
 
+// Encode workspace: the block sums (nblocks + 1 words), then room for a wide schema's field set.
+constexpr size_t WIDE_FIELDS_BYTES = 32768; // >= SPEC_MAX_FIELDS x (2 + 1 + 2 + 8 + 8 + 8) + alignment
+size_t enc_ws_sums(uint64_t n) {
+    const uint64_t nblocks = (n + spec::ENC_BLOCK - 1) / spec::ENC_BLOCK;
+    return (size_t)(((nblocks + 1) * sizeof(uint64_t) + 255) & ~(uint64_t)255);
+}
+
+// A schema with more than SPEC_KFIELDS fields: its field set (tags, kinds, table positions,
+// columns, heaps) written into the workspace after the block sums, from a pinned slot on the
+// call's stream; the kernel argument holds the pointers.
+int fill_wide_encode_args(spec::WideEncodeArgs &a, const spec_schema *schema, const void *const *columns,
+                          const uint8_t *const *heaps, const uint64_t *heap_lens, uint64_t n, void *workspace,
+                          hipStream_t st) {
+    memset(&a, 0, sizeof(a));
+    const uint32_t N = schema->nfields;
+    a.n = n;
+    a.nblocks = (n + spec::ENC_BLOCK - 1) / spec::ENC_BLOCK;
+    uint8_t *dev = (uint8_t *)workspace + enc_ws_sums(n);
+    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const size_t o_tags = 0, o_kinds = al(o_tags + 2 * N), o_inv = al(o_kinds + N), o_cols = al(o_inv + 2 * N),
+                 o_heaps = o_cols + 8 * N, o_lens = o_heaps + 8 * N, bytes = o_lens + 8 * N;
+    if (bytes > WIDE_FIELDS_BYTES) return SPEC_E_INVALID_ARGUMENT;
+    std::vector<uint8_t> h(bytes, 0);
+    uint16_t order[SPEC_MAX_FIELDS];
+    table_order(schema, order);
+    for (uint32_t f = 0; f < N; f++) {
+        ((uint16_t *)(h.data() + o_tags))[f] = schema->fields[f].tag;
+        h[o_kinds + f] = schema->fields[f].kind;
+        ((uint16_t *)(h.data() + o_inv))[order[f]] = (uint16_t)f;
+        ((const void **)(h.data() + o_cols))[f] = columns ? columns[f] : nullptr;
+        const int k = schema->fields[f].kind;
+        if (heaps && heap_lens && (k == SPEC_KIND_STRING || k == SPEC_KIND_BYTES)) {
+            if (!heaps[f] && heap_lens[f]) return SPEC_E_INVALID_ARGUMENT;
+            ((const uint8_t **)(h.data() + o_heaps))[f] = heaps[f];
+            ((uint64_t *)(h.data() + o_lens))[f] = heap_lens[f];
+        }
+        if (schema->fields[f].tag > 255) a.f.table_big_forced = 1;
+    }
+    a.f.nfields = N;
+    a.f.tags = (const uint16_t *)(dev + o_tags);
+    a.f.kinds = dev + o_kinds;
+    a.f.inv_order = (const uint16_t *)(dev + o_inv);
+    a.f.cols = (const void *const *)(dev + o_cols);
+    a.f.heaps = (const uint8_t *const *)(dev + o_heaps);
+    a.f.heap_lens = (const uint64_t *)(dev + o_lens);
+    const hipError_t e = upload_async(dev, h.data(), bytes, st);
+    return e == hipSuccess ? SPEC_OK : hip_rc(e);
+}
+
 } // namespace
 
 namespace spec {
@@ -122,6 +220,24 @@ int encode_flat_passes(const spec_schema *schema, const void *const *columns, co
     if (rc) return rc;
     if (!columns || !workspace || (n && (!ends || !out))) return SPEC_E_INVALID_ARGUMENT;
     if (workspace_size < spec_encode_flat_workspace_size(n)) return SPEC_E_WORKSPACE;
+    if (schema->nfields > SPEC_KFIELDS) {
+        for (uint32_t f = 0; f < schema->nfields; f++) {
+            const int k = schema->fields[f].kind;
+            if ((k == SPEC_KIND_STRING || k == SPEC_KIND_BYTES) && (!heaps || !heap_lens)) return SPEC_E_INVALID_ARGUMENT;
+        }
+        WideEncodeArgs w{};
+        if ((rc = fill_wide_encode_args(w, schema, columns, heaps, heap_lens, n, workspace, stream))) return rc;
+        w.check_heaps = 1;
+        w.out = out;
+        w.out_cap = out_cap;
+        w.ends = ends;
+        w.ends_base = ends_base;
+        w.block_sums = (uint64_t *)workspace;
+        w.total = total;
+        if ((passes & ENC_PASS_SIZE) && launch_encode_wide_size(w, stream)) return hip_rc(hipGetLastError());
+        if ((passes & ENC_PASS_WRITE) && launch_encode_wide_write(w, stream)) return hip_rc(hipGetLastError());
+        return SPEC_OK;
+    }
     EncodeArgs a{};
     fill_encode_args(a, schema, columns, n);
     for (uint32_t f = 0; f < schema->nfields; f++) {
@@ -213,11 +329,23 @@ static int decode_flat_impl(const spec_schema *schema, const uint8_t *stream_byt
     a.n = r1;
     a.r0 = r0;
     a.head = head;
-    fill_field_set(a.f, schema, columns, status);
-    a.f.errmask = errmask;
     // LDS slab from the mean record size of the range (the caller knows the range's bytes;
     // for a whole batch it is stream_len / n)
     double avg = range_bytes ? (double)range_bytes / (double)(r1 - r0) : (double)stream_len / (double)r1;
+    if (schema->nfields > SPEC_KFIELDS) {
+        // a wide schema: the generic kernel once per chunk of SPEC_KFIELDS fields, each chunk's
+        // getters against the record's whole table (ranks in the full Writer table); chunk 0
+        // writes the status (OpenMessageErr, the same for every chunk), chunk c the errmask words
+        // errmask[c * r1 + r] (bit f = field 64 c + f)
+        for (uint32_t f0 = 0; f0 < schema->nfields; f0 += SPEC_KFIELDS) {
+            fill_field_set(a.f, schema, columns, f0 ? nullptr : status, f0, f0 + SPEC_KFIELDS);
+            a.f.errmask = errmask ? errmask + (uint64_t)(f0 / SPEC_KFIELDS) * r1 : nullptr;
+            if (spec::launch_decode_flat(a, avg, (hipStream_t)stream)) return hip_rc(hipGetLastError());
+        }
+        return SPEC_OK;
+    }
+    fill_field_set(a.f, schema, columns, status);
+    a.f.errmask = errmask;
     // field error masks: the schema-specialised kernel's errmask variant (or the generic path)
     int j = spec::jit_launch_decode_flat(schema, a, avg, (hipStream_t)stream);
     if (j < 0) return hip_rc(hipGetLastError());
@@ -496,10 +624,7 @@ int spec_encode_nested(const spec_nested_schema *schema, const void *const *oute
     return SPEC_OK;
 }
 
-size_t spec_encode_flat_workspace_size(uint64_t n) {
-    uint64_t nblocks = (n + spec::ENC_BLOCK - 1) / spec::ENC_BLOCK;
-    return (size_t)((nblocks + 1) * sizeof(uint64_t));
-}
+size_t spec_encode_flat_workspace_size(uint64_t n) { return enc_ws_sums(n) + WIDE_FIELDS_BYTES; }
 
 int spec_encode_flat_size(const spec_schema *schema, const void *const *columns, uint64_t n,
                           void *workspace, size_t workspace_size, uint64_t *total, void *stream) {
@@ -507,6 +632,15 @@ int spec_encode_flat_size(const spec_schema *schema, const void *const *columns,
     if (rc) return rc;
     if (!columns || !workspace) return SPEC_E_INVALID_ARGUMENT;
     if (workspace_size < spec_encode_flat_workspace_size(n)) return SPEC_E_WORKSPACE;
+    if (schema->nfields > SPEC_KFIELDS) {
+        spec::WideEncodeArgs w{};
+        if ((rc = fill_wide_encode_args(w, schema, columns, nullptr, nullptr, n, workspace, (hipStream_t)stream)))
+            return rc;
+        w.block_sums = (uint64_t *)workspace;
+        w.total = total;
+        if (spec::launch_encode_wide_size(w, (hipStream_t)stream)) return hip_rc(hipGetLastError());
+        return SPEC_OK;
+    }
     spec::EncodeArgs a{};
     fill_encode_args(a, schema, columns, n);
     a.block_sums = (uint64_t *)workspace;

@@ -31,19 +31,16 @@
 
 namespace spec {
 
-#ifndef SPEC_MAX_FIELDS
-#define SPEC_MAX_FIELDS 64
-#endif
 
 // The fields a record decode produces: one column per schema field + the status column.
 struct FieldSet {
     uint8_t *status;
     uint64_t *errmask; // optional: bit f = field f's <Kind>Err getter errs
     uint32_t nfields;
-    uint16_t tags[SPEC_MAX_FIELDS];
-    uint8_t kinds[SPEC_MAX_FIELDS];
-    uint8_t rank[SPEC_MAX_FIELDS]; // index of the field's tag in the sorted table a writer emits
-    void *cols[SPEC_MAX_FIELDS];
+    uint16_t tags[SPEC_KFIELDS];
+    uint8_t kinds[SPEC_KFIELDS];
+    uint16_t rank[SPEC_KFIELDS]; // index of the field's tag in the sorted table a writer emits
+    void *cols[SPEC_KFIELDS];
 };
 
 // Passed by value as the kernel argument (lives in the kernarg segment => scalar loads,
@@ -584,7 +581,7 @@ struct RuntimeSpec {
 };
 
 // Spec (generated by jit.cpp) provides:
-//   N              number of fields (1..SPEC_MAX_FIELDS; the register-resident fast path below
+//   N              number of fields (1..SPEC_KFIELDS; the register-resident fast path below
 //                  takes up to FAST_MAX_FIELDS small-table fields, fast_wide the rest)
 //   kind[f], rank[f]  per schema field
 //   stag[k]        k-th tag of the table a Writer emits (strictly increasing)

@@ -8,22 +8,33 @@
 
 #include "spec_device.hpp"
 
-#ifndef SPEC_MAX_FIELDS
-#define SPEC_MAX_FIELDS 64
-#endif
 
 namespace spec {
 
 // The columns one message's fields are written from.
 struct EncFields {
     uint32_t nfields;
-    uint16_t tags[SPEC_MAX_FIELDS];
-    uint8_t kinds[SPEC_MAX_FIELDS];
-    uint8_t order[SPEC_MAX_FIELDS]; // table order: order[j] = schema index of j-th table entry
-    const void *cols[SPEC_MAX_FIELDS];
-    const uint8_t *heaps[SPEC_MAX_FIELDS];
-    uint64_t heap_lens[SPEC_MAX_FIELDS];
+    uint16_t tags[SPEC_KFIELDS];
+    uint8_t kinds[SPEC_KFIELDS];
+    uint8_t order[SPEC_KFIELDS]; // table order: order[j] = schema index of j-th table entry
+    const void *cols[SPEC_KFIELDS];
+    const uint8_t *heaps[SPEC_KFIELDS];
+    uint64_t heap_lens[SPEC_KFIELDS];
     uint32_t table_big_forced; // 1 if any tag > 255 (IsBigMessage holds for every record)
+};
+
+// The field set of a schema with more than SPEC_KFIELDS fields: the same members as EncFields,
+// as arrays in device memory (the caller's workspace, uploaded per call), so the kernel argument
+// stays small.  field_size / record_size / emit_message read either through the same names.
+struct WideEncFields {
+    uint32_t nfields;
+    uint32_t table_big_forced;
+    const uint16_t *tags;
+    const uint8_t *kinds;
+    const uint16_t *inv_order; // table position of each field (the inverse of the Writer's order)
+    const void *const *cols;
+    const uint8_t *const *heaps;
+    const uint64_t *heap_lens;
 };
 
 // Passed by value as the kernel argument (lives in the kernarg segment => scalar loads,
@@ -39,6 +50,22 @@ struct EncodeArgs {
     uint64_t *block_sums;  // workspace: per-block encoded bytes, then exclusive offsets
     uint64_t nblocks;
     uint64_t *total;
+    static constexpr bool kWide = false;
+};
+
+// EncodeArgs of a schema with more than SPEC_KFIELDS fields (encode_flat.hip wide kernels).
+struct WideEncodeArgs {
+    uint64_t n;
+    WideEncFields f;
+    uint32_t check_heaps;
+    uint8_t *out;
+    uint64_t out_cap;
+    uint64_t *ends;
+    uint64_t ends_base;
+    uint64_t *block_sums;
+    uint64_t nblocks;
+    uint64_t *total;
+    static constexpr bool kWide = true;
 };
 
 constexpr int ENC_BLOCK = 256;            // records per encode block (4 waves, one record per lane)
@@ -68,8 +95,8 @@ __device__ __forceinline__ uint32_t kind_width(uint32_t k) {
 
 // Encoded size of field f of record r (value | type, internal/encode/...); err set on an
 // encoder error (string/bytes > MaxSize or outside its heap).
-__device__ __forceinline__ uint64_t field_size(const EncFields &a, uint32_t f, uint64_t r, bool check_heaps,
-                                               bool &err) {
+template <class FS>
+__device__ __forceinline__ uint64_t field_size(const FS &a, uint32_t f, uint64_t r, bool check_heaps, bool &err) {
     const uint8_t *col = (const uint8_t *)a.cols[f];
     switch (a.kinds[f]) {
     case K_BOOL: return 1;
@@ -105,8 +132,8 @@ struct NoLists {
     __device__ __forceinline__ uint64_t operator()(uint32_t, uint64_t) const { return 0; }
 };
 
-template <class Lists = NoLists>
-__device__ __forceinline__ RecSize record_size(const EncFields &a, uint64_t r, bool check_heaps, bool &err,
+template <class Lists = NoLists, class FS>
+__device__ __forceinline__ RecSize record_size(const FS &a, uint64_t r, bool check_heaps, bool &err,
                                                const Lists &lists = Lists()) {
     uint64_t data = 0;
     for (uint32_t f = 0; f < a.nfields; f++)
@@ -500,10 +527,9 @@ struct NoListEmit {
 
 // One message (internal/writer/writer.go:376-553): fields in write order, table entries at
 // their sorted positions, trailer.  Returns the end position.
-template <class Sink, class Pos, class Lists = NoListEmit>
-__device__ __forceinline__ Pos emit_message(const EncFields &a, const Sink &k, Pos start, uint64_t r,
-                                            const RecSize &rs, const uint8_t *inv_order,
-                                            const Lists &lists = Lists()) {
+template <class Sink, class Pos, class Lists = NoListEmit, class FS, class Inv>
+__device__ __forceinline__ Pos emit_message(const FS &a, const Sink &k, Pos start, uint64_t r, const RecSize &rs,
+                                            const Inv *inv_order, const Lists &lists = Lists()) {
     Emit<Sink, Pos> em(k, start);
     const Pos tstart = start + (Pos)rs.data;
     const uint32_t esize = rs.big ? 6 : 3;
@@ -560,7 +586,7 @@ __device__ __forceinline__ Pos emit_message(const EncFields &a, const Sink &k, P
         }
         end = (uint64_t)(em.pos - start);
         // table entry for this field at its sorted position (encode/msg.go:58-72)
-        Pos p = tstart + (Pos)(inv_order[f] * esize);
+        Pos p = tstart + (Pos)((uint32_t)inv_order[f] * esize);
         uint32_t tag = a.tags[f];
         if (rs.big) {
             k.st1(p, tag >> 8);
@@ -597,17 +623,20 @@ __device__ __forceinline__ Pos emit_message(const EncFields &a, const Sink &k, P
 
 struct RuntimeEnc {
     struct Rec {};
-    static __device__ __forceinline__ Rec load(const EncFields &, uint64_t) { return Rec{}; }
-    static __device__ __forceinline__ void load_cols(const EncFields &, uint64_t, Rec &) {}
-    static __device__ __forceinline__ void load_heaps(const EncFields &, Rec &) {}
-    template <class Lists = NoLists>
-    static __device__ __forceinline__ RecSize size(const EncFields &f, const Rec &, uint64_t r, bool check,
-                                                   bool &err, const Lists &lists = Lists()) {
+    template <class FS>
+    static __device__ __forceinline__ Rec load(const FS &, uint64_t) { return Rec{}; }
+    template <class FS>
+    static __device__ __forceinline__ void load_cols(const FS &, uint64_t, Rec &) {}
+    template <class FS>
+    static __device__ __forceinline__ void load_heaps(const FS &, Rec &) {}
+    template <class Lists = NoLists, class FS>
+    static __device__ __forceinline__ RecSize size(const FS &f, const Rec &, uint64_t r, bool check, bool &err,
+                                                   const Lists &lists = Lists()) {
         return record_size(f, r, check, err, lists);
     }
-    template <class Sink, class Pos, class Lists = NoListEmit>
-    static __device__ __forceinline__ void emit(const EncFields &f, const Sink &k, Pos p, uint64_t r, const Rec &,
-                                                const RecSize &rs, const uint8_t *inv_order,
+    template <class Sink, class Pos, class Lists = NoListEmit, class FS, class Inv>
+    static __device__ __forceinline__ void emit(const FS &f, const Sink &k, Pos p, uint64_t r, const Rec &,
+                                                const RecSize &rs, const Inv *inv_order,
                                                 const Lists &lists = Lists()) {
         emit_message(f, k, p, r, rs, inv_order, lists);
     }
@@ -927,8 +956,8 @@ struct SpecEnc {
 };
 
 // Pass 1: per-block encoded bytes (all-ones on an encoder error).
-template <class P>
-__device__ __forceinline__ void encode_size_body(const EncodeArgs &a) {
+template <class P, class A>
+__device__ __forceinline__ void encode_size_body(const A &a) {
     __shared__ uint64_t part[ENC_BLOCK / 64];
     __shared__ int errs;
     if (threadIdx.x == 0) errs = 0;
@@ -984,10 +1013,16 @@ __device__ __forceinline__ void copy_slab_out(const uint8_t *slab, uint8_t *gbas
 // into the wave's LDS slab, the wave copies the slab to HBM with 16-byte stores; ends[]
 // written coalesced.  A wave whose output span does not fit the slab emits straight to HBM.
 // smem: ENC_LDS_HEAD bytes of header, then ENC_BLOCK / 64 slabs of ENC_SLAB bytes.
-template <class P>
-__device__ __forceinline__ void encode_write_body(const EncodeArgs &a, uint8_t *smem) {
+template <class P, class A>
+__device__ __forceinline__ void encode_write_body(const A &a, uint8_t *smem) {
     uint64_t *wsum = (uint64_t *)smem;
-    uint8_t *inv_order = smem + 8 * (ENC_BLOCK / 64);
+    // the table position of every field: built in LDS from the Writer's order, or (a wide
+    // schema) precomputed in device memory
+    uint8_t *inv_lds = smem + 8 * (ENC_BLOCK / 64);
+    const auto *inv_order = [&] {
+        if constexpr (A::kWide) return a.f.inv_order;
+        else return (const uint8_t *)inv_lds;
+    }();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t r = (uint64_t)blockIdx.x * ENC_BLOCK + threadIdx.x;
     const bool valid = r < a.n;
@@ -996,7 +1031,8 @@ __device__ __forceinline__ void encode_write_body(const EncodeArgs &a, uint8_t *
     const typename P::Rec rec = P::load(a.f, valid ? r : a.n - 1);
     const uint64_t total = a.block_sums[a.nblocks], blk_pre = a.block_sums[blockIdx.x];
     if (total > a.out_cap) return; // capacity error or encoder error (total == ~0)
-    if (threadIdx.x < a.f.nfields) inv_order[a.f.order[threadIdx.x]] = (uint8_t)threadIdx.x;
+    if constexpr (!A::kWide)
+        if (threadIdx.x < a.f.nfields) inv_lds[a.f.order[threadIdx.x]] = (uint8_t)threadIdx.x;
     bool err = false;
     RecSize rs = P::size(a.f, rec, r, false, err);
     if (!valid) rs.total = 0;

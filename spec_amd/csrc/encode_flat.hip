@@ -42,6 +42,34 @@ __global__ __launch_bounds__(ENC_BLOCK) void encode_write_kernel(EncodeArgs a) {
     encode_write_body<RuntimeEnc>(a, smem);
 }
 
+// Schemas with more than SPEC_KFIELDS fields: the same bodies over a field set in device memory
+// (RuntimeEnc reads it through WideEncFields' pointers; no schema-specialised kernel).
+__global__ __launch_bounds__(ENC_BLOCK) void encode_wide_size_kernel(WideEncodeArgs a) {
+    encode_size_body<RuntimeEnc>(a);
+}
+
+__global__ __launch_bounds__(1024) void encode_wide_scan_kernel(WideEncodeArgs a) {
+    scan_block_sums(a.block_sums, a.nblocks, a.total);
+}
+
+__global__ __launch_bounds__(ENC_BLOCK) void encode_wide_write_kernel(WideEncodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    encode_write_body<RuntimeEnc>(a, smem);
+}
+
+int launch_encode_wide_size(const WideEncodeArgs &a, hipStream_t stream) {
+    if (a.nblocks) hipLaunchKernelGGL(encode_wide_size_kernel, dim3((unsigned)a.nblocks), dim3(ENC_BLOCK), 0, stream, a);
+    hipLaunchKernelGGL(encode_wide_scan_kernel, dim3(1), dim3(1024), 0, stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_encode_wide_write(const WideEncodeArgs &a, hipStream_t stream) {
+    if (!a.nblocks) return 0;
+    hipLaunchKernelGGL(encode_wide_write_kernel, dim3((unsigned)a.nblocks), dim3(ENC_BLOCK), enc_write_lds_bytes(),
+                       stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_encode_size(const spec_schema *schema, const EncodeArgs &a, hipStream_t stream) {
     int j = a.nblocks ? jit_launch_encode(schema, a, false, stream) : 1;
     if (j < 0) return -1;

@@ -81,11 +81,11 @@ void writer_order(const spec_schema *s, uint8_t *order, uint16_t *sorted) {
 // Writer's table is strictly increasing: any field count, tags <= 255 (small tables) or with a
 // tag > 255 (every table big).
 bool has_flat_fast_path(const spec_schema *s) {
-    if (s->nfields == 0 || s->nfields > SPEC_MAX_FIELDS) return false;
+    if (s->nfields == 0 || s->nfields > SPEC_KFIELDS) return false;
     for (uint32_t f = 0; f < s->nfields; f++)
         if (s->fields[f].kind == SPEC_KIND_LIST) return false;
-    uint8_t order[SPEC_MAX_FIELDS];
-    uint16_t sorted[SPEC_MAX_FIELDS];
+    uint8_t order[SPEC_KFIELDS];
+    uint16_t sorted[SPEC_KFIELDS];
     writer_order(s, order, sorted);
     for (uint32_t k = 0; k < s->nfields; k++) {
         if (sorted[k] == 0) return false;
@@ -98,8 +98,8 @@ bool has_flat_fast_path(const spec_schema *s) {
 // FAST_MAX_FIELDS fields.
 bool has_fast_path(const spec_schema *s) {
     if (s->nfields == 0 || s->nfields > (uint32_t)spec::FAST_MAX_FIELDS) return false;
-    uint8_t order[SPEC_MAX_FIELDS];
-    uint16_t sorted[SPEC_MAX_FIELDS];
+    uint8_t order[SPEC_KFIELDS];
+    uint16_t sorted[SPEC_KFIELDS];
     writer_order(s, order, sorted);
     for (uint32_t k = 0; k < s->nfields; k++) {
         if (sorted[k] > 255 || sorted[k] == 0) return false;
@@ -128,10 +128,10 @@ std::string key_of(const spec_schema *s, int device, Prog p) {
 
 // struct <name> { N, kind[], rank[], stag[] }: the fast-path schema of decode_core.hpp
 void emit_spec(std::ostringstream &o, const char *name, const spec_schema *s) {
-    uint8_t order[SPEC_MAX_FIELDS];
-    uint16_t sorted[SPEC_MAX_FIELDS];
+    uint8_t order[SPEC_KFIELDS];
+    uint16_t sorted[SPEC_KFIELDS];
     writer_order(s, order, sorted);
-    uint8_t rank[SPEC_MAX_FIELDS];
+    uint8_t rank[SPEC_KFIELDS];
     for (uint32_t k = 0; k < s->nfields; k++) rank[order[k]] = (uint8_t)k;
     o << "struct " << name << " {\n  static constexpr int N = " << s->nfields << ";\n"
       << "  static constexpr uint32_t kind[N] = {";
@@ -184,8 +184,8 @@ std::string generate_nested(const spec_nested_schema *s) {
 // The generated Write() of internal/lang/generator/message.go:319-439 as constants: fields in
 // write order, the Writer's table order, IsBigMessage forced by a tag > 255.
 void emit_enc_spec(std::ostringstream &o, const char *name, const spec_schema *s) {
-    uint8_t order[SPEC_MAX_FIELDS];
-    uint16_t sorted[SPEC_MAX_FIELDS];
+    uint8_t order[SPEC_KFIELDS];
+    uint16_t sorted[SPEC_KFIELDS];
     writer_order(s, order, sorted);
     bool big = false;
     o << "struct " << name << " {\n  static constexpr int N = " << s->nfields << ";\n"
@@ -415,7 +415,7 @@ const Entry *lookup_key(const std::string &k, Prog p, Make make) {
 }
 
 const Entry *lookup(const spec_schema *s, Prog p) {
-    if (!enabled()) return nullptr;
+    if (!enabled() || s->nfields > SPEC_KFIELDS) return nullptr; // wide schemas: generic kernels
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     // the last few (device, program, schema) answers of this thread: a repeated call (every
@@ -425,7 +425,7 @@ const Entry *lookup(const spec_schema *s, Prog p) {
         bool valid = false;
         int dev = 0, prog = 0;
         uint32_t nfields = 0;
-        spec_field f[SPEC_MAX_FIELDS];
+        spec_field f[SPEC_KFIELDS];
         const Entry *e = nullptr;
     };
     thread_local Hit hits[8];

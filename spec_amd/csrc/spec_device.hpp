@@ -31,6 +31,11 @@ typedef __hip_internal::int64_t int64_t;
 #include <stdint.h>
 #endif
 
+// Fields of one kernel-side field set (decode_core.hpp FieldSet, encode_core.hpp EncFields): a
+// schema with more fields (include/spec_amd.h SPEC_MAX_FIELDS) is decoded in chunks of this many
+// fields and encoded by the wide kernels, whose field set lives in device memory.
+#define SPEC_KFIELDS 64
+
 namespace spec {
 
 // ---- type codes, internal/format/type.go:20-52

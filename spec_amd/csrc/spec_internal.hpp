@@ -68,6 +68,8 @@ int encode_flat_passes(const spec_schema *schema, const void *const *columns, co
                        uint64_t ends_base, void *workspace, size_t workspace_size, uint64_t *total, int passes,
                        hipStream_t stream);
 int launch_encode_write(const spec_schema *schema, const EncodeArgs &a, hipStream_t stream);
+int launch_encode_wide_size(const WideEncodeArgs &a, hipStream_t stream);
+int launch_encode_wide_write(const WideEncodeArgs &a, hipStream_t stream);
 // jit.cpp: schema-specialised encode pass 1 (write=false) or 3; 1 launched, 0 use the
 // precompiled kernel, <0 HIP error.
 int jit_launch_encode(const spec_schema *schema, const EncodeArgs &a, bool write, hipStream_t stream);

@@ -130,6 +130,10 @@ class NestedSchema:
 
         self.outer = Schema(outer) if not isinstance(outer, Schema) else outer
         self.item = Schema(item) if not isinstance(item, Schema) else item
+        from ._lib import SPEC_NESTED_MAX_FIELDS
+
+        if max(len(self.outer), len(self.item)) > SPEC_NESTED_MAX_FIELDS:
+            raise ValueError(f"a nested schema's outer and item hold at most {SPEC_NESTED_MAX_FIELDS} fields each")
         lists = [i for i, f in enumerate(self.outer.fields) if f.kind == Kind.LIST]
         if len(lists) != 1 or any(f.kind == Kind.LIST for f in self.item.fields):
             raise ValueError("outer needs exactly one Kind.LIST field; items must be flat")

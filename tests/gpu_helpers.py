@@ -87,8 +87,11 @@ def check_errors(dev, schema, stream: np.ndarray, ends: np.ndarray, label=""):
     for f in range(len(schema)):
         assert np.array_equal(got.cols[f].cpu().numpy(), want_cols[f]), f"{label}: field {f}"
     gm = mask.cpu().numpy().view(np.uint64)
+    assert gm.shape == want_mask.shape, (gm.shape, want_mask.shape)
     if not np.array_equal(gm, want_mask):
-        i = int(np.nonzero(gm != want_mask)[0][0])
-        raise AssertionError(f"{label}: errmask[{i}] gpu={gm[i]:x} oracle={want_mask[i]:x} "
+        bad = np.argwhere(gm != want_mask)[0]
+        i = int(bad[-1])
+        raise AssertionError(f"{label}: errmask{tuple(int(b) for b in bad)} gpu={int(gm[tuple(bad)]):x} "
+                             f"oracle={int(want_mask[tuple(bad)]):x} "
                              f"record={_rec(stream, ends, i).tobytes().hex()}")
     return gm

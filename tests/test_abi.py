@@ -82,8 +82,12 @@ def test_encode_tree_requires_begin_columns_without_gpu():
 def test_schema_limits():
     import pytest
 
+    wide = spec_amd.Schema([(i + 1, spec_amd.Kind.INT64) for i in range(1024)])  # chunked / wide kernels
+    assert len(wide) == 1024
     with pytest.raises(ValueError):
-        spec_amd.Schema([(i + 1, spec_amd.Kind.INT64) for i in range(65)])
+        spec_amd.Schema([(i + 1, spec_amd.Kind.INT64) for i in range(1025)])
+    with pytest.raises(ValueError):  # the nested kernels take both halves as kernel arguments
+        spec_amd.NestedSchema([(1, spec_amd.Kind.LIST)], [(i + 1, spec_amd.Kind.INT32) for i in range(65)])
 
 
 def test_jit_source_compiles_for_gfx950():
