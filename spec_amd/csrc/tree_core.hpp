@@ -633,15 +633,148 @@ struct BEmit {
         put_n(__builtin_bswap64(v) >> (8 * (8 - nb)), (uint32_t)nb);
     }
     __device__ __forceinline__ void le(uint64_t v, int nb) { put_n(v, (uint32_t)nb); }
-    // heap bytes [off, off + len): 16 at a time from four dword loads issued together, appended
-    // 8 at a time (range-checked: bytes past the heap read as 0 and are never used)
+    // heap bytes [off, off + len): 16 at a time from one 16-byte load (4-byte aligned; a load
+    // straddling the heap's end reads per dword, bytes past it as 0 and never used), appended 8
+    // at a time
     __device__ __forceinline__ void heap(const uint8_t *h, uint64_t hlen, uint32_t off, uint32_t len) {
         const __amdgpu_buffer_rsrc_t r = uniform_rsrc(h, hlen);
         uint32_t i = 0;
         while (i < len) {
             const uint32_t a = (off + i) & ~3u;
-            const uint64_t lo = (uint64_t)buf_ld32(r, a, hlen) | ((uint64_t)buf_ld32(r, a + 4, hlen) << 32);
-            const uint64_t hi = (uint64_t)buf_ld32(r, a + 8, hlen) | ((uint64_t)buf_ld32(r, a + 12, hlen) << 32);
+            uint64_t lo, hi;
+            if ((uint64_t)a + 16 <= hlen) {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, a, 0, 0);
+                lo = (uint64_t)q[0] | ((uint64_t)q[1] << 32);
+                hi = (uint64_t)q[2] | ((uint64_t)q[3] << 32);
+            } else {
+                lo = (uint64_t)buf_ld32(r, a, hlen) | ((uint64_t)buf_ld32(r, a + 4, hlen) << 32);
+                hi = (uint64_t)buf_ld32(r, a + 8, hlen) | ((uint64_t)buf_ld32(r, a + 12, hlen) << 32);
+            }
+            const uint32_t q = off + i - a; // 0..3: bytes [q, 16) of (lo, hi) are heap bytes
+            const uint32_t n1 = min(8u, len - i);
+            put_n((lo >> (8 * q)) | (q ? hi << (64 - 8 * q) : 0ull), n1);
+            i += n1;
+            if (i < len) {
+                const uint32_t n2 = min(8u - q, len - i); // the rest of the 16 loaded bytes
+                put_n(hi >> (8 * q), n2);
+                i += n2;
+            }
+        }
+    }
+};
+
+// BEmit16: the same contract with 16-byte chunks (the generated writer of the records' table,
+// whose rows are long: jit.cpp gen_write_table).  A row's bytes at out[pos..] are merged into the
+// 16-byte chunk (16-byte aligned in memory) they
+// fall in, and a chunk the row covers whole is stored with ONE 16-byte store: the 64 lanes of a
+// store instruction write 64 different rows, i.e. 64 different cache lines, and the memory pipe
+// takes such an instruction a line at a time, so wide stores move 4x the bytes per line slot of
+// dword stores.  The row's first and last chunks, which it shares with the neighbouring rows
+// (other lanes), are stored as whole dwords where they lie inside the row and bytewise at its
+// edges, from `lo` (the row start) and up to the end (finish()).  skip(n) jumps over a child's
+// bytes (a sub-message, list elements) written by a LATER launch: a chunk stored across such a
+// gap may hold zeros for the child's bytes, which the child's own launch then overwrites.
+struct BEmit16 {
+    uint8_t *out;
+    uint64_t pos;
+    uint64_t lo;             // first byte of the row (bytes below belong to another row)
+    uint64_t c0 = 0, c1 = 0; // the chunk holding pos: bytes below pos (emitted, or gap zeros)
+
+    // the position of pos within its 16-byte memory chunk
+    __device__ __forceinline__ uint32_t phase(uint64_t p) const { return (uint32_t)(((unsigned long long)out + p) & 15); }
+    // bytes [max(base, lo), end) of the chunk at base (16-byte aligned in memory), end <= base + 16
+    __device__ __forceinline__ void store_chunk(uint64_t base, uint64_t end) {
+        if (base >= lo && end == base + 16) {
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            v4u v = {(uint32_t)c0, (uint32_t)(c0 >> 32), (uint32_t)c1, (uint32_t)(c1 >> 32)};
+            *(v4u *)(out + base) = v;
+            return;
+        }
+        for (uint64_t q = base > lo ? base : lo; q < end;) {
+            const uint32_t k = (uint32_t)(q - base);
+            const uint64_t word = k < 8 ? c0 : c1;
+            const uint32_t sh = 8 * (k & 7);
+            if ((k & 3) == 0 && q + 4 <= end) {
+                *(uint32_t *)(out + q) = (uint32_t)(word >> sh);
+                q += 4;
+            } else {
+                out[q] = (uint8_t)(word >> sh);
+                q++;
+            }
+        }
+    }
+    // nb (<= 8) bytes of v, lowest first (bytes of v above nb are ignored)
+    __device__ __forceinline__ void put_n(uint64_t v, uint32_t nb) {
+        v &= nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1);
+        const uint32_t p = phase(pos), sh = 8 * (p & 7);
+        const uint64_t l64 = v << sh, h64 = sh ? v >> (64 - sh) : 0ull;
+        uint64_t carry = 0;
+        if (p < 8) {
+            c0 |= l64;
+            c1 |= h64;
+        } else {
+            c1 |= l64;
+            carry = h64; // the next chunk's first bytes
+        }
+        pos += nb;
+        if (p + nb >= 16) { // the chunk is complete (p >= 8 here: nb <= 8)
+            store_chunk(pos - (p + nb - 16) - 16, pos - (p + nb - 16));
+            c0 = carry;
+            c1 = 0;
+        }
+    }
+    __device__ __forceinline__ void put1(uint32_t b) { put_n(b, 1); }
+    __device__ __forceinline__ void skip(uint64_t n) {
+        if (!n) return;
+        const uint32_t p = phase(pos);
+        const uint64_t base = pos - p;
+        pos += n;
+        if (pos >= base + 16) { // leaves the chunk: store it (the rest of it is the child's gap)
+            if (p) store_chunk(base, base + 16);
+            c0 = c1 = 0;
+        }
+    }
+    __device__ __forceinline__ void finish() {
+        const uint32_t p = phase(pos);
+        if (p) store_chunk(pos - p, pos);
+        c0 = c1 = 0;
+    }
+    // reverse varint (oracle/compactint.c so_put_reverse_*): top group first, MSB clear, the
+    // following groups with 0x80; up to 8 bytes (values < 2^56) built in a register at once
+    __device__ __forceinline__ void rvarint(uint64_t v) {
+        const uint32_t L = vlen64(v);
+        if (L <= 8) {
+            uint64_t x = v & 0x00ffffffffffffffull; // 7-bit groups -> bytes
+            x = (x & 0x000000000fffffffull) | ((x << 4) & 0x0fffffff00000000ull);
+            x = (x & 0x00003fff00003fffull) | ((x << 2) & 0x3fff00003fff0000ull);
+            x = (x & 0x007f007f007f007full) | ((x << 1) & 0x7f007f007f007f00ull);
+            const uint32_t drop = 8 * (8 - L);
+            put_n((__builtin_bswap64(x) >> drop) | ((0x8080808080808080ull >> drop) & ~0xffull), L);
+            return;
+        }
+        for (uint32_t i = 0; i < L; i++) put1(((uint32_t)(v >> (7 * (L - 1 - i))) & 0x7f) | (i ? 0x80 : 0));
+    }
+    __device__ __forceinline__ void be(uint64_t v, int nb) { // the low nb bytes of v, big-endian
+        put_n(__builtin_bswap64(v) >> (8 * (8 - nb)), (uint32_t)nb);
+    }
+    __device__ __forceinline__ void le(uint64_t v, int nb) { put_n(v, (uint32_t)nb); }
+    // heap bytes [off, off + len): 16 at a time from one 16-byte load (4-byte aligned; a load
+    // straddling the heap's end reads per dword, bytes past it as 0 and never used), appended 8
+    // at a time
+    __device__ __forceinline__ void heap(const uint8_t *h, uint64_t hlen, uint32_t off, uint32_t len) {
+        const __amdgpu_buffer_rsrc_t r = uniform_rsrc(h, hlen);
+        uint32_t i = 0;
+        while (i < len) {
+            const uint32_t a = (off + i) & ~3u;
+            uint64_t lo, hi;
+            if ((uint64_t)a + 16 <= hlen) {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, a, 0, 0);
+                lo = (uint64_t)q[0] | ((uint64_t)q[1] << 32);
+                hi = (uint64_t)q[2] | ((uint64_t)q[3] << 32);
+            } else {
+                lo = (uint64_t)buf_ld32(r, a, hlen) | ((uint64_t)buf_ld32(r, a + 4, hlen) << 32);
+                hi = (uint64_t)buf_ld32(r, a + 8, hlen) | ((uint64_t)buf_ld32(r, a + 12, hlen) << 32);
+            }
             const uint32_t q = off + i - a; // 0..3: bytes [q, 16) of (lo, hi) are heap bytes
             const uint32_t n1 = min(8u, len - i);
             put_n((lo >> (8 * q)) | (q ? hi << (64 - 8 * q) : 0ull), n1);
@@ -679,8 +812,8 @@ __device__ __forceinline__ void load_value_k(const void *col, uint64_t row, uint
 }
 
 // The element through its encoder (internal/encode/...), as emit_value; string/bytes from heap h
-template <uint32_t K>
-__device__ __forceinline__ void emit_value_k(BEmit &em, const uint64_t (&v)[4], const uint8_t *h, uint64_t hlen) {
+template <uint32_t K, class E>
+__device__ __forceinline__ void emit_value_k(E &em, const uint64_t (&v)[4], const uint8_t *h, uint64_t hlen) {
     if constexpr (K == K_BOOL) em.put1(v[0] ? T_TRUE : T_FALSE);
     else if constexpr (K == K_BYTE) em.put_n(v[0] | ((uint64_t)T_BYTE << 8), 2);
     else if constexpr (K == K_INT16) { em.rvarint(zigzag32((int16_t)v[0])); em.put1(T_INT16); }
@@ -711,7 +844,8 @@ __device__ __forceinline__ void emit_value_k(BEmit &em, const uint64_t (&v)[4], 
 }
 
 // One column element through its encoder (internal/encode/...)
-__device__ __forceinline__ void emit_value(BEmit &em, const TreeBufs &B, const TreeDesc &D, int c, uint32_t kind,
+template <class E>
+__device__ __forceinline__ void emit_value(E &em, const TreeBufs &B, const TreeDesc &D, int c, uint32_t kind,
                                            uint64_t row) {
     const uint8_t *p = cell(B, D, c, row);
     switch (kind) {
@@ -752,7 +886,8 @@ __device__ __forceinline__ void emit_value(BEmit &em, const TreeBufs &B, const T
     }
 }
 
-__device__ __forceinline__ void emit_struct(BEmit &em, const TreeBufs &B, const TreeDesc &D, uint32_t sf, uint64_t row) {
+template <class E>
+__device__ __forceinline__ void emit_struct(E &em, const TreeBufs &B, const TreeDesc &D, uint32_t sf, uint64_t row) {
     const TField &F = D.f[sf];
     if (!F.nested) {
         const uint64_t start = em.pos;
