@@ -462,9 +462,10 @@ __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
     const uint64_t ngroups = (a.n + 63) / 64;
     uint64_t g;
     if constexpr (ONEPASS) {
-        uint32_t t = 0;
-        if (lane == 0) t = atomicAdd((unsigned int *)&a.group_base[ngroups], 1u);
-        g = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
+        // group = block order: workgroups are dispatched in increasing id, so every group a
+        // group waits on (a smaller id) is running or done — the lowest running group never waits
+        // (round 4 took a ticket from one global counter: 16 K agent-scope atomics on one address)
+        g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
     } else {
         // blocks are dealt round-robin to the 8 XCDs: with xcd = 1, block b takes the b/8-th slot
         // of XCD b%8's contiguous share, so neighbouring groups (sharing the item columns' cache
