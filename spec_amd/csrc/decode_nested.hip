@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void nested_decode_kernel(NestedArgs a) {
     nested_decode_body<RuntimeSpec, RuntimeSpec, false>(a);
 }
 
-__global__ __launch_bounds__(64) void nested_onepass_kernel(NestedArgs a) {
+__global__ __launch_bounds__(64 * DEC_WAVES) void nested_onepass_kernel(NestedArgs a) {
     nested_decode_body<RuntimeSpec, RuntimeSpec, true>(a);
 }
 
@@ -158,10 +158,9 @@ int launch_nested_decode(const spec_nested_schema *schema, NestedArgs a, double 
 bool nested_lookback() { return SPEC_AB_LOOKBACK != 0; }
 
 // spec_decode_nested_onepass: by default the index kernels + the decode kernel back to back
-// (no host round trip; measured faster on MI355X than the look-back kernel, whose global
-// ticket and look-back words cross the XCDs through memory); with SPEC_AB_LOOKBACK: one wave
-// per block, one group per wave in ticket order, look-back words and ticket
-// (group_base[0 .. ngroups]) zeroed first, on the same stream.
+// (no host round trip); with SPEC_AB_LOOKBACK: DEC_WAVES groups per block (one per wave), one
+// look-back per block over the earlier blocks, the look-back words (group_base[0 .. blocks])
+// zeroed first, on the same stream.
 int launch_nested_onepass(const spec_nested_schema *schema, NestedArgs a, double avg_record, hipStream_t stream) {
     if (a.n == 0) {
         (void)hipMemsetAsync(a.total, 0, sizeof(uint64_t), stream);
@@ -173,10 +172,13 @@ int launch_nested_onepass(const spec_nested_schema *schema, NestedArgs a, double
     }
     a.slab = nested_slab_bytes(avg_record);
     const uint64_t groups = (a.n + 63) / 64;
-    if (hipMemsetAsync(a.group_base, 0, (groups + 1) * sizeof(uint64_t), stream) != hipSuccess) return -1;
+    const uint64_t blocks = (groups + DEC_WAVES - 1) / DEC_WAVES;
+    if (hipMemsetAsync(a.group_base, 0, (blocks + 1) * sizeof(uint64_t), stream) != hipSuccess) return -1;
     const int j = jit_launch_nested(schema, a, NESTED_ONEPASS, stream);
     if (j < 0) return -1;
-    if (j == 0) hipLaunchKernelGGL(nested_onepass_kernel, dim3((unsigned)groups), dim3(64), (size_t)a.slab, stream, a);
+    if (j == 0)
+        hipLaunchKernelGGL(nested_onepass_kernel, dim3((unsigned)blocks), dim3(64 * DEC_WAVES),
+                           (size_t)DEC_WAVES * a.slab, stream, a);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

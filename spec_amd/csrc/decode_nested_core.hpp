@@ -354,10 +354,10 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
     return v;
 }
 
-// Publish group g's item count `agg`, return the items of groups [0, g).  Every group < g
-// holds a ticket taken before g's, so its wave is resident and will publish: the wait ends.
-// The window looks back 256 groups per round (4 per lane, nearest first): all resident groups
-// start together, so the inclusive prefixes move forward a window per round.
+// Publish unit g's item count `agg`, return the items of units [0, g).  Units are blocks of
+// DEC_WAVES groups in block order (workgroups are dispatched in increasing id, so every unit < g
+// is resident or done and will publish: the wait ends).  The window looks back 256 units per
+// round (4 per lane, nearest first); 1,024 per round (16 per lane) measured no faster.
 __device__ __forceinline__ uint64_t lookback(uint64_t *state, uint64_t g, uint64_t agg, int lane) {
     constexpr int K = 4;
     if (lane == 0) lb_store(&state[g], (g == 0 ? LB_PRE : LB_AGG) | agg);
@@ -400,20 +400,43 @@ __device__ __forceinline__ uint64_t lookback(uint64_t *state, uint64_t g, uint64
     return excl;
 }
 
+// ONEPASS: the block's groups (one per wave) sum their item totals in LDS (xch); wave 0 publishes
+// the block's total and looks back over the earlier blocks; each wave's first item = the block's
+// base + the totals of the block's earlier waves.  Every wave of the block calls this once (a
+// wave past the batch's end with total 0).
+__device__ __forceinline__ uint64_t onepass_base(const NestedArgs &a, uint32_t total, int lane, uint64_t *xch) {
+    const int wave = threadIdx.x >> 6;
+    if (lane == 0) xch[wave] = total;
+    __syncthreads();
+    uint64_t before = 0, bt = 0;
+#pragma unroll
+    for (int w = 0; w < DEC_WAVES; w++) {
+        const uint64_t t = xch[w];
+        before += w < wave ? t : 0;
+        bt += t;
+    }
+    if (wave == 0) {
+        const uint64_t b = uniform64(lookback(a.group_base, blockIdx.x, bt, lane));
+        if (lane == 0) xch[DEC_WAVES] = b;
+    }
+    __syncthreads();
+    return uniform64(xch[DEC_WAVES] + before);
+}
+
 // Decode a group: outer records (lane = record), then items (item-parallel).  item_base =
 // the group's first item; ONEPASS: item_base is found here by look-back (state = a.group_base).
 template <class OSpec, class ISpec, bool ONEPASS, int U = NESTED_ITEM_U, class Src>
 __device__ __forceinline__ uint32_t nested_group_body(const Src &s, long long rs, long long re, bool valid,
                                                       uint64_t r, uint64_t g, uint64_t item_base, int lane,
                                                       long long to_stream, const NestedArgs &a,
-                                                      uint32_t *rng = nullptr) {
+                                                      uint32_t *rng = nullptr, uint64_t *xch = nullptr) {
     ListInfo li = {0, 0, 0, 0, false};
     if (valid) li = decode_outer<OSpec>(s, rs, re, r, to_stream, a);
     const uint32_t incl = wave_incl_scan(li.count, lane);
     const uint32_t excl = incl - li.count;
     const uint32_t total = __shfl(incl, 63);
     if constexpr (ONEPASS) {
-        item_base = uniform64(lookback(a.group_base, g, total, lane));
+        item_base = onepass_base(a, total, lane, xch);
         if (g == (a.n - 1) / 64 && lane == 0) *a.total = item_base + total;
     }
     if (valid) {
@@ -452,14 +475,13 @@ __device__ __forceinline__ uint32_t nested_decode_part(const NestedArgs &a, __am
                                                   item_base, lane, 0, a);
 }
 
-// Kernel body for one group per wave.  ONEPASS: group = ticket order (a.group_base = state
-// words, ticket at state[ngroups], both zeroed by the launcher); else group = wave index and
-// a.group_base holds the exclusive item offsets from the index kernels.
+// Kernel body for one group per wave.  ONEPASS: group = wave index, a.group_base = one state word
+// per block (zeroed by the launcher); else group = wave index and a.group_base holds the
+// exclusive item offsets from the index kernels.
 template <class OSpec, class ISpec, bool ONEPASS, bool RANGES = false, int U = NESTED_ITEM_U>
 __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t ngroups = (a.n + 63) / 64;
     uint64_t g;
     if constexpr (ONEPASS) {
         // group = block order: workgroups are dispatched in increasing id, so every group a
@@ -478,7 +500,11 @@ __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
         g = blk * (blockDim.x >> 6) + wave;
     }
     const uint64_t base = g * 64;
-    if (base >= a.n) return;
+    __shared__ uint64_t xch[DEC_WAVES + 1]; // ONEPASS: the block's wave totals, then its base
+    if (base >= a.n) {
+        if constexpr (ONEPASS) onepass_base(a, 0u, lane, xch); // the block's barriers
+        return;
+    }
     // per wave: the slab, then (RANGES) the item range window
     uint8_t *slab = smem + wave * (a.slab + (RANGES ? NESTED_RANGE_BYTES : 0u));
     __amdgpu_buffer_rsrc_t rsrc =
@@ -513,11 +539,11 @@ __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
         nested_group_body<OSpec, ISpec, ONEPASS>(s, SLAB_GUARD + (long long)(gr.rec_lo - gr.aligned_lo),
                                                  SLAB_GUARD + (long long)(gr.rec_hi - gr.aligned_lo), valid, r, g,
                                                  item_base, lane, (long long)gr.aligned_lo - SLAB_GUARD, a,
-                                                 RANGES ? (uint32_t *)(slab + a.slab) : nullptr);
+                                                 RANGES ? (uint32_t *)(slab + a.slab) : nullptr, xch);
     } else {
         GlobalSrc s{a.stream, a.stream_len};
         nested_group_body<OSpec, ISpec, ONEPASS>(s, (long long)gr.rec_lo, (long long)gr.rec_hi, valid, r, g,
-                                                 item_base, lane, 0, a);
+                                                 item_base, lane, 0, a, nullptr, xch);
     }
 }
 

@@ -172,7 +172,7 @@ std::string generate_nested(const spec_nested_schema *s) {
     if (fi) emit_spec(o, "GenItem", &s->item);
     const std::string specs = std::string(fo ? "GenOuter" : "spec::RuntimeSpec") + ", " +
                               (fi ? "GenItem" : "spec::RuntimeSpec");
-    o << "extern \"C\" __global__ __launch_bounds__(64) void spec_decode_nested_jit(spec::NestedArgs a) {\n"
+    o << "extern \"C\" __global__ __launch_bounds__(256) void spec_decode_nested_jit(spec::NestedArgs a) {\n"
       << "  spec::nested_decode_body<" << specs << ", true>(a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(64) void spec_decode_nested2_jit(spec::NestedArgs a) {\n"
       << "  spec::nested_decode_body<" << specs << ", false>(a);\n}\n"
@@ -1110,8 +1110,14 @@ int jit_launch_nested(const spec_nested_schema *schema, const NestedArgs &a, int
     unsigned grid = (unsigned)((a.n + 63) / 64);
     if (args.xcd && mode != NESTED_ONEPASS) grid = (grid + 7) / 8 * 8; // 8 equal XCD shares
     else args.xcd = 0;
-    const size_t lds = a.slab + (mode == NESTED_RANGES ? NESTED_RANGE_BYTES : 0u);
-    hipError_t rc = hipModuleLaunchKernel(e->fn[mode], grid, 1, 1, 64, 1, 1, (unsigned)lds, stream, nullptr, extra);
+    size_t lds = a.slab + (mode == NESTED_RANGES ? NESTED_RANGE_BYTES : 0u);
+    unsigned threads = 64;
+    if (mode == NESTED_ONEPASS) { // DEC_WAVES groups per block: one look-back per block
+        grid = (grid + DEC_WAVES - 1) / DEC_WAVES;
+        threads = 64 * DEC_WAVES;
+        lds *= DEC_WAVES;
+    }
+    hipError_t rc = hipModuleLaunchKernel(e->fn[mode], grid, 1, 1, threads, 1, 1, (unsigned)lds, stream, nullptr, extra);
     return rc == hipSuccess ? 1 : -1;
 }
 
