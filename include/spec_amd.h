@@ -511,6 +511,24 @@ int spec_shard_host_decode(spec_shard *c, const uint8_t *stream_host, uint64_t s
 int spec_parse_messages(const uint8_t *stream_bytes, uint64_t stream_len, const uint64_t *ends, uint64_t n,
                         uint32_t head, uint8_t *status, uint32_t *sizes, void *stream);
 
+/* spec_parse_batch: the same recursive validation from another root, per record:
+ *   SPEC_PARSE_MESSAGE  spec.ParseMessage (= spec_parse_messages);
+ *   SPEC_PARSE_LIST     spec.ParseList (list.go:26-29 -> internal/types/list.go:35-53): the list
+ *                       table (its error class, 1-5), then ParseValue on every non-empty element;
+ *                       an empty record is an empty list;
+ *   SPEC_PARSE_VALUE    spec.ParseValue (value.go:30-33 -> internal/types/value.go:49-113): the
+ *                       value's type (its last byte), its decoder's checks, lists and messages
+ *                       recursively; any error SPEC_STATUS_INVALID_VALUE (an empty record:
+ *                       "unsupported type 0").
+ * A value whose size exceeds its slice (DecodeStruct does not bound its data size) makes
+ * value.go:110's b[len(b)-n:] panic: SPEC_STATUS_PANIC, at any depth.  sizes[i] = the parsed
+ * size (ParseValue's n; the bytes of the list / message). */
+#define SPEC_PARSE_MESSAGE 0u
+#define SPEC_PARSE_LIST 1u
+#define SPEC_PARSE_VALUE 2u
+int spec_parse_batch(uint32_t root, const uint8_t *stream_bytes, uint64_t stream_len, const uint64_t *ends, uint64_t n,
+                     uint32_t head, uint8_t *status, uint32_t *sizes, void *stream);
+
 /* spec_decode_flat_prepare: compile (once per device, schema and record-size class) the
  * schema-specialised decode kernel that spec_decode_flat uses when one exists — the
  * analogue of the reference's generated readers (internal/lang/generator/message.go:97-186).

@@ -311,6 +311,43 @@ int so_parse_batch(const uint8_t *stream, const uint64_t *ends, uint64_t n, uint
     return 0;
 }
 
+/* spec_parse_batch semantics: root 0 = ParseMessage (so_parse_batch), 1 = ParseList
+ * (internal/types/list.go:35-53: DecodeListTable's error class, then ParseValue on every non-empty
+ * element), 2 = ParseValue (internal/types/value.go:49-113: any error => 7, INVALID_VALUE; an
+ * empty value is "unsupported type 0").  Nested errors => 7, Go panics => ST_PANIC; sizes[r] =
+ * the parsed size (ParseValue's n). */
+int so_parse_batch_root(int root, const uint8_t *stream, const uint64_t *ends, uint64_t n, uint32_t head,
+                        uint8_t *status, uint32_t *sizes) {
+    if (root == 0) return so_parse_batch(stream, ends, n, head, status, sizes);
+    for (uint64_t r = 0; r < n; r++) {
+        uint64_t s = (r ? ends[r - 1] : 0) + head;
+        uint64_t e = ends[r] < s ? s : ends[r];
+        const uint8_t *b = stream + s;
+        const size_t len = (size_t)(e - s);
+        sizes[r] = 0;
+        so_err err = NULL;
+        int size = 0;
+        if (root == 1) {
+            so_list l;
+            err = so_open_list_err(b, len, &l);
+            if (err) {
+                status[r] = classify(err);
+                continue;
+            }
+            err = so_parse_list(b, len, &size);
+        } else {
+            err = so_parse_value(b, len, &size);
+        }
+        if (err) {
+            status[r] = strstr(err, "index out of range") ? ST_PANIC : 7;
+            continue;
+        }
+        status[r] = 0;
+        sizes[r] = (uint32_t)size;
+    }
+    return 0;
+}
+
 /* mpx frame read loop (mpx/conn_reader.go:179-194, connReader.read): io.ReadFull of the 4-byte
  * head, size = binary.BigEndian.Uint32(head), then io.ReadFull of size bytes — repeated over a
  * received buffer.  A read that would run past len stops the loop (ReadFull would block for

@@ -218,6 +218,8 @@ def _declare(L):
     L.so_decode_nested_counts.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
     L.so_decode_nested_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64] + [C.c_void_p] * 9
     L.so_parse_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]
+    L.so_parse_batch_root.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p,
+                                      C.c_void_p]
     L.so_decode_flat_errors.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                         C.c_void_p]
     L.so_tree_layout.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.POINTER(C.c_int), C.c_void_p, C.POINTER(C.c_int)]
@@ -636,14 +638,19 @@ def decode_nested_batch(stream: np.ndarray, ends: np.ndarray):
     return out
 
 
-def parse_batch(stream: np.ndarray, ends: np.ndarray, head: int = 0):
-    """ParseMessage per record -> (status uint8[n], sizes uint32[n]) (spec_parse_messages semantics)."""
+PARSE_MESSAGE, PARSE_LIST, PARSE_VALUE = 0, 1, 2
+
+
+def parse_batch(stream: np.ndarray, ends: np.ndarray, head: int = 0, root: int = PARSE_MESSAGE):
+    """ParseMessage (root 0), ParseList (1) or ParseValue (2) per record -> (status uint8[n], sizes
+    uint32[n]) (spec_parse_batch semantics)."""
     n = len(ends)
     stream = np.ascontiguousarray(stream, dtype=np.uint8)
     ends = np.ascontiguousarray(ends, dtype=np.uint64)
     st = np.zeros(n, np.uint8)
     sz = np.zeros(n, np.uint32)
-    lib().so_parse_batch(_ptr(stream), _ptr(ends), n, head, _ptr(st), _ptr(sz))
+    lib().so_parse_batch_root(root, _ptr(stream) if stream.size else None, _ptr(ends) if n else None, n, head,
+                              _ptr(st), _ptr(sz))
     return st, sz
 
 

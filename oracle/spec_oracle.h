@@ -215,6 +215,7 @@ int so_list_len(const so_list *l);
 int so_list_get_bytes(const so_list *l, int i, const uint8_t **p, size_t *len);
 
 so_err so_parse_value(const uint8_t *b, size_t len, int *n);
+so_err so_parse_list(const uint8_t *b, size_t len, int *size);
 
 /* ---- Writer (internal/writer/...) ---- */
 typedef struct so_writer so_writer;
@@ -343,6 +344,8 @@ int so_decode_nested_batch(const uint8_t *stream, const uint64_t *ends, uint64_t
 /* ParseMessage per record (spec_parse_messages semantics): status 0 ok, 1-5 trailer class,
  * 6 panic (list element start > end), 7 nested value error; sizes = message bytes or 0.
  * head = bytes before each record (4 for mpx frames). */
+int so_parse_batch_root(int root, const uint8_t *stream, const uint64_t *ends, uint64_t n, uint32_t head,
+                        uint8_t *status, uint32_t *sizes);
 int so_parse_batch(const uint8_t *stream, const uint64_t *ends, uint64_t n, uint32_t head, uint8_t *status,
                    uint32_t *sizes);
 

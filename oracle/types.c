@@ -212,7 +212,8 @@ int so_list_get_bytes(const so_list *l, int i, const uint8_t **p, size_t *len) {
 
 /* ---- ParseMessage / ParseList / ParseValue (recursive validation) ---- */
 
-static so_err parse_list(const uint8_t *b, size_t len, int *size) {
+/* ParseList, internal/types/list.go:35-53 */
+so_err so_parse_list(const uint8_t *b, size_t len, int *size) {
     so_list l;
     so_err e = so_open_list_err(b, len, &l);
     *size = 0;
@@ -286,7 +287,7 @@ so_err so_parse_value(const uint8_t *b, size_t len, int *n) {
     case SO_TYPE_BYTES: e = so_decode_bytes(b, len, &off, &vlen, n); break;
     case SO_TYPE_STRING: e = so_decode_string(b, len, &off, &vlen, n); break;
     case SO_TYPE_LIST:
-    case SO_TYPE_BIG_LIST: e = parse_list(b, len, n); break;
+    case SO_TYPE_BIG_LIST: e = so_parse_list(b, len, n); break;
     case SO_TYPE_MESSAGE:
     case SO_TYPE_BIG_MESSAGE: e = so_parse_message(b, len, &m, n); break;
     case SO_TYPE_STRUCT: e = so_decode_struct(b, len, &v.i, n); break;
@@ -294,5 +295,8 @@ so_err so_parse_value(const uint8_t *b, size_t len, int *n) {
         *n = 0;
         return "unsupported type";
     }
+    /* value.go:110: return b[len(b)-n:] — a size past the slice (DecodeStruct does not bound its
+     * data size) panics: slice bounds out of range */
+    if (!e && (size_t)*n > len) return "parse value: slice bounds out of range (index out of range)";
     return e;
 }

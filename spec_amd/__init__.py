@@ -6,8 +6,8 @@ decoded into SoA columns / encoded from them by hand-written gfx950 kernels
 (spec_amd/csrc, C ABI in include/spec_amd.h).  See DESIGN.md.
 """
 from ._lib import LIB_PATH, SpecError, header_symbols, lib, set_jit
-from .batch import (Columns, Decoder, Encoder, alloc_columns, decode_flat, decode_flat_errors, encode_flat,
-                    parse_messages)
+from .batch import (PARSE_LIST, PARSE_MESSAGE, PARSE_VALUE, Columns, Decoder, Encoder, alloc_columns, decode_flat,
+                    decode_flat_errors, encode_flat, parse_messages)
 from . import lz4
 from .frames import decode_frames, frames_index, frames_index_device, make_frames, make_frames_device
 from .pipeline import HostDecoder
@@ -18,7 +18,8 @@ from .tree import (ListOf, Message, Struct, Tree, TreeColumns, TreeDecoder, Tree
 
 __all__ = [
     "HostDecoder", "decode_frames", "frames_index", "frames_index_device", "make_frames", "make_frames_device", "LIB_PATH", "SpecError", "header_symbols", "lib", "set_jit", "Columns", "Decoder", "Encoder", "alloc_columns",
-    "decode_flat", "decode_flat_errors", "encode_flat", "parse_messages", "FLAT16", "Field", "Kind", "Schema",
+    "decode_flat", "decode_flat_errors", "encode_flat", "parse_messages", "PARSE_MESSAGE", "PARSE_LIST", "PARSE_VALUE",
+    "FLAT16", "Field", "Kind", "Schema",
     "NESTED", "NestedSchema", "NestedColumns", "NestedDecoder", "NestedEncoder", "decode_nested",
     "encode_nested", "ListOf", "Message", "Struct", "Tree", "TreeColumns", "TreeDecoder", "TreeEncoder", "decode_tree",
     "decode_values", "encode_tree", "pkg1_message", "pkg1_tree", "tree_rows",

@@ -95,6 +95,7 @@ def _declare(L):
     L.spec_frames_index_device_workspace_size.restype = C.c_size_t
     L.spec_frames_index_device.argtypes = [vp, C.c_uint64, vp, C.c_uint64, vp, vp, vp, vp, C.c_size_t, vp]
     L.spec_parse_messages.argtypes = [vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, vp, vp, vp]
+    L.spec_parse_batch.argtypes = [C.c_uint32, vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, vp, vp, vp]
     L.spec_decode_flat_prepare.argtypes = [C.POINTER(SpecSchema), C.c_uint64, C.c_uint64]
     L.spec_set_jit.argtypes = [C.c_int]
     L.spec_set_jit.restype = None

@@ -199,15 +199,20 @@ def encode_flat(schema: Schema, cols, heaps: dict, n: int | None = None, cuda_st
     return out[:total], ends
 
 
-def parse_messages(stream: torch.Tensor, ends: torch.Tensor, head: int = 0, sizes: bool = True, cuda_stream=None):
-    """spec_parse_messages: spec.ParseMessage (recursive validation) of every record.
+PARSE_MESSAGE, PARSE_LIST, PARSE_VALUE = 0, 1, 2  # include/spec_amd.h SPEC_PARSE_*
+
+
+def parse_messages(stream: torch.Tensor, ends: torch.Tensor, head: int = 0, sizes: bool = True, cuda_stream=None,
+                   root: int = PARSE_MESSAGE):
+    """spec_parse_batch: spec.ParseMessage (root PARSE_MESSAGE), ParseList (PARSE_LIST) or
+    ParseValue (PARSE_VALUE) — recursive validation — of every record.
     Returns (status uint8 [n], sizes int32 view of uint32 [n] or None)."""
     _check_dev(stream, "stream", torch.uint8)
     _check_dev(ends, "ends", torch.int64)
     n = ends.numel()
     st = torch.empty(n, dtype=torch.uint8, device=stream.device)
     sz = torch.empty(n, dtype=torch.int32, device=stream.device) if sizes else None
-    rc = _lib.lib().spec_parse_messages(_ptr(stream), stream.numel(), _ptr(ends), n, head, _ptr(st), _ptr(sz),
-                                        _stream_handle(cuda_stream))
-    _lib.check(rc, "spec_parse_messages")
+    rc = _lib.lib().spec_parse_batch(root, _ptr(stream), stream.numel(), _ptr(ends), n, head, _ptr(st), _ptr(sz),
+                                     _stream_handle(cuda_stream))
+    _lib.check(rc, "spec_parse_batch")
     return st, sz

@@ -417,6 +417,12 @@ int spec_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends, u
 
 int spec_parse_messages(const uint8_t *stream_bytes, uint64_t stream_len, const uint64_t *ends, uint64_t n,
                         uint32_t head, uint8_t *status, uint32_t *sizes, void *stream) {
+    return spec_parse_batch(SPEC_PARSE_MESSAGE, stream_bytes, stream_len, ends, n, head, status, sizes, stream);
+}
+
+int spec_parse_batch(uint32_t root, const uint8_t *stream_bytes, uint64_t stream_len, const uint64_t *ends,
+                     uint64_t n, uint32_t head, uint8_t *status, uint32_t *sizes, void *stream) {
+    if (root > SPEC_PARSE_VALUE) return SPEC_E_INVALID_ARGUMENT;
     if (n == 0) return SPEC_OK;
     if (!ends || !status || (!stream_bytes && stream_len)) return SPEC_E_INVALID_ARGUMENT;
     if (stream_len >= (1ull << 32)) return SPEC_E_TOO_LARGE;
@@ -428,7 +434,7 @@ int spec_parse_messages(const uint8_t *stream_bytes, uint64_t stream_len, const 
     a.n = n;
     a.head = head;
     a.f.status = status;
-    if (spec::launch_parse(a, sizes, (double)stream_len / (double)n, (hipStream_t)stream))
+    if (spec::launch_parse(a, sizes, root, (double)stream_len / (double)n, (hipStream_t)stream))
         return hip_rc(hipGetLastError());
     return SPEC_OK;
 }

@@ -1,4 +1,5 @@
-// validate.hip — bulk ParseMessage: recursive validation of every record.
+// validate.hip — bulk ParseMessage / ParseList / ParseValue: recursive validation of every record
+// (SURVEY.md §8(f) #2).
 //
 // What mpx runs on every received frame (mpx/conn_reader.go:119: pmpx.ParseMessage):
 //   ParseMessage(b)  internal/types/msg.go:58-82  — DecodeMessageTable, then ParseValue on
@@ -28,51 +29,66 @@ struct Frame {
     uint8_t list, big;
 };
 
-// The decoder error checks ParseValue runs for a scalar of type `type` ending at e.
+// The decoder error checks ParseValue runs for a scalar of type `type` ending at e, and the size
+// it reports (value.go:49-113: n = bytes the decoder consumed from the end): 0 ok, 1 an error,
+// 2 a Go panic (value.go:110 returns b[len(b)-n:]: DecodeStruct does not bound its data size, so
+// a struct larger than its slice panics).
 template <class Src>
-__device__ __forceinline__ bool scalar_ok(const Src &s, uint32_t type, long long lo, long long e) {
+__device__ __forceinline__ int scalar_check(const Src &s, uint32_t type, long long lo, long long e, uint32_t &n) {
     const long long flen = e - lo;
     const Tail t = load_tail(s, (typename Src::pos_t)e);
     const uint64_t R = tail_r(t);
     const uint32_t R2 = tail_r2(t);
     const long long avail = flen - 1;
     int m;
+    n = 0;
     switch (type) {
     case T_TRUE:
-    case T_FALSE: return true;
-    case T_BYTE: return flen >= 2;                                   // byte.go:16-34
+    case T_FALSE: n = 1; return 0;
+    case T_BYTE: n = 2; return flen >= 2 ? 0 : 1;                     // byte.go:16-34
     case T_INT16: {                                                  // int.go:16-62
         const int32_t x = unzigzag32((uint32_t)rvarint_bf(R, R2, avail, 5, m));
-        return m >= 0 && x >= -32768 && x <= 32767;
+        n = 1 + (uint32_t)m;
+        return m >= 0 && x >= -32768 && x <= 32767 ? 0 : 1;
     }
     case T_INT32:
-    case T_UINT32: rvarint_bf(R, R2, avail, 5, m); return m >= 0;   // int.go:64-103, uint.go:58-95
+    case T_UINT32: rvarint_bf(R, R2, avail, 5, m); n = 1 + (uint32_t)m; return m >= 0 ? 0 : 1; // int.go:64-103
     case T_INT64:
-    case T_UINT64: rvarint_bf(R, R2, avail, 10, m); return m >= 0;  // int.go:105-135, uint.go:97-125
+    case T_UINT64: rvarint_bf(R, R2, avail, 10, m); n = 1 + (uint32_t)m; return m >= 0 ? 0 : 1; // int.go:105-135
     case T_UINT16: {                                                 // uint.go:16-56
         const uint64_t x = rvarint_bf(R, R2, avail, 5, m);
-        return m >= 0 && x <= 0xffff;
+        n = 1 + (uint32_t)m;
+        return m >= 0 && x <= 0xffff ? 0 : 1;
     }
-    case T_BIN64: return flen >= 9;                                  // bin.go:15-112
-    case T_BIN128: return flen >= 17;
-    case T_BIN256: return flen >= 33;
+    case T_BIN64: n = 9; return flen >= 9 ? 0 : 1;                   // bin.go:15-112
+    case T_BIN128: n = 17; return flen >= 17 ? 0 : 1;
+    case T_BIN256: n = 33; return flen >= 33 ? 0 : 1;
     case T_FLOAT32: {                                                // float.go:15-32: +-Inf > MaxFloat32
         const uint32_t b = (uint32_t)(R & 0xffffffffu);
-        return flen >= 5 && (b & 0x7fffffffu) != 0x7f800000u;
+        n = 5;
+        return flen >= 5 && (b & 0x7fffffffu) != 0x7f800000u ? 0 : 1;
     }
-    case T_FLOAT64: return flen >= 9;                                // float.go:34-49
+    case T_FLOAT64: n = 9; return flen >= 9 ? 0 : 1;                 // float.go:34-49
     case T_BYTES: {                                                  // bytes.go:14-58
         const uint32_t ds = (uint32_t)rvarint_bf(R, R2, avail, 5, m);
-        return m >= 0 && (e - 1 - m) - (long long)ds >= lo;
+        n = 1 + (uint32_t)m + ds;
+        return m >= 0 && (e - 1 - m) - (long long)ds >= lo ? 0 : 1;
     }
     case T_STRING: {                                                 // string.go:15-47 (+1: the NUL)
         const uint32_t ds = (uint32_t)rvarint_bf(R, R2, avail, 5, m);
         const long long end = e - 1 - m - 1;
-        return m >= 0 && end >= lo && end - (long long)ds >= lo;
+        n = 2 + (uint32_t)m + ds;
+        return m >= 0 && end >= lo && end - (long long)ds >= lo ? 0 : 1;
     }
-    case T_STRUCT: rvarint_bf(R, R2, avail, 5, m); return m >= 0;   // struct.go:14-42 (no bound check)
+    case T_STRUCT: {                                                 // struct.go:14-42 (no bound check)
+        const uint32_t ds = (uint32_t)rvarint_bf(R, R2, avail, 5, m);
+        if (m < 0) return 1;
+        const long long size = 1 + (long long)m + ds;
+        n = (uint32_t)size;
+        return size > flen ? 2 : 0;
     }
-    return false; // "unsupported type", value.go:103-104
+    }
+    return 1; // "unsupported type", value.go:103-104
 }
 
 template <class Src>
@@ -82,17 +98,33 @@ __device__ __forceinline__ uint32_t be_at(const Src &s, long long p, int bytes) 
     return v;
 }
 
-// ParseMessage of record [rs, re): status and size (message bytes, 0 on error).
+// ParseMessage (root PARSE_MESSAGE), ParseList (PARSE_LIST) or ParseValue (PARSE_VALUE) of record
+// [rs, re): status and size (the parsed size; 0 on error).
 template <class Src>
-__device__ __forceinline__ uint32_t parse_record(const Src &s, long long rs, long long re, uint32_t &size) {
+__device__ __forceinline__ uint32_t parse_record(const Src &s, long long rs, long long re, uint32_t root,
+                                                 uint32_t &size) {
     using pos_t = typename Src::pos_t;
     size = 0;
-    if (re <= rs) return ST_OK; // empty input: zero message, no error
-    const Trailer top = parse_trailer<false>(s, (pos_t)rs, (pos_t)re);
-    if (top.st != ST_OK) return top.st;
+    bool list = root == SPEC_PARSE_LIST;
+    if (root == SPEC_PARSE_VALUE) {
+        if (re <= rs) return ST_INVALID_VALUE; // DecodeType(empty) = TypeUndefined: "unsupported type 0"
+        const uint32_t type = s.u8((pos_t)(re - 1));
+        if (type != T_LIST && type != T_BIG_LIST && type != T_MESSAGE && type != T_BIG_MESSAGE) {
+            uint32_t n;
+            const int r = scalar_check(s, type, rs, re, n);
+            if (r) return r == 2 ? ST_PANIC : ST_INVALID_VALUE;
+            size = n;
+            return ST_OK;
+        }
+        list = type == T_LIST || type == T_BIG_LIST;
+    }
+    if (re <= rs) return ST_OK; // empty input: zero message / list, no error
+    const Trailer top = list ? parse_trailer<true>(s, (pos_t)rs, (pos_t)re) : parse_trailer<false>(s, (pos_t)rs, (pos_t)re);
+    if (top.st != ST_OK) return root == SPEC_PARSE_VALUE ? (uint32_t)ST_INVALID_VALUE : top.st;
     Frame stk[VAL_MAX_DEPTH];
     int sp = 0;
-    stk[sp++] = Frame{top.dstart, top.tstart, top.tsize / (top.big ? 6u : 3u), 0, top.dsize, 0, (uint8_t)top.big};
+    const uint32_t es0 = list ? (top.big ? 4u : 2u) : (top.big ? 6u : 3u);
+    stk[sp++] = Frame{top.dstart, top.tstart, top.tsize / es0, 0, top.dsize, (uint8_t)list, (uint8_t)top.big};
     while (sp > 0) {
         Frame &f = stk[sp - 1];
         if (f.i >= f.nent) {
@@ -117,21 +149,23 @@ __device__ __forceinline__ uint32_t parse_record(const Src &s, long long rs, lon
         if (e <= lo) continue; // empty value: skipped
         const uint32_t type = s.u8((pos_t)(e - 1));
         if (type == T_LIST || type == T_BIG_LIST || type == T_MESSAGE || type == T_BIG_MESSAGE) {
-            const bool list = type == T_LIST || type == T_BIG_LIST;
-            const Trailer tr = list ? parse_trailer<true>(s, (pos_t)lo, (pos_t)e) : parse_trailer<false>(s, (pos_t)lo, (pos_t)e);
+            const bool sub = type == T_LIST || type == T_BIG_LIST;
+            const Trailer tr = sub ? parse_trailer<true>(s, (pos_t)lo, (pos_t)e) : parse_trailer<false>(s, (pos_t)lo, (pos_t)e);
             if (tr.st != ST_OK) return ST_INVALID_VALUE;
             if (sp == VAL_MAX_DEPTH) return ST_TOO_DEEP;
-            const uint32_t es = list ? (tr.big ? 4u : 2u) : (tr.big ? 6u : 3u);
-            stk[sp++] = Frame{tr.dstart, tr.tstart, tr.tsize / es, 0, tr.dsize, (uint8_t)list, (uint8_t)tr.big};
-        } else if (!scalar_ok(s, type, lo, e)) {
-            return ST_INVALID_VALUE;
+            const uint32_t es = sub ? (tr.big ? 4u : 2u) : (tr.big ? 6u : 3u);
+            stk[sp++] = Frame{tr.dstart, tr.tstart, tr.tsize / es, 0, tr.dsize, (uint8_t)sub, (uint8_t)tr.big};
+        } else {
+            uint32_t n;
+            const int r = scalar_check(s, type, lo, e, n);
+            if (r) return r == 2 ? ST_PANIC : ST_INVALID_VALUE;
         }
     }
     size = (uint32_t)(re - top.dstart);
     return ST_OK;
 }
 
-__global__ __launch_bounds__(256) void parse_kernel(DecodeArgs a, uint32_t *sizes) {
+__global__ __launch_bounds__(256) void parse_kernel(DecodeArgs a, uint32_t *sizes, uint32_t root) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t base = a.r0 + ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * 64;
@@ -152,11 +186,11 @@ __global__ __launch_bounds__(256) void parse_kernel(DecodeArgs a, uint32_t *size
         if (!valid) return;
         LdsSrc s{(lds_u8 *)slab};
         st = parse_record(s, SLAB_GUARD + (long long)(gr.rec_lo - gr.aligned_lo),
-                          SLAB_GUARD + (long long)(gr.rec_hi - gr.aligned_lo), size);
+                          SLAB_GUARD + (long long)(gr.rec_hi - gr.aligned_lo), root, size);
     } else {
         if (!valid) return;
         GlobalSrc s{a.stream, a.stream_len};
-        st = parse_record(s, (long long)gr.rec_lo, (long long)gr.rec_hi, size);
+        st = parse_record(s, (long long)gr.rec_lo, (long long)gr.rec_hi, root, size);
     }
     a.f.status[r] = (uint8_t)st;
     if (sizes) sizes[r] = size;
@@ -164,11 +198,11 @@ __global__ __launch_bounds__(256) void parse_kernel(DecodeArgs a, uint32_t *size
 
 } // namespace
 
-int launch_parse(DecodeArgs a, uint32_t *sizes, double avg_record, hipStream_t stream) {
+int launch_parse(DecodeArgs a, uint32_t *sizes, uint32_t root, double avg_record, hipStream_t stream) {
     if (a.n <= a.r0) return 0;
     const DecodeLaunch L = decode_launch(a.n - a.r0, avg_record, device_cus(), false, 1);
     a.slab = L.slab;
-    hipLaunchKernelGGL(parse_kernel, dim3(L.blocks), dim3(64 * L.wpb), L.lds, stream, a, sizes);
+    hipLaunchKernelGGL(parse_kernel, dim3(L.blocks), dim3(64 * L.wpb), L.lds, stream, a, sizes, root);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -136,6 +136,7 @@ def _header_prototypes():
     src = open(_lib.HEADER_PATH).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     src = re.sub(r"//[^\n]*", "", src)
+    src = re.sub(r"^\s*#[^\n]*", ";", src, flags=re.M)  # preprocessor lines end a declaration
     out = []
     for m in re.finditer(r"(?:^|;|\})\s*((?:const\s+)?[A-Za-z_][\w ]*?[\s\*]+)(spec_[a-z0-9_]+)\s*\(", src):
         out.append((" ".join(m.group(1).split()), m.group(2)))
