@@ -24,6 +24,7 @@
 #include <utime.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <mutex>
 #include <sstream>
@@ -554,9 +555,12 @@ void gen_struct(std::ostringstream &o, const TreeDesc &D, uint32_t sf, const std
 
 // a message table's row: lo/hi expressions, its status column written (root: a panicked range
 // is ST_PANIC)
+// sel (the root table of a wave pair, gen_pair_rows): only the direct fields k with sel[k] are
+// decoded, and the table's status and *Err bits go to ro (RowOut) for the pair's exchange
 void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, const std::string &lo,
-                       const std::string &hi, bool root) {
+                       const std::string &hi, bool root, const std::vector<char> *sel = nullptr) {
     const TTable &T = D.t[t];
+    auto skip = [&](uint32_t k) { return sel && !(*sel)[k]; };
     uint64_t m[4] = {0, 0, 0, 0};
     for (uint32_t k = 0; k < T.nd; k++) {
         const uint32_t tag = D.f[D.direct[T.d0 + k]].tag;
@@ -581,7 +585,7 @@ void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, con
     bool any_nt = false;
     for (uint32_t k = 0; k < T.nd; k++) {
         const TField &F = D.f[D.direct[T.d0 + k]];
-        if (F.kind < spec::K_BOOL || F.kind > spec::K_BYTES) continue;
+        if (F.kind < spec::K_BOOL || F.kind > spec::K_BYTES || skip(k)) continue;
         o << "      const long long end" << k << " = tree_end<" << F.rank << ">(s, o);\n"
           << "      const long long e" << k << " = end" << k << " > 0 ? ds + end" << k << " : ds;\n"
           << "      const Win w" << k << " = load_win<" << (int)F.kind << ", true>(s, e" << k << ");\n";
@@ -589,7 +593,7 @@ void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, con
     o << "      bool slow = false;\n";
     for (uint32_t k = 0; k < T.nd; k++) {
         const TField &F = D.f[D.direct[T.d0 + k]];
-        if (F.kind < spec::K_BOOL || F.kind > spec::K_BYTES) continue;
+        if (F.kind < spec::K_BOOL || F.kind > spec::K_BYTES || skip(k)) continue;
         const uint32_t nt = spec::cross_kind_type(F.kind);
         o << "      bool ok" << k << " = true;\n"
           << "      Val v" << k << " = decode_tail_k<" << (int)F.kind << ", true>(w" << k << ", ds, e" << k << ", 0, &ok" << k
@@ -605,7 +609,7 @@ void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, con
         o << "      if (slow) {\n";
         for (uint32_t k = 0; k < T.nd; k++) {
             const TField &F = D.f[D.direct[T.d0 + k]];
-            if (F.kind < spec::K_BOOL || F.kind > spec::K_BYTES || !spec::cross_kind_type(F.kind)) continue;
+            if (F.kind < spec::K_BOOL || F.kind > spec::K_BYTES || !spec::cross_kind_type(F.kind) || skip(k)) continue;
             o << "        if (!nat" << k << ") v" << k << " = decode_tail_k<" << (int)F.kind << ">(load_win<" << (int)F.kind
               << ">(s, e" << k << "), ds, e" << k << ", 0, &ok" << k << ");\n";
         }
@@ -613,7 +617,7 @@ void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, con
     }
     for (uint32_t k = 0; k < T.nd; k++) {
         const TField &F = D.f[D.direct[T.d0 + k]];
-        if (F.kind < spec::K_BOOL || F.kind > spec::K_BYTES) continue;
+        if (F.kind < spec::K_BOOL || F.kind > spec::K_BYTES || skip(k)) continue;
         const std::string bit = k < 64 ? "(1ull << " + std::to_string(k) + ")" : "0ull";
         o << "      store_value_k<" << (int)F.kind << ">(" << col_expr(F.col) << ", row, v" << k << ");\n"
           << "      errs |= (ok" << k << " || end" << k << " <= 0) ? 0ull : " << bit << ";\n";
@@ -621,7 +625,7 @@ void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, con
     for (uint32_t k = 0; k < T.nd; k++) {
         const uint32_t fi = D.direct[T.d0 + k];
         const TField &F = D.f[fi];
-        if (F.kind >= spec::K_BOOL && F.kind <= spec::K_BYTES) continue;
+        if ((F.kind >= spec::K_BOOL && F.kind <= spec::K_BYTES) || skip(k)) continue;
         const std::string bit = k < 64 ? "(1ull << " + std::to_string(k) + ")" : "0ull";
         o << "      { // field " << fi << " tag " << F.tag << " kind " << (int)F.kind << "\n"
           << "        const long long end = tree_end<" << F.rank << ">(s, o);\n";
@@ -675,6 +679,15 @@ void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, con
             break;
         }
         o << "      }\n";
+    }
+    if (sel) {
+        o << "      (void)errp;\n      ro.errs = errs;\n"
+          << "    } else {\n"
+          << "      st = tree_message_fallback(s, D, B, " << t << "u, row, tlo, thi, gr);\n"
+          << "    }\n"
+          << "    ro.st = st;\n    ro.fast = o.fast ? 1u : 0u;\n"
+          << "  }\n";
+        return;
     }
     o << "      if (errp) errp[row] = errs;\n"
       << "    } else {\n"
@@ -843,6 +856,104 @@ void gen_size_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
       << "  }\n}\n";
 }
 
+// ---- the root group on a wave pair (tree_decode_core.hpp tree_rows_pair) ----
+// A cost per field, about its LDS reads and VALU: the pair split balances these.
+uint32_t tree_table_cost(const TreeDesc &D, uint32_t t);
+uint32_t tree_field_cost(const TreeDesc &D, uint32_t fi) {
+    const TField &F = D.f[fi];
+    switch (F.kind) {
+    case spec::K_STRING: case spec::K_BYTES: case spec::K_BIN128: case spec::K_BIN256: return 3;
+    case spec::K_STRUCT: return 2 + 2 * (F.send - fi - 1);
+    case spec::K_ANY: return 5;
+    case spec::K_LIST: return 5;
+    case spec::K_MESSAGE: return 3 + tree_table_cost(D, F.table);
+    default: return 2;
+    }
+}
+uint32_t tree_table_cost(const TreeDesc &D, uint32_t t) {
+    const TTable &T = D.t[t];
+    uint32_t c = 4;
+    for (uint32_t k = 0; k < T.nd; k++) c += tree_field_cost(D, D.direct[T.d0 + k]);
+    return c;
+}
+
+// Group root x split over two waves: sel[w][k] = wave w decodes root field k (with the sub-message
+// tables below it, which need the range it finds).  Heaviest first, each to the lighter wave.
+// false when the root has too few fields to split.
+bool pair_split(const TreeDesc &D, uint32_t x, std::vector<char> sel[2], uint32_t *table_wave) {
+    const TTable &T = D.t[x];
+    if (T.shape != spec::SHAPE_MESSAGE || T.nd < 4) return false;
+    std::vector<uint32_t> ks(T.nd);
+    for (uint32_t k = 0; k < T.nd; k++) ks[k] = k;
+    std::stable_sort(ks.begin(), ks.end(), [&](uint32_t a, uint32_t b) {
+        return tree_field_cost(D, D.direct[T.d0 + a]) > tree_field_cost(D, D.direct[T.d0 + b]);
+    });
+    uint32_t load[2] = {0, 0};
+    sel[0].assign(T.nd, 0);
+    sel[1].assign(T.nd, 0);
+    for (uint32_t k : ks) {
+        const int w = load[1] < load[0] ? 1 : 0;
+        sel[w][k] = 1;
+        load[w] += tree_field_cost(D, D.direct[T.d0 + k]);
+    }
+    for (uint32_t g = 1; g < T.gn; g++) {
+        const uint32_t y = D.group[T.g0 + g];
+        uint32_t a = y;
+        while (D.t[a].parent != x) a = D.t[a].parent;
+        table_wave[y] = 0;
+        for (uint32_t k = 0; k < T.nd; k++)
+            if (D.direct[T.d0 + k] == D.t[a].field) table_wave[y] = sel[1][k] ? 1 : 0;
+    }
+    return true;
+}
+
+// spec_tree_group_<x>p: the group's row code split over a wave pair (pair_split)
+void gen_pair_rows(std::ostringstream &o, const TreeDesc &D, uint32_t x) {
+    std::vector<char> sel[2];
+    uint32_t tw[spec::TREE_MAX_T] = {};
+    if (!pair_split(D, x, sel, tw)) return;
+    const TTable &T = D.t[x];
+    for (int w = 0; w < 2; w++) {
+        o << "template <class Src>\n__device__ __forceinline__ void gen_pair_" << x << "_w" << w
+          << "(const Src &s, const TreeDesc &D, const TreeBufs &B, uint64_t row, long long lo, long long hi, uint2 *gr, "
+             "RowOut &ro) {\n"
+          << "  const bool panic = false; (void)panic;\n";
+        gen_message_table(o, D, x, "lo", "hi", true, &sel[w]);
+        for (uint32_t g = 1; g < T.gn; g++) {
+            const uint32_t y = D.group[T.g0 + g];
+            if (tw[y] != (uint32_t)w) continue;
+            const std::string r = "gr[" + std::to_string(D.t[y].gslot) + " * 64]";
+            gen_message_table(o, D, y, "(long long)" + r + ".x", "(long long)" + r + ".y", false);
+        }
+        o << "}\n";
+    }
+    o << "extern \"C\" __global__ __launch_bounds__(128) void spec_tree_group_" << x
+      << "p(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x, uint32_t slab, uint32_t wave_bytes, uint32_t rpw) {\n"
+      << "  const TreeDesc &D = *Dp;\n"
+      << "  const TreeBufs &B = *Bp;\n"
+      << "  const uint64_t rows = dec_rows(D, B, x);\n"
+      << "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+      << "  uint2 *gr = (uint2 *)(smem + slab + (threadIdx.x >> 6) * wave_bytes) + (threadIdx.x & 63);\n"
+      << "  uint4 *xch = (uint4 *)(smem + slab + 2 * wave_bytes);\n"
+      << "  (void)rpw;\n"
+      << "  tree_rows_pair(B, x, rows, slab, xch,\n"
+      << "    [&](const TreeLds &s, uint64_t row, long long lo, long long hi, RowOut &ro) {\n"
+      << "      if (threadIdx.x < 64) gen_pair_" << x << "_w0(s, D, B, row, lo, hi, gr, ro);\n"
+      << "      else gen_pair_" << x << "_w1(s, D, B, row, lo, hi, gr, ro);\n"
+      << "    },\n"
+      << "    [&](const GlobalSrc &s, uint64_t row, long long lo, long long hi, RowOut &ro) {\n"
+      << "      if (threadIdx.x < 64) gen_pair_" << x << "_w0(s, D, B, row, lo, hi, gr, ro);\n"
+      << "      else gen_pair_" << x << "_w1(s, D, B, row, lo, hi, gr, ro);\n"
+      << "    },\n"
+      << "    [&](uint64_t row, bool panic, const RowOut &a, const RowOut &b) {\n"
+      << "      uint64_t *errp = " << (T.err_col >= 0 ? "(uint64_t *)" + col_expr(T.err_col) : std::string("nullptr")) << ";\n"
+      << "      if (a.fast && errp) errp[row] = a.errs | b.errs;\n"
+      << "      const uint32_t st = a.st == ST_PANIC || b.st == ST_PANIC ? (uint32_t)ST_PANIC : a.st;\n"
+      << "      store_u8(" << col_expr(T.status_col) << ", row, panic ? (uint32_t)ST_PANIC : st);\n"
+      << "    });\n"
+      << "}\n";
+}
+
 std::string generate_tree(const TreeDesc &D, bool *has) {
     std::ostringstream o;
     o << "#include \"tree_decode_core.hpp\"\nusing namespace spec;\n";
@@ -949,6 +1060,7 @@ std::string generate_tree(const TreeDesc &D, bool *has) {
           << "    gen_row_" << x << "(s, D, B, row, lo, hi, panic, gr);\n"
           << "  });\n"
           << "}\n";
+        if (x == 0) gen_pair_rows(o, D, x);
     }
     // level-fused list groups: the groups one decode level holds (lists owned by the previous
     // level's groups, rows from HBM) in ONE launch, blockIdx.y picking the group — each group is
@@ -978,7 +1090,8 @@ std::string generate_tree(const TreeDesc &D, bool *has) {
 
 struct TreeEntry {
     hipModule_t mod = nullptr;
-    // [x]: decode, staged rows; [TREE_MAX_T + x]: decode, rows from HBM; [4 TREE_MAX_T], [+1]: the
+    // [x]: decode, staged rows; [TREE_MAX_T + x]: decode, rows from HBM; [2 TREE_MAX_T + x]: decode
+    // on wave pairs (the root group, gen_pair_rows; nullptr if not split); [4 TREE_MAX_T], [+1]: the
     // level-fused encode size / write kernels; [+2]: the level-fused list-group decode kernel
     hipFunction_t fn[4 * spec::TREE_MAX_T + 3] = {};
     bool failed = false;
@@ -999,6 +1112,7 @@ long long jit_compile_only_tree(const TreeDesc &D) {
 
 // The schema-specialised group kernels of a tree: fn[x] for each group root x that has one
 // (nullptr where the run-time kernel runs), fn[TREE_MAX_T + x] its variant without staging,
+// fn[2 TREE_MAX_T + x] its wave-pair variant (root group only; nullptr when not split),
 // fn[4 TREE_MAX_T] / fn[4 TREE_MAX_T + 1] the level-fused size / write kernels of the encoder,
 // fn[4 TREE_MAX_T + 2] the level-fused list-group decode kernel; nullptr when the JIT is off or failed.
 const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
@@ -1036,6 +1150,10 @@ const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
             const std::string name = "spec_tree_group_" + std::to_string(x);
             ok = hipModuleGetFunction(&e.fn[x], e.mod, name.c_str()) == hipSuccess &&
                  hipModuleGetFunction(&e.fn[TREE_MAX_T + x], e.mod, (name + "g").c_str()) == hipSuccess;
+            std::vector<char> sel[2];
+            uint32_t tw[TREE_MAX_T];
+            if (ok && x == 0 && pair_split(D, x, sel, tw))
+                ok = hipModuleGetFunction(&e.fn[2 * TREE_MAX_T + x], e.mod, (name + "p").c_str()) == hipSuccess;
         }
         if (!ok) {
             (void)hipGetLastError();

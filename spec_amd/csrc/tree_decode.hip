@@ -29,6 +29,13 @@
 namespace spec {
 namespace {
 
+// Build-time A/B (make HIPFLAGS+="-DSPEC_AB_TREE_PAIR=0"), never the environment: 0 runs the
+// root group's staged kernel one wave per 64 rows instead of on wave pairs.
+#ifndef SPEC_AB_TREE_PAIR
+#define SPEC_AB_TREE_PAIR 1
+#endif
+constexpr bool tree_pair() { return SPEC_AB_TREE_PAIR != 0; }
+
 // Group root x (the records or a list table) and the sub-message tables below it, a lane per
 // row, run-time schema.  LDS per wave: the staging slab, then a range slot per sub-message table
 // of the group.
@@ -450,7 +457,21 @@ int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, 
             const uint64_t per_block = (uint64_t)(TB / 64) * gs.rpw;
             const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((cap + per_block - 1) / per_block, 1u << 20));
             const size_t lds = (size_t)(TB / 64) * gs.wave_bytes;
-            if (d->jit && d->jit[x] && all_cols) {
+            if (tree_pair() && d->jit && d->jit[2 * TREE_MAX_T + x] && all_cols && gs.slab) {
+                // the root group on wave pairs: one slab per 64 rows, two waves decoding it
+                // (tree_rows_pair); wave_bytes here = one wave's range slots (no padding: pkg1's
+                // 35 KiB slab + 2 x 2 KiB slots + the 1 KiB exchange = 40 KiB, four blocks per CU)
+                const uint32_t gn = D.t[x].gn;
+                uint32_t xx = x, slab = gs.slab, wb = 512u * (gn > 1 ? gn - 1 : 0), rpw = 64;
+                void *args[] = {(void *)&Dd, (void *)&Bd, &xx, &slab, &wb, &rpw};
+                const unsigned grid = (unsigned)std::min<uint64_t>((cap + 63) / 64, 1u << 20);
+                const hipError_t le = hipModuleLaunchKernel(d->jit[2 * TREE_MAX_T + x], grid, 1, 1, 128, 1, 1,
+                                                            slab + 2 * wb + 64 * 16, st, args, nullptr);
+                if (le != hipSuccess) {
+                    note_hip_error(le);
+                    return SPEC_E_HIP;
+                }
+            } else if (d->jit && d->jit[x] && all_cols) {
                 uint32_t xx = x, slab = gs.slab, wb = gs.wave_bytes, rpw = gs.rpw;
                 void *args[] = {(void *)&Dd, (void *)&Bd, &xx, &slab, &wb, &rpw};
                 // rows from HBM: the kernel without staging code (fewer registers, more waves)

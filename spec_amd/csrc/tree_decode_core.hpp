@@ -139,6 +139,75 @@ __device__ __forceinline__ void tree_rows(const TreeBufs &B, uint32_t x, uint64_
     }
 }
 
+// The root table's outcome on one wave of a pair (tree_rows_pair): its status, whether the
+// table took the specialised path, and the *Err bits of the fields that wave decoded.
+struct RowOut {
+    uint64_t errs;
+    uint32_t st, fast;
+};
+
+// tree_rows for a wave pair (a 128-thread block): both waves take the same 64 rows, staged ONCE
+// in the block's slab (each wave issues half the LDS-DMA chunks), and each decodes its share of
+// the group's fields (jit.cpp gen_pair_rows); wave 1 then hands its RowOut to wave 0 through LDS
+// (xch, 64 entries) and fin(row, panic, ro0, ro1) stores the root table's status and *Err mask.
+// Two waves per 64 rows at the same LDS per row: a SIMD holds two waves, so one's LDS round
+// trips overlap the other's decode.  Rows whose span exceeds the slab parse from HBM (the lane
+// windows of tree_rows are not used here).
+template <class LdsBody, class GlobBody, class Fin>
+__device__ __forceinline__ void tree_rows_pair(const TreeBufs &B, uint32_t x, uint64_t rows, uint32_t slab_bytes,
+                                               uint4 *xch, LdsBody lds_body, GlobBody glob_body, Fin fin) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint8_t *slab = smem;
+    const __amdgpu_buffer_rsrc_t rsrc = stream_rsrc(B);
+    const GlobalSrc gs{B.stream, B.stream_len};
+    for (uint64_t base = (uint64_t)blockIdx.x * 64; base < rows; base += (uint64_t)gridDim.x * 64) {
+        const uint64_t row = base + lane;
+        const bool valid = row < rows;
+        long long lo = 0, hi = 0;
+        bool panic = false;
+        if (valid) row_range(B, x, row, lo, hi, panic);
+        const bool some = valid && hi > lo;
+        long long slo = some ? lo : (long long)B.stream_len, shi = some ? hi : 0;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            const long long a = __shfl_xor(slo, d), b2 = __shfl_xor(shi, d);
+            slo = a < slo ? a : slo;
+            shi = b2 > shi ? b2 : shi;
+        }
+        slo = (long long)uniform64((uint64_t)slo);
+        shi = (long long)uniform64((uint64_t)shi);
+        const long long sb = (slo > GUARD ? slo - GUARD : 0) & ~15ll, se = (shi + 16 + 15) & ~15ll;
+        const bool span = slab_bytes && slo < shi && se - sb + 16 <= (long long)slab_bytes;
+        if (span) {
+            const uint32_t chunks = (uint32_t)((se - sb + 1023) >> 10);
+            for (uint32_t c = (uint32_t)wave; c < chunks; c += 2)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(slab + c * 1024),
+                                                         16, (uint32_t)sb + c * 1024 + lane * 16, 0, 0, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // the straddling chunk is refilled by the wave that loaded it (after its own DMA landed)
+            const uint64_t tail = B.stream_len & ~15ull;
+            if (tail < B.stream_len && (long long)tail >= sb && (long long)tail < sb + (long long)chunks * 1024 &&
+                (int)(((tail - sb) >> 10) & 1) == wave && lane < 16 && tail + lane < B.stream_len)
+                slab[tail - sb + lane] = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)(tail + lane), 0, 0);
+        }
+        __syncthreads(); // the slab is whole; the previous rows' exchange has been read
+        RowOut ro = {0, 0, 0};
+        if (valid) {
+            if (span)
+                lds_body(TreeLds{(lds_u8 *)slab, sb, (int)slab_bytes}, row, lo, hi, ro);
+            else
+                glob_body(gs, row, lo, hi, ro);
+        }
+        if (wave == 1) xch[lane] = make_uint4((uint32_t)ro.errs, (uint32_t)(ro.errs >> 32), ro.st, ro.fast);
+        __syncthreads(); // wave 1's outcome is in xch; both waves are done with the slab
+        if (wave == 0 && valid) {
+            const uint4 q = xch[lane];
+            fin(row, panic, ro, RowOut{(uint64_t)q.x | ((uint64_t)q.y << 32), q.z, q.w});
+        }
+    }
+}
+
 // tree_rows without staging (slab 0): every row parsed from HBM.  A kernel of its own, so its
 // register budget is the row code's alone (the staging paths' 16-chunk lane windows would
 // otherwise set it) and the CU holds as many waves as the latency of the reads needs.
