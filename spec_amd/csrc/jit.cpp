@@ -558,7 +558,8 @@ void gen_struct(std::ostringstream &o, const TreeDesc &D, uint32_t sf, const std
 // sel (the root table of a wave pair, gen_pair_rows): only the direct fields k with sel[k] are
 // decoded, and the table's status and *Err bits go to ro (RowOut) for the pair's exchange
 void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, const std::string &lo,
-                       const std::string &hi, bool root, const std::vector<char> *sel = nullptr) {
+                       const std::string &hi, bool root, const std::vector<char> *sel = nullptr,
+                       const std::string &fallback = "tree_message_fallback", const std::string &on_bad = "") {
     const TTable &T = D.t[t];
     auto skip = [&](uint32_t k) { return sel && !(*sel)[k]; };
     uint64_t m[4] = {0, 0, 0, 0};
@@ -569,8 +570,9 @@ void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, con
     o << "  { // table " << t << "\n"
       << "    const long long tlo = " << lo << ", thi = " << hi << ";\n"
       << "    const TOpen o = tree_open<" << T.nd << ", 0x" << std::hex << m[0] << "ull, 0x" << m[1] << "ull, 0x" << m[2]
-      << "ull, 0x" << m[3] << "ull" << std::dec << ">(s, tlo, thi);\n"
-      << "    uint32_t st;\n"
+      << "ull, 0x" << m[3] << "ull" << std::dec << ">(s, tlo, thi);\n";
+    if (!on_bad.empty()) o << "    if (o.st != ST_OK) { " << on_bad << " } // the owner field's *Err bit\n";
+    o << "    uint32_t st;\n"
       << "    if (o.fast) {\n"
       << "      st = o.st;\n"
       << "      const long long ds = o.ds;\n"
@@ -633,8 +635,9 @@ void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, con
         case spec::K_MESSAGE:
             o << "        const long long e = end >= 0 ? ds + end : ds;\n"
               << "        store_u8(" << col_expr(F.present) << ", row, end >= 0 ? 1u : 0u);\n"
-              << "        gr[" << D.t[F.table].gslot << " * 64] = end >= 0 ? make_uint2((uint32_t)ds, (uint32_t)e) : make_uint2(0, 0);\n"
-              << "        if (errp && e > ds && parse_trailer<false>(s, ds, e).st != ST_OK) errs |= " << bit << ";\n";
+              << "        gr[" << D.t[F.table].gslot << " * 64] = end >= 0 ? make_uint2((uint32_t)ds, (uint32_t)e) : make_uint2(0, 0);\n";
+            // (its *Err bit — the sub-message's trailer invalid — is set by the sub-table's own
+            // tree_open over the same range, gen_sub_tables: the trailer is parsed once)
             break;
         case spec::K_LIST:
             o << "        const long long e = end >= 0 ? ds + end : ds;\n"
@@ -683,7 +686,7 @@ void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, con
     if (sel) {
         o << "      (void)errp;\n      ro.errs = errs;\n"
           << "    } else {\n"
-          << "      st = tree_message_fallback(s, D, B, " << t << "u, row, tlo, thi, gr);\n"
+          << "      st = " << fallback << "(s, D, B, " << t << "u, row, tlo, thi, gr);\n"
           << "    }\n"
           << "    ro.st = st;\n    ro.fast = o.fast ? 1u : 0u;\n"
           << "  }\n";
@@ -691,7 +694,7 @@ void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, con
     }
     o << "      if (errp) errp[row] = errs;\n"
       << "    } else {\n"
-      << "      st = tree_message_fallback(s, D, B, " << t << "u, row, tlo, thi, gr);\n"
+      << "      st = " << fallback << "(s, D, B, " << t << "u, row, tlo, thi, gr);\n"
       << "    }\n"
       << "    store_u8(" << col_expr(T.status_col) << ", row, " << (root ? "panic ? (uint32_t)ST_PANIC : st" : "st")
       << ");\n"
@@ -856,6 +859,30 @@ void gen_size_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
       << "  }\n}\n";
 }
 
+// The sub-message tables of group root x after its root table's code, each over the range its
+// owner field left in its slot; a sub-table whose trailer is invalid sets its owner field's *Err
+// bit (the owner's getter would have failed on the same trailer): on a wave group's root through
+// ro (pair), else into the owner's ERRMASK column, which the owner's code stored before.
+void gen_sub_tables(std::ostringstream &o, const TreeDesc &D, uint32_t x, int pair_w, const uint32_t *tw,
+                    const std::string &fb) {
+    const TTable &T = D.t[x];
+    for (uint32_t g = 1; g < T.gn; g++) {
+        const uint32_t y = D.group[T.g0 + g];
+        if (pair_w >= 0 && tw[y] != (uint32_t)pair_w) continue;
+        const TTable &Y = D.t[y], &Pt = D.t[Y.parent];
+        std::string bad;
+        uint32_t k = 0;
+        while (k < Pt.nd && D.direct[Pt.d0 + k] != Y.field) k++;
+        if (Pt.err_col >= 0 && k < 64) {
+            const std::string bit = "(1ull << " + std::to_string(k) + ")";
+            bad = pair_w >= 0 && Y.parent == x ? "ro.errs |= " + bit + ";"
+                                               : "((uint64_t *)" + col_expr(Pt.err_col) + ")[row] |= " + bit + ";";
+        }
+        const std::string r = "gr[" + std::to_string(Y.gslot) + " * 64]";
+        gen_message_table(o, D, y, "(long long)" + r + ".x", "(long long)" + r + ".y", false, nullptr, fb, bad);
+    }
+}
+
 // ---- the root group on a wave pair (tree_decode_core.hpp tree_rows_pair) ----
 // A cost per field, about its LDS reads and VALU: the pair split balances these.
 uint32_t tree_table_cost(const TreeDesc &D, uint32_t t);
@@ -877,22 +904,23 @@ uint32_t tree_table_cost(const TreeDesc &D, uint32_t t) {
     return c;
 }
 
-// Group root x split over two waves: sel[w][k] = wave w decodes root field k (with the sub-message
-// tables below it, which need the range it finds).  Heaviest first, each to the lighter wave.
-// false when the root has too few fields to split.
-bool pair_split(const TreeDesc &D, uint32_t x, std::vector<char> sel[2], uint32_t *table_wave) {
+// Group root x split over P waves: sel[w][k] = wave w decodes root field k (with the sub-message
+// tables below it, which need the range it finds).  Heaviest first, each to the least loaded
+// wave.  false when the root has too few fields to split.
+bool pair_split(const TreeDesc &D, uint32_t x, int P, std::vector<char> *sel, uint32_t *table_wave) {
     const TTable &T = D.t[x];
-    if (T.shape != spec::SHAPE_MESSAGE || T.nd < 4) return false;
+    if (T.shape != spec::SHAPE_MESSAGE || T.nd < (uint32_t)(2 * P)) return false;
     std::vector<uint32_t> ks(T.nd);
     for (uint32_t k = 0; k < T.nd; k++) ks[k] = k;
     std::stable_sort(ks.begin(), ks.end(), [&](uint32_t a, uint32_t b) {
         return tree_field_cost(D, D.direct[T.d0 + a]) > tree_field_cost(D, D.direct[T.d0 + b]);
     });
-    uint32_t load[2] = {0, 0};
-    sel[0].assign(T.nd, 0);
-    sel[1].assign(T.nd, 0);
+    uint32_t load[4] = {0, 0, 0, 0};
+    for (int w = 0; w < P; w++) sel[w].assign(T.nd, 0);
     for (uint32_t k : ks) {
-        const int w = load[1] < load[0] ? 1 : 0;
+        int w = 0;
+        for (int v = 1; v < P; v++)
+            if (load[v] < load[w]) w = v;
         sel[w][k] = 1;
         load[w] += tree_field_cost(D, D.direct[T.d0 + k]);
     }
@@ -902,49 +930,53 @@ bool pair_split(const TreeDesc &D, uint32_t x, std::vector<char> sel[2], uint32_
         while (D.t[a].parent != x) a = D.t[a].parent;
         table_wave[y] = 0;
         for (uint32_t k = 0; k < T.nd; k++)
-            if (D.direct[T.d0 + k] == D.t[a].field) table_wave[y] = sel[1][k] ? 1 : 0;
+            if (D.direct[T.d0 + k] == D.t[a].field)
+                for (int w = 0; w < P; w++)
+                    if (sel[w][k]) table_wave[y] = (uint32_t)w;
     }
     return true;
 }
 
-// spec_tree_group_<x>p: the group's row code split over a wave pair (pair_split)
-void gen_pair_rows(std::ostringstream &o, const TreeDesc &D, uint32_t x) {
-    std::vector<char> sel[2];
+// spec_tree_group_<x>p<P>: the group's row code split over P waves (pair_split).  The waves
+// share one set of range slots: a sub-message table's slot is written and read by the wave that
+// owns it (a row on the run-time path has every wave write every slot, with the same values).
+void gen_pair_rows(std::ostringstream &o, const TreeDesc &D, uint32_t x, int P) {
+    std::vector<char> sel[4];
     uint32_t tw[spec::TREE_MAX_T] = {};
-    if (!pair_split(D, x, sel, tw)) return;
+    if (!pair_split(D, x, P, sel, tw)) return;
     const TTable &T = D.t[x];
-    for (int w = 0; w < 2; w++) {
-        o << "template <class Src>\n__device__ __forceinline__ void gen_pair_" << x << "_w" << w
+    const std::string fn = "gen_pair_" + std::to_string(x) + "_" + std::to_string(P) + "_w";
+    for (int w = 0; w < P; w++) {
+        o << "template <class Src>\n__device__ __forceinline__ void " << fn << w
           << "(const Src &s, const TreeDesc &D, const TreeBufs &B, uint64_t row, long long lo, long long hi, uint2 *gr, "
-             "RowOut &ro) {\n"
-          << "  const bool panic = false; (void)panic;\n";
-        gen_message_table(o, D, x, "lo", "hi", true, &sel[w]);
-        for (uint32_t g = 1; g < T.gn; g++) {
-            const uint32_t y = D.group[T.g0 + g];
-            if (tw[y] != (uint32_t)w) continue;
-            const std::string r = "gr[" + std::to_string(D.t[y].gslot) + " * 64]";
-            gen_message_table(o, D, y, "(long long)" + r + ".x", "(long long)" + r + ".y", false);
-        }
+             "RowOut &ro) {\n";
+        const std::string fb = "tree_message_fallback_p<" + std::to_string(P) + ">";
+        gen_message_table(o, D, x, "lo", "hi", true, &sel[w], fb);
+        gen_sub_tables(o, D, x, w, tw, fb);
         o << "}\n";
     }
-    o << "extern \"C\" __global__ __launch_bounds__(128) void spec_tree_group_" << x
-      << "p(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x, uint32_t slab, uint32_t wave_bytes, uint32_t rpw) {\n"
+    std::ostringstream call;
+    call << "      switch (threadIdx.x >> 6) {\n";
+    for (int w = 0; w < P; w++)
+        call << "      case " << w << ": " << fn << w << "(s, D, B, row, lo, hi, gr, ro); break;\n";
+    call << "      default: break;\n      }\n";
+    // P waves of one block per SIMD... and as many blocks per CU as the LDS holds (four for
+    // pkg1): registers for 8 / 4 waves per SIMD-pair budget -> at most 512 / P VGPRs
+    o << "extern \"C\" __global__ __launch_bounds__(" << 64 * P << ") __attribute__((amdgpu_waves_per_eu(" << P
+      << "))) void spec_tree_group_" << x << "p" << P
+      << "(const TreeDesc *Dp, const TreeBufs *Bp, uint32_t x, uint32_t slab, uint32_t slots, uint32_t rpw) {\n"
       << "  const TreeDesc &D = *Dp;\n"
       << "  const TreeBufs &B = *Bp;\n"
       << "  const uint64_t rows = dec_rows(D, B, x);\n"
       << "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
-      << "  uint2 *gr = (uint2 *)(smem + slab + (threadIdx.x >> 6) * wave_bytes) + (threadIdx.x & 63);\n"
-      << "  uint4 *xch = (uint4 *)(smem + slab + 2 * wave_bytes);\n"
+      << "  uint2 *gr = (uint2 *)(smem + slab) + (threadIdx.x & 63);\n"
+      << "  uint4 *xch = (uint4 *)(smem + slab + slots);\n"
       << "  (void)rpw;\n"
-      << "  tree_rows_pair(B, x, rows, slab, xch,\n"
+      << "  tree_rows_pair<" << P << ">(B, x, rows, slab, xch,\n"
       << "    [&](const TreeLds &s, uint64_t row, long long lo, long long hi, RowOut &ro) {\n"
-      << "      if (threadIdx.x < 64) gen_pair_" << x << "_w0(s, D, B, row, lo, hi, gr, ro);\n"
-      << "      else gen_pair_" << x << "_w1(s, D, B, row, lo, hi, gr, ro);\n"
-      << "    },\n"
+      << call.str() << "    },\n"
       << "    [&](const GlobalSrc &s, uint64_t row, long long lo, long long hi, RowOut &ro) {\n"
-      << "      if (threadIdx.x < 64) gen_pair_" << x << "_w0(s, D, B, row, lo, hi, gr, ro);\n"
-      << "      else gen_pair_" << x << "_w1(s, D, B, row, lo, hi, gr, ro);\n"
-      << "    },\n"
+      << call.str() << "    },\n"
       << "    [&](uint64_t row, bool panic, const RowOut &a, const RowOut &b) {\n"
       << "      uint64_t *errp = " << (T.err_col >= 0 ? "(uint64_t *)" + col_expr(T.err_col) : std::string("nullptr")) << ";\n"
       << "      if (a.fast && errp) errp[row] = a.errs | b.errs;\n"
@@ -1027,11 +1059,7 @@ std::string generate_tree(const TreeDesc &D, bool *has) {
             o << "  store_u8(" << col_expr(T.status_col) << ", row, panic ? (uint32_t)ST_PANIC : sst);\n";
         } else {
             gen_message_table(o, D, x, "lo", "hi", true);
-            for (uint32_t g = 1; g < T.gn; g++) {
-                const uint32_t y = D.group[T.g0 + g];
-                const std::string r = "gr[" + std::to_string(D.t[y].gslot) + " * 64]";
-                gen_message_table(o, D, y, "(long long)" + r + ".x", "(long long)" + r + ".y", false);
-            }
+            gen_sub_tables(o, D, x, -1, nullptr, "tree_message_fallback");
         }
         o << "}\n"
           << "extern \"C\" __global__ __launch_bounds__(256) void spec_tree_group_" << x
@@ -1060,7 +1088,9 @@ std::string generate_tree(const TreeDesc &D, bool *has) {
           << "    gen_row_" << x << "(s, D, B, row, lo, hi, panic, gr);\n"
           << "  });\n"
           << "}\n";
-        if (x == 0) gen_pair_rows(o, D, x);
+        // (4 waves per 64 rows: 110 vs 100 us for pkg1 — registers cap it at 3 waves per SIMD,
+        // so 3 slabs per CU instead of 4)
+        if (x == 0) gen_pair_rows(o, D, x, 2);
     }
     // level-fused list groups: the groups one decode level holds (lists owned by the previous
     // level's groups, rows from HBM) in ONE launch, blockIdx.y picking the group — each group is
@@ -1090,8 +1120,9 @@ std::string generate_tree(const TreeDesc &D, bool *has) {
 
 struct TreeEntry {
     hipModule_t mod = nullptr;
-    // [x]: decode, staged rows; [TREE_MAX_T + x]: decode, rows from HBM; [2 TREE_MAX_T + x]: decode
-    // on wave pairs (the root group, gen_pair_rows; nullptr if not split); [4 TREE_MAX_T], [+1]: the
+    // [x]: decode, staged rows; [TREE_MAX_T + x]: decode, rows from HBM; [2 TREE_MAX_T + x]:
+    // decode on 2 waves per 64 rows (the root group, gen_pair_rows; nullptr if not split);
+    // [4 TREE_MAX_T], [+1]: the
     // level-fused encode size / write kernels; [+2]: the level-fused list-group decode kernel
     hipFunction_t fn[4 * spec::TREE_MAX_T + 3] = {};
     bool failed = false;
@@ -1112,7 +1143,7 @@ long long jit_compile_only_tree(const TreeDesc &D) {
 
 // The schema-specialised group kernels of a tree: fn[x] for each group root x that has one
 // (nullptr where the run-time kernel runs), fn[TREE_MAX_T + x] its variant without staging,
-// fn[2 TREE_MAX_T + x] its wave-pair variant (root group only; nullptr when not split),
+// fn[2 TREE_MAX_T + x] its 2-wave variant (root group only; nullptr when not split),
 // fn[4 TREE_MAX_T] / fn[4 TREE_MAX_T + 1] the level-fused size / write kernels of the encoder,
 // fn[4 TREE_MAX_T + 2] the level-fused list-group decode kernel; nullptr when the JIT is off or failed.
 const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
@@ -1150,10 +1181,10 @@ const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
             const std::string name = "spec_tree_group_" + std::to_string(x);
             ok = hipModuleGetFunction(&e.fn[x], e.mod, name.c_str()) == hipSuccess &&
                  hipModuleGetFunction(&e.fn[TREE_MAX_T + x], e.mod, (name + "g").c_str()) == hipSuccess;
-            std::vector<char> sel[2];
+            std::vector<char> sel[4];
             uint32_t tw[TREE_MAX_T];
-            if (ok && x == 0 && pair_split(D, x, sel, tw))
-                ok = hipModuleGetFunction(&e.fn[2 * TREE_MAX_T + x], e.mod, (name + "p").c_str()) == hipSuccess;
+            if (ok && x == 0 && pair_split(D, x, 2, sel, tw))
+                ok = hipModuleGetFunction(&e.fn[2 * TREE_MAX_T + x], e.mod, (name + "p2").c_str()) == hipSuccess;
         }
         if (!ok) {
             (void)hipGetLastError();

@@ -30,11 +30,12 @@ namespace spec {
 namespace {
 
 // Build-time A/B (make HIPFLAGS+="-DSPEC_AB_TREE_PAIR=0"), never the environment: 0 runs the
-// root group's staged kernel one wave per 64 rows instead of on wave pairs.
+// root group's staged kernel one wave per 64 rows instead of two (gen_pair_rows; pkg1: 158 vs
+// 100 us).
 #ifndef SPEC_AB_TREE_PAIR
-#define SPEC_AB_TREE_PAIR 1
+#define SPEC_AB_TREE_PAIR 2
 #endif
-constexpr bool tree_pair() { return SPEC_AB_TREE_PAIR != 0; }
+constexpr int tree_pair() { return SPEC_AB_TREE_PAIR == 2 ? 2 : 0; }
 
 // Group root x (the records or a list table) and the sub-message tables below it, a lane per
 // row, run-time schema.  LDS per wave: the staging slab, then a range slot per sub-message table
@@ -457,16 +458,18 @@ int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, 
             const uint64_t per_block = (uint64_t)(TB / 64) * gs.rpw;
             const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((cap + per_block - 1) / per_block, 1u << 20));
             const size_t lds = (size_t)(TB / 64) * gs.wave_bytes;
-            if (tree_pair() && d->jit && d->jit[2 * TREE_MAX_T + x] && all_cols && gs.slab) {
-                // the root group on wave pairs: one slab per 64 rows, two waves decoding it
-                // (tree_rows_pair); wave_bytes here = one wave's range slots (no padding: pkg1's
-                // 35 KiB slab + 2 x 2 KiB slots + the 1 KiB exchange = 40 KiB, four blocks per CU)
-                const uint32_t gn = D.t[x].gn;
-                uint32_t xx = x, slab = gs.slab, wb = 512u * (gn > 1 ? gn - 1 : 0), rpw = 64;
-                void *args[] = {(void *)&Dd, (void *)&Bd, &xx, &slab, &wb, &rpw};
+            const hipFunction_t pair_fn =
+                tree_pair() && d->jit && all_cols && gs.slab ? d->jit[2 * TREE_MAX_T + x] : nullptr;
+            if (pair_fn) {
+                // the root group on P waves per 64 rows: one slab, the waves decoding it
+                // (tree_rows_pair), one set of range slots, a 1 KiB exchange per extra wave (pkg1:
+                // 35 KiB slab + 2 KiB slots + 1-3 KiB = four blocks per CU)
+                const uint32_t gn = D.t[x].gn, P = (uint32_t)tree_pair();
+                uint32_t xx = x, slab = gs.slab, slots = 512u * (gn > 1 ? gn - 1 : 0), rpw = 64;
+                void *args[] = {(void *)&Dd, (void *)&Bd, &xx, &slab, &slots, &rpw};
                 const unsigned grid = (unsigned)std::min<uint64_t>((cap + 63) / 64, 1u << 20);
-                const hipError_t le = hipModuleLaunchKernel(d->jit[2 * TREE_MAX_T + x], grid, 1, 1, 128, 1, 1,
-                                                            slab + 2 * wb + 64 * 16, st, args, nullptr);
+                const hipError_t le = hipModuleLaunchKernel(pair_fn, grid, 1, 1, 64 * P, 1, 1, slab + slots + (P - 1) * 1024,
+                                                            st, args, nullptr);
                 if (le != hipSuccess) {
                     note_hip_error(le);
                     return SPEC_E_HIP;

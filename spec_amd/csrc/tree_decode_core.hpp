@@ -139,21 +139,22 @@ __device__ __forceinline__ void tree_rows(const TreeBufs &B, uint32_t x, uint64_
     }
 }
 
-// The root table's outcome on one wave of a pair (tree_rows_pair): its status, whether the
-// table took the specialised path, and the *Err bits of the fields that wave decoded.
+// The root table's outcome on one wave of a wave group (tree_rows_pair): its status, whether
+// the table took the specialised path, and the *Err bits of the fields that wave decoded.
 struct RowOut {
     uint64_t errs;
     uint32_t st, fast;
 };
 
-// tree_rows for a wave pair (a 128-thread block): both waves take the same 64 rows, staged ONCE
-// in the block's slab (each wave issues half the LDS-DMA chunks), and each decodes its share of
-// the group's fields (jit.cpp gen_pair_rows); wave 1 then hands its RowOut to wave 0 through LDS
-// (xch, 64 entries) and fin(row, panic, ro0, ro1) stores the root table's status and *Err mask.
-// Two waves per 64 rows at the same LDS per row: a SIMD holds two waves, so one's LDS round
-// trips overlap the other's decode.  Rows whose span exceeds the slab parse from HBM (the lane
-// windows of tree_rows are not used here).
-template <class LdsBody, class GlobBody, class Fin>
+// tree_rows for a group of P waves (a 64 P-thread block): every wave takes the same 64 rows,
+// staged ONCE in the block's slab (the waves issue the LDS-DMA chunks round-robin), and decodes
+// its share of the group's fields (jit.cpp gen_pair_rows); waves 1..P-1 then hand their RowOut
+// to wave 0 through LDS (xch, 64 entries each) and fin(row, panic, ro0, ro_rest) stores the root
+// table's status and *Err mask (ro_rest: the others' bits ORed, ST_PANIC if any panicked).
+// P waves per 64 rows at the same LDS per row: a SIMD holds P waves, so one's LDS round trips
+// overlap the others' decode.  Rows whose span exceeds the slab parse from HBM (the lane windows
+// of tree_rows are not used here).
+template <int P, class LdsBody, class GlobBody, class Fin>
 __device__ __forceinline__ void tree_rows_pair(const TreeBufs &B, uint32_t x, uint64_t rows, uint32_t slab_bytes,
                                                uint4 *xch, LdsBody lds_body, GlobBody glob_body, Fin fin) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -181,14 +182,14 @@ __device__ __forceinline__ void tree_rows_pair(const TreeBufs &B, uint32_t x, ui
         const bool span = slab_bytes && slo < shi && se - sb + 16 <= (long long)slab_bytes;
         if (span) {
             const uint32_t chunks = (uint32_t)((se - sb + 1023) >> 10);
-            for (uint32_t c = (uint32_t)wave; c < chunks; c += 2)
+            for (uint32_t c = (uint32_t)wave; c < chunks; c += P)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(slab + c * 1024),
                                                          16, (uint32_t)sb + c * 1024 + lane * 16, 0, 0, 0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             // the straddling chunk is refilled by the wave that loaded it (after its own DMA landed)
             const uint64_t tail = B.stream_len & ~15ull;
             if (tail < B.stream_len && (long long)tail >= sb && (long long)tail < sb + (long long)chunks * 1024 &&
-                (int)(((tail - sb) >> 10) & 1) == wave && lane < 16 && tail + lane < B.stream_len)
+                (int)(((tail - sb) >> 10) % P) == wave && lane < 16 && tail + lane < B.stream_len)
                 slab[tail - sb + lane] = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)(tail + lane), 0, 0);
         }
         __syncthreads(); // the slab is whole; the previous rows' exchange has been read
@@ -199,11 +200,17 @@ __device__ __forceinline__ void tree_rows_pair(const TreeBufs &B, uint32_t x, ui
             else
                 glob_body(gs, row, lo, hi, ro);
         }
-        if (wave == 1) xch[lane] = make_uint4((uint32_t)ro.errs, (uint32_t)(ro.errs >> 32), ro.st, ro.fast);
-        __syncthreads(); // wave 1's outcome is in xch; both waves are done with the slab
+        if (wave) xch[(wave - 1) * 64 + lane] = make_uint4((uint32_t)ro.errs, (uint32_t)(ro.errs >> 32), ro.st, ro.fast);
+        __syncthreads(); // the others' outcomes are in xch; every wave is done with the slab
         if (wave == 0 && valid) {
-            const uint4 q = xch[lane];
-            fin(row, panic, ro, RowOut{(uint64_t)q.x | ((uint64_t)q.y << 32), q.z, q.w});
+            RowOut r = {0, 0, 0};
+#pragma unroll
+            for (int w = 1; w < P; w++) {
+                const uint4 q = xch[(w - 1) * 64 + lane];
+                r.errs |= (uint64_t)q.x | ((uint64_t)q.y << 32);
+                r.st = q.z == ST_PANIC ? (uint32_t)ST_PANIC : r.st;
+            }
+            fin(row, panic, ro, r);
         }
     }
 }
@@ -326,6 +333,13 @@ __device__ __noinline__ uint32_t tree_message_row(const Src &s, const TreeDesc &
 // The schema-specialised rows' fallback for a table the fast path rejects: out of line when the
 // row is parsed from LDS (the kernel's register budget is set by its staging code anyway), inline
 // when it is parsed from HBM (a call's register saves would set the no-staging kernel's budget).
+// the run-time path of a wave-group kernel (gen_pair_rows): out of line from either source, one
+// instance per group size Tag, so the kernel's register budget (amdgpu_waves_per_eu) reaches it
+template <int Tag, class Src>
+__device__ __noinline__ uint32_t tree_message_fallback_p(const Src &s, const TreeDesc &D, const TreeBufs &B, uint32_t t,
+                                                         uint64_t row, long long lo, long long hi, uint2 *gr) {
+    return tree_message_row_inl(s, D, B, t, row, lo, hi, gr);
+}
 __device__ __forceinline__ uint32_t tree_message_fallback(const TreeLds &s, const TreeDesc &D, const TreeBufs &B,
                                                           uint32_t t, uint64_t row, long long lo, long long hi,
                                                           uint2 *gr) {
