@@ -15,6 +15,12 @@
 
 namespace spec {
 
+// Build-time measurement switch (make HIPFLAGS+="-DSPEC_AB_TREE_ENC_SPLIT=1"): the encoder's
+// level-fused size / write launches split into one launch per table.
+#ifndef SPEC_AB_TREE_ENC_SPLIT
+#define SPEC_AB_TREE_ENC_SPLIT 0
+#endif
+
 unsigned row_grid(uint64_t rows) {
     const uint64_t b = (rows + TB - 1) / TB;
     const uint64_t cap = (uint64_t)device_cus() * 16;
@@ -680,6 +686,21 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
                 most = std::max(most, rows[x]);
             }
         if (!ts.n) return true;
+#if SPEC_AB_TREE_ENC_SPLIT
+        // (measurement build: one launch per table, so a kernel trace times each table)
+        for (uint32_t j = 0; j < ts.n; j++) {
+            TableSet one;
+            one.n = 1;
+            one.t[0] = ts.t[j];
+            void *a1[] = {(void *)&Dd, (void *)&Bd, &one};
+            const hipError_t l1 = hipModuleLaunchKernel(fn, row_grid(rows[ts.t[j]]), 1, 1, TB, 1, 1, 0, st, a1, nullptr);
+            if (l1 != hipSuccess) {
+                note_hip_error(l1);
+                return false;
+            }
+        }
+        return true;
+#endif
         void *args[] = {(void *)&Dd, (void *)&Bd, &ts};
         const hipError_t le = hipModuleLaunchKernel(fn, row_grid(most), ts.n, 1, TB, 1, 1, 0, st, args, nullptr);
         if (le != hipSuccess) note_hip_error(le);
