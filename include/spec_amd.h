@@ -153,8 +153,9 @@ typedef struct spec_nested_schema {
  *     MESSAGE, LIST   PRESENT uint8 m.HasField(tag)                 (msg.go:101-106)
  *   a list of scalars: VALUE = ValueList.Get(i) (list_value.go:87-92); a list of structs: a
  *   VALUE per scalar member (pre-order);
- *   ERRMASK uint64 (MESSAGE-shaped tables: records, sub-messages, message-list items): bit k
- *   set when the k-th direct field's (write order, k < 64) *Err getter errs — scalars
+ *   ERRMASK uint64 x W (MESSAGE-shaped tables: records, sub-messages, message-list items; W =
+ *   ceil(direct fields / 64), at least 1: the column is 8 W bytes wide): bit k % 64 of word k / 64
+ *   set when the k-th direct field's (write order) *Err getter errs — scalars
  *   <Kind>Err (msg.go:233-459), ANY OpenValueErr (value.go:35-46), MESSAGE MessageErr, LIST
  *   ListErr (msg.go:453-463), STRUCT DecodeXxx (generator/struct.go:60-64); an absent field never
  *   errs;
@@ -165,10 +166,10 @@ typedef struct spec_nested_schema {
  * Encode input uses the same columns (STATUS, ERRMASK, TYPE ignored): scalars and structs are always written,
  * MESSAGE / LIST fields when PRESENT is non-zero (a present list may be empty), ANY when its span
  * is non-empty (FieldWriter.Any copies the bytes: internal/writer/writer.go:438-456). */
-#define SPEC_TREE_MAX_FIELDS 256
+#define SPEC_TREE_MAX_FIELDS 1024
 #define SPEC_TREE_MAX_TABLES 64
-#define SPEC_TREE_MAX_COLUMNS 512
-#define SPEC_TREE_MAX_DIRECT 64 /* direct fields of one message / members of one struct */
+#define SPEC_TREE_MAX_COLUMNS 2048
+#define SPEC_TREE_MAX_DIRECT 1024 /* direct fields of one message / members of one struct (any, up to the tree's fields) */
 #define SPEC_TREE_MAX_STRUCT_DEPTH 8 /* structs nested in structs (the outermost counts 1) */
 
 typedef struct spec_tree_field {

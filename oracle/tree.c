@@ -32,9 +32,9 @@ enum { REL_ROOT = 0, REL_ONE = 1, REL_MANY = 2 };
 enum { SHAPE_MESSAGE = 0, SHAPE_VALUE = 1, SHAPE_STRUCT = 2 };
 enum { ROLE_VALUE = 0, ROLE_PRESENT = 1, ROLE_BEGIN = 2, ROLE_STATUS = 3, ROLE_ERRMASK = 4, ROLE_TYPE = 5 };
 enum { ST_OK = 0, ST_PANIC = 6, ST_INVALID_VALUE = 7 };
-#define MAX_F 256
+#define MAX_F 1024
 #define MAX_T 64
-#define MAX_C 512
+#define MAX_C 2048
 
 static int scalar(int k) { return k >= SO_KIND_BOOL && k <= SO_KIND_BYTES; }
 
@@ -160,7 +160,11 @@ static int build(tree *t, const so_tree_field *f, int nf) {
             }
         }
         t->err_col[x] = -1;
-        if (tb->shape == SHAPE_MESSAGE && (t->err_col[x] = add_col(t, x, d, ROLE_ERRMASK, 0, 8)) < 0) return -1;
+        if (tb->shape == SHAPE_MESSAGE) { /* a bit per direct field: ceil(direct / 64) words, at least 1 */
+            int nd = 0;
+            for (int i = d + 1; i < t->nf; i++) nd += t->f[i].parent == d;
+            if ((t->err_col[x] = add_col(t, x, d, ROLE_ERRMASK, 0, 8 * (nd > 64 ? (nd + 63) / 64 : 1))) < 0) return -1;
+        }
         if ((t->status_col[x] = add_col(t, x, d, ROLE_STATUS, 0, 1)) < 0) return -1;
         tb->ncolumns = (uint16_t)(t->nc - tb->first_column);
     }
@@ -348,7 +352,7 @@ static void decode_message(tree *t, int x, uint64_t row, const uint8_t *b, size_
     so_err e = so_open_message_err(b, len, &m);
     if (e) memset(&m, 0, sizeof(m));
     uint8_t st = classify(e);
-    uint64_t errs = 0;
+    uint64_t errs[MAX_F / 64] = {0};
     int kth = 0;
     const int d = t->T[x].field;
     for (int i = d + 1; i < t->nf; i++) {
@@ -416,9 +420,9 @@ static void decode_message(tree *t, int x, uint64_t row, const uint8_t *b, size_
                 decode_element(t, y, er, p, plen);
             }
         }
-        if (bad && bit < 64) errs |= 1ull << bit;
+        if (bad) errs[bit >> 6] |= 1ull << (bit & 63);
     }
-    put(t, t->err_col[x], row, &errs, 8);
+    put(t, t->err_col[x], row, errs, t->C[t->err_col[x]].width);
     put_u8(t, t->status_col[x], row, st);
 }
 

@@ -30,9 +30,9 @@ class SpecNestedSchema(C.Structure):
     _fields_ = [("outer", SpecSchema), ("item", SpecSchema)]
 
 
-SPEC_TREE_MAX_FIELDS = 256
+SPEC_TREE_MAX_FIELDS = 1024
 SPEC_TREE_MAX_TABLES = 64
-SPEC_TREE_MAX_COLUMNS = 512
+SPEC_TREE_MAX_COLUMNS = 2048
 
 
 class SpecTreeField(C.Structure):

@@ -253,6 +253,19 @@ std::vector<char> compile_uncached(const std::string &src, Prog p, const char *c
                               kEncodeNestedCoreHpp, kTreeCoreHpp, kTreeDecodeCoreHpp};
     const char *hdr_name[7] = {"spec_device.hpp", "decode_core.hpp", "encode_core.hpp", "decode_nested_core.hpp",
                                "encode_nested_core.hpp", "tree_core.hpp", "tree_decode_core.hpp"};
+    // SPEC_AMD_JIT_DUMP=prefix: the source is written before the compile (a slow compile can be
+    // inspected while it runs), the code object after it
+    if (const char *d = getenv("SPEC_AMD_JIT_DUMP")) {
+        const std::string base = std::string(d) + (p == ENCODE       ? "encode"
+                                                   : p == TREE       ? "tree"
+                                                   : p == NESTED     ? "nested"
+                                                   : p == NESTED_ENC ? "nested_encode"
+                                                                     : "decode");
+        if (FILE *f = fopen((base + ".hip").c_str(), "w")) {
+            fwrite(src.data(), 1, src.size(), f);
+            fclose(f);
+        }
+    }
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), prog_name(p), 7, hdr_src, hdr_name) != HIPRTC_SUCCESS) return {};
     // the product kernels are compiled with fixed options only: no environment variable can
@@ -278,17 +291,12 @@ std::vector<char> compile_uncached(const std::string &src, Prog p, const char *c
     std::vector<char> code(cs);
     hiprtcGetCode(prog, code.data());
     hiprtcDestroyProgram(&prog);
-    // SPEC_AMD_JIT_DUMP=prefix: write the source and code object (ISA inspection)
-    if (const char *d = getenv("SPEC_AMD_JIT_DUMP")) {
+    if (const char *d = getenv("SPEC_AMD_JIT_DUMP")) { // the code object (ISA inspection)
         std::string base = std::string(d) + (p == ENCODE       ? "encode"
                                              : p == TREE       ? "tree"
                                              : p == NESTED     ? "nested"
                                              : p == NESTED_ENC ? "nested_encode"
                                                                : "decode");
-        if (FILE *f = fopen((base + ".hip").c_str(), "w")) {
-            fwrite(src.data(), 1, src.size(), f);
-            fclose(f);
-        }
         if (FILE *f = fopen((base + ".co").c_str(), "wb")) {
             fwrite(code.data(), 1, code.size(), f);
             fclose(f);
@@ -708,30 +716,44 @@ void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, con
 // list elements are children written by their tables' later launches into the gaps skipped here.
 void gen_write_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
     const TTable &T = D.t[t];
-    o << "template <class E>\n__device__ __forceinline__ void gen_wrow_" << t
+    // a table of more than 64 direct fields loads each value where it is written (all of them in
+    // flight at once would hold ~4 registers per field), and its writer is a function of its own:
+    // inlined into the level-fused kernel, hiprtc spent minutes allocating registers over it
+    const bool eager = T.nd <= 64;
+    o << "template <class E>\n__device__ " << (eager ? "__forceinline__" : "__noinline__") << " void gen_wrow_" << t
       << "(E &em, const TreeDesc &D, const TreeBufs &B, uint64_t row, uint64_t start) {\n";
+    auto load = [&](uint32_t k, const TField &F, const char *ind) {
+        o << ind << "uint64_t a" << k << "[4];\n" << ind << "load_value_k<" << (int)F.kind << ">(" << col_expr(F.col)
+          << ", row, a" << k << ");\n";
+    };
     for (uint32_t k = 0; k < T.nd; k++) {
         const TField &F = D.f[D.direct[T.d0 + k]];
-        if ((F.kind >= spec::K_BOOL && F.kind <= spec::K_BYTES) || F.kind == spec::K_ANY)
-            o << "  uint64_t a" << k << "[4];\n  load_value_k<" << (int)F.kind << ">(" << col_expr(F.col) << ", row, a" << k
-              << ");\n";
-        else if (F.kind == spec::K_MESSAGE || F.kind == spec::K_LIST)
+        if ((F.kind >= spec::K_BOOL && F.kind <= spec::K_BYTES) || F.kind == spec::K_ANY) {
+            if (eager) load(k, F, "  ");
+        } else if (F.kind == spec::K_MESSAGE || F.kind == spec::K_LIST)
             o << "  const uint32_t pr" << k << " = ((const uint8_t *)" << col_expr(F.present) << ")[row];\n";
         if (F.kind == spec::K_MESSAGE) o << "  const uint32_t sz" << k << " = B.size[" << F.table << "][row];\n";
     }
     o << "  uint32_t nf = 0;\n  bool bigtag = false;\n";
+    // field ends: registers (e<k>), or for a wide table an array the table loop reads at run time
+    if (!eager) o << "  uint32_t ends_[" << T.nd << "];\n";
+    auto ev = [&](uint32_t k) { return eager ? "e" + std::to_string(k) : "ends_[" + std::to_string(k) + "]"; };
     for (uint32_t k = 0; k < T.nd; k++) {
         const uint32_t fi = D.direct[T.d0 + k];
         const TField &F = D.f[fi];
-        const std::string mark = "    e" + std::to_string(k) + " = (uint32_t)(em.pos - start);\n    nf++;\n" +
+        const std::string mark = "    " + ev(k) + " = (uint32_t)(em.pos - start);\n    nf++;\n" +
                                  (F.tag > 255 ? "    bigtag = true;\n" : "");
-        o << "  uint32_t e" << k << " = 0xffffffffu; // field " << fi << " tag " << F.tag << "\n";
+        if (eager) o << "  uint32_t e" << k << " = 0xffffffffu; // field " << fi << " tag " << F.tag << "\n";
+        else o << "  ends_[" << k << "] = 0xffffffffu; // field " << fi << " tag " << F.tag << "\n";
         if (F.kind >= spec::K_BOOL && F.kind <= spec::K_BYTES) {
             const bool heap = F.kind == spec::K_STRING || F.kind == spec::K_BYTES;
-            o << "  {\n    emit_value_k<" << (int)F.kind << ">(em, a" << k << ", "
+            o << "  {\n";
+            if (!eager) load(k, F, "    ");
+            o << "    emit_value_k<" << (int)F.kind << ">(em, a" << k << ", "
               << (heap ? "B.heaps[" + std::to_string(F.col) + "], B.heap_lens[" + std::to_string(F.col) + "]" : "nullptr, 0")
               << ");\n" << mark << "  }\n";
         } else if (F.kind == spec::K_ANY) {
+            if (!eager) load(k, F, "  ");
             o << "  if ((uint32_t)(a" << k << "[0] >> 32)) {\n    emit_value_k<" << (int)F.kind << ">(em, a" << k
               << ", B.heaps[" << F.col << "], B.heap_lens[" << F.col << "]);\n" << mark << "  }\n";
         } else if (F.kind == spec::K_STRUCT) {
@@ -760,8 +782,20 @@ void gen_write_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
     }
     // IsBigMessage (internal/format/msg.go:43-61), the table (encode/msg.go:58-72), the trailer
     o << "  const uint64_t data = em.pos - start;\n"
-      << "  const bool big = bigtag || (nf > 0 && data > 65535);\n"
-      << "  if (!big) {\n";
+      << "  const bool big = bigtag || (nf > 0 && data > 65535);\n";
+    if (!eager) {
+        // the wide table's entries in a run-time loop over the Writer's order (tree.hip layout:
+        // sorted[], sslot[]): a third of the unrolled code
+        o << "  for (uint32_t j = 0; j < " << T.nd << "u; j++) {\n"
+          << "    const uint32_t e = ends_[D.sslot[" << T.d0 << "u + j]];\n"
+          << "    if (e == 0xffffffffu) continue;\n"
+          << "    const uint32_t tag = D.f[D.sorted[" << T.d0 << "u + j]].tag;\n"
+          << "    if (!big) em.put_n(tag | ((uint64_t)__builtin_bswap16((uint16_t)e) << 8), 3);\n"
+          << "    else { em.be(tag, 2); em.be(e, 4); }\n  }\n"
+          << "  em.rvarint(data);\n  em.rvarint((uint64_t)nf * (big ? 6 : 3));\n"
+          << "  em.put1(big ? T_BIG_MESSAGE : T_MESSAGE);\n  em.finish();\n}\n";
+    } else {
+    o << "  if (!big) {\n";
     for (uint32_t j = 0; j < T.nd; j++) {
         const uint32_t fi = D.sorted[T.d0 + j], slot = D.sslot[T.d0 + j];
         if (D.f[fi].tag > 255) continue; // a present one makes the table big
@@ -776,6 +810,7 @@ void gen_write_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
     o << "  }\n"
       << "  em.rvarint(data);\n  em.rvarint((uint64_t)nf * (big ? 6 : 3));\n"
       << "  em.put1(big ? T_BIG_MESSAGE : T_MESSAGE);\n  em.finish();\n}\n";
+    }
     // a row no owner placed (its own owner absent or unplaced): its children are not written either
     o << "__device__ __forceinline__ void gen_unplace_" << t << "(const TreeDesc &D, const TreeBufs &B, uint64_t row) {\n";
     for (uint32_t k = 0; k < T.nd; k++) {

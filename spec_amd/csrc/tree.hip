@@ -451,12 +451,12 @@ bool build_layout(const spec_tree *tr, Layout &L) {
                 for (int q = (int)k; q > 0 && D.f[srt[q - 1]].tag >= D.f[srt[q]].tag; q--) std::swap(srt[q - 1], srt[q]);
             }
             for (uint32_t k = 0; k < T.nd; k++) D.f[srt[k]].rank = (uint16_t)k;
-            for (uint32_t k = 0; k < T.nd; k++)
-                for (uint32_t q = 0; q < T.nd; q++)
-                    if (D.direct[T.d0 + q] == srt[k]) D.sslot[T.d0 + k] = (uint16_t)q;
+            for (uint32_t q = 0; q < T.nd; q++) D.sslot[T.d0 + D.f[D.direct[T.d0 + q]].rank] = (uint16_t)q;
         }
         T.err_col = -1;
-        if (t.shape == SPEC_SHAPE_MESSAGE && (T.err_col = (int16_t)add_col(L, x, d, SPEC_COL_ERRMASK, 0, 8)) < 0)
+        // ERRMASK: a bit per direct field, ceil(nd / 64) words (at least one)
+        if (t.shape == SPEC_SHAPE_MESSAGE &&
+            (T.err_col = (int16_t)add_col(L, x, d, SPEC_COL_ERRMASK, 0, 8 * std::max<uint32_t>(1, (T.nd + 63) / 64))) < 0)
             return false;
         if ((T.status_col = (int16_t)add_col(L, x, d, SPEC_COL_STATUS, 0, 1)) < 0) return false;
         t.ncolumns = (uint16_t)(L.nc - t.first_column);
@@ -737,15 +737,27 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
         }
     }
     for (int d = 0; sets && ok && out && d <= maxd; d++) ok = launch_set(jit[4 * TREE_MAX_T + 1], depth, d);
-    for (uint32_t x = 0; !sets && ok && out && x < L.nt; x++)
+    bool too_wide = false;
+    for (uint32_t x = 0; !sets && ok && out && !too_wide && x < L.nt; x++)
         if (rows[x]) {
             const TTable &T = L.desc.t[x];
-            const size_t lds = T.shape == SHAPE_MESSAGE ? (size_t)(TB / 64) * T.nd * 64 * sizeof(uint32_t) : 0;
-            hipLaunchKernelGGL(tree_write_kernel, dim3(row_grid(rows[x])), dim3(TB), lds, st, Dd, Bd, x, rows[x]);
+            // a message's field ends live in LDS ([wave][field][lane], 256 B per field per wave):
+            // fewer waves per block for a wide table (160 KiB per block at most); a table of more
+            // than 640 direct fields needs the generated writer (jit.cpp)
+            const size_t per_wave = T.shape == SHAPE_MESSAGE ? (size_t)T.nd * 64 * sizeof(uint32_t) : 0;
+            const unsigned wpb = per_wave ? (unsigned)std::min<size_t>(TB / 64, 163840 / per_wave) : TB / 64;
+            if (wpb == 0) {
+                too_wide = true;
+                break;
+            }
+            const uint64_t blocks = std::min<uint64_t>((rows[x] + 64 * wpb - 1) / (64 * wpb), (uint64_t)row_grid(rows[x]) * (TB / 64) / wpb);
+            hipLaunchKernelGGL(tree_write_kernel, dim3((unsigned)std::max<uint64_t>(blocks, 1)), dim3(64 * wpb), wpb * per_wave, st,
+                               Dd, Bd, x, rows[x]);
         }
     const hipError_t e = hipGetLastError();
     delete B;
     delete Lp;
+    if (too_wide) return SPEC_E_TOO_LARGE;
     if (!ok || e != hipSuccess) {
         note_hip_error(e);
         return SPEC_E_HIP;

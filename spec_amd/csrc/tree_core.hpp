@@ -23,7 +23,7 @@
 namespace spec {
 
 constexpr int TB = 256; // threads per block of the row kernels
-constexpr int TREE_MAX_F = 256, TREE_MAX_T = 64, TREE_MAX_C = 512, TREE_MAX_D = 64;
+constexpr int TREE_MAX_F = 1024, TREE_MAX_T = 64, TREE_MAX_C = 2048, TREE_MAX_D = 1024;
 constexpr int TREE_MAX_SD = 8; // structs nested in structs (include/spec_amd.h SPEC_TREE_MAX_STRUCT_DEPTH)
 enum : uint32_t { K_STRUCT = 17, K_MESSAGE = 18, K_ANY = 19 };
 enum : uint32_t { REL_ROOT = 0, REL_ONE = 1, REL_MANY = 2 };

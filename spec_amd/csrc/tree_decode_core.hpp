@@ -255,7 +255,10 @@ __device__ __forceinline__ uint32_t tree_message_row_inl(const Src &s, const Tre
     const RecInfo ri = rec_open(s, lo, hi); // empty (or panicked) range => empty message
     uint32_t st = ri.tr.st;
     const long long ds = ri.tr.dstart;
-    uint64_t *errp = T.err_col >= 0 ? (uint64_t *)B.cols[T.err_col] : nullptr;
+    // ERRMASK: W words per row (a bit per direct field), each stored once its 64 fields are done
+    // (the index pass runs with no columns: a null column stays null, not null + row * W)
+    uint64_t *const ecol = T.err_col >= 0 ? (uint64_t *)B.cols[T.err_col] : nullptr;
+    uint64_t *errp = ecol ? ecol + row * ((uint32_t)D.width[T.err_col] / 8) : nullptr;
     uint64_t errs = 0;
     for (uint32_t k = 0; k < T.nd; k++) {
         const uint32_t fi = D.direct[T.d0 + k];
@@ -318,9 +321,13 @@ __device__ __forceinline__ uint32_t tree_message_row_inl(const Src &s, const Tre
         default:
             bad = !tree_scalar(s, F.kind, ds, end, B.cols[F.col], row, errp != nullptr);
         }
-        if (bad && k < 64) errs |= 1ull << k;
+        if (bad) errs |= 1ull << (k & 63);
+        if ((k & 63) == 63 && k + 1 < T.nd) {
+            if (errp) errp[k >> 6] = errs;
+            errs = 0;
+        }
     }
-    if (errp) errp[row] = errs;
+    if (errp) errp[T.nd ? (T.nd - 1) >> 6 : 0] = errs;
     return st;
 }
 

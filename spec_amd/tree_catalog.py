@@ -44,6 +44,21 @@ def nested_struct_tree() -> Tree:
     return Tree(root)
 
 
+def wide_tree() -> Tree:
+    """Messages and a struct with more than 64 direct fields (the reference's tables take any
+    number of u16 tags: internal/format/msg.go:13-61): a record of 130 direct fields (scalars of
+    every kind, tags past 255 making its table big, a 70-member struct, an 80-field sub-message,
+    a list of them, any) — multi-word ERRMASK columns, the run-time decode group, generated
+    writers over 100+ fields."""
+    scalars = [Kind.BOOL, Kind.BYTE, Kind.INT16, Kind.INT32, Kind.INT64, Kind.UINT16, Kind.UINT32, Kind.UINT64,
+               Kind.FLOAT32, Kind.FLOAT64, Kind.BIN64, Kind.BIN128, Kind.STRING, Kind.BYTES]
+    wide = Message("Wide", [(f"w{i}", i + 1, scalars[(3 * i) % len(scalars)]) for i in range(80)])
+    big_s = Struct("BigStruct", [(f"m{i}", scalars[(5 * i + 2) % len(scalars)]) for i in range(70)])
+    fields = [(f"f{i}", (i + 1) if i % 40 != 39 else 300 + i, scalars[i % len(scalars)]) for i in range(126)]
+    fields += [("st", 200, big_s), ("sub", 201, wide), ("subs", 202, ListOf(wide)), ("any", 203, Kind.ANY)]
+    return Tree(Message("WideRoot", fields))
+
+
 # the trees spec_amd.specfile derives from the reference's own .spec files (pkg1.spec,
 # proto/pmpx/mpx.spec, proto/prpc/rpc.spec), as flattened descriptors (path, tag, kind, elem,
 # parent) — package data written by tests/golden/make_spec_trees.py with the test fixture
@@ -60,7 +75,7 @@ def reference_trees() -> dict:
 def precompiled_trees() -> list:
     """Every tree the GPU tests and the bench decode and encode: build() compiles their
     schema-specialised kernels into the code-object cache that travels with the library."""
-    trees = [pkg1_tree(k) for k in (1, 2, 3)] + [shapes_tree(), nested_struct_tree()]
+    trees = [pkg1_tree(k) for k in (1, 2, 3)] + [shapes_tree(), nested_struct_tree(), wide_tree()]
     trees += list(reference_trees().values())
     base = pkg1_tree()
     for shift in (1, 4, 9):  # test_errmask_cross_kind's readers

@@ -12,6 +12,7 @@ import torch
 import spec_amd
 from spec_amd import workload
 from tests.test_tree import _test_object_columns
+from spec_amd.tree_catalog import wide_tree
 from tests.tree_helpers import (mismatches, nested_struct_tree, oracle_decode, oracle_encode, roundtrip_mismatches,
                                 shapes_tree)
 
@@ -143,6 +144,34 @@ def test_nested_structs_fuzzed(dev, seed):
     got_rows, got = gpu_decode(tree, s, e, dev)
     assert got_rows == want_rows
     assert mismatches(tree, got, want) == []
+
+
+@pytest.mark.parametrize("n", [1, 300, 5000])
+def test_wide_encode_decode(dev, n):
+    """More than 64 direct fields (internal/format/msg.go:13-61 takes any number of u16 tags):
+    a 130-field record with a big table, a 70-member struct, an 80-field sub-message and list
+    item — encode bit-exact (generated writers), decode identical to the oracle (the run-time
+    group kernel: multi-word ERRMASK)."""
+    tree = wide_tree()
+    cols, heaps, rows = workload.tree_batch(tree, n, 500 + n, count=(0, 3))
+    check_encode_decode(tree, cols, heaps, rows, dev, n)
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_wide_fuzzed(dev, seed):
+    """Mutated and truncated 130-field records: the *Err bits of fields past 64 (ERRMASK words
+    1 and 2) identical to the oracle's."""
+    tree = wide_tree()
+    n = 1500
+    cols, heaps, rows = workload.tree_batch(tree, n, 600 + seed, count=(0, 3))
+    stream, ends = oracle_encode(tree, cols, heaps, n)
+    s, e = _fuzz(stream, ends, 60 + seed, n)
+    want_rows, want = oracle_decode(tree, s, e)
+    got_rows, got = gpu_decode(tree, s, e, dev)
+    assert got_rows == want_rows
+    assert mismatches(tree, got, want) == []
+    em = {c.name: w for c, w in zip(tree.columns, want)}["#errmask"].view(np.uint64)
+    assert em.shape[1] == 3 and em[:, 1:].any()  # errors reported past the first 64 fields
 
 
 def test_encoder_error_span_outside_heap(dev):

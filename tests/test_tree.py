@@ -13,6 +13,7 @@ import pytest
 import spec_amd
 from oracle import oracle as O
 from spec_amd import Kind, ListOf, Message, Struct, Tree, workload
+from spec_amd.tree_catalog import wide_tree
 from tests.tree_helpers import oracle_decode, oracle_encode, oracle_fields, roundtrip_mismatches, shapes_tree
 
 
@@ -327,6 +328,46 @@ def test_oracle_errmask_and_type():
     g = {c.name: v for c, v in zip(tree.columns, got)}
     assert int(g["#errmask"].view(np.uint64)[0, 0]) == 0b01001
     assert g["v#type"][0, 0] == 41 and g["#status"][0, 0] == 0
+
+
+def test_layout_matches_oracle_wide():
+    """More than 64 direct fields (a message of 130, a struct of 70 members, an 80-field
+    sub-message and list item): the same layout, ERRMASK ceil(direct / 64) words wide."""
+    tree = wide_tree()
+    _layout_equal(tree)
+    assert [(c.name, c.width) for c in tree.columns if c.role == spec_amd.tree.ROLE_ERRMASK] == [
+        ("#errmask", 24), ("sub#errmask", 16), ("subs[]#errmask", 16)]
+
+
+@pytest.mark.parametrize("seed,n", [(1, 60), (2, 1)])
+def test_oracle_roundtrip_wide(seed, n):
+    tree = wide_tree()
+    cols, heaps, rows = workload.tree_batch(tree, n, seed)
+    stream, ends = oracle_encode(tree, cols, heaps, n)
+    st, _ = O.parse_batch(stream, ends)
+    assert not st.any()
+    got_rows, got = oracle_decode(tree, stream, ends)
+    assert got_rows == rows
+    assert roundtrip_mismatches(tree, cols, heaps, got, stream) == []
+
+
+def test_oracle_errmask_words():
+    """ERRMASK past 64 direct fields: the k-th field's *Err bit is bit k % 64 of word k / 64 —
+    fields 0 and 66 of a 70-field message hold strings where int32s are read."""
+    wr = O.Writer()
+    wr.message()
+    for i in range(70):
+        if i in (0, 66):
+            wr.field(i + 1, "string", "x")
+        else:
+            wr.field(i + 1, "int32", i)
+    b, err = wr.end()
+    assert err is None
+    tree = Tree(Message("M", [(f"f{i}", i + 1, Kind.INT32) for i in range(70)]))
+    rows, got = oracle_decode(tree, np.frombuffer(b, np.uint8), np.array([len(b)], np.uint64))
+    g = {c.name: v for c, v in zip(tree.columns, got)}
+    assert g["#errmask"].view(np.uint64)[0].tolist() == [1, 1 << 2]
+    assert int(g["f65"].view(np.int32)[0, 0]) == 65
 
 
 def test_oracle_spans_equal_records():
