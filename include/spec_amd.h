@@ -167,10 +167,10 @@ typedef struct spec_nested_schema {
  * MESSAGE / LIST fields when PRESENT is non-zero (a present list may be empty), ANY when its span
  * is non-empty (FieldWriter.Any copies the bytes: internal/writer/writer.go:438-456). */
 #define SPEC_TREE_MAX_FIELDS 1024
-#define SPEC_TREE_MAX_TABLES 64
+#define SPEC_TREE_MAX_TABLES 128
 #define SPEC_TREE_MAX_COLUMNS 2048
 #define SPEC_TREE_MAX_DIRECT 1024 /* direct fields of one message / members of one struct (any, up to the tree's fields) */
-#define SPEC_TREE_MAX_STRUCT_DEPTH 8 /* structs nested in structs (the outermost counts 1) */
+#define SPEC_TREE_MAX_STRUCT_DEPTH 16 /* structs nested in structs (the outermost counts 1) */
 
 typedef struct spec_tree_field {
     uint16_t tag;    /* field tag (ignored for struct members) */

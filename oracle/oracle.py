@@ -672,7 +672,7 @@ def tree_fields(fields) -> np.ndarray:
 
 def tree_layout(fields: np.ndarray):
     """so_tree_layout -> (tables, columns) structured arrays, or None for an invalid tree."""
-    t = np.zeros(64, TREE_TABLE)
+    t = np.zeros(128, TREE_TABLE)  # so_tree MAX_T
     c = np.zeros(2048, TREE_COLUMN)  # so_tree MAX_C
     nt, nc = C.c_int(0), C.c_int(0)
     rc = lib().so_tree_layout(_ptr(fields), len(fields), _ptr(t), C.byref(nt), _ptr(c), C.byref(nc))

@@ -33,7 +33,7 @@ enum { SHAPE_MESSAGE = 0, SHAPE_VALUE = 1, SHAPE_STRUCT = 2 };
 enum { ROLE_VALUE = 0, ROLE_PRESENT = 1, ROLE_BEGIN = 2, ROLE_STATUS = 3, ROLE_ERRMASK = 4, ROLE_TYPE = 5 };
 enum { ST_OK = 0, ST_PANIC = 6, ST_INVALID_VALUE = 7 };
 #define MAX_F 1024
-#define MAX_T 64
+#define MAX_T 128
 #define MAX_C 2048
 
 static int scalar(int k) { return k >= SO_KIND_BOOL && k <= SO_KIND_BYTES; }
@@ -105,12 +105,12 @@ static int build(tree *t, const so_tree_field *f, int nf) {
             if (pk != SO_KIND_STRUCT && pk != SO_KIND_MESSAGE && pk != SO_KIND_LIST) return -1;
         }
     }
-    /* struct nesting depth (at most 8 structs deep, spec_amd.h SPEC_TREE_MAX_STRUCT_DEPTH) */
+    /* struct nesting depth (at most 16 structs deep, spec_amd.h SPEC_TREE_MAX_STRUCT_DEPTH) */
     for (int i = 0; i < nf; i++) {
         int depth = f[i].kind == SO_KIND_STRUCT;
         for (int p = f[i].parent; p >= 0; p = f[p].parent)
             depth += f[p].kind == SO_KIND_STRUCT || (f[p].kind == SO_KIND_LIST && f[p].elem == SO_KIND_STRUCT);
-        if (depth > 8) return -1;
+        if (depth > 16) return -1;
     }
     /* tables: the root, then one per MESSAGE / LIST field in field order */
     so_tree_table root = {-1, -1, REL_ROOT, SHAPE_MESSAGE, 0, 0};

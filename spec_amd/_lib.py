@@ -31,7 +31,7 @@ class SpecNestedSchema(C.Structure):
 
 
 SPEC_TREE_MAX_FIELDS = 1024
-SPEC_TREE_MAX_TABLES = 64
+SPEC_TREE_MAX_TABLES = 128
 SPEC_TREE_MAX_COLUMNS = 2048
 
 

@@ -504,6 +504,9 @@ bool tree_table_ok(const TreeDesc &D, uint32_t t) {
 
 bool tree_group_ok(const TreeDesc &D, uint32_t x) {
     const TTable &T = D.t[x];
+    // a group of more than 24 tables (sub-messages decoded with their owner) runs the run-time
+    // kernel: its generated reader is inlined per source and wave variant
+    if (T.gn > 24) return false;
     for (uint32_t g = 0; g < T.gn; g++)
         if (!tree_table_ok(D, D.group[T.g0 + g])) return false;
     return true;
@@ -720,7 +723,10 @@ void gen_write_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
     // flight at once would hold ~4 registers per field), and its writer is a function of its own:
     // inlined into the level-fused kernel, hiprtc spent minutes allocating registers over it
     const bool eager = T.nd <= 64;
-    o << "template <class E>\n__device__ " << (eager ? "__forceinline__" : "__noinline__") << " void gen_wrow_" << t
+    // (and out of line in a tree of many tables too: 114 writers inlined into the one level-fused
+    // kernel took hiprtc 13 minutes)
+    const bool inl = eager && D.ntables <= 32;
+    o << "template <class E>\n__device__ " << (inl ? "__forceinline__" : "__noinline__") << " void gen_wrow_" << t
       << "(E &em, const TreeDesc &D, const TreeBufs &B, uint64_t row, uint64_t start) {\n";
     auto load = [&](uint32_t k, const TField &F, const char *ind) {
         o << ind << "uint64_t a" << k << "[4];\n" << ind << "load_value_k<" << (int)F.kind << ">(" << col_expr(F.col)

@@ -23,8 +23,8 @@
 namespace spec {
 
 constexpr int TB = 256; // threads per block of the row kernels
-constexpr int TREE_MAX_F = 1024, TREE_MAX_T = 64, TREE_MAX_C = 2048, TREE_MAX_D = 1024;
-constexpr int TREE_MAX_SD = 8; // structs nested in structs (include/spec_amd.h SPEC_TREE_MAX_STRUCT_DEPTH)
+constexpr int TREE_MAX_F = 1024, TREE_MAX_T = 128, TREE_MAX_C = 2048, TREE_MAX_D = 1024;
+constexpr int TREE_MAX_SD = 16; // structs nested in structs (include/spec_amd.h SPEC_TREE_MAX_STRUCT_DEPTH)
 enum : uint32_t { K_STRUCT = 17, K_MESSAGE = 18, K_ANY = 19 };
 enum : uint32_t { REL_ROOT = 0, REL_ONE = 1, REL_MANY = 2 };
 enum : uint32_t { SHAPE_MESSAGE = 0, SHAPE_VALUE = 1, SHAPE_STRUCT = 2 };

@@ -301,6 +301,12 @@ GroupShape group_shape(const Layout &L, uint32_t x, uint64_t stream_len, uint64_
     return g;
 }
 
+// Waves per block of a group kernel: TB / 64, fewer when the waves' LDS (slab + one 512-byte
+// range slot per sub-message table of the group: up to 127 of them) would pass a CU's 160 KiB.
+unsigned group_waves(uint32_t wave_bytes) {
+    return std::max<unsigned>(1, std::min<unsigned>(TB / 64, 163840u / std::max<uint32_t>(wave_bytes, 1)));
+}
+
 int grow(DevBuf &b, size_t bytes) { return b.reserve(std::max<size_t>(bytes, 256)); }
 
 // Buffers for the batch (n records) and the current list capacities; fills d->B.
@@ -443,8 +449,9 @@ int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, 
         if (fused.n >= 2) { // (one group: its own kernel below)
             for (uint32_t j = 0; j < fused.n; j++) in_set[fused.t[j]] = true;
             void *args[] = {(void *)&Dd, (void *)&Bd, &fused, &fused_wb};
-            const hipError_t le = hipModuleLaunchKernel(set_fn, fused_grid, fused.n, 1, TB, 1, 1,
-                                                        (unsigned)((TB / 64) * fused_wb), st, args, nullptr);
+            const unsigned fw = group_waves(fused_wb);
+            const hipError_t le = hipModuleLaunchKernel(set_fn, fused_grid, fused.n, 1, 64 * fw, 1, 1,
+                                                        (unsigned)(fw * fused_wb), st, args, nullptr);
             if (le != hipSuccess) {
                 note_hip_error(le);
                 return SPEC_E_HIP;
@@ -455,9 +462,10 @@ int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, 
             const uint64_t cap = x == 0 ? n : d->caps[x];
             if (cap == 0) continue;
             const GroupShape gs = group_shape(L, x, stream_len, cap);
-            const uint64_t per_block = (uint64_t)(TB / 64) * gs.rpw;
+            const unsigned wpb = group_waves(gs.wave_bytes);
+            const uint64_t per_block = (uint64_t)wpb * gs.rpw;
             const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>((cap + per_block - 1) / per_block, 1u << 20));
-            const size_t lds = (size_t)(TB / 64) * gs.wave_bytes;
+            const size_t lds = (size_t)wpb * gs.wave_bytes;
             const hipFunction_t pair_fn =
                 tree_pair() && d->jit && all_cols && gs.slab ? d->jit[2 * TREE_MAX_T + x] : nullptr;
             if (pair_fn) {
@@ -481,13 +489,13 @@ int run(spec_tree_decoder *d, const uint8_t *stream_bytes, uint64_t stream_len, 
                 const hipFunction_t fn = gs.slab == 0 && d->jit[TREE_MAX_T + x] ? d->jit[TREE_MAX_T + x] : d->jit[x];
                 const unsigned grid = gs.slab == 0 ? row_grid(cap) : (unsigned)blocks;
                 const hipError_t le =
-                    hipModuleLaunchKernel(fn, grid, 1, 1, TB, 1, 1, (unsigned)lds, st, args, nullptr);
+                    hipModuleLaunchKernel(fn, grid, 1, 1, 64 * wpb, 1, 1, (unsigned)lds, st, args, nullptr);
                 if (le != hipSuccess) {
                     note_hip_error(le);
                     return SPEC_E_HIP;
                 }
             } else {
-                hipLaunchKernelGGL(tree_group_kernel, dim3((unsigned)blocks), dim3(TB), lds, st, Dd, Bd, x, gs.slab,
+                hipLaunchKernelGGL(tree_group_kernel, dim3((unsigned)blocks), dim3(64 * wpb), lds, st, Dd, Bd, x, gs.slab,
                                    gs.wave_bytes, gs.rpw);
             }
         }

@@ -70,8 +70,9 @@ __device__ __forceinline__ void tree_rows(const TreeBufs &B, uint32_t x, uint64_
     uint8_t *slab = smem + wave * wave_bytes;
     const __amdgpu_buffer_rsrc_t rsrc = stream_rsrc(B);
     const GlobalSrc gs{B.stream, B.stream_len};
-    const uint64_t wstride = (uint64_t)gridDim.x * (TB / 64) * rpw;
-    for (uint64_t base = ((uint64_t)blockIdx.x * (TB / 64) + wave) * rpw; base < rows; base += wstride) {
+    const uint64_t wpb = blockDim.x >> 6; // (fewer than TB / 64 waves when the range slots are large)
+    const uint64_t wstride = (uint64_t)gridDim.x * wpb * rpw;
+    for (uint64_t base = ((uint64_t)blockIdx.x * wpb + wave) * rpw; base < rows; base += wstride) {
         const uint64_t row = base + lane;
         const bool valid = row < rows && (uint32_t)lane < rpw;
         long long lo = 0, hi = 0;
@@ -221,7 +222,7 @@ __device__ __forceinline__ void tree_rows_pair(const TreeBufs &B, uint32_t x, ui
 template <class GlobBody>
 __device__ __forceinline__ void tree_rows_global(const TreeBufs &B, uint32_t x, uint64_t rows, GlobBody glob_body) {
     const GlobalSrc gs{B.stream, B.stream_len};
-    for (uint64_t row = (uint64_t)blockIdx.x * TB + threadIdx.x; row < rows; row += (uint64_t)gridDim.x * TB) {
+    for (uint64_t row = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; row < rows; row += (uint64_t)gridDim.x * blockDim.x) {
         long long lo = 0, hi = 0;
         bool panic = false;
         row_range(B, x, row, lo, hi, panic);

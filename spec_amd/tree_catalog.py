@@ -59,6 +59,21 @@ def wide_tree() -> Tree:
     return Tree(Message("WideRoot", fields))
 
 
+def many_tables_tree() -> Tree:
+    """More than 64 tables and deep structs: a record with 100 sub-messages (one table each, all
+    in the records' decode group: 100 range slots, so fewer waves per workgroup), a list of
+    items holding 12 sub-messages each, and a struct chain 14 levels deep."""
+    subs = [Message(f"S{i}", [("k", 1, Kind.INT32), ("s", 2, Kind.STRING)]) for i in range(100)]
+    item_subs = [Message(f"T{i}", [("u", 1, Kind.UINT64), ("b", 2, Kind.BYTES)]) for i in range(12)]
+    item = Message("Item", [("id", 1, Kind.INT64)] + [(f"t{i}", i + 2, m) for i, m in enumerate(item_subs)])
+    deep = Struct("L0", [("v", Kind.INT32)])
+    for k in range(1, 14):
+        deep = Struct(f"L{k}", [("s", deep), ("v", Kind.INT16)])
+    fields = [(f"s{i}", i + 1, m) for i, m in enumerate(subs)]
+    fields += [("items", 101, ListOf(item)), ("deep", 102, deep), ("tail", 103, Kind.STRING)]
+    return Tree(Message("ManyTables", fields))
+
+
 # the trees spec_amd.specfile derives from the reference's own .spec files (pkg1.spec,
 # proto/pmpx/mpx.spec, proto/prpc/rpc.spec), as flattened descriptors (path, tag, kind, elem,
 # parent) — package data written by tests/golden/make_spec_trees.py with the test fixture
@@ -75,7 +90,7 @@ def reference_trees() -> dict:
 def precompiled_trees() -> list:
     """Every tree the GPU tests and the bench decode and encode: build() compiles their
     schema-specialised kernels into the code-object cache that travels with the library."""
-    trees = [pkg1_tree(k) for k in (1, 2, 3)] + [shapes_tree(), nested_struct_tree(), wide_tree()]
+    trees = [pkg1_tree(k) for k in (1, 2, 3)] + [shapes_tree(), nested_struct_tree(), wide_tree(), many_tables_tree()]
     trees += list(reference_trees().values())
     base = pkg1_tree()
     for shift in (1, 4, 9):  # test_errmask_cross_kind's readers

@@ -12,7 +12,7 @@ import torch
 import spec_amd
 from spec_amd import workload
 from tests.test_tree import _test_object_columns
-from spec_amd.tree_catalog import wide_tree
+from spec_amd.tree_catalog import many_tables_tree, wide_tree
 from tests.tree_helpers import (mismatches, nested_struct_tree, oracle_decode, oracle_encode, roundtrip_mismatches,
                                 shapes_tree)
 
@@ -172,6 +172,27 @@ def test_wide_fuzzed(dev, seed):
     assert mismatches(tree, got, want) == []
     em = {c.name: w for c, w in zip(tree.columns, want)}["#errmask"].view(np.uint64)
     assert em.shape[1] == 3 and em[:, 1:].any()  # errors reported past the first 64 fields
+
+
+@pytest.mark.parametrize("n", [1, 2000])
+def test_many_tables_encode_decode(dev, n):
+    """114 tables (100 sub-message range slots in the records' decode group: fewer waves per
+    workgroup) and a struct chain 14 deep: encode bit-exact, decode identical to the oracle."""
+    tree = many_tables_tree()
+    cols, heaps, rows = workload.tree_batch(tree, n, 700 + n, count=(0, 3))
+    check_encode_decode(tree, cols, heaps, rows, dev, n)
+
+
+def test_many_tables_fuzzed(dev):
+    tree = many_tables_tree()
+    n = 800
+    cols, heaps, rows = workload.tree_batch(tree, n, 707, count=(0, 3))
+    stream, ends = oracle_encode(tree, cols, heaps, n)
+    s, e = _fuzz(stream, ends, 71, n)
+    want_rows, want = oracle_decode(tree, s, e)
+    got_rows, got = gpu_decode(tree, s, e, dev)
+    assert got_rows == want_rows
+    assert mismatches(tree, got, want) == []
 
 
 def test_encoder_error_span_outside_heap(dev):

@@ -13,7 +13,7 @@ import pytest
 import spec_amd
 from oracle import oracle as O
 from spec_amd import Kind, ListOf, Message, Struct, Tree, workload
-from spec_amd.tree_catalog import wide_tree
+from spec_amd.tree_catalog import many_tables_tree, wide_tree
 from tests.tree_helpers import oracle_decode, oracle_encode, oracle_fields, roundtrip_mismatches, shapes_tree
 
 
@@ -275,20 +275,20 @@ def test_oracle_roundtrip_nested_structs(seed, n):
 
 
 def test_struct_depth_limit():
-    """At most 8 structs deep (SPEC_TREE_MAX_STRUCT_DEPTH); both the engine and the oracle
-    reject a 9th level."""
+    """At most 16 structs deep (SPEC_TREE_MAX_STRUCT_DEPTH); both the engine and the oracle
+    reject a 17th level."""
     def chain(levels):
         s = Struct("L0", [("v", Kind.INT32)])
         for k in range(1, levels):
             s = Struct(f"L{k}", [("s", s), ("v", Kind.INT32)])
         return Message("M", [("s", 1, s)])
 
-    t8 = Tree(chain(8))
-    _layout_equal(t8)
+    t16 = Tree(chain(16))
+    _layout_equal(t16)
     with pytest.raises(spec_amd.SpecError):
-        Tree(chain(9))
-    assert O.tree_layout(O.tree_fields([(1, Kind.STRUCT, 0, -1)] + [(0, Kind.STRUCT, 0, i) for i in range(8)]
-                                       + [(0, Kind.INT32, 0, 8)])) is None
+        Tree(chain(17))
+    assert O.tree_layout(O.tree_fields([(1, Kind.STRUCT, 0, -1)] + [(0, Kind.STRUCT, 0, i) for i in range(16)]
+                                       + [(0, Kind.INT32, 0, 16)])) is None
 
 
 def test_specfile_nested_struct():
@@ -346,6 +346,19 @@ def test_oracle_roundtrip_wide(seed, n):
     stream, ends = oracle_encode(tree, cols, heaps, n)
     st, _ = O.parse_batch(stream, ends)
     assert not st.any()
+    got_rows, got = oracle_decode(tree, stream, ends)
+    assert got_rows == rows
+    assert roundtrip_mismatches(tree, cols, heaps, got, stream) == []
+
+
+def test_layout_matches_oracle_many_tables():
+    """114 tables (100 sub-messages of the record, a list of items with 12 each) and a struct
+    chain 14 deep: the same layout as the oracle's, and an oracle round trip."""
+    tree = many_tables_tree()
+    assert len(tree.tables) == 114
+    _layout_equal(tree)
+    cols, heaps, rows = workload.tree_batch(tree, 40, 3, count=(0, 3))
+    stream, ends = oracle_encode(tree, cols, heaps, 40)
     got_rows, got = oracle_decode(tree, stream, ends)
     assert got_rows == rows
     assert roundtrip_mismatches(tree, cols, heaps, got, stream) == []
