@@ -37,9 +37,12 @@ extern "C" {
 /* Fields of a flat schema.  Schemas of up to 64 fields run the schema-specialised kernels; wider
  * ones decode in chunks of 64 fields (the generic kernel once per chunk, each getter against the
  * record's whole table) and encode through the wide kernels, whose field set the call writes into
- * the workspace.  A nested schema's outer and item halves hold at most 64 fields each. */
+ * the workspace.  A nested schema's halves hold up to 1024 fields each (together at most
+ * SPEC_TREE_MAX_FIELDS - 1 when a half holds more than 64: such a schema decodes in chunks of 64
+ * fields per half and encodes through the schema-tree encoder, with its scratch allocated
+ * stream-ordered by the call). */
 #define SPEC_MAX_FIELDS 1024
-#define SPEC_NESTED_MAX_FIELDS 64
+#define SPEC_NESTED_MAX_FIELDS 1024
 
 /* Column kinds: one per typed getter / FieldWriter method
  * (internal/types/msg.go:219-421, internal/writer/msg.go:99-211). */

@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(_HERE, "libspec_amd.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "spec_amd.h")
 
 SPEC_MAX_FIELDS = 1024  # include/spec_amd.h (schemas over 64 fields: chunked decode, wide encode)
-SPEC_NESTED_MAX_FIELDS = 64
+SPEC_NESTED_MAX_FIELDS = 1024  # (halves over 64 fields: chunked decode, tree-encoder encode)
 
 
 class SpecField(C.Structure):

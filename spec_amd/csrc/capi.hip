@@ -58,8 +58,10 @@ int check_schema(const spec_schema *s) {
 
 // outer schema of a nested decode: flat kinds plus exactly one SPEC_KIND_LIST; *list_f = its index
 int check_nested(const spec_nested_schema *s, uint32_t *list_f) {
-    if (!s || s->outer.nfields > SPEC_KFIELDS || check_schema(&s->item) || s->item.nfields > SPEC_KFIELDS)
-        return SPEC_E_INVALID_ARGUMENT; // the nested kernels take both field sets as kernel arguments
+    // (a half of more than SPEC_KFIELDS fields: decoded in field chunks, encoded through the tree
+    // encoder — nested_decode_chunks, nested_encode_wide)
+    if (!s || s->outer.nfields > SPEC_MAX_FIELDS || check_schema(&s->item))
+        return SPEC_E_INVALID_ARGUMENT;
     int lists = 0;
     for (uint32_t f = 0; f < s->outer.nfields; f++) {
         if (s->outer.fields[f].kind == SPEC_KIND_LIST) {
@@ -477,11 +479,38 @@ static int nested_args(spec::NestedArgs &a, const spec_nested_schema *schema, co
     a.stream_len = stream_len;
     a.ends = ends;
     a.n = n;
-    fill_field_set(a.outer, &schema->outer, nullptr, nullptr);
-    fill_field_set(a.item, &schema->item, nullptr, nullptr);
+    fill_field_set(a.outer, &schema->outer, nullptr, nullptr, 0, SPEC_KFIELDS);
+    fill_field_set(a.item, &schema->item, nullptr, nullptr, 0, SPEC_KFIELDS);
     a.list_tag = schema->outer.fields[list_f].tag;
-    a.list_rank = a.outer.rank[list_f];
+    uint16_t order[SPEC_MAX_FIELDS];
+    table_order(&schema->outer, order);
+    for (uint32_t j = 0; j < schema->outer.nfields; j++)
+        if (order[j] == list_f) a.list_rank = j; // the list field's index in the whole Writer table
     a.group_base = (uint64_t *)workspace;
+    return SPEC_OK;
+}
+
+// The nested decode pass over the columns: one launch, or for a schema with a half of more than
+// SPEC_KFIELDS fields one launch per chunk of SPEC_KFIELDS fields of each half (every chunk's
+// getters against the records' whole tables; chunk 0 writes both status columns, every chunk
+// the same item_begin)
+static int nested_decode_chunks(const spec_nested_schema *schema, spec::NestedArgs &a, void *const *outer_columns,
+                                uint8_t *status, void *const *item_columns, uint8_t *item_status, double avg,
+                                hipStream_t stream) {
+    const uint32_t no = schema->outer.nfields, ni = schema->item.nfields;
+    const uint32_t chunks = std::max<uint32_t>(1, std::max((no + SPEC_KFIELDS - 1) / SPEC_KFIELDS, (ni + SPEC_KFIELDS - 1) / SPEC_KFIELDS));
+    std::vector<void *> oc(no, nullptr);
+    for (uint32_t f = 0; f < no; f++)
+        if (schema->outer.fields[f].kind != SPEC_KIND_LIST) oc[f] = outer_columns[f];
+    for (uint32_t c = 0; c < chunks; c++) {
+        const uint32_t f0 = c * SPEC_KFIELDS;
+        if (f0 < no) fill_field_set(a.outer, &schema->outer, oc.data(), c ? nullptr : status, f0, f0 + SPEC_KFIELDS);
+        else fill_field_set(a.outer, &schema->outer, nullptr, nullptr, no, no);
+        if (f0 < ni && a.item_cap)
+            fill_field_set(a.item, &schema->item, item_columns, c ? nullptr : item_status, f0, f0 + SPEC_KFIELDS);
+        else fill_field_set(a.item, &schema->item, nullptr, c ? nullptr : (a.item_cap ? item_status : nullptr), ni, ni);
+        if (spec::launch_nested_decode(schema, a, avg, stream)) return hip_rc(hipGetLastError());
+    }
     return SPEC_OK;
 }
 
@@ -507,22 +536,14 @@ int spec_decode_nested(const spec_nested_schema *schema, const uint8_t *stream_b
     if (rc) return rc;
     if (n == 0) return SPEC_OK;
     if (!outer_columns || !item_begin || (item_cap && !item_columns)) return SPEC_E_INVALID_ARGUMENT;
-    for (uint32_t f = 0; f < schema->outer.nfields; f++) {
-        if (schema->outer.fields[f].kind == SPEC_KIND_LIST) continue;
-        if (!outer_columns[f]) return SPEC_E_INVALID_ARGUMENT;
-        a.outer.cols[f] = outer_columns[f];
-    }
-    for (uint32_t f = 0; f < schema->item.nfields && item_cap; f++) {
+    for (uint32_t f = 0; f < schema->outer.nfields; f++)
+        if (schema->outer.fields[f].kind != SPEC_KIND_LIST && !outer_columns[f]) return SPEC_E_INVALID_ARGUMENT;
+    for (uint32_t f = 0; f < schema->item.nfields && item_cap; f++)
         if (!item_columns[f]) return SPEC_E_INVALID_ARGUMENT;
-        a.item.cols[f] = item_columns[f];
-    }
-    a.outer.status = status;
-    a.item.status = item_cap ? item_status : nullptr;
     a.item_begin = item_begin;
     a.item_cap = item_cap;
     double avg = (double)stream_len / (double)n;
-    if (spec::launch_nested_decode(schema, a, avg, (hipStream_t)stream)) return hip_rc(hipGetLastError());
-    return SPEC_OK;
+    return nested_decode_chunks(schema, a, outer_columns, status, item_columns, item_status, avg, (hipStream_t)stream);
 }
 
 int spec_decode_nested_onepass(const spec_nested_schema *schema, const uint8_t *stream_bytes, uint64_t stream_len,
@@ -540,18 +561,28 @@ int spec_decode_nested_onepass(const spec_nested_schema *schema, const uint8_t *
         for (uint32_t f = 0; f < schema->outer.nfields; f++) {
             if (schema->outer.fields[f].kind == SPEC_KIND_LIST) continue;
             if (!outer_columns[f]) return SPEC_E_INVALID_ARGUMENT;
-            a.outer.cols[f] = outer_columns[f];
+            if (f < SPEC_KFIELDS) a.outer.cols[f] = outer_columns[f];
         }
         for (uint32_t f = 0; f < schema->item.nfields && item_cap; f++) {
             if (!item_columns[f]) return SPEC_E_INVALID_ARGUMENT;
-            a.item.cols[f] = item_columns[f];
+            if (f < SPEC_KFIELDS) a.item.cols[f] = item_columns[f];
         }
     }
-    a.outer.status = status;
-    a.item.status = item_cap ? item_status : nullptr;
     a.item_begin = item_begin;
     a.item_cap = item_cap;
     double avg = n ? (double)stream_len / (double)n : 0.0;
+    if (schema->outer.nfields > SPEC_KFIELDS || schema->item.nfields > SPEC_KFIELDS) {
+        // a wide schema: the index kernels, then the decode in field chunks
+        if (n == 0) {
+            if (hipMemsetAsync(total_items, 0, sizeof(uint64_t), (hipStream_t)stream) != hipSuccess)
+                return hip_rc(hipGetLastError());
+            return SPEC_OK;
+        }
+        if (spec::launch_nested_index(a, avg, (hipStream_t)stream)) return hip_rc(hipGetLastError());
+        return nested_decode_chunks(schema, a, outer_columns, status, item_columns, item_status, avg, (hipStream_t)stream);
+    }
+    a.outer.status = status;
+    a.item.status = item_cap ? item_status : nullptr;
     if (spec::launch_nested_onepass(schema, a, avg, (hipStream_t)stream)) return hip_rc(hipGetLastError());
     return SPEC_OK;
 }
@@ -590,6 +621,81 @@ static int heaps_of(spec::EncFields &e, const spec_schema *s, const uint8_t *con
     return SPEC_OK;
 }
 
+// A nested schema with a half of more than SPEC_KFIELDS fields, encoded by the schema-tree
+// encoder (spec_encode_tree): the records' message with the list field as a LIST of MESSAGE
+// items — the same Writer calls (writer_list_msg.go:8-47), so the same bytes.  The list is always
+// written (its PRESENT column all ones, from scratch), item_begin is the list table's BEGIN; the
+// tree encoder's workspace is stream-ordered scratch (hipMallocAsync / hipFreeAsync), so the
+// call stays asynchronous and the nested workspace contract is unchanged.
+static int nested_encode_wide(const spec_nested_schema *schema, uint32_t list_f, const void *const *outer_columns,
+                              const uint8_t *const *outer_heaps, const uint64_t *outer_heap_lens,
+                              const uint32_t *item_begin, const void *const *item_columns,
+                              const uint8_t *const *item_heaps, const uint64_t *item_heap_lens, uint64_t nitems,
+                              uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *ends, uint64_t *total,
+                              hipStream_t st) {
+    const uint32_t no = schema->outer.nfields, ni = schema->item.nfields;
+    if (no + ni > SPEC_TREE_MAX_FIELDS) return SPEC_E_INVALID_ARGUMENT;
+    std::vector<spec_tree> tv(1);
+    spec_tree &T = tv[0];
+    memset(&T, 0, sizeof(T));
+    std::vector<int> half(no + ni), idx(no + ni); // tree field -> (0 outer / 1 item, schema index)
+    uint32_t k = 0;
+    int list_tf = -1;
+    for (uint32_t f = 0; f < no; f++) {
+        const spec_field &F = schema->outer.fields[f];
+        T.fields[k].tag = F.tag;
+        T.fields[k].parent = -1;
+        half[k] = 0;
+        idx[k] = (int)f;
+        if (f == list_f) {
+            T.fields[k].kind = SPEC_KIND_LIST;
+            T.fields[k].elem = SPEC_KIND_MESSAGE;
+            list_tf = (int)k++;
+            for (uint32_t g = 0; g < ni; g++, k++) { // the items' fields, pre-order under the list
+                T.fields[k].tag = schema->item.fields[g].tag;
+                T.fields[k].kind = schema->item.fields[g].kind;
+                T.fields[k].parent = (int16_t)list_tf;
+                half[k] = 1;
+                idx[k] = (int)g;
+            }
+        } else {
+            T.fields[k++].kind = F.kind;
+        }
+    }
+    T.nfields = k;
+    std::vector<spec_tree_table> tables(SPEC_TREE_MAX_TABLES);
+    std::vector<spec_tree_column> cols(SPEC_TREE_MAX_COLUMNS);
+    uint32_t nt = 0, nc = 0;
+    if (spec_tree_layout(&T, tables.data(), &nt, cols.data(), &nc) || nt != 2) return SPEC_E_INVALID_ARGUMENT;
+    const uint64_t rows[2] = {n, nitems};
+    const size_t tws = (spec_encode_tree_workspace_size(&T, rows) + 255) & ~(size_t)255;
+    uint8_t *scratch = nullptr;
+    if (hipMallocAsync((void **)&scratch, tws + std::max<uint64_t>(n, 1), st) != hipSuccess) return hip_rc(hipGetLastError());
+    uint8_t *present = scratch + tws;
+    std::vector<const void *> tc(nc, nullptr);
+    std::vector<const uint8_t *> th(nc, nullptr);
+    std::vector<uint64_t> tl(nc, 0);
+    for (uint32_t c = 0; c < nc; c++) {
+        const spec_tree_column &C = cols[c];
+        if (C.role == SPEC_COL_PRESENT) {
+            tc[c] = present;
+        } else if (C.role == SPEC_COL_BEGIN) {
+            tc[c] = item_begin;
+        } else if (C.role == SPEC_COL_VALUE) {
+            const int f = idx[C.field];
+            tc[c] = half[C.field] ? (item_columns ? item_columns[f] : nullptr) : outer_columns[f];
+            th[c] = half[C.field] ? (item_heaps ? item_heaps[f] : nullptr) : (outer_heaps ? outer_heaps[f] : nullptr);
+            tl[c] = half[C.field] ? (item_heap_lens ? item_heap_lens[f] : 0) : (outer_heap_lens ? outer_heap_lens[f] : 0);
+        }
+    }
+    int rc = SPEC_OK;
+    if (hipMemsetAsync(present, 1, std::max<uint64_t>(n, 1), st) != hipSuccess) rc = hip_rc(hipGetLastError());
+    if (!rc)
+        rc = spec_encode_tree(&T, tc.data(), th.data(), tl.data(), rows, out, out_cap, ends, scratch, tws, total, st);
+    if (hipFreeAsync(scratch, st) != hipSuccess && !rc) rc = hip_rc(hipGetLastError());
+    return rc;
+}
+
 int spec_encode_nested(const spec_nested_schema *schema, const void *const *outer_columns,
                        const uint8_t *const *outer_heaps, const uint64_t *outer_heap_lens, const uint32_t *item_begin,
                        const void *const *item_columns, const uint8_t *const *item_heaps,
@@ -602,6 +708,12 @@ int spec_encode_nested(const spec_nested_schema *schema, const void *const *oute
     if (nitems && !item_columns) return SPEC_E_INVALID_ARGUMENT;
     if (out && !ends && n) return SPEC_E_INVALID_ARGUMENT;
     if (workspace_size < spec_encode_nested_workspace_size(n)) return SPEC_E_WORKSPACE;
+    if (schema->outer.nfields > SPEC_KFIELDS || schema->item.nfields > SPEC_KFIELDS) {
+        for (uint32_t f = 0; f < schema->outer.nfields && n; f++)
+            if (f != list_f && !outer_columns[f]) return SPEC_E_INVALID_ARGUMENT;
+        return nested_encode_wide(schema, list_f, outer_columns, outer_heaps, outer_heap_lens, item_begin, item_columns,
+                                  item_heaps, item_heap_lens, nitems, n, out, out_cap, ends, total, (hipStream_t)stream);
+    }
     spec::NestedEncodeArgs a{};
     memset(&a, 0, sizeof(a));
     a.n = n;

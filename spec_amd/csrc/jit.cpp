@@ -205,8 +205,9 @@ void emit_enc_spec(std::ostringstream &o, const char *name, const spec_schema *s
 // Nested encode: SpecEnc for the outer schema (its list field handled by the nested encoder's
 // hooks) and for the item schema, RuntimeEnc for a side without a specialised encoder.
 bool has_outer_encoder(const spec_schema *s) { return s->nfields > 0 && s->nfields <= ENC_MAX_FIELDS; }
+bool nested_wide(const spec_nested_schema *s);
 bool has_nested_encoder(const spec_nested_schema *s) {
-    return has_outer_encoder(&s->outer) || has_encoder(&s->item);
+    return !nested_wide(s) && (has_outer_encoder(&s->outer) || has_encoder(&s->item));
 }
 
 std::string generate_nested_encode(const spec_nested_schema *s) {
@@ -457,7 +458,14 @@ const Entry *lookup(const spec_schema *s, Prog p) {
 }
 
 // a nested kernel is worth compiling when the outer or the item schema has a fast path
-bool has_nested_fast_path(const spec_nested_schema *s) { return has_fast_path(&s->outer) || has_fast_path(&s->item); }
+// (a half of more than SPEC_KFIELDS fields: the nested schema is decoded in field chunks by the
+// run-time kernels, capi.hip nested_decode_chunks, never by a generated kernel)
+bool nested_wide(const spec_nested_schema *s) {
+    return s->outer.nfields > (uint32_t)SPEC_KFIELDS || s->item.nfields > (uint32_t)SPEC_KFIELDS;
+}
+bool has_nested_fast_path(const spec_nested_schema *s) {
+    return !nested_wide(s) && (has_fast_path(&s->outer) || has_fast_path(&s->item));
+}
 
 const Entry *lookup_nested(const spec_nested_schema *s) {
     if (!enabled() || !has_nested_fast_path(s)) return nullptr;

@@ -86,8 +86,11 @@ def test_schema_limits():
     assert len(wide) == 1024
     with pytest.raises(ValueError):
         spec_amd.Schema([(i + 1, spec_amd.Kind.INT64) for i in range(1025)])
-    with pytest.raises(ValueError):  # the nested kernels take both halves as kernel arguments
-        spec_amd.NestedSchema([(1, spec_amd.Kind.LIST)], [(i + 1, spec_amd.Kind.INT32) for i in range(65)])
+    # a nested half of more than 64 fields: chunked decode, encode through the tree encoder
+    wn = spec_amd.NestedSchema([(1, spec_amd.Kind.LIST)], [(i + 1, spec_amd.Kind.INT32) for i in range(65)])
+    assert len(wn.item) == 65
+    with pytest.raises(ValueError):
+        spec_amd.NestedSchema([(1, spec_amd.Kind.LIST)], [(i + 1, spec_amd.Kind.INT32) for i in range(1025)])
 
 
 def test_jit_source_compiles_for_gfx950():

@@ -433,3 +433,100 @@ def test_nested_encode_errors(dev, kernel):
     ib2[100] = ib2[102] + 1
     with pytest.raises(spec_amd.SpecError):
         spec_amd.encode_nested(NESTED, oc, oh, to_dev(ib2.view(np.int32), dev), ic, ih, n)
+
+
+# ---- nested schemas with a half of more than 64 fields (round 5) --------------------------------
+# Decoded in chunks of 64 fields per half (the run-time kernels), encoded through the schema-tree
+# encoder; the oracle is the tree oracle over the equivalent tree (a record message whose list
+# field is a list of item messages: the same Writer calls, writer_list_msg.go:8-47).
+
+_WK = [Kind.BOOL, Kind.BYTE, Kind.INT16, Kind.INT32, Kind.INT64, Kind.UINT16, Kind.UINT32, Kind.UINT64,
+       Kind.FLOAT32, Kind.FLOAT64, Kind.BIN64, Kind.BIN128, Kind.STRING, Kind.BYTES]
+
+
+def _wide_nested(no=70, ni=80, list_at=30):
+    from spec_amd.tree import ListOf, Message, Tree
+
+    outer = [(i + 1, _WK[i % len(_WK)]) for i in range(no)]
+    outer[list_at] = (list_at + 1, Kind.LIST)
+    outer[5] = (400, outer[5][1])  # a tag past 255: big record tables
+    item = [(j + 1, _WK[(3 * j + 1) % len(_WK)]) for j in range(ni)]
+    schema = spec_amd.NestedSchema(outer, item)
+    imsg = Message("Item", [(f"w{j}", t, k) for j, (t, k) in enumerate(item)])
+    tree = Tree(Message("Outer", [(f"o{i}", t, ListOf(imsg) if k == Kind.LIST else k) for i, (t, k) in enumerate(outer)]))
+    return schema, tree, list_at
+
+
+def _wide_inputs(tree, schema, list_at, n, seed, dev):
+    from tests.tree_helpers import oracle_encode
+
+    cols, heaps, rows = workload.tree_batch(tree, n, seed, count=(0, 4))
+    lp = f"o{list_at}"
+    cols[f"{lp}?"] = np.ones_like(cols[f"{lp}?"])  # a nested list is always written
+    rows = [n, int(cols[f"{lp}#begin"].view(np.uint32).reshape(-1)[n])]
+    want_stream, want_ends = oracle_encode(tree, cols, heaps, n)
+    outer = [None if k == Kind.LIST else to_dev(cols[f"o{i}"], dev) for i, k in enumerate(f.kind for f in schema.outer.fields)]
+    oh = {i: to_dev(heaps[f"o{i}"], dev) for i, k in enumerate(f.kind for f in schema.outer.fields)
+          if k in (Kind.STRING, Kind.BYTES)}
+    items = [to_dev(cols[f"{lp}[].w{j}"], dev) for j in range(len(schema.item.fields))]
+    ih = {j: to_dev(heaps[f"{lp}[].w{j}"], dev) for j, k in enumerate(f.kind for f in schema.item.fields)
+          if k in (Kind.STRING, Kind.BYTES)}
+    ib = to_dev(cols[f"{lp}#begin"].view(np.uint32).reshape(-1).view(np.int32), dev)
+    return cols, heaps, rows, want_stream, want_ends, outer, oh, items, ih, ib
+
+
+@pytest.mark.parametrize("n", [1, 700])
+def test_nested_wide_encode_decode(dev, n):
+    """Halves of 70 (a big-tag table, the list in the middle) and 80 fields: encoded bytes and
+    ends bit-exact against the tree oracle; decoded (index + chunked decode, and one pass) outer
+    and item columns identical to the tree oracle's VALUE columns, item_begin = its BEGIN."""
+    import torch
+
+    from tests.tree_helpers import oracle_decode
+
+    schema, tree, list_at = _wide_nested()
+    cols, heaps, rows, ws, we, outer, oh, items, ih, ib = _wide_inputs(tree, schema, list_at, n, 900 + n, dev)
+    out, ends = spec_amd.encode_nested(schema, outer, oh, ib, items, ih, n)
+    torch.cuda.synchronize()
+    assert np.array_equal(ends.cpu().numpy().view(np.uint64), we)
+    assert np.array_equal(out.cpu().numpy(), ws)
+    wrows, want = oracle_decode(tree, ws, we)
+    wcol = {c.name: w for c, w in zip(tree.columns, want)}
+    d_s, d_e = to_dev(ws, dev), to_dev(we.view(np.int64), dev)
+    for onepass in (False, True):
+        got = spec_amd.decode_nested(schema, d_s, d_e, onepass=onepass)
+        torch.cuda.synchronize()
+        assert got.total_items == wrows[1]
+        assert np.array_equal(got.item_begin.cpu().numpy().view(np.uint32), wcol[f"o{list_at}#begin"].view(np.uint32).reshape(-1))
+        assert not got.status.cpu().numpy().any()
+        for i, k in enumerate(f.kind for f in schema.outer.fields):
+            if k == Kind.LIST:
+                continue
+            g = got.outer[i].cpu().numpy()
+            w = wcol[f"o{i}"].reshape(g.shape)
+            if k in (Kind.STRING, Kind.BYTES):  # spans: same stream, same offsets
+                assert np.array_equal(g, w), (onepass, i)
+            else:
+                assert np.array_equal(g, w), (onepass, i)
+        for j in range(len(schema.item.fields)):
+            g = got.items[j].cpu().numpy()[: wrows[1]]
+            assert np.array_equal(g, wcol[f"o{list_at}[].w{j}"].reshape(g.shape)), (onepass, j)
+
+
+def test_nested_wide_encode_errors(dev):
+    """A wide nested schema's encoder errors: an item string outside its heap, item_begin not
+    monotonic (*total all-ones: spec_encode_nested raises)."""
+    schema, tree, list_at = _wide_nested()
+    n = 200
+    cols, heaps, rows, ws, we, outer, oh, items, ih, ib = _wide_inputs(tree, schema, list_at, n, 950, dev)
+    j = next(j for j, k in enumerate(f.kind for f in schema.item.fields) if k == Kind.STRING)
+    bad = cols[f"o{list_at}[].w{j}"].copy()
+    bad.view(np.uint32).reshape(-1, 2)[len(bad) // 2, 1] = 1 << 24
+    items2 = list(items)
+    items2[j] = to_dev(bad, dev)
+    with pytest.raises(spec_amd.SpecError):
+        spec_amd.encode_nested(schema, outer, oh, ib, items2, ih, n)
+    b2 = cols[f"o{list_at}#begin"].view(np.uint32).reshape(-1).copy()
+    b2[100] = b2[102] + 1
+    with pytest.raises(spec_amd.SpecError):
+        spec_amd.encode_nested(schema, outer, oh, to_dev(b2.view(np.int32), dev), items, ih, n)
