@@ -848,6 +848,36 @@ struct WideBatches {
     }
 };
 
+// table entries [J0, JE) in batches of FAST_BATCH (a wave pair's half of a wide record)
+template <class Spec, int J0, int JE>
+struct WideBatchesTo {
+    static __device__ __forceinline__ bool run(const LdsSrc &s, int ts, int ds, uint32_t dsize, uint64_t r,
+                                               const FieldSet &fs, long long to_stream, uint64_t &errs) {
+        if constexpr (J0 >= JE) {
+            return true;
+        } else {
+            constexpr int J1 = J0 + FAST_BATCH < JE ? J0 + FAST_BATCH : JE;
+            if (!wide_batch<Spec, J0, J1, false>(s, ts, ds, dsize, r, fs, to_stream, errs)) return false;
+            return WideBatchesTo<Spec, J1, JE>::run(s, ts, ds, dsize, r, fs, to_stream, errs);
+        }
+    }
+};
+
+// Half h of a wide record's fields (table entries [0, H) or [H, N), H on a batch boundary) for a
+// wave pair (decode_flat_pair): false when this half needs the generic path.  No status: the
+// pair's first wave writes it once both halves succeeded.
+template <class Spec>
+__device__ __forceinline__ bool fast_wide_half(const LdsSrc &s, int rs, int re, uint64_t r, const FieldSet &fs,
+                                               long long to_stream, int h) {
+    if (re <= rs) return false;
+    const Trailer tr = parse_trailer(s, rs, re);
+    if ((tr.st != ST_OK) | (tr.big != Spec::big) | (tr.tsize != (Spec::big ? 6u : 3u) * (uint32_t)Spec::N)) return false;
+    constexpr int H = ((Spec::N / 2 + FAST_BATCH - 1) / FAST_BATCH) * FAST_BATCH;
+    uint64_t errs = 0;
+    if (h == 0) return WideBatchesTo<Spec, 0, H>::run(s, (int)tr.tstart, (int)tr.dstart, tr.dsize, r, fs, to_stream, errs);
+    return WideBatchesTo<Spec, H, Spec::N>::run(s, (int)tr.tstart, (int)tr.dstart, tr.dsize, r, fs, to_stream, errs);
+}
+
 // The whole record (columns, status, errmask); false: nothing final written, run the generic path.
 template <class Spec, bool ERR = false>
 __device__ __forceinline__ bool fast_wide(const LdsSrc &s, int rs, int re, uint64_t r, const FieldSet &fs,
@@ -1053,6 +1083,68 @@ __device__ __forceinline__ void decode_flat_once(const DecodeArgs &a) {
     } else if (valid) {
         GlobalSrc s{a.stream, a.stream_len};
         decode_record_generic(s, (long long)cur.rec_lo, (long long)cur.rec_hi, r, a.f, 0);
+    }
+}
+
+// A wide schema's group of 64 records on a wave PAIR (a 128-thread block): both waves stage the
+// group's span once in the block's slab (each issues half the LDS-DMA chunks), each decodes half
+// of the fields (fast_wide_half), wave 1 hands its verdict to wave 0 through LDS, and wave 0
+// writes the status — or, where either half needs it, runs the generic path over the whole
+// record (it rewrites every column).  Same LDS per 64 records, twice the waves: one wave's LDS
+// and memory latency overlaps the other's decode.  No error-mask variant (that one keeps a wave
+// per group).
+template <class Spec>
+__device__ __forceinline__ void decode_flat_pair(const DecodeArgs &a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    uint64_t blk = blockIdx.x;
+    if (a.xcd) {
+        const uint64_t per = (gridDim.x + 7) / 8;
+        blk = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    }
+    const uint64_t base = a.r0 + blk * 64;
+    if (base >= a.n) return; // (block-uniform)
+    const uint64_t r = base + lane;
+    const bool valid = r < a.n;
+    uint8_t *slab = smem;
+    uint32_t *xch = (uint32_t *)(smem + a.slab);
+    __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(a.stream, a.stream_len);
+    const uint64_t hi = a.ends[valid ? r : a.n - 1];
+    uint64_t lo = __shfl_up(hi, 1);
+    if (lane == 0) lo = r == 0 ? 0 : a.ends[r - 1];
+    lo += a.head;
+    const Group cur = make_group(a, base, lane, lo, hi, a.slab);
+    if (!cur.in_lds) {
+        if (wave == 0 && valid) {
+            GlobalSrc s{a.stream, a.stream_len};
+            decode_record_generic(s, (long long)cur.rec_lo, (long long)cur.rec_hi, r, a.f, 0);
+        }
+        return;
+    }
+    for (uint32_t c = (uint32_t)wave; c < cur.chunks; c += 2)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(slab + SLAB_GUARD + c * 1024),
+                                                 16, (uint32_t)cur.aligned_lo + c * 1024 + lane * 16, 0, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the chunk straddling the stream end is refilled by the wave that loaded it
+    const uint64_t tail = a.stream_len & ~15ull;
+    if (tail < a.stream_len && tail >= cur.aligned_lo && tail < cur.aligned_lo + (uint64_t)cur.chunks * 1024 &&
+        (int)(((tail - cur.aligned_lo) >> 10) & 1) == wave && lane < 16 && tail + lane < a.stream_len)
+        slab[SLAB_GUARD + (tail - cur.aligned_lo) + lane] = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)(tail + lane), 0, 0);
+    __syncthreads(); // the slab is whole
+    LdsSrc s{(lds_u8 *)slab};
+    const int rs = SLAB_GUARD + (int)(cur.rec_lo - cur.aligned_lo);
+    const int re = SLAB_GUARD + (int)(cur.rec_hi - cur.aligned_lo);
+    const long long to_stream = (long long)cur.aligned_lo - SLAB_GUARD;
+    const bool ok = valid && fast_wide_half<Spec>(s, rs, re, r, a.f, to_stream, wave);
+    if (wave == 1) xch[lane] = ok ? 1u : 0u;
+    __syncthreads(); // wave 1's verdict (and its column stores) are in
+    if (wave == 0 && valid) {
+        if (ok && xch[lane]) {
+            if (a.f.status) a.f.status[r] = ST_OK;
+        } else {
+            decode_record_generic(s, rs, re, r, a.f, to_stream);
+        }
     }
 }
 

@@ -32,6 +32,11 @@ __global__ __launch_bounds__(256) void decode_flat_kernel_persistent(DecodeArgs 
 bool persistent_decode() { return SPEC_AB_PERSIST != 0; }
 bool xcd_swizzle_decode() { return SPEC_AB_NOXCD == 0; }
 unsigned decode_wpb() { return SPEC_AB_WPB >= 1 && SPEC_AB_WPB <= 4 ? SPEC_AB_WPB : 1; }
+//   SPEC_AB_FLAT_PAIR=0  wide schemas (fast_wide) one wave per group instead of a wave pair
+#ifndef SPEC_AB_FLAT_PAIR
+#define SPEC_AB_FLAT_PAIR 1
+#endif
+bool flat_pair() { return SPEC_AB_FLAT_PAIR != 0; }
 
 int device_cus() {
     static int cus[64] = {0};

@@ -161,6 +161,10 @@ std::string generate_decode(const spec_schema *s) {
       << "  spec::decode_flat_entry<" << pers << ", GenSpec>(a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void spec_decode_flat" << w << "_err_jit(spec::DecodeArgs a) {\n"
       << "  spec::decode_flat_entry<" << pers << ", GenSpec, true>(a);\n}\n";
+    // the fast_wide schemas: also the wave-pair kernel (decode_core.hpp decode_flat_pair)
+    if (*w)
+        o << "extern \"C\" __global__ __launch_bounds__(128) void spec_decode_flat_wide_pair_jit(spec::DecodeArgs a) {\n"
+          << "  spec::decode_flat_pair<GenSpec>(a);\n}\n";
     return o.str();
 }
 
@@ -400,6 +404,7 @@ Entry load(const std::vector<char> &code, Prog p) {
         (void)hipGetLastError(); // a wide / big-table schema (generate_decode): its own kernel names
         names[p][0] = "spec_decode_flat_wide_jit";
         names[p][1] = "spec_decode_flat_wide_err_jit";
+        names[p][2] = "spec_decode_flat_wide_pair_jit";
     }
     for (int i = 0; ok && i < 4; i++)
         if (names[p][i]) ok = hipModuleGetFunction(&e.fn[i], e.mod, names[p][i]) == hipSuccess;
@@ -1269,6 +1274,20 @@ int jit_launch_decode_flat(const spec_schema *schema, const DecodeArgs &a, doubl
     if (!ent) return 0;
     hipFunction_t fn = ent->fn[a.f.errmask ? 1 : 0]; // the errmask variant for spec_decode_flat_errors
     if (a.n <= a.r0) return 1;
+    if (flat_pair() && ent->fn[2] && !a.f.errmask && !persistent_decode()) {
+        // a wide schema: a wave pair per 64 records, one slab per pair (+ 256 B exchange)
+        DecodeArgs args = a;
+        args.slab = decode_slab_bytes(avg_record);
+        args.xcd = xcd_swizzle_decode();
+        uint64_t groups = (a.n - a.r0 + 63) / 64;
+        if (args.xcd) groups = (groups + 7) / 8 * 8;
+        size_t size = sizeof(args);
+        void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
+                         HIP_LAUNCH_PARAM_END};
+        hipError_t e = hipModuleLaunchKernel(ent->fn[2], (unsigned)groups, 1, 1, 128, 1, 1, args.slab + 256, stream,
+                                             nullptr, extra);
+        return e == hipSuccess ? 1 : -1;
+    }
     const DecodeLaunch L = decode_launch(a.n - a.r0, avg_record, device_cus(), persistent_decode(), decode_wpb());
     DecodeArgs args = a;
     args.slab = L.slab;
