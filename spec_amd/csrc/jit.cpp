@@ -161,10 +161,10 @@ std::string generate_decode(const spec_schema *s) {
       << "  spec::decode_flat_entry<" << pers << ", GenSpec>(a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(256) void spec_decode_flat" << w << "_err_jit(spec::DecodeArgs a) {\n"
       << "  spec::decode_flat_entry<" << pers << ", GenSpec, true>(a);\n}\n";
-    // the fast_wide schemas: also the wave-pair kernel (decode_core.hpp decode_flat_pair)
-    if (*w)
-        o << "extern \"C\" __global__ __launch_bounds__(128) void spec_decode_flat_wide_pair_jit(spec::DecodeArgs a) {\n"
-          << "  spec::decode_flat_pair<GenSpec>(a);\n}\n";
+    // the wave-pair kernel (decode_core.hpp decode_flat_pair), the default launch for every
+    // schema (decode_flat.hip SPEC_AB_FLAT_PAIR)
+    o << "extern \"C\" __global__ __launch_bounds__(128) void spec_decode_flat" << w << "_pair_jit(spec::DecodeArgs a) {\n"
+      << "  spec::decode_flat_pair<GenSpec>(a);\n}\n";
     return o.str();
 }
 
@@ -395,7 +395,7 @@ Entry load(const std::vector<char> &code, Prog p) {
         e.failed = true;
         return e;
     }
-    const char *names[4][4] = {{"spec_decode_flat_jit", "spec_decode_flat_err_jit", nullptr, nullptr},
+    const char *names[4][4] = {{"spec_decode_flat_jit", "spec_decode_flat_err_jit", "spec_decode_flat_pair_jit", nullptr},
                                {"spec_encode_size_jit", "spec_encode_write_jit", nullptr, nullptr},
                                {"spec_decode_nested_jit", "spec_decode_nested2_jit", "spec_decode_nested3_jit", nullptr},
                                {"spec_encode_nested_size_jit", "spec_encode_nested_write_jit", nullptr, nullptr}};
@@ -1274,7 +1274,12 @@ int jit_launch_decode_flat(const spec_schema *schema, const DecodeArgs &a, doubl
     if (!ent) return 0;
     hipFunction_t fn = ent->fn[a.f.errmask ? 1 : 0]; // the errmask variant for spec_decode_flat_errors
     if (a.n <= a.r0) return 1;
-    if (flat_pair() && ent->fn[2] && !a.f.errmask && !persistent_decode()) {
+    const bool wide = schema->nfields > (uint32_t)FAST_MAX_FIELDS || [&] {
+        for (uint32_t f = 0; f < schema->nfields; f++)
+            if (schema->fields[f].tag > 255) return true;
+        return false;
+    }();
+    if (flat_pair() >= (wide ? 1 : 2) && ent->fn[2] && !a.f.errmask && !persistent_decode()) {
         // a wide schema: a wave pair per 64 records, one slab per pair (+ 256 B exchange)
         DecodeArgs args = a;
         args.slab = decode_slab_bytes(avg_record);
