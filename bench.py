@@ -993,7 +993,7 @@ def run(args, env):
     # The passes record the device-source revision they measured (source_rev): a traffic figure
     # measured on other kernel code is not reported (traffic null, traffic_rev says which).
     traffic, traffic_rev = None, None
-    kname = "spec_decode_flat_jit" if jit else "decode_flat_kernel"
+    kname = "spec_decode_flat_pair_jit" if jit else "decode_flat_kernel"
     rev = source_rev()
     if os.path.exists(args.traffic):
         try:

@@ -29,8 +29,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 find $OUT/prof -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats.csv \;
 cut -d, -f1-4 $OUT/kernel_stats.csv | head -n 14
 f=$(find $OUT/prof -name '*kernel_trace.csv' | head -n 1)
-python3 tools/trace_stats.py $f spec_decode_flat_jit 1048576 --json $OUT/decode_flat_1M_trace.json > $OUT/decode_flat_1M_trace.txt && head -n 2 $OUT/decode_flat_1M_trace.txt
+python3 tools/trace_stats.py $f spec_decode_flat_pair_jit 2097152 --json $OUT/decode_flat_1M_trace.json > $OUT/decode_flat_1M_trace.txt && head -n 2 $OUT/decode_flat_1M_trace.txt
 # config 5's 2M-record blocks, the flat encoder's passes at 1M records (per-launch-size traces)
-python3 tools/trace_stats.py $f spec_decode_flat_jit 2097152 --json $OUT/decode_flat_2M_trace.json > $OUT/decode_flat_2M_trace.txt && head -n 1 $OUT/decode_flat_2M_trace.txt
+python3 tools/trace_stats.py $f spec_decode_flat_pair_jit 4194304 --json $OUT/decode_flat_2M_trace.json > $OUT/decode_flat_2M_trace.txt && head -n 1 $OUT/decode_flat_2M_trace.txt
 python3 tools/trace_stats.py $f spec_encode_write_jit 1048576 --json $OUT/encode_write_1M_trace.json > $OUT/encode_write_1M_trace.txt && head -n 1 $OUT/encode_write_1M_trace.txt
 python3 tools/trace_stats.py $f spec_encode_size_jit 1048576 --json $OUT/encode_size_1M_trace.json > $OUT/encode_size_1M_trace.txt && head -n 1 $OUT/encode_size_1M_trace.txt

@@ -4,7 +4,7 @@ median/mean/min/max, gaps between consecutive dispatches, medians over windows o
 
 Usage: python3 tools/trace_stats.py RUN_kernel_trace.csv [KERNEL_NAME_SUBSTRING] [GRID_SIZE_X] [--json OUT]
 GRID_SIZE_X keeps only the dispatches of that grid (work-items): one launch size, e.g. the
-headline's 1,048,576-record decode (16,384 one-wave blocks = 1,048,576 work-items).
+headline's 1,048,576-record decode (16,384 two-wave blocks = 2,097,152 work-items).
 """
 import csv
 import statistics

@@ -1,6 +1,6 @@
 """Split tools/prof_wide.sh's wide-kernel launches by schema: bench.wide_leg runs the 40-field
 schema's launches first, then (after the generic kernel's) the big-tag schema's, so consecutive
-runs of spec_decode_flat_wide_jit dispatches are one schema each.  Writes OUT/wide_split.json:
+runs of spec_decode_flat_wide_pair_jit dispatches are one schema each.  Writes OUT/wide_split.json:
 per segment the median launch time (kernel trace) and the mean of every PMC counter."""
 import csv
 import glob
