@@ -849,7 +849,7 @@ struct WideBatches {
 };
 
 // table entries [J0, JE) in batches of FAST_BATCH (a wave pair's half of a wide record)
-template <class Spec, int J0, int JE>
+template <class Spec, int J0, int JE, bool ERR = false>
 struct WideBatchesTo {
     static __device__ __forceinline__ bool run(const LdsSrc &s, int ts, int ds, uint32_t dsize, uint64_t r,
                                                const FieldSet &fs, long long to_stream, uint64_t &errs) {
@@ -857,25 +857,24 @@ struct WideBatchesTo {
             return true;
         } else {
             constexpr int J1 = J0 + FAST_BATCH < JE ? J0 + FAST_BATCH : JE;
-            if (!wide_batch<Spec, J0, J1, false>(s, ts, ds, dsize, r, fs, to_stream, errs)) return false;
-            return WideBatchesTo<Spec, J1, JE>::run(s, ts, ds, dsize, r, fs, to_stream, errs);
+            if (!wide_batch<Spec, J0, J1, ERR>(s, ts, ds, dsize, r, fs, to_stream, errs)) return false;
+            return WideBatchesTo<Spec, J1, JE, ERR>::run(s, ts, ds, dsize, r, fs, to_stream, errs);
         }
     }
 };
 
 // Half h of a wide record's fields (table entries [0, H) or [H, N), H on a batch boundary) for a
 // wave pair (decode_flat_pair): false when this half needs the generic path.  No status: the
-// pair's first wave writes it once both halves succeeded.
-template <class Spec>
+// pair's first wave writes it once both halves succeeded.  ERR: this half's error-mask bits in errs.
+template <class Spec, bool ERR = false>
 __device__ __forceinline__ bool fast_wide_half(const LdsSrc &s, int rs, int re, uint64_t r, const FieldSet &fs,
-                                               long long to_stream, int h) {
+                                               long long to_stream, int h, uint64_t &errs) {
     if (re <= rs) return false;
     const Trailer tr = parse_trailer(s, rs, re);
     if ((tr.st != ST_OK) | (tr.big != Spec::big) | (tr.tsize != (Spec::big ? 6u : 3u) * (uint32_t)Spec::N)) return false;
     constexpr int H = ((Spec::N / 2 + FAST_BATCH - 1) / FAST_BATCH) * FAST_BATCH;
-    uint64_t errs = 0;
-    if (h == 0) return WideBatchesTo<Spec, 0, H>::run(s, (int)tr.tstart, (int)tr.dstart, tr.dsize, r, fs, to_stream, errs);
-    return WideBatchesTo<Spec, H, Spec::N>::run(s, (int)tr.tstart, (int)tr.dstart, tr.dsize, r, fs, to_stream, errs);
+    if (h == 0) return WideBatchesTo<Spec, 0, H, ERR>::run(s, (int)tr.tstart, (int)tr.dstart, tr.dsize, r, fs, to_stream, errs);
+    return WideBatchesTo<Spec, H, Spec::N, ERR>::run(s, (int)tr.tstart, (int)tr.dstart, tr.dsize, r, fs, to_stream, errs);
 }
 
 // The whole record (columns, status, errmask); false: nothing final written, run the generic path.
@@ -1093,7 +1092,7 @@ __device__ __forceinline__ void decode_flat_once(const DecodeArgs &a) {
 // record (it rewrites every column).  Same LDS per 64 records, twice the waves: one wave's LDS
 // and memory latency overlaps the other's decode.  No error-mask variant (that one keeps a wave
 // per group).
-template <class Spec>
+template <class Spec, bool ERR = false>
 __device__ __forceinline__ void decode_flat_pair(const DecodeArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6;
@@ -1136,12 +1135,18 @@ __device__ __forceinline__ void decode_flat_pair(const DecodeArgs &a) {
     const int rs = SLAB_GUARD + (int)(cur.rec_lo - cur.aligned_lo);
     const int re = SLAB_GUARD + (int)(cur.rec_hi - cur.aligned_lo);
     const long long to_stream = (long long)cur.aligned_lo - SLAB_GUARD;
-    const bool ok = valid && fast_wide_half<Spec>(s, rs, re, r, a.f, to_stream, wave);
-    if (wave == 1) xch[lane] = ok ? 1u : 0u;
+    uint64_t errs = 0;
+    const bool ok = valid && fast_wide_half<Spec, ERR>(s, rs, re, r, a.f, to_stream, wave, errs);
+    uint64_t *xerr = (uint64_t *)(xch + 64); // ERR: wave 1's mask bits (LDS slab + 256 .. + 768)
+    if (wave == 1) {
+        xch[lane] = ok ? 1u : 0u;
+        if constexpr (ERR) xerr[lane] = errs;
+    }
     __syncthreads(); // wave 1's verdict (and its column stores) are in
     if (wave == 0 && valid) {
         if (ok && xch[lane]) {
             if (a.f.status) a.f.status[r] = ST_OK;
+            if constexpr (ERR) a.f.errmask[r] = errs | xerr[lane];
         } else {
             decode_record_generic(s, rs, re, r, a.f, to_stream);
         }

@@ -157,6 +157,13 @@ int launch_nested_decode(const spec_nested_schema *schema, NestedArgs a, double 
 #endif
 bool nested_lookback() { return SPEC_AB_LOOKBACK != 0; }
 
+// The two-pass decode on a wave pair per group (decode_nested_core.hpp nested_decode_pair; the
+// JIT kernels only): -DSPEC_AB_NESTED_PAIR=0 runs a wave per group instead.
+#ifndef SPEC_AB_NESTED_PAIR
+#define SPEC_AB_NESTED_PAIR 1
+#endif
+bool nested_pair() { return SPEC_AB_NESTED_PAIR != 0; }
+
 // spec_decode_nested_onepass: by default the index kernels + the decode kernel back to back
 // (no host round trip); with SPEC_AB_LOOKBACK: DEC_WAVES groups per block (one per wave), one
 // look-back per block over the earlier blocks, the look-back words (group_base[0 .. blocks])

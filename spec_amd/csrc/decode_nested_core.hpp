@@ -241,11 +241,13 @@ __device__ __forceinline__ ListInfo item_owner(const ListInfo &li, uint32_t excl
 #ifndef NESTED_ITEM_U
 #define NESTED_ITEM_U 2
 #endif
+// (j_first, j_step: a wave pair's waves take alternate rounds of 64 * U items, nested_decode_pair)
 template <class ISpec, int U = NESTED_ITEM_U, class Src>
 __device__ __forceinline__ void decode_group_items(const Src &s, const ListInfo &li, uint32_t excl, uint32_t total,
                                                    uint64_t item_base, int lane, long long to_stream,
-                                                   const NestedArgs &a) {
-    for (uint32_t j0 = 0; j0 < total; j0 += 64 * U) {
+                                                   const NestedArgs &a, uint32_t j_first = 0,
+                                                   uint32_t j_step = 64 * U) {
+    for (uint32_t j0 = j_first; j0 < total; j0 += j_step) {
         ListInfo own[U];
         uint32_t idx[U];
 #pragma unroll
@@ -545,6 +547,91 @@ __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
         nested_group_body<OSpec, ISpec, ONEPASS>(s, (long long)gr.rec_lo, (long long)gr.rec_hi, valid, r, g,
                                                  item_base, lane, 0, a, nullptr, xch);
     }
+}
+
+// Two-pass decode on a WAVE PAIR (round 5; decode_core.hpp decode_flat_pair is the flat
+// analogue): a 128-thread block takes one group of 64 records.  Both waves stage the group's
+// span into ONE slab (1 KiB DMA chunks issued round-robin; the chunk straddling the stream end
+// refilled by the wave that issued it), wave 0 decodes the 64 outer records and posts each
+// record's list (count, data / table start, data size, big) to LDS after the slab, then both
+// waves decode the group's items, alternating rounds of 64 * U items.  Twice the waves per
+// staged byte: the items' LDS reads are latency-bound.  A group larger
+// than the slab: wave 0 alone, in two halves of 32 records (nested_decode_part).
+template <class OSpec, class ISpec, int U = NESTED_ITEM_U>
+__device__ __forceinline__ void nested_decode_pair(const NestedArgs &a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint64_t g = blockIdx.x;
+    if (a.xcd) {
+        const uint64_t per = (gridDim.x + 7) / 8;
+        g = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    }
+    const uint64_t base = g * 64;
+    if (base >= a.n) return; // (block-uniform)
+    uint8_t *slab = smem;
+    uint32_t *xl = (uint32_t *)(smem + a.slab); // [4][64]: count, dsize | big << 31, dstart, tstart
+    __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(a.stream, a.stream_len);
+    const uint64_t item_base = uniform64(a.group_base[g]);
+    DecodeArgs d;
+    d.stream = a.stream;
+    d.stream_len = a.stream_len;
+    d.ends = a.ends;
+    d.n = a.n;
+    d.r0 = 0;
+    d.head = 0;
+    uint64_t lo, hi;
+    load_group_ends(d, base, lane, lo, hi);
+    const Group gr = make_group(d, base, lane, lo, hi, a.slab);
+    if (!gr.in_lds) {
+        if (wave == 0) {
+            const uint32_t first = nested_decode_part<OSpec, ISpec, false, U>(a, rsrc, slab, g, item_base, lane, 0, 32);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the first half's LDS reads done
+            __builtin_amdgcn_wave_barrier();
+            nested_decode_part<OSpec, ISpec, false, U>(a, rsrc, slab, g, item_base + first, lane, 32, 64);
+        }
+        return;
+    }
+    for (uint32_t c = (uint32_t)wave; c < gr.chunks; c += 2)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(slab + SLAB_GUARD + c * 1024),
+                                                 16, (uint32_t)gr.aligned_lo + c * 1024 + lane * 16, 0, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint64_t tail = a.stream_len & ~15ull;
+    if (tail < a.stream_len && tail >= gr.aligned_lo && tail < gr.aligned_lo + (uint64_t)gr.chunks * 1024 &&
+        (int)(((tail - gr.aligned_lo) >> 10) & 1) == wave && lane < 16 && tail + lane < a.stream_len)
+        slab[SLAB_GUARD + (tail - gr.aligned_lo) + lane] = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)(tail + lane), 0, 0);
+    __syncthreads(); // the slab is whole
+    LdsSrc s{(lds_u8 *)slab};
+    const long long to_stream = (long long)gr.aligned_lo - SLAB_GUARD;
+    const uint64_t r = base + lane;
+    const bool valid = r < a.n;
+    ListInfo li = {0, 0, 0, 0, false};
+    if (wave == 0) {
+        if (valid)
+            li = decode_outer<OSpec>(s, SLAB_GUARD + (long long)(gr.rec_lo - gr.aligned_lo),
+                                     SLAB_GUARD + (long long)(gr.rec_hi - gr.aligned_lo), r, to_stream, a);
+        xl[lane] = li.count;
+        xl[64 + lane] = li.dsize | ((uint32_t)li.big << 31);
+        xl[128 + lane] = (uint32_t)li.dstart;
+        xl[192 + lane] = (uint32_t)li.tstart;
+    }
+    __syncthreads(); // the lists are posted
+    if (wave == 1) {
+        li.count = xl[lane];
+        const uint32_t ds = xl[64 + lane];
+        li.dsize = ds & 0x7fffffffu;
+        li.big = (ds >> 31) != 0;
+        li.dstart = xl[128 + lane];
+        li.tstart = xl[192 + lane];
+    }
+    const uint32_t incl = wave_incl_scan(li.count, lane);
+    const uint32_t excl = incl - li.count;
+    const uint32_t total = __shfl(incl, 63);
+    if (wave == 0 && valid) {
+        a.item_begin[r] = (uint32_t)(item_base + excl);
+        if (r == a.n - 1) a.item_begin[a.n] = (uint32_t)(item_base + incl);
+    }
+    decode_group_items<ISpec, U>(s, li, excl, total, item_base, lane, to_stream, a, (uint32_t)wave * 64 * U,
+                                 2 * 64 * U);
 }
 
 // Count kernel of the two-pass index: per group, the item total.

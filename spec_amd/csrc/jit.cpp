@@ -164,7 +164,9 @@ std::string generate_decode(const spec_schema *s) {
     // the wave-pair kernel (decode_core.hpp decode_flat_pair), the default launch for every
     // schema (decode_flat.hip SPEC_AB_FLAT_PAIR)
     o << "extern \"C\" __global__ __launch_bounds__(128) void spec_decode_flat" << w << "_pair_jit(spec::DecodeArgs a) {\n"
-      << "  spec::decode_flat_pair<GenSpec>(a);\n}\n";
+      << "  spec::decode_flat_pair<GenSpec>(a);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(128) void spec_decode_flat" << w << "_err_pair_jit(spec::DecodeArgs a) {\n"
+      << "  spec::decode_flat_pair<GenSpec, true>(a);\n}\n";
     return o.str();
 }
 
@@ -182,7 +184,9 @@ std::string generate_nested(const spec_nested_schema *s) {
       << "extern \"C\" __global__ __launch_bounds__(64) void spec_decode_nested2_jit(spec::NestedArgs a) {\n"
       << "  spec::nested_decode_body<" << specs << ", false>(a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(64) void spec_decode_nested3_jit(spec::NestedArgs a) {\n"
-      << "  spec::nested_decode_body<" << specs << ", false, true>(a);\n}\n";
+      << "  spec::nested_decode_body<" << specs << ", false, true>(a);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(128) void spec_decode_nested_pair_jit(spec::NestedArgs a) {\n"
+      << "  spec::nested_decode_pair<" << specs << ">(a);\n}\n";
     return o.str();
 }
 
@@ -395,9 +399,11 @@ Entry load(const std::vector<char> &code, Prog p) {
         e.failed = true;
         return e;
     }
-    const char *names[4][4] = {{"spec_decode_flat_jit", "spec_decode_flat_err_jit", "spec_decode_flat_pair_jit", nullptr},
+    const char *names[4][4] = {{"spec_decode_flat_jit", "spec_decode_flat_err_jit", "spec_decode_flat_pair_jit",
+                                "spec_decode_flat_err_pair_jit"},
                                {"spec_encode_size_jit", "spec_encode_write_jit", nullptr, nullptr},
-                               {"spec_decode_nested_jit", "spec_decode_nested2_jit", "spec_decode_nested3_jit", nullptr},
+                               {"spec_decode_nested_jit", "spec_decode_nested2_jit", "spec_decode_nested3_jit",
+                                "spec_decode_nested_pair_jit"},
                                {"spec_encode_nested_size_jit", "spec_encode_nested_write_jit", nullptr, nullptr}};
     bool ok = hipModuleLoadData(&e.mod, code.data()) == hipSuccess;
     if (ok && p == DECODE && hipModuleGetFunction(&e.fn[0], e.mod, names[p][0]) != hipSuccess) {
@@ -405,6 +411,7 @@ Entry load(const std::vector<char> &code, Prog p) {
         names[p][0] = "spec_decode_flat_wide_jit";
         names[p][1] = "spec_decode_flat_wide_err_jit";
         names[p][2] = "spec_decode_flat_wide_pair_jit";
+        names[p][3] = "spec_decode_flat_wide_err_pair_jit";
     }
     for (int i = 0; ok && i < 4; i++)
         if (names[p][i]) ok = hipModuleGetFunction(&e.fn[i], e.mod, names[p][i]) == hipSuccess;
@@ -1279,8 +1286,8 @@ int jit_launch_decode_flat(const spec_schema *schema, const DecodeArgs &a, doubl
             if (schema->fields[f].tag > 255) return true;
         return false;
     }();
-    if (flat_pair() >= (wide ? 1 : 2) && ent->fn[2] && !a.f.errmask && !persistent_decode()) {
-        // a wide schema: a wave pair per 64 records, one slab per pair (+ 256 B exchange)
+    if (flat_pair() >= (wide ? 1 : 2) && ent->fn[a.f.errmask ? 3 : 2] && !persistent_decode()) {
+        // a wave pair per 64 records, one slab per pair (+ 256 B exchange, + 512 B of masks)
         DecodeArgs args = a;
         args.slab = decode_slab_bytes(avg_record);
         args.xcd = xcd_swizzle_decode();
@@ -1289,8 +1296,8 @@ int jit_launch_decode_flat(const spec_schema *schema, const DecodeArgs &a, doubl
         size_t size = sizeof(args);
         void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                          HIP_LAUNCH_PARAM_END};
-        hipError_t e = hipModuleLaunchKernel(ent->fn[2], (unsigned)groups, 1, 1, 128, 1, 1, args.slab + 256, stream,
-                                             nullptr, extra);
+        hipError_t e = hipModuleLaunchKernel(ent->fn[a.f.errmask ? 3 : 2], (unsigned)groups, 1, 1, 128, 1, 1,
+                                             args.slab + (a.f.errmask ? 768 : 256), stream, nullptr, extra);
         return e == hipSuccess ? 1 : -1;
     }
     const DecodeLaunch L = decode_launch(a.n - a.r0, avg_record, device_cus(), persistent_decode(), decode_wpb());
@@ -1334,6 +1341,11 @@ int jit_launch_nested(const spec_nested_schema *schema, const NestedArgs &a, int
     else args.xcd = 0;
     size_t lds = a.slab + (mode == NESTED_RANGES ? NESTED_RANGE_BYTES : 0u);
     unsigned threads = 64;
+    if (mode == NESTED_GROUPS && nested_pair() && e->fn[3]) { // a wave pair per group (nested_decode_pair)
+        mode = 3;
+        threads = 128;
+        lds = a.slab + 1024; // the posted lists: 4 words per record
+    }
     if (mode == NESTED_ONEPASS) { // DEC_WAVES groups per block: one look-back per block
         grid = (grid + DEC_WAVES - 1) / DEC_WAVES;
         threads = 64 * DEC_WAVES;

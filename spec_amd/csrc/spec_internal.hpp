@@ -35,7 +35,8 @@ int device_cus(); // CUs of the current device (cached)
 void note_hip_error(hipError_t e); // capi.hip: remembered for spec_last_hip_error()
 bool persistent_decode(); // build-time A/B variants (decode_flat.hip): SPEC_AB_PERSIST
 unsigned decode_wpb();     // SPEC_AB_WPB (waves per block, default 1)
-int flat_pair();           // SPEC_AB_FLAT_PAIR: 1 wide schemas / 2 every schema on wave pairs (decode_flat_pair)
+int flat_pair();
+bool nested_pair(); // decode_nested.hip: SPEC_AB_NESTED_PAIR           // SPEC_AB_FLAT_PAIR: 1 wide schemas / 2 every schema on wave pairs (decode_flat_pair)
 int launch_parse(DecodeArgs a, uint32_t *sizes, uint32_t root, double avg_record, hipStream_t stream);
 int launch_nested_index(NestedArgs a, double avg_record, hipStream_t stream);
 int launch_nested_decode(const spec_nested_schema *schema, NestedArgs a, double avg_record, hipStream_t stream);

@@ -12,7 +12,7 @@ for v in default "$@"; do
   if [ $v != default ]; then cp spec_amd/libspec_amd_$v.so spec_amd/libspec_amd.so; fi
   for i in 1 2; do
     timeout -k 10 300 python3 tools/bench_nested.py > $OUT/bench_$v$i.json 2> $OUT/bench_$v$i.err || { tail -n 20 $OUT/bench_$v$i.err; exit 1; }
-    python3 -c "import json; d=json.load(open('$OUT/bench_$v$i.json'))['nested']; print('$v', 'enc', d['encode_ms'], 'dec', d['decode_ms'], d.get('roundtrip_ok'))"
+    python3 -c "import json; d=json.load(open('$OUT/bench_$v$i.json'))['nested']; print('$v', 'enc', d['encode_ms'], 'dec', d['onepass_ms'], d['twopass_ms'], d.get('ok'))"
   done
 done
 cp /tmp/libspec_amd_default.so spec_amd/libspec_amd.so
