@@ -557,7 +557,9 @@ __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
 // waves decode the group's items, alternating rounds of 64 * U items.  Twice the waves per
 // staged byte: the items' LDS reads are latency-bound.  A group larger
 // than the slab: wave 0 alone, in two halves of 32 records (nested_decode_part).
-template <class OSpec, class ISpec, int U = NESTED_ITEM_U>
+// SELF: the other waves open each record's list themselves (rec_open + list_open, the generic
+// path's lookup) instead of waiting for wave 0's posted lists.
+template <class OSpec, class ISpec, int U = NESTED_ITEM_U, int P = 2, bool SELF = false>
 __device__ __forceinline__ void nested_decode_pair(const NestedArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -591,13 +593,13 @@ __device__ __forceinline__ void nested_decode_pair(const NestedArgs &a) {
         }
         return;
     }
-    for (uint32_t c = (uint32_t)wave; c < gr.chunks; c += 2)
+    for (uint32_t c = (uint32_t)wave; c < gr.chunks; c += P)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(slab + SLAB_GUARD + c * 1024),
                                                  16, (uint32_t)gr.aligned_lo + c * 1024 + lane * 16, 0, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint64_t tail = a.stream_len & ~15ull;
     if (tail < a.stream_len && tail >= gr.aligned_lo && tail < gr.aligned_lo + (uint64_t)gr.chunks * 1024 &&
-        (int)(((tail - gr.aligned_lo) >> 10) & 1) == wave && lane < 16 && tail + lane < a.stream_len)
+        (int)(((tail - gr.aligned_lo) >> 10) % P) == wave && lane < 16 && tail + lane < a.stream_len)
         slab[SLAB_GUARD + (tail - gr.aligned_lo) + lane] = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)(tail + lane), 0, 0);
     __syncthreads(); // the slab is whole
     LdsSrc s{(lds_u8 *)slab};
@@ -605,17 +607,21 @@ __device__ __forceinline__ void nested_decode_pair(const NestedArgs &a) {
     const uint64_t r = base + lane;
     const bool valid = r < a.n;
     ListInfo li = {0, 0, 0, 0, false};
-    if (wave == 0) {
-        if (valid)
-            li = decode_outer<OSpec>(s, SLAB_GUARD + (long long)(gr.rec_lo - gr.aligned_lo),
-                                     SLAB_GUARD + (long long)(gr.rec_hi - gr.aligned_lo), r, to_stream, a);
+    const int rs = SLAB_GUARD + (int)(gr.rec_lo - gr.aligned_lo), re = SLAB_GUARD + (int)(gr.rec_hi - gr.aligned_lo);
+    if constexpr (SELF) {
+        if (valid) {
+            if (wave == 0) li = decode_outer<OSpec>(s, rs, re, r, to_stream, a);
+            else li = list_open(s, rec_open(s, rs, re), a);
+        }
+    } else if (wave == 0) {
+        if (valid) li = decode_outer<OSpec>(s, rs, re, r, to_stream, a);
         xl[lane] = li.count;
         xl[64 + lane] = li.dsize | ((uint32_t)li.big << 31);
         xl[128 + lane] = (uint32_t)li.dstart;
         xl[192 + lane] = (uint32_t)li.tstart;
     }
-    __syncthreads(); // the lists are posted
-    if (wave == 1) {
+    if constexpr (!SELF) __syncthreads(); // the lists are posted
+    if (!SELF && wave != 0) {
         li.count = xl[lane];
         const uint32_t ds = xl[64 + lane];
         li.dsize = ds & 0x7fffffffu;
@@ -631,7 +637,7 @@ __device__ __forceinline__ void nested_decode_pair(const NestedArgs &a) {
         if (r == a.n - 1) a.item_begin[a.n] = (uint32_t)(item_base + incl);
     }
     decode_group_items<ISpec, U>(s, li, excl, total, item_base, lane, to_stream, a, (uint32_t)wave * 64 * U,
-                                 2 * 64 * U);
+                                 P * 64 * U);
 }
 
 // Count kernel of the two-pass index: per group, the item total.

@@ -170,6 +170,18 @@ std::string generate_decode(const spec_schema *s) {
     return o.str();
 }
 
+// The nested decode's wave group (decode_nested_core.hpp nested_decode_pair): waves per group
+// and item rounds of 64 per wave in flight; build-time A/B only.
+#ifndef SPEC_AB_NESTED_WAVES
+#define SPEC_AB_NESTED_WAVES 2
+#endif
+#ifndef SPEC_AB_NESTED_U
+#define SPEC_AB_NESTED_U 1
+#endif
+#ifndef SPEC_AB_NESTED_SELF
+#define SPEC_AB_NESTED_SELF 0
+#endif
+
 // One-pass nested decode: outer and item fast paths where the schema has one.
 std::string generate_nested(const spec_nested_schema *s) {
     std::ostringstream o;
@@ -185,8 +197,10 @@ std::string generate_nested(const spec_nested_schema *s) {
       << "  spec::nested_decode_body<" << specs << ", false>(a);\n}\n"
       << "extern \"C\" __global__ __launch_bounds__(64) void spec_decode_nested3_jit(spec::NestedArgs a) {\n"
       << "  spec::nested_decode_body<" << specs << ", false, true>(a);\n}\n"
-      << "extern \"C\" __global__ __launch_bounds__(128) void spec_decode_nested_pair_jit(spec::NestedArgs a) {\n"
-      << "  spec::nested_decode_pair<" << specs << ">(a);\n}\n";
+      << "extern \"C\" __global__ __launch_bounds__(" << 64 * SPEC_AB_NESTED_WAVES
+      << ") void spec_decode_nested_pair_jit(spec::NestedArgs a) {\n"
+      << "  spec::nested_decode_pair<" << specs << ", " << SPEC_AB_NESTED_U << ", " << SPEC_AB_NESTED_WAVES
+      << ", " << (SPEC_AB_NESTED_SELF ? "true" : "false") << ">(a);\n}\n";
     return o.str();
 }
 
@@ -1343,7 +1357,7 @@ int jit_launch_nested(const spec_nested_schema *schema, const NestedArgs &a, int
     unsigned threads = 64;
     if (mode == NESTED_GROUPS && nested_pair() && e->fn[3]) { // a wave pair per group (nested_decode_pair)
         mode = 3;
-        threads = 128;
+        threads = 64 * SPEC_AB_NESTED_WAVES;
         lds = a.slab + 1024; // the posted lists: 4 words per record
     }
     if (mode == NESTED_ONEPASS) { // DEC_WAVES groups per block: one look-back per block
