@@ -94,6 +94,27 @@ def test_nested_large_records_generic(dev, name_len):
         spec_amd.set_jit(True)
 
 
+@pytest.mark.parametrize("big_at,shape", [(0, "huge"), (5, "double"), (15, "huge"), (15, "double")])
+def test_nested_pair_group_over_slab(dev, big_at, shape):
+    """The two-pass decode runs a wave pair per group (nested_decode_pair): one group of 64 records
+    with long lists in a batch of short ones is larger than the slab sized from the batch's mean,
+    so that group goes to wave 0 alone in two halves (or from HBM) while its neighbours run on
+    pairs; item offsets on both sides of it must still line up.  "double": ~2x the mean record
+    (each half of the group fits the slab); "huge": ~14x (the halves parse from HBM)."""
+    small = workload.nested(1024, seed=40 + big_at)
+    count, label_len = ((40, 60), (20, 40)) if shape == "huge" else ((6, 9), (6, 12))
+    big = workload.nested(64, seed=41 + big_at, count=count, label_len=label_len)
+    s1, e1 = O.encode_nested_batch(small)
+    s2, e2 = O.encode_nested_batch(big)
+    e1 = e1.astype(np.uint64)
+    e2 = e2.astype(np.uint64)
+    k = 64 * big_at  # the big group's first record
+    cut = int(e1[k - 1]) if k else 0
+    stream = np.concatenate([s1[:cut], s2, s1[cut:]])
+    ends = np.concatenate([e1[:k], e2 + np.uint64(cut), e1[k:] + np.uint64(s2.size)])
+    check_nested(dev, stream, ends, f"big group {big_at} {shape}", modes=("twopass", "twopass-xcd", "onepass"))
+
+
 def test_nested_golden(dev):
     g = np.load(os.path.join(GOLDEN, "nested_small.npz"), allow_pickle=False)
     got, _ = check_nested(dev, g["stream"], g["ends"], "golden")
