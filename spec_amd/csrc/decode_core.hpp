@@ -863,18 +863,35 @@ struct WideBatchesTo {
     }
 };
 
-// Half h of a wide record's fields (table entries [0, H) or [H, N), H on a batch boundary) for a
-// wave pair (decode_flat_pair): false when this half needs the generic path.  No status: the
-// pair's first wave writes it once both halves succeeded.  ERR: this half's error-mask bits in errs.
-template <class Spec, bool ERR = false>
+// Part h of P of a record's fields (table entries [lo(h), lo(h + 1)); for a pair the boundary is
+// the batch boundary near N/2) for the waves of one group (decode_flat_pair): false when this part
+// needs the generic path.  No status: the group's first wave writes it once every part succeeded.
+// ERR: this part's error-mask bits in errs.
+template <class Spec, int P>
+__host__ __device__ constexpr int flat_part_lo(int h) {
+    if (h >= P) return Spec::N;
+    if (P == 2) return h == 0 ? 0 : ((Spec::N / 2 + FAST_BATCH - 1) / FAST_BATCH) * FAST_BATCH;
+    return (h * Spec::N) / P;
+}
+template <class Spec, bool ERR, int P, int H = 0>
+__device__ __forceinline__ bool wide_part_run(const LdsSrc &s, const Trailer &tr, uint64_t r, const FieldSet &fs,
+                                              long long to_stream, int h, uint64_t &errs) {
+    if constexpr (H >= P) {
+        return true;
+    } else {
+        constexpr int J0 = flat_part_lo<Spec, P>(H), J1 = flat_part_lo<Spec, P>(H + 1);
+        if (h == H)
+            return WideBatchesTo<Spec, J0, J1, ERR>::run(s, (int)tr.tstart, (int)tr.dstart, tr.dsize, r, fs, to_stream, errs);
+        return wide_part_run<Spec, ERR, P, H + 1>(s, tr, r, fs, to_stream, h, errs);
+    }
+}
+template <class Spec, bool ERR = false, int P = 2>
 __device__ __forceinline__ bool fast_wide_half(const LdsSrc &s, int rs, int re, uint64_t r, const FieldSet &fs,
                                                long long to_stream, int h, uint64_t &errs) {
     if (re <= rs) return false;
     const Trailer tr = parse_trailer(s, rs, re);
     if ((tr.st != ST_OK) | (tr.big != Spec::big) | (tr.tsize != (Spec::big ? 6u : 3u) * (uint32_t)Spec::N)) return false;
-    constexpr int H = ((Spec::N / 2 + FAST_BATCH - 1) / FAST_BATCH) * FAST_BATCH;
-    if (h == 0) return WideBatchesTo<Spec, 0, H, ERR>::run(s, (int)tr.tstart, (int)tr.dstart, tr.dsize, r, fs, to_stream, errs);
-    return WideBatchesTo<Spec, H, Spec::N, ERR>::run(s, (int)tr.tstart, (int)tr.dstart, tr.dsize, r, fs, to_stream, errs);
+    return wide_part_run<Spec, ERR, P>(s, tr, r, fs, to_stream, h, errs);
 }
 
 // The whole record (columns, status, errmask); false: nothing final written, run the generic path.
@@ -1090,9 +1107,9 @@ __device__ __forceinline__ void decode_flat_once(const DecodeArgs &a) {
 // of the fields (fast_wide_half), wave 1 hands its verdict to wave 0 through LDS, and wave 0
 // writes the status — or, where either half needs it, runs the generic path over the whole
 // record (it rewrites every column).  Same LDS per 64 records, twice the waves: one wave's LDS
-// and memory latency overlaps the other's decode.  No error-mask variant (that one keeps a wave
-// per group).
-template <class Spec, bool ERR = false>
+// and memory latency overlaps the other's decode.  ERR: every wave's mask bits, OR-ed by wave 0.
+// P waves per group in general (P parts of the fields; build-time A/B, jit.cpp SPEC_AB_FLAT_WAVES).
+template <class Spec, bool ERR = false, int P = 2>
 __device__ __forceinline__ void decode_flat_pair(const DecodeArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6;
@@ -1121,14 +1138,14 @@ __device__ __forceinline__ void decode_flat_pair(const DecodeArgs &a) {
         }
         return;
     }
-    for (uint32_t c = (uint32_t)wave; c < cur.chunks; c += 2)
+    for (uint32_t c = (uint32_t)wave; c < cur.chunks; c += P)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void *)(slab + SLAB_GUARD + c * 1024),
                                                  16, (uint32_t)cur.aligned_lo + c * 1024 + lane * 16, 0, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // the chunk straddling the stream end is refilled by the wave that loaded it
     const uint64_t tail = a.stream_len & ~15ull;
     if (tail < a.stream_len && tail >= cur.aligned_lo && tail < cur.aligned_lo + (uint64_t)cur.chunks * 1024 &&
-        (int)(((tail - cur.aligned_lo) >> 10) & 1) == wave && lane < 16 && tail + lane < a.stream_len)
+        (int)(((tail - cur.aligned_lo) >> 10) % P) == wave && lane < 16 && tail + lane < a.stream_len)
         slab[SLAB_GUARD + (tail - cur.aligned_lo) + lane] = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)(tail + lane), 0, 0);
     __syncthreads(); // the slab is whole
     LdsSrc s{(lds_u8 *)slab};
@@ -1136,17 +1153,25 @@ __device__ __forceinline__ void decode_flat_pair(const DecodeArgs &a) {
     const int re = SLAB_GUARD + (int)(cur.rec_hi - cur.aligned_lo);
     const long long to_stream = (long long)cur.aligned_lo - SLAB_GUARD;
     uint64_t errs = 0;
-    const bool ok = valid && fast_wide_half<Spec, ERR>(s, rs, re, r, a.f, to_stream, wave, errs);
-    uint64_t *xerr = (uint64_t *)(xch + 64); // ERR: wave 1's mask bits (LDS slab + 256 .. + 768)
-    if (wave == 1) {
-        xch[lane] = ok ? 1u : 0u;
-        if constexpr (ERR) xerr[lane] = errs;
+    const bool ok = valid && fast_wide_half<Spec, ERR, P>(s, rs, re, r, a.f, to_stream, wave, errs);
+    // waves 1 .. P-1: verdicts at slab + 256 (w - 1), ERR: mask bits after them (512 B per wave)
+    uint64_t *xerr = (uint64_t *)(xch + 64 * (P - 1));
+    if (wave > 0) {
+        xch[64 * (wave - 1) + lane] = ok ? 1u : 0u;
+        if constexpr (ERR) xerr[64 * (wave - 1) + lane] = errs;
     }
-    __syncthreads(); // wave 1's verdict (and its column stores) are in
+    __syncthreads(); // the other waves' verdicts (and their column stores) are in
     if (wave == 0 && valid) {
-        if (ok && xch[lane]) {
+        bool all = ok;
+        uint64_t m = errs;
+#pragma unroll
+        for (int w = 1; w < P; w++) {
+            all = all && xch[64 * (w - 1) + lane] != 0;
+            if constexpr (ERR) m |= xerr[64 * (w - 1) + lane];
+        }
+        if (all) {
             if (a.f.status) a.f.status[r] = ST_OK;
-            if constexpr (ERR) a.f.errmask[r] = errs | xerr[lane];
+            if constexpr (ERR) a.f.errmask[r] = m;
         } else {
             decode_record_generic(s, rs, re, r, a.f, to_stream);
         }

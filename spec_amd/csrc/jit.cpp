@@ -148,6 +148,11 @@ void emit_spec(std::ostringstream &o, const char *name, const spec_schema *s) {
     o << "};\n  static constexpr bool big = " << (big ? "true" : "false") << ";\n};\n";
 }
 
+// waves per 64-record group of the flat decode (decode_core.hpp decode_flat_pair); build-time A/B
+#ifndef SPEC_AB_FLAT_WAVES
+#define SPEC_AB_FLAT_WAVES 2
+#endif
+
 std::string generate_decode(const spec_schema *s) {
     std::ostringstream o;
     o << "#include \"decode_core.hpp\"\n";
@@ -163,10 +168,13 @@ std::string generate_decode(const spec_schema *s) {
       << "  spec::decode_flat_entry<" << pers << ", GenSpec, true>(a);\n}\n";
     // the wave-pair kernel (decode_core.hpp decode_flat_pair), the default launch for every
     // schema (decode_flat.hip SPEC_AB_FLAT_PAIR)
-    o << "extern \"C\" __global__ __launch_bounds__(128) void spec_decode_flat" << w << "_pair_jit(spec::DecodeArgs a) {\n"
-      << "  spec::decode_flat_pair<GenSpec>(a);\n}\n"
-      << "extern \"C\" __global__ __launch_bounds__(128) void spec_decode_flat" << w << "_err_pair_jit(spec::DecodeArgs a) {\n"
-      << "  spec::decode_flat_pair<GenSpec, true>(a);\n}\n";
+    const int P = SPEC_AB_FLAT_WAVES;
+    o << "extern \"C\" __global__ __launch_bounds__(" << 64 * P << ") void spec_decode_flat" << w
+      << "_pair_jit(spec::DecodeArgs a) {\n"
+      << "  spec::decode_flat_pair<GenSpec, false, " << P << ">(a);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(" << 64 * P << ") void spec_decode_flat" << w
+      << "_err_pair_jit(spec::DecodeArgs a) {\n"
+      << "  spec::decode_flat_pair<GenSpec, true, " << P << ">(a);\n}\n";
     return o.str();
 }
 
@@ -1310,8 +1318,10 @@ int jit_launch_decode_flat(const spec_schema *schema, const DecodeArgs &a, doubl
         size_t size = sizeof(args);
         void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                          HIP_LAUNCH_PARAM_END};
-        hipError_t e = hipModuleLaunchKernel(ent->fn[a.f.errmask ? 3 : 2], (unsigned)groups, 1, 1, 128, 1, 1,
-                                             args.slab + (a.f.errmask ? 768 : 256), stream, nullptr, extra);
+        hipError_t e = hipModuleLaunchKernel(ent->fn[a.f.errmask ? 3 : 2], (unsigned)groups, 1, 1,
+                                             64 * SPEC_AB_FLAT_WAVES, 1, 1,
+                                             args.slab + (SPEC_AB_FLAT_WAVES - 1) * (a.f.errmask ? 768 : 256), stream,
+                                             nullptr, extra);
         return e == hipSuccess ? 1 : -1;
     }
     const DecodeLaunch L = decode_launch(a.n - a.r0, avg_record, device_cus(), persistent_decode(), decode_wpb());
