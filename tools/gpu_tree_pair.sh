@@ -16,6 +16,6 @@ for v in default "$@"; do
     python3 -c "import json; d=json.load(open('$OUT/bench_$v$i.json'))['tree_pkg1']; print('$v', d['decode_ms'], d['encode_ms'], d['bit_exact_and_parity_vs_oracle'])"
   done
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/prof_$v -o run -- python3 tools/bench_tree.py > $OUT/prof_$v.log 2>&1 || { tail -n 20 $OUT/prof_$v.log; exit 1; }
-  f=$(find $OUT/prof_$v -name "*kernel_trace.csv" | head -n 1); python3 tools/tree_trace.py $f 1 | grep -E "group_0|kernels"; python3 tools/tree_enc_trace.py $f | tail -n 6
+  f=$(find $OUT/prof_$v -name "*kernel_trace.csv" | head -n 1); python3 tools/tree_trace.py $f 1 | grep -E "group_0|list_apply|kernels"; python3 tools/tree_enc_trace.py $f | tail -n 6
 done
 cp /tmp/libspec_amd_default.so spec_amd/libspec_amd.so
