@@ -67,16 +67,16 @@ def parse(argv=None):
 
 
 def source_rev() -> str:
-    """Hash of the engine's device and host sources (spec_amd/csrc): the code revision a kernel
-    time or a PMC traffic figure belongs to."""
+    """Hash of the engine's device and host sources (spec_amd/csrc) and its public header
+    (include/): the code revision a kernel time or a PMC traffic figure belongs to."""
     import hashlib
 
     h = hashlib.sha1()
-    d = os.path.join(ROOT, "spec_amd", "csrc")
-    for f in sorted(os.listdir(d)):
-        if f.endswith((".hip", ".hpp", ".cpp", ".h")):
-            h.update(f.encode())
-            h.update(open(os.path.join(d, f), "rb").read())
+    for d in (os.path.join(ROOT, "spec_amd", "csrc"), os.path.join(ROOT, "include")):
+        for f in sorted(os.listdir(d)):
+            if f.endswith((".hip", ".hpp", ".cpp", ".h")):
+                h.update(f.encode())
+                h.update(open(os.path.join(d, f), "rb").read())
     return h.hexdigest()[:12]
 
 

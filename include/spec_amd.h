@@ -33,14 +33,20 @@
 extern "C" {
 #endif
 
-#define SPEC_AMD_ABI_VERSION 1
+/* ABI version history (a binding compares spec_abi_version() with the header it was built against,
+ * and spec_struct_size / spec_struct_offset with its own struct mirrors):
+ *   1  rounds 1-4: SPEC_MAX_FIELDS 64, SPEC_TREE_MAX_FIELDS 256 (spec_schema 260 B, spec_tree 2052 B);
+ *   2  SPEC_MAX_FIELDS / SPEC_NESTED_MAX_FIELDS / SPEC_TREE_MAX_FIELDS 1024: spec_schema 4100 B,
+ *      spec_nested_schema.item at offset 4100, spec_tree 8196 B; spec_struct_size / _offset added. */
+#define SPEC_AMD_ABI_VERSION 2
 /* Fields of a flat schema.  Schemas of up to 64 fields run the schema-specialised kernels; wider
  * ones decode in chunks of 64 fields (the generic kernel once per chunk, each getter against the
  * record's whole table) and encode through the wide kernels, whose field set the call writes into
- * the workspace.  A nested schema's halves hold up to 1024 fields each (together at most
- * SPEC_TREE_MAX_FIELDS - 1 when a half holds more than 64: such a schema decodes in chunks of 64
+ * the workspace.  A nested schema's halves hold up to 1024 fields each; when a half holds more
+ * than 64, outer + item fields (the list field included) are at most SPEC_TREE_MAX_FIELDS, else
+ * every nested entry point returns SPEC_E_INVALID_ARGUMENT: such a schema decodes in chunks of 64
  * fields per half and encodes through the schema-tree encoder, with its scratch allocated
- * stream-ordered by the call). */
+ * stream-ordered by the call. */
 #define SPEC_MAX_FIELDS 1024
 #define SPEC_NESTED_MAX_FIELDS 1024
 
@@ -359,8 +365,28 @@ int spec_shard_encode(spec_shard *c, const spec_schema *schema, const void *cons
                       uint64_t *byte_bases);
 int spec_shard_sync(spec_shard *c);
 
-/* ---- introspection ---- */
+/* ---- introspection ----
+ * spec_abi_version: SPEC_AMD_ABI_VERSION of the library (a binding refuses to run on a mismatch).
+ * spec_struct_size(which): sizeof the struct as the library was built (0 for an unknown id);
+ * spec_struct_offset(which, member): offsetof its member-th member in declaration order
+ * ((size_t)-1 past the last member or for an unknown id).  A binding that mirrors these structs
+ * (cgo, ctypes) checks its own layout against them once at load time. */
+typedef enum spec_abi_struct {
+    SPEC_ABI_SPAN = 0,          /* spec_span {off, len} */
+    SPEC_ABI_FIELD = 1,         /* spec_field {tag, kind, reserved} */
+    SPEC_ABI_SCHEMA = 2,        /* spec_schema {nfields, fields} */
+    SPEC_ABI_NESTED_SCHEMA = 3, /* spec_nested_schema {outer, item} */
+    SPEC_ABI_TREE_FIELD = 4,    /* spec_tree_field {tag, kind, elem, parent, reserved} */
+    SPEC_ABI_TREE = 5,          /* spec_tree {nfields, fields} */
+    SPEC_ABI_TREE_TABLE = 6,    /* spec_tree_table {parent, field, rel, shape, first_column, ncolumns} */
+    SPEC_ABI_TREE_COLUMN = 7,   /* spec_tree_column {table, field, role, kind, width} */
+    SPEC_ABI_LZ4_BLOCK = 8,     /* spec_lz4_block {src_off, src_len, stored} */
+    SPEC_ABI_LZ4_STATE = 9,     /* spec_lz4_state {in_frame, block_max, flags, reserved} */
+    SPEC_ABI_NSTRUCTS = 10
+} spec_abi_struct;
 int spec_abi_version(void);
+size_t spec_struct_size(int which);
+size_t spec_struct_offset(int which, int member);
 int spec_kind_width(int kind);
 const char *spec_strerror(int rc);
 int spec_last_hip_error(void);

@@ -17,7 +17,7 @@
  * Signed values use zigzag like Go's encoding/binary.PutVarint.  Overflow rules follow
  * encoding/binary.Uvarint with MaxLen32 = 5, MaxLen64 = 10.
  * Keep this the ONLY place the varint layout is defined on the oracle side; the device
- * side mirror is spec_amd/csrc/spec_varint.hpp.
+ * side mirror is spec_amd/csrc/spec_device.hpp (rvarint_bf and the encoders' varint emitters).
  */
 #include "spec_oracle.h"
 

@@ -18,6 +18,10 @@ SPEC_MAX_FIELDS = 1024  # include/spec_amd.h (schemas over 64 fields: chunked de
 SPEC_NESTED_MAX_FIELDS = 1024  # (halves over 64 fields: chunked decode, tree-encoder encode)
 
 
+class SpecSpan(C.Structure):
+    _fields_ = [("off", C.c_uint32), ("len", C.c_uint32)]
+
+
 class SpecField(C.Structure):
     _fields_ = [("tag", C.c_uint16), ("kind", C.c_uint8), ("reserved", C.c_uint8)]
 
@@ -70,8 +74,40 @@ def lib():
             raise RuntimeError(f"spec_amd: {LIB_PATH} not built (run make -C spec_amd/csrc)")
         L = C.CDLL(LIB_PATH)
         _declare(L)
+        if L.spec_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"spec_amd: {LIB_PATH} has ABI version {L.spec_abi_version()}, this binding "
+                               f"was written for {ABI_VERSION} (rebuild the library)")
+        bad = struct_mismatches(L)
+        if bad:
+            raise RuntimeError(f"spec_amd: struct layout differs from {LIB_PATH}: {bad}")
         _lib = L
     return _lib
+
+
+# include/spec_amd.h: SPEC_AMD_ABI_VERSION and the spec_abi_struct ids of the mirrored structs
+ABI_VERSION = 2
+
+
+def struct_mirrors():
+    """{spec_abi_struct id: ctypes mirror} — every public struct this binding mirrors."""
+    from .lz4 import Lz4Block, Lz4State
+
+    return {0: SpecSpan, 1: SpecField, 2: SpecSchema, 3: SpecNestedSchema, 4: SpecTreeField, 5: SpecTree,
+            6: SpecTreeTable, 7: SpecTreeColumn, 8: Lz4Block, 9: Lz4State}
+
+
+def struct_mismatches(L) -> list:
+    """(struct id, what, ours, the library's) for every size / member offset that differs."""
+    bad = []
+    for which, T in struct_mirrors().items():
+        if C.sizeof(T) != L.spec_struct_size(which):
+            bad.append((T.__name__, "sizeof", C.sizeof(T), L.spec_struct_size(which)))
+        for m, (name, _) in enumerate(T._fields_):
+            if getattr(T, name).offset != L.spec_struct_offset(which, m):
+                bad.append((T.__name__, name, getattr(T, name).offset, L.spec_struct_offset(which, m)))
+        if L.spec_struct_offset(which, len(T._fields_)) != C.c_size_t(-1).value:
+            bad.append((T.__name__, "members", len(T._fields_), "more"))
+    return bad
 
 
 def _declare(L):
@@ -83,6 +119,10 @@ def _declare(L):
     L.spec_last_hip_error.restype = C.c_int
     L.spec_last_hip_error.argtypes = []
     L.spec_abi_version.argtypes = []
+    L.spec_struct_size.argtypes = [C.c_int]
+    L.spec_struct_size.restype = C.c_size_t
+    L.spec_struct_offset.argtypes = [C.c_int, C.c_int]
+    L.spec_struct_offset.restype = C.c_size_t
     L.spec_decode_flat.argtypes = [C.POINTER(SpecSchema), vp, C.c_uint64, vp, C.c_uint64,
                                    C.POINTER(vp), vp, vp]
     L.spec_decode_flat_range.argtypes = [C.POINTER(SpecSchema), vp, C.c_uint64, vp, C.c_uint64, C.c_uint64,

@@ -3,7 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
+#include <new>
 #include <vector>
 
 #include "../../include/spec_amd.h"
@@ -29,24 +31,15 @@ int kind_width(int kind) {
 // Table order a Writer produces for this schema: messageStack.insert over the tags in write
 // order, insertion sort where an equal tag written later moves before the earlier one
 // (internal/writer/stack_msg.go:37-61).  order[j] = schema index of the j-th table entry.
+// The insertion moves a new entry left past every entry whose tag is >= its own, so the result
+// is the unique order by (tag ascending, write index descending): sorted in O(n log n) here
+// (a 1024-field schema in reverse tag order cost ~0.5 M swaps per call as an insertion sort).
 template <class T>
 void table_order(const spec_schema *s, T *order) {
-    uint16_t tags[SPEC_MAX_FIELDS];
-    uint16_t idx[SPEC_MAX_FIELDS];
-    for (uint32_t f = 0; f < s->nfields; f++) {
-        tags[f] = s->fields[f].tag;
-        idx[f] = (uint16_t)f;
-        for (int i = (int)f; i > 0; i--) {
-            if (tags[i - 1] < tags[i]) break;
-            uint16_t t = tags[i - 1];
-            tags[i - 1] = tags[i];
-            tags[i] = t;
-            uint16_t x = idx[i - 1];
-            idx[i - 1] = idx[i];
-            idx[i] = x;
-        }
-    }
-    for (uint32_t j = 0; j < s->nfields; j++) order[j] = (T)idx[j];
+    uint32_t key[SPEC_MAX_FIELDS]; // tag << 16 | (0xffff - index): ascending = the Writer's order
+    for (uint32_t f = 0; f < s->nfields; f++) key[f] = (uint32_t)s->fields[f].tag << 16 | (0xffffu - f);
+    std::sort(key, key + s->nfields);
+    for (uint32_t j = 0; j < s->nfields; j++) order[j] = (T)(0xffffu - (key[j] & 0xffffu));
 }
 
 int check_schema(const spec_schema *s) {
@@ -62,6 +55,11 @@ int check_nested(const spec_nested_schema *s, uint32_t *list_f) {
     // encoder — nested_decode_chunks, nested_encode_wide)
     if (!s || s->outer.nfields > SPEC_MAX_FIELDS || check_schema(&s->item))
         return SPEC_E_INVALID_ARGUMENT;
+    // a wide schema encodes as one schema tree of outer + item fields: the same limit for decode,
+    // so a schema either decodes and encodes or is rejected up front
+    if ((s->outer.nfields > SPEC_KFIELDS || s->item.nfields > SPEC_KFIELDS) &&
+        s->outer.nfields + s->item.nfields > SPEC_TREE_MAX_FIELDS)
+        return SPEC_E_INVALID_ARGUMENT;
     int lists = 0;
     for (uint32_t f = 0; f < s->outer.nfields; f++) {
         if (s->outer.fields[f].kind == SPEC_KIND_LIST) {
@@ -74,42 +72,75 @@ int check_nested(const spec_nested_schema *s, uint32_t *list_f) {
     return lists == 1 ? SPEC_OK : SPEC_E_INVALID_ARGUMENT;
 }
 
-// ---- pinned uploads: per-call kernel data too large for the kernel arguments (the field set of a
-// wide schema) goes to the device from a ring of pinned slots per device, a slot reused once the
-// copy out of it has run (its event), so a call never synchronises with the device
-struct UploadRing {
-    static constexpr int SLOTS = 8;
-    struct Slot {
-        uint8_t *p = nullptr;
-        size_t cap = 0;
-        hipEvent_t ev = nullptr;
-    } slot[SLOTS];
-    int next = 0;
-};
-std::mutex g_upload_mu;
-UploadRing g_upload[64];
+} // namespace
 
-hipError_t upload_async(void *dst, const void *src, size_t bytes, hipStream_t st) {
+namespace spec {
+// ---- pinned uploads: per-call kernel data too large for the kernel arguments (a wide schema's
+// field set, a schema tree's descriptor block) goes to the device from a pool of pinned slots
+// per device.  A slot is reused once the copy out of it has run (its event has completed,
+// hipEventQuery: no wait); when every slot is still in flight the pool grows by one, so a call
+// never waits on the device, and the lock (one per device) is held only to claim or release a
+// slot, never across a HIP copy.  Such a call cannot be captured into a HIP graph (its copy
+// source is a pooled slot that later calls refill).
+namespace {
+struct UploadSlot {
+    uint8_t *p = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    bool busy = false; // claimed by a call that has not yet recorded its event
+};
+struct UploadPool {
+    std::mutex mu;
+    std::vector<UploadSlot *> slots;
+};
+UploadPool g_upload[64];
+} // namespace
+
+hipError_t pinned_upload(void *dst, const void *src, size_t bytes, hipStream_t st) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-    std::lock_guard<std::mutex> lk(g_upload_mu);
-    UploadRing &R = g_upload[dev];
-    UploadRing::Slot &S = R.slot[R.next];
-    R.next = (R.next + 1) % UploadRing::SLOTS;
-    if (S.ev && (e = hipEventSynchronize(S.ev)) != hipSuccess) return e; // its previous copy has run
-    if (!S.ev && (e = hipEventCreateWithFlags(&S.ev, hipEventDisableTiming)) != hipSuccess) return e;
-    if (S.cap < bytes) {
-        if (S.p) (void)hipHostFree(S.p);
-        S.p = nullptr;
-        S.cap = 0;
-        if ((e = hipHostMalloc((void **)&S.p, bytes, hipHostMallocDefault)) != hipSuccess) return e;
-        S.cap = bytes;
+    UploadPool &P = g_upload[dev];
+    UploadSlot *S = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(P.mu);
+        for (UploadSlot *s : P.slots)
+            if (!s->busy && (!s->ev || hipEventQuery(s->ev) == hipSuccess)) {
+                S = s;
+                break;
+            }
+        if (!S) {
+            S = new (std::nothrow) UploadSlot();
+            if (!S) return hipErrorOutOfMemory;
+            P.slots.push_back(S);
+        }
+        S->busy = true;
     }
-    memcpy(S.p, src, bytes);
-    if ((e = hipMemcpyAsync(dst, S.p, bytes, hipMemcpyHostToDevice, st)) != hipSuccess) return e;
-    return hipEventRecord(S.ev, st);
+    auto fill = [&]() -> hipError_t {
+        hipError_t r;
+        if (!S->ev && (r = hipEventCreateWithFlags(&S->ev, hipEventDisableTiming)) != hipSuccess) return r;
+        if (S->cap < bytes) {
+            if (S->p) (void)hipHostFree(S->p);
+            S->p = nullptr;
+            S->cap = 0;
+            if ((r = hipHostMalloc((void **)&S->p, bytes, hipHostMallocDefault)) != hipSuccess) return r;
+            S->cap = bytes;
+        }
+        memcpy(S->p, src, bytes);
+        if ((r = hipMemcpyAsync(dst, S->p, bytes, hipMemcpyHostToDevice, st)) != hipSuccess) return r;
+        return hipEventRecord(S->ev, st);
+    };
+    e = fill();
+    std::lock_guard<std::mutex> lk(P.mu);
+    S->busy = false;
+    return e;
+}
+} // namespace spec
+
+namespace {
+hipError_t upload_async(void *dst, const void *src, size_t bytes, hipStream_t st) {
+    return spec::pinned_upload(dst, src, bytes, st);
 }
 
 int hip_rc(hipError_t e) {
@@ -266,6 +297,59 @@ int encode_flat_passes(const spec_schema *schema, const void *const *columns, co
 extern "C" {
 
 int spec_abi_version(void) { return SPEC_AMD_ABI_VERSION; }
+
+size_t spec_struct_size(int which) {
+    switch (which) {
+    case SPEC_ABI_SPAN: return sizeof(spec_span);
+    case SPEC_ABI_FIELD: return sizeof(spec_field);
+    case SPEC_ABI_SCHEMA: return sizeof(spec_schema);
+    case SPEC_ABI_NESTED_SCHEMA: return sizeof(spec_nested_schema);
+    case SPEC_ABI_TREE_FIELD: return sizeof(spec_tree_field);
+    case SPEC_ABI_TREE: return sizeof(spec_tree);
+    case SPEC_ABI_TREE_TABLE: return sizeof(spec_tree_table);
+    case SPEC_ABI_TREE_COLUMN: return sizeof(spec_tree_column);
+    case SPEC_ABI_LZ4_BLOCK: return sizeof(spec_lz4_block);
+    case SPEC_ABI_LZ4_STATE: return sizeof(spec_lz4_state);
+    }
+    return 0;
+}
+
+size_t spec_struct_offset(int which, int member) {
+#define SPEC_OFFS(T, ...)                                                                                              \
+    do {                                                                                                               \
+        const size_t o[] = {__VA_ARGS__};                                                                              \
+        return member >= 0 && member < (int)(sizeof(o) / sizeof(o[0])) ? o[member] : (size_t)-1;                       \
+    } while (0)
+    switch (which) {
+    case SPEC_ABI_SPAN: SPEC_OFFS(spec_span, offsetof(spec_span, off), offsetof(spec_span, len));
+    case SPEC_ABI_FIELD:
+        SPEC_OFFS(spec_field, offsetof(spec_field, tag), offsetof(spec_field, kind), offsetof(spec_field, reserved));
+    case SPEC_ABI_SCHEMA: SPEC_OFFS(spec_schema, offsetof(spec_schema, nfields), offsetof(spec_schema, fields));
+    case SPEC_ABI_NESTED_SCHEMA:
+        SPEC_OFFS(spec_nested_schema, offsetof(spec_nested_schema, outer), offsetof(spec_nested_schema, item));
+    case SPEC_ABI_TREE_FIELD:
+        SPEC_OFFS(spec_tree_field, offsetof(spec_tree_field, tag), offsetof(spec_tree_field, kind),
+                  offsetof(spec_tree_field, elem), offsetof(spec_tree_field, parent),
+                  offsetof(spec_tree_field, reserved));
+    case SPEC_ABI_TREE: SPEC_OFFS(spec_tree, offsetof(spec_tree, nfields), offsetof(spec_tree, fields));
+    case SPEC_ABI_TREE_TABLE:
+        SPEC_OFFS(spec_tree_table, offsetof(spec_tree_table, parent), offsetof(spec_tree_table, field),
+                  offsetof(spec_tree_table, rel), offsetof(spec_tree_table, shape),
+                  offsetof(spec_tree_table, first_column), offsetof(spec_tree_table, ncolumns));
+    case SPEC_ABI_TREE_COLUMN:
+        SPEC_OFFS(spec_tree_column, offsetof(spec_tree_column, table), offsetof(spec_tree_column, field),
+                  offsetof(spec_tree_column, role), offsetof(spec_tree_column, kind),
+                  offsetof(spec_tree_column, width));
+    case SPEC_ABI_LZ4_BLOCK:
+        SPEC_OFFS(spec_lz4_block, offsetof(spec_lz4_block, src_off), offsetof(spec_lz4_block, src_len),
+                  offsetof(spec_lz4_block, stored));
+    case SPEC_ABI_LZ4_STATE:
+        SPEC_OFFS(spec_lz4_state, offsetof(spec_lz4_state, in_frame), offsetof(spec_lz4_state, block_max),
+                  offsetof(spec_lz4_state, flags), offsetof(spec_lz4_state, reserved));
+    }
+#undef SPEC_OFFS
+    return (size_t)-1;
+}
 
 int spec_kind_width(int kind) { return kind_width(kind); }
 

@@ -33,6 +33,9 @@ int launch_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends,
                                uint64_t *consumed, int32_t *status, void *ws, hipStream_t stream);
 int device_cus(); // CUs of the current device (cached)
 void note_hip_error(hipError_t e); // capi.hip: remembered for spec_last_hip_error()
+// capi.hip: bytes copied to the device on st from a pooled pinned slot of the current device (no
+// host wait: the pool grows while every slot's copy is in flight; not graph-capturable)
+hipError_t pinned_upload(void *dst, const void *src, size_t bytes, hipStream_t st);
 bool persistent_decode(); // build-time A/B variants (decode_flat.hip): SPEC_AB_PERSIST
 unsigned decode_wpb();     // SPEC_AB_WPB (waves per block, default 1)
 int flat_pair();

@@ -547,43 +547,15 @@ size_t enc_plan(const Layout &L, const uint64_t *rows, EncWs &w) {
 } // namespace
 
 namespace {
-// Pinned staging for the descriptor + buffer block each spec_encode_tree call uploads: a ring of
-// slots per device, a slot reused once the copy out of it has run (its event), so the call
-// never synchronises with the device.
-struct UploadRing {
-    static constexpr int SLOTS = 16;
-    struct Slot {
-        uint8_t *p = nullptr;
-        hipEvent_t ev = nullptr;
-    } slot[SLOTS];
-    int next = 0;
-};
-std::mutex g_ring_mu;
-UploadRing g_rings[64];
-
-// copies the workspace head [desc | bufs | err = 0] (ENC_HEAD bytes) to the device on st from a
-// pinned slot; false on a HIP error
+// copies the workspace head [desc | bufs | err = 0] (ENC_HEAD bytes) to the device on st through
+// the library's pinned upload pool (spec::pinned_upload: no host wait on the device); false on a
+// HIP error
 bool upload_head(const TreeDesc &desc, const TreeBufs &bufs, void *dhead, hipStream_t st) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
-    std::lock_guard<std::mutex> lk(g_ring_mu);
-    UploadRing &R = g_rings[dev];
-    UploadRing::Slot &S = R.slot[R.next];
-    R.next = (R.next + 1) % UploadRing::SLOTS;
-    if (!S.p) {
-        if (hipHostMalloc((void **)&S.p, ENC_HEAD, hipHostMallocDefault) != hipSuccess ||
-            hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) != hipSuccess) {
-            S.p = nullptr;
-            return false;
-        }
-    } else if (hipEventSynchronize(S.ev) != hipSuccess) { // the slot's previous copy has run
-        return false;
-    }
-    memset(S.p, 0, ENC_HEAD);
-    memcpy(S.p + ENC_HEAD_DESC, &desc, sizeof(TreeDesc));
-    memcpy(S.p + ENC_HEAD_BUFS, &bufs, sizeof(TreeBufs));
-    return hipMemcpyAsync(dhead, S.p, ENC_HEAD, hipMemcpyHostToDevice, st) == hipSuccess &&
-           hipEventRecord(S.ev, st) == hipSuccess;
+    thread_local std::vector<uint8_t> h;
+    h.assign(ENC_HEAD, 0);
+    memcpy(h.data() + ENC_HEAD_DESC, &desc, sizeof(TreeDesc));
+    memcpy(h.data() + ENC_HEAD_BUFS, &bufs, sizeof(TreeBufs));
+    return spec::pinned_upload(dhead, h.data(), ENC_HEAD, st) == hipSuccess;
 }
 } // namespace
 
@@ -659,13 +631,23 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
     B->err = (uint32_t *)(ws + w.err);
     const TreeDesc *Dd = (const TreeDesc *)(ws + w.desc);
     TreeBufs *Bd = (TreeBufs *)(ws + w.bufs);
-    bool ok = upload_head(L.desc, *B, ws, st);
     // the generated writers and size passes (jit.cpp) for message tables, else the run-time row kernels
     const hipFunction_t *jit = jit_tree_kernels(L.desc);
     // level-fused launches (tree_core.hpp TableSet) when the generated module has them: the
     // tables of one height sized together (children have smaller heights), the tables of one
     // depth written together (owners have smaller depths)
     const bool sets = jit && jit[4 * TREE_MAX_T] && jit[4 * TREE_MAX_T + 1];
+    // the run-time writer keeps a message's field ends in LDS ([wave][field][lane], 256 B per field
+    // per wave, 160 KiB per block at most): a table of more than 640 direct fields needs the
+    // generated writer (jit.cpp).  Checked before anything is issued, so a call that cannot run
+    // leaves the stream, *total and out untouched.
+    for (uint32_t x = 0; !sets && out && x < L.nt; x++)
+        if (rows[x] && L.desc.t[x].shape == SHAPE_MESSAGE && (size_t)L.desc.t[x].nd * 64 * sizeof(uint32_t) > 163840) {
+            delete B;
+            delete Lp;
+            return SPEC_E_TOO_LARGE;
+        }
+    bool ok = upload_head(L.desc, *B, ws, st);
     int height[TREE_MAX_T] = {0}, depth[TREE_MAX_T] = {0}, maxh = 0, maxd = 0;
     for (uint32_t x = 1; x < L.nt; x++) depth[x] = depth[L.desc.t[x].parent] + 1;
     for (int x = (int)L.nt - 1; x > 0; x--) {

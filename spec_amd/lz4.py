@@ -19,6 +19,11 @@ from .batch import _check_dev, _ptr, _stream_handle
 BLOCK_DTYPE = np.dtype([("src_off", "<u8"), ("src_len", "<u4"), ("stored", "<u4")])
 
 
+class Lz4Block(C.Structure):
+    """spec_lz4_block (the records BLOCK_DTYPE arrays hold)."""
+    _fields_ = [("src_off", C.c_uint64), ("src_len", C.c_uint32), ("stored", C.c_uint32)]
+
+
 class Lz4State(C.Structure):
     """An open frame carried across calls (zero for a new connection)."""
     _fields_ = [("in_frame", C.c_uint32), ("block_max", C.c_uint32), ("flags", C.c_uint32), ("reserved", C.c_uint32)]

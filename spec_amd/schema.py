@@ -132,8 +132,14 @@ class NestedSchema:
         self.item = Schema(item) if not isinstance(item, Schema) else item
         from ._lib import SPEC_NESTED_MAX_FIELDS
 
+        from ._lib import SPEC_TREE_MAX_FIELDS
+
         if max(len(self.outer), len(self.item)) > SPEC_NESTED_MAX_FIELDS:
             raise ValueError(f"a nested schema's outer and item hold at most {SPEC_NESTED_MAX_FIELDS} fields each")
+        # a half of more than 64 fields encodes as one schema tree (check_nested, capi.hip)
+        if max(len(self.outer), len(self.item)) > 64 and len(self.outer) + len(self.item) > SPEC_TREE_MAX_FIELDS:
+            raise ValueError(f"a nested schema with a half of more than 64 fields holds at most "
+                             f"{SPEC_TREE_MAX_FIELDS} fields in all")
         lists = [i for i, f in enumerate(self.outer.fields) if f.kind == Kind.LIST]
         if len(lists) != 1 or any(f.kind == Kind.LIST for f in self.item.fields):
             raise ValueError("outer needs exactly one Kind.LIST field; items must be flat")

@@ -23,6 +23,12 @@
 
 int main(void) {
     const uint64_t n = 10007;
+    /* the load-time check a binding makes (the Go init()) */
+    if (spec_abi_version() != SPEC_AMD_ABI_VERSION || spec_struct_size(SPEC_ABI_SCHEMA) != sizeof(spec_schema) ||
+        spec_struct_offset(SPEC_ABI_NESTED_SCHEMA, 1) != offsetof(spec_nested_schema, item)) {
+        fprintf(stderr, "ABI mismatch\n");
+        return 1;
+    }
     /* schema: 1 int64, 2 string, 5 float64, 9 bool, 300 uint32 (big table) */
     spec_schema s;
     memset(&s, 0, sizeof(s));

@@ -27,9 +27,60 @@ def test_library_has_gfx950_code_object():
     assert b"amdgcn-amd-amdhsa--gfx950" in data
 
 
+def test_struct_layouts_match_header():
+    """ABI version 2 (SPEC_MAX_FIELDS / SPEC_TREE_MAX_FIELDS 64 / 256 -> 1024 grew spec_schema to
+    4100 B and moved spec_nested_schema.item to offset 4100): every ctypes mirror has the
+    library's sizeof and member offsets (spec_struct_size / spec_struct_offset), and the library's
+    agree with a plain C program compiled here against include/spec_amd.h (gcc)."""
+    import os
+    import re
+    import tempfile
+
+    from spec_amd.lz4 import BLOCK_DTYPE, Lz4Block
+
+    L = spec_amd.lib()
+    assert L.spec_abi_version() == _lib.ABI_VERSION == 2
+    hdr = open(_lib.HEADER_PATH).read()
+    assert int(re.search(r"#define SPEC_AMD_ABI_VERSION (\d+)", hdr).group(1)) == _lib.ABI_VERSION
+    for name in ("SPEC_MAX_FIELDS", "SPEC_NESTED_MAX_FIELDS", "SPEC_TREE_MAX_FIELDS", "SPEC_TREE_MAX_TABLES",
+                 "SPEC_TREE_MAX_COLUMNS"):
+        assert int(re.search(rf"#define {name} (\d+)", hdr).group(1)) == getattr(_lib, name), name
+    assert _lib.struct_mismatches(L) == []
+    assert C.sizeof(_lib.SpecSchema) == 4100 and _lib.SpecNestedSchema.item.offset == 4100
+    assert C.sizeof(_lib.SpecTree) == 8196
+    assert L.spec_struct_size(99) == 0 and L.spec_struct_offset(99, 0) == C.c_size_t(-1).value
+    assert BLOCK_DTYPE.itemsize == C.sizeof(Lz4Block)
+    assert [BLOCK_DTYPE.fields[n][1] for n in BLOCK_DTYPE.names] == [getattr(Lz4Block, n).offset for n in BLOCK_DTYPE.names]
+    # an independent compile of the header (what a cgo binding sees)
+    structs = {0: ("spec_span", ["off", "len"]), 1: ("spec_field", ["tag", "kind", "reserved"]),
+               2: ("spec_schema", ["nfields", "fields"]), 3: ("spec_nested_schema", ["outer", "item"]),
+               4: ("spec_tree_field", ["tag", "kind", "elem", "parent", "reserved"]),
+               5: ("spec_tree", ["nfields", "fields"]),
+               6: ("spec_tree_table", ["parent", "field", "rel", "shape", "first_column", "ncolumns"]),
+               7: ("spec_tree_column", ["table", "field", "role", "kind", "width"]),
+               8: ("spec_lz4_block", ["src_off", "src_len", "stored"]),
+               9: ("spec_lz4_state", ["in_frame", "block_max", "flags", "reserved"])}
+    assert len(structs) == len(_lib.struct_mirrors())
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "spec_amd.h"', "int main(void) {"]
+    for which, (s, members) in structs.items():
+        lines.append(f'printf("{which} -1 %zu\\n", sizeof({s}));')
+        lines += [f'printf("{which} {m} %zu\\n", offsetof({s}, {f}));' for m, f in enumerate(members)]
+    lines.append("return 0; }")
+    with tempfile.TemporaryDirectory() as d:
+        src, exe = os.path.join(d, "layout.c"), os.path.join(d, "layout")
+        open(src, "w").write("\n".join(lines))
+        subprocess.run(["gcc", "-std=c99", "-I", os.path.dirname(_lib.HEADER_PATH), src, "-o", exe], check=True)
+        out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout
+    for line in out.split("\n"):
+        if line:
+            which, m, v = (int(x) for x in line.split())
+            got = L.spec_struct_size(which) if m < 0 else L.spec_struct_offset(which, m)
+            assert got == v, (structs[which], m, got, v)
+
+
 def test_introspection():
     L = spec_amd.lib()
-    assert L.spec_abi_version() == 1
+    assert L.spec_abi_version() == 2
     widths = {1: 1, 2: 1, 3: 2, 4: 4, 5: 8, 6: 2, 7: 4, 8: 8, 9: 4, 10: 8, 11: 8, 12: 16, 13: 32, 14: 8, 15: 8}
     for k, w in widths.items():
         assert L.spec_kind_width(k) == w

@@ -12,7 +12,7 @@ import torch
 import spec_amd
 from spec_amd import workload
 from tests.test_tree import _test_object_columns
-from spec_amd.tree_catalog import many_tables_tree, wide_tree
+from tests.trees import many_tables_tree, wide_tree
 from tests.tree_helpers import (mismatches, nested_struct_tree, oracle_decode, oracle_encode, roundtrip_mismatches,
                                 shapes_tree)
 
@@ -50,6 +50,74 @@ def test_pkg1_encode_decode(dev, n):
     tree = spec_amd.pkg1_tree()
     cols, heaps, rows = workload.tree_batch(tree, n, 100 + n)
     check_encode_decode(tree, cols, heaps, rows, dev, n)
+
+
+def _root_windows(ends: np.ndarray, extra: int):
+    """The root group's staging per 64-record window, restated from tree_decode.hip group_shape
+    and tree_decode_core.hpp tree_rows_pair: the slab (0: no staging), and per window whether its
+    span fits the slab (else both waves parse it from HBM) and, for the window holding the stream's
+    last partial 16-byte chunk, which wave's 1 KiB DMA chunk it is in (that wave refills it)."""
+    n, total = len(ends), int(ends[-1])
+    slab = (int(64.0 * total / n * 1.15 + 128 + 64) + 1023) & ~1023
+    if slab + extra > 40960:  # WAVE_LDS_MAX
+        return 0, []
+    starts = np.concatenate([[0], ends[:-1]]).astype(np.int64)
+    out = []
+    for w in range((n + 63) // 64):
+        lo, hi = int(starts[w * 64]), int(ends[min(n, w * 64 + 64) - 1])
+        sb, se = max(lo - 64, 0) & ~15, (hi + 31) & ~15
+        fits = se - sb + 16 <= slab
+        tail, chunks = total & ~15, (se - sb + 1023) >> 10
+        tw = ((tail - sb) >> 10) % 2 if fits and total % 16 and sb <= tail < sb + chunks * 1024 else None
+        out.append((fits, tw))
+    return slab, out
+
+
+@pytest.mark.parametrize("case", ["tail_wave0", "tail_wave1", "last_over_slab"])
+def test_pkg1_root_pair_over_slab_and_stream_end(dev, case):
+    """The root group on wave pairs (tree_rows_pair) at the two edges its staging has: a 64-record
+    window whose span exceeds the slab (both waves parse it from HBM, range-checked) among staged
+    windows, and the window holding the stream's last partial 16-byte chunk, which comes back
+    zeroed from the LDS-DMA and is refilled bytewise by the wave whose round-robin 1 KiB chunk
+    holds it (wave 0 or wave 1), or, in the third case, that last window over the slab itself.
+    The records are a pkg1 batch rearranged (records are independent): window 1 (or the last
+    window) is 64 copies of the batch's largest record; the record count is chosen so the
+    windows land as the case needs, and the test asserts they do.  Against the oracle's decode of
+    the same stream (round 5's first pair-kernel run, gpurun_out/pair1, failed pkg1 at 131,072
+    records with 41 columns wrong; DESIGN.md §3.7 "pair1")."""
+    from spec_amd.tree import REL_ONE
+
+    tree = spec_amd.pkg1_tree()
+    cols, heaps, rows = workload.tree_batch(tree, 1500, 77)
+    s, e = oracle_encode(tree, cols, heaps, 1500)
+    e = e.astype(np.int64)
+    st = np.concatenate([[0], e[:-1]])
+    sz = e - st
+    big = int(np.argmax(sz))
+    gn = 1 + sum(1 for t in tree.tables if t.index and t.rel == REL_ONE and tree.tables[t.parent].rel != 2)
+    extra = 512 * (gn - 1) + 16
+    pick = None
+    for m in range(600, 1500):
+        order = list(range(64)) + [big] * 64 + list(range(128, m))
+        if case == "last_over_slab":
+            order = list(range(m - 64)) + [big] * 64
+        slab, w = _root_windows(np.cumsum(sz[order]), extra)
+        if not slab:
+            continue
+        if case == "last_over_slab":
+            ok = not w[-1][0] and all(f for f, _ in w[:-1]) and int(np.sum(sz[order])) % 16
+        else:
+            ok = not w[1][0] and all(f for f, _ in w[:1] + w[2:]) and w[-1][1] == int(case[-1])
+        if ok:
+            pick = order
+            break
+    assert pick is not None, "no record count puts the windows where the case needs them"
+    stream = np.concatenate([s[st[i]: e[i]] for i in pick])
+    ends = np.cumsum(sz[pick]).astype(np.uint64)
+    want_rows, want = oracle_decode(tree, stream, ends)
+    got_rows, got = gpu_decode(tree, stream, ends, dev)
+    assert got_rows == want_rows
+    assert mismatches(tree, got, want) == []
 
 
 @pytest.mark.parametrize("depth", [1, 3])

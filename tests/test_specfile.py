@@ -188,3 +188,15 @@ def test_package_reference_trees_match_fixture():
         assert pkg[k] == gold[k], k
     assert [t.to_fields() for t in reference_trees().values()] == \
         [[tuple(f) for f in gold[k]] for k in REFERENCE_TREE_NAMES]
+
+
+def test_precompile_list_is_current():
+    """build()'s list of test-only trees (tests/golden/precompile_trees.json, written by
+    make_precompile_trees.py) holds exactly tests/trees.py's extra_trees(), so every tree the GPU
+    tests decode has its kernels in the shipped code-object cache."""
+    from spec_amd.tree_catalog import extra_trees as listed
+    from tests.trees import extra_trees
+
+    want = {k: t.to_fields() for k, t in extra_trees().items()}
+    got = {k: t.to_fields() for k, t in listed().items()}
+    assert got == want

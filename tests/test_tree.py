@@ -13,7 +13,7 @@ import pytest
 import spec_amd
 from oracle import oracle as O
 from spec_amd import Kind, ListOf, Message, Struct, Tree, workload
-from spec_amd.tree_catalog import many_tables_tree, wide_tree
+from tests.trees import many_tables_tree, wide_tree
 from tests.tree_helpers import oracle_decode, oracle_encode, oracle_fields, roundtrip_mismatches, shapes_tree
 
 

@@ -45,4 +45,4 @@ def roundtrip_mismatches(tree: Tree, inputs: dict, heaps: dict, got: list, strea
 
 
 
-from spec_amd.tree_catalog import nested_struct_tree, shapes_tree  # noqa: E402,F401  (trees used by the tests)
+from tests.trees import nested_struct_tree, shapes_tree  # noqa: E402,F401  (trees used by the tests)
