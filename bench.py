@@ -302,9 +302,76 @@ def cpu_baseline(stream_np, ends_np, seconds):
     return res, threads, n
 
 
-def nested_leg(n, seed, dev):
+def host_cpu_model() -> str:
+    """The host CPU's model name (/proc/cpuinfo), recorded next to the baseline's core count."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
+
+
+def _cpu_rate(fn, n, seconds):
+    """Records per second of fn() (one pass over n records), repeated for ~seconds after a warm run."""
+    fn()
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            break
+    return n * reps / dt / 1e6
+
+
+def cpu_encode_baseline(cols, heaps, n, stream_bytes, seconds):
+    """BASELINE config 3's CPU path beside the encode leg: the oracle's Writer loop
+    (NewMessageWriterBuffer + 16 FieldWriter calls + Build per record, internal/bench/write_test.go:
+    16-78) over the same 1M Flat16 columns, on 1 host thread and on every core (contiguous shards,
+    one output buffer per thread)."""
+    from oracle import oracle as O
+
+    threads = host_cores()
+    hl = [heaps.get(f) for f in range(len(FLAT16))]
+    res = {}
+    for th in sorted({1, threads}):
+        run, _, _ = O.encode_flat_batch_mt(FLAT16.tags, FLAT16.kinds, cols, hl, n, 2 * stream_bytes + (64 << 20), th)
+        res[th] = _cpu_rate(run, n, seconds / 2)
+    return {"value": round(res[threads], 2), "unit": "Mmsg/s", "cores": threads, "kind": "port",
+            "host_model": host_cpu_model(), "single_core_value": round(res[1], 2),
+            "sample": f"{n} Flat16 records (the leg's batch) encoded repeatedly for ~{seconds / 2:.0f} s per thread "
+                      f"count on {threads} host threads and on 1; C restatement of the Writer loop"}
+
+
+def cpu_nested_baseline(w, stream_np, ends_np, seconds):
+    """BASELINE config 4's CPU path beside the nested leg: the oracle's nested Writer loop
+    (FieldWriter.List + MessageListWriter.Add/End per item, writer_list_msg.go:22-47) and its
+    reader loop (OpenMessageErr + outer getters + MessageList.Len/Get + item getters,
+    list_msg.go:88-92) over the same records, on 1 host thread and on every core."""
+    from oracle import oracle as O
+
+    threads = host_cores()
+    n = len(ends_np)
+    out = {}
+    for th in sorted({1, threads}):
+        enc, dec, _, _, _ = O.nested_batch_mt(w, stream_np, ends_np, 2 * stream_np.size + (64 << 20), th)
+        out[th] = (_cpu_rate(enc, n, seconds / 4), _cpu_rate(dec, n, seconds / 4))
+    return {"encode_value": round(out[threads][0], 2), "decode_value": round(out[threads][1], 2), "unit": "Mmsg/s",
+            "cores": threads, "kind": "port", "host_model": host_cpu_model(),
+            "single_core_encode_value": round(out[1][0], 2), "single_core_decode_value": round(out[1][1], 2),
+            "sample": f"{n} Nested records (the leg's batch) encoded and decoded repeatedly for ~{seconds / 4:.0f} s "
+                      f"each per thread count on {threads} host threads and on 1; C restatement of the reference's "
+                      f"nested Writer and MessageList reader loops"}
+
+
+def nested_leg(n, seed, dev, cpu_seconds=0.0):
     """BASELINE config 4: n Nested records (list<message>), GPU encode then GPU decode
-    (index + decode launches), device-resident; kernel time via HIP events."""
+    (index + decode launches), device-resident; kernel time via HIP events.  cpu_seconds > 0:
+    the CPU baseline of the same records beside it (cpu_nested_baseline)."""
     from spec_amd import NESTED
 
     w = workload.nested(n, seed)
@@ -345,7 +412,10 @@ def nested_leg(n, seed, dev):
     sb = stream.numel()
     dec_alg = sb + 8 * n + n * (16 + 8 + 8 + 1 + 4) + m * (4 + 8 + 8 + 1)
     enc_alg = n * (16 + 8 + 8 + 4) + m * (4 + 8 + 8) + int(w["name_heap"].size + w["label_heap"].size) + sb + 8 * n
-    return {"records": n, "items": m, "mean_record_bytes": round(sb / n, 1),
+    cpu = None
+    if cpu_seconds > 0:
+        cpu = cpu_nested_baseline(w, stream.cpu().numpy(), ends.cpu().numpy().view(np.uint64), cpu_seconds)
+    return {"records": n, "items": m, "mean_record_bytes": round(sb / n, 1), "cpu_baseline": cpu,
             "decode_mmsg_s": round(n / (dec_ms * 1e-3) / 1e6, 1), "decode_ms": round(dec_ms, 4),
             "decode_gb_s": round(dec_alg / (dec_ms * 1e-3) / 1e9, 1),
             "decode_frac": round(dec_alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3),
@@ -1024,6 +1094,11 @@ def run(args, env):
                             "gb_s": round(enc_alg / (enc_ms * 1e-3) / 1e9, 1),
                             "frac": round(enc_alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "alg_bytes": int(enc_alg),
                             "ms": round(enc_ms, 4), "bit_exact_vs_decode_input": bool(enc_same)}
+        if rank == 0 and world == 1 and not args.no_cpu:
+            try:
+                extras["encode"]["cpu_baseline"] = cpu_encode_baseline(cols, heaps, n, stream_bytes, args.cpu_seconds)
+            except Exception as e:
+                extras["encode"]["cpu_baseline"] = {"error": repr(e)[:300]}
         if not args.no_jit and jit:
             try:
                 extras["decode_generic"] = generic_leg(stream, ends, out_cols, status, avg_ms)
@@ -1048,7 +1123,7 @@ def run(args, env):
             except Exception as e:
                 extras["decode_wide"] = {"error": repr(e)[:300]}
             try:
-                extras["nested"] = nested_leg(n, args.seed, dev)
+                extras["nested"] = nested_leg(n, args.seed, dev, 0.0 if args.no_cpu else args.cpu_seconds)
             except Exception as e:
                 extras["nested"] = {"error": repr(e)[:300]}
             try:
@@ -1089,7 +1164,7 @@ def run(args, env):
                "sample": f"{sample} Flat16 records (the full batch) decoded repeatedly for ~{args.cpu_seconds/2:.0f} s "
                          f"per thread count on {threads} host threads (all cores this process may use) and on 1; "
                          f"C restatement of OpenMessageErr + 16 getters",
-               "single_core_value": round(res[1], 2)}
+               "single_core_value": round(res[1], 2), "host_model": host_cpu_model()}
 
     # the native one-process multi-device leg (spec_shard_*): a child of rank 0 drives every device
     # while the ranks wait (the others on the rendezvous store: no GPU work of theirs runs meanwhile)

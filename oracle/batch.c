@@ -160,9 +160,10 @@ static so_err write_field(so_writer *w, uint16_t tag, int kind, const uint8_t *s
     return "unknown kind";
 }
 
-int so_encode_flat_batch(int nfields, const uint16_t *tags, const uint8_t *kinds,
-                         const void *const *columns, const uint8_t *const *heaps, uint64_t n,
-                         uint8_t *out, uint64_t out_cap, uint64_t *ends) {
+/* Records [r0, r1) written back to back into out (ends[r] relative to out). */
+static int encode_flat_range(int nfields, const uint16_t *tags, const uint8_t *kinds, const void *const *columns,
+                             const uint8_t *const *heaps, uint64_t r0, uint64_t r1, uint8_t *out, uint64_t out_cap,
+                             uint64_t *ends) {
     so_buf buf;
     so_buf_init_fixed(&buf, out, (size_t)out_cap);
     so_writer *w = so_writer_new(&buf);
@@ -170,7 +171,7 @@ int so_encode_flat_batch(int nfields, const uint16_t *tags, const uint8_t *kinds
     if (nfields > 1024) return -1;
     for (int f = 0; f < nfields; f++) widths[f] = so_kind_width(kinds[f]);
     int rc = 0;
-    for (uint64_t r = 0; r < n; r++) {
+    for (uint64_t r = r0; r < r1; r++) {
         so_writer_reset(w, &buf);
         so_writer_begin_message(w);
         for (int f = 0; f < nfields; f++) {
@@ -192,6 +193,134 @@ int so_encode_flat_batch(int nfields, const uint16_t *tags, const uint8_t *kinds
     return rc;
 }
 
+int so_encode_flat_batch(int nfields, const uint16_t *tags, const uint8_t *kinds,
+                         const void *const *columns, const uint8_t *const *heaps, uint64_t n,
+                         uint8_t *out, uint64_t out_cap, uint64_t *ends) {
+    return encode_flat_range(nfields, tags, kinds, columns, heaps, 0, n, out, out_cap, ends);
+}
+
+/* ---- the CPU baseline on several host threads (bench.py): contiguous record shards, one per
+ * thread, each with its own output region out + t * (out_cap / nthreads) and ends relative to
+ * it — what nthreads goroutines each running the reference's loop with their own buffer do ---- */
+
+typedef struct {
+    int kind; /* 0 flat encode, 1 nested encode, 2 nested decode */
+    uint64_t r0, r1;
+    uint8_t *out;
+    uint64_t cap;
+    int rc;
+    /* flat */
+    int nfields;
+    const uint16_t *tags;
+    const uint8_t *kinds;
+    const void *const *columns;
+    const uint8_t *const *heaps;
+    /* nested: id, seq, name, name_heap, item_begin, key, value, label, label_heap; decode adds
+     * stream, ends and the output columns */
+    const void *nv[9];
+    const uint8_t *stream;
+    const uint64_t *ends_in;
+    void *dv[8];
+    uint64_t *ends;
+} mt_job;
+
+static int encode_nested_range(const uint8_t *id, const int64_t *seq, const uint32_t *name, const uint8_t *name_heap,
+                               const uint32_t *item_begin, const int32_t *key, const double *value,
+                               const uint32_t *label, const uint8_t *label_heap, uint64_t r0, uint64_t r1,
+                               uint8_t *out, uint64_t out_cap, uint64_t *ends);
+static void decode_nested_range(const uint8_t *stream, const uint64_t *ends, uint64_t r0, uint64_t r1,
+                                const uint32_t *item_begin, uint8_t *id, int64_t *seq, uint32_t *name, int32_t *key,
+                                double *value, uint32_t *label, uint8_t *item_status, uint8_t *status);
+
+static void *mt_run(void *arg) {
+    mt_job *j = (mt_job *)arg;
+    if (j->kind == 0) {
+        j->rc = encode_flat_range(j->nfields, j->tags, j->kinds, j->columns, j->heaps, j->r0, j->r1, j->out, j->cap,
+                                  j->ends);
+    } else if (j->kind == 1) {
+        j->rc = encode_nested_range(j->nv[0], j->nv[1], j->nv[2], j->nv[3], j->nv[4], j->nv[5], j->nv[6], j->nv[7],
+                                    j->nv[8], j->r0, j->r1, j->out, j->cap, j->ends);
+    } else {
+        decode_nested_range(j->stream, j->ends_in, j->r0, j->r1, j->nv[4], j->dv[0], j->dv[1], j->dv[2], j->dv[3],
+                            j->dv[4], j->dv[5], j->dv[6], j->dv[7]);
+        j->rc = 0;
+    }
+    return NULL;
+}
+
+static int mt_launch(mt_job *proto, uint64_t n, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    if ((uint64_t)nthreads > n) nthreads = n ? (int)n : 1;
+    mt_job jobs[256];
+    pthread_t th[256];
+    const uint64_t share = proto->cap / (uint64_t)nthreads;
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = *proto;
+        jobs[t].r0 = n * (uint64_t)t / (uint64_t)nthreads;
+        jobs[t].r1 = n * (uint64_t)(t + 1) / (uint64_t)nthreads;
+        jobs[t].out = proto->out ? proto->out + share * (uint64_t)t : NULL;
+        jobs[t].cap = share;
+    }
+    if (nthreads == 1) {
+        mt_run(&jobs[0]);
+        return jobs[0].rc;
+    }
+    for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, mt_run, &jobs[t]);
+    int rc = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        if (jobs[t].rc) rc = jobs[t].rc;
+    }
+    return rc;
+}
+
+int so_encode_flat_batch_mt(int nfields, const uint16_t *tags, const uint8_t *kinds, const void *const *columns,
+                            const uint8_t *const *heaps, uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *ends,
+                            int nthreads) {
+    mt_job j;
+    memset(&j, 0, sizeof(j));
+    j.kind = 0;
+    j.nfields = nfields;
+    j.tags = tags;
+    j.kinds = kinds;
+    j.columns = columns;
+    j.heaps = heaps;
+    j.out = out;
+    j.cap = out_cap;
+    j.ends = ends;
+    return mt_launch(&j, n, nthreads);
+}
+
+int so_encode_nested_batch_mt(const uint8_t *id, const int64_t *seq, const uint32_t *name, const uint8_t *name_heap,
+                              const uint32_t *item_begin, const int32_t *key, const double *value,
+                              const uint32_t *label, const uint8_t *label_heap, uint64_t n, uint8_t *out,
+                              uint64_t out_cap, uint64_t *ends, int nthreads) {
+    mt_job j;
+    memset(&j, 0, sizeof(j));
+    j.kind = 1;
+    const void *nv[9] = {id, seq, name, name_heap, item_begin, key, value, label, label_heap};
+    memcpy(j.nv, nv, sizeof(nv));
+    j.out = out;
+    j.cap = out_cap;
+    j.ends = ends;
+    return mt_launch(&j, n, nthreads);
+}
+
+int so_decode_nested_batch_mt(const uint8_t *stream, const uint64_t *ends, uint64_t n, const uint32_t *item_begin,
+                              uint8_t *id, int64_t *seq, uint32_t *name, int32_t *key, double *value, uint32_t *label,
+                              uint8_t *item_status, uint8_t *status, int nthreads) {
+    mt_job j;
+    memset(&j, 0, sizeof(j));
+    j.kind = 2;
+    j.stream = stream;
+    j.ends_in = ends;
+    j.nv[4] = item_begin;
+    void *dv[8] = {id, seq, name, key, value, label, item_status, status};
+    memcpy(j.dv, dv, sizeof(dv));
+    return mt_launch(&j, n, nthreads);
+}
+
 /* ---- Nested (config 4) ---- */
 
 int so_encode_nested_batch(const uint8_t *id, const int64_t *seq, const uint32_t *name,
@@ -199,11 +328,19 @@ int so_encode_nested_batch(const uint8_t *id, const int64_t *seq, const uint32_t
                            const int32_t *key, const double *value, const uint32_t *label,
                            const uint8_t *label_heap, uint64_t n, uint8_t *out,
                            uint64_t out_cap, uint64_t *ends) {
+    return encode_nested_range(id, seq, name, name_heap, item_begin, key, value, label, label_heap, 0, n, out,
+                               out_cap, ends);
+}
+
+static int encode_nested_range(const uint8_t *id, const int64_t *seq, const uint32_t *name, const uint8_t *name_heap,
+                               const uint32_t *item_begin, const int32_t *key, const double *value,
+                               const uint32_t *label, const uint8_t *label_heap, uint64_t r0, uint64_t r1,
+                               uint8_t *out, uint64_t out_cap, uint64_t *ends) {
     so_buf buf;
     so_buf_init_fixed(&buf, out, (size_t)out_cap);
     so_writer *w = so_writer_new(&buf);
     int rc = 0;
-    for (uint64_t r = 0; r < n; r++) {
+    for (uint64_t r = r0; r < r1; r++) {
         so_writer_reset(w, &buf);
         so_writer_begin_message(w);
         so_field_bin128(w, 1, id + 16 * r);
@@ -251,7 +388,16 @@ int so_decode_nested_batch(const uint8_t *stream, const uint64_t *ends, uint64_t
                            const uint32_t *item_begin, uint8_t *id, int64_t *seq,
                            uint32_t *name, int32_t *key, double *value, uint32_t *label,
                            uint8_t *item_status, uint8_t *status) {
-    for (uint64_t r = 0; r < n; r++) {
+    decode_nested_range(stream, ends, 0, n, item_begin, id, seq, name, key, value, label, item_status, status);
+    return 0;
+}
+
+/* Per record: OpenMessageErr, the outer getters, MessageList Len/Get + the item getters
+ * (list_msg.go:88-92); items land at item_begin[r] + i. */
+static void decode_nested_range(const uint8_t *stream, const uint64_t *ends, uint64_t r0, uint64_t r1,
+                                const uint32_t *item_begin, uint8_t *id, int64_t *seq, uint32_t *name, int32_t *key,
+                                double *value, uint32_t *label, uint8_t *item_status, uint8_t *status) {
+    for (uint64_t r = r0; r < r1; r++) {
         uint64_t s = rec_start(ends, r);
         so_message m;
         so_err e = so_open_message_err(stream + s, (size_t)(ends[r] - s), &m);
@@ -283,7 +429,6 @@ int so_decode_nested_batch(const uint8_t *stream, const uint64_t *ends, uint64_t
             label[2 * o + 1] = q ? (uint32_t)len : 0;
         }
     }
-    return 0;
 }
 
 /* ---- ParseMessage over a batch (spec_parse_messages semantics) ---- */

@@ -217,6 +217,9 @@ def _declare(L):
                                                             C.c_void_p]
     L.so_decode_nested_counts.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
     L.so_decode_nested_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64] + [C.c_void_p] * 9
+    L.so_encode_flat_batch_mt.argtypes = L.so_encode_flat_batch.argtypes + [C.c_int]
+    L.so_encode_nested_batch_mt.argtypes = L.so_encode_nested_batch.argtypes + [C.c_int]
+    L.so_decode_nested_batch_mt.argtypes = L.so_decode_nested_batch.argtypes + [C.c_int]
     L.so_parse_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]
     L.so_parse_batch_root.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p,
                                       C.c_void_p]
@@ -609,6 +612,58 @@ def encode_nested_batch(w: dict, cap=None):
         raise RuntimeError(f"so_encode_nested_batch rc={rc}")
     total = int(ends[-1]) if n else 0
     return out[:total].copy(), ends
+
+
+def encode_flat_batch_mt(tags, kinds, columns, heaps, n, cap, nthreads):
+    """The Writer loop on nthreads host threads (CPU baseline): -> (out, ends) where thread t's
+    records sit in out[t * (cap // nthreads):] with ends relative to that region."""
+    tags_a = np.asarray(tags, dtype=np.uint16)
+    kinds_a = np.asarray(kinds, dtype=np.uint8)
+    cols = [np.ascontiguousarray(c) for c in columns]
+    colptrs = (C.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
+    hs = [np.ascontiguousarray(h, dtype=np.uint8) if h is not None else np.zeros(1, np.uint8) for h in heaps]
+    heapptrs = (C.c_void_p * len(hs))(*[h.ctypes.data for h in hs])
+    out = np.zeros(cap, dtype=np.uint8)
+    ends = np.zeros(n, dtype=np.uint64)
+
+    def run():
+        rc = lib().so_encode_flat_batch_mt(len(tags), _ptr(tags_a), _ptr(kinds_a), colptrs, heapptrs, n, _ptr(out),
+                                           cap, _ptr(ends), nthreads)
+        if rc != 0:
+            raise RuntimeError(f"so_encode_flat_batch_mt rc={rc}")
+
+    return run, out, ends
+
+
+def nested_batch_mt(w: dict, stream: np.ndarray, ends_in: np.ndarray, cap, nthreads):
+    """The nested Writer loop and the nested reader loop (OpenMessageErr + outer getters +
+    MessageList Len/Get + item getters) on nthreads host threads (CPU baseline) -> (encode(),
+    decode()) callables over preallocated buffers."""
+    n = len(w["seq"])
+    args = [np.ascontiguousarray(w[k]) for k in ("id", "seq", "name", "name_heap", "item_begin", "key", "value",
+                                                 "label", "label_heap")]
+    out = np.zeros(cap, dtype=np.uint8)
+    ends = np.zeros(n, dtype=np.uint64)
+    m = int(w["item_begin"][-1])
+    stream = np.ascontiguousarray(stream, dtype=np.uint8)
+    ends_in = np.ascontiguousarray(ends_in, dtype=np.uint64)
+    d = {"id": np.zeros((n, 16), np.uint8), "seq": np.zeros(n, np.int64), "name": np.zeros((n, 2), np.uint32),
+         "key": np.zeros(max(m, 1), np.int32), "value": np.zeros(max(m, 1), np.float64),
+         "label": np.zeros((max(m, 1), 2), np.uint32), "item_status": np.zeros(max(m, 1), np.uint8),
+         "status": np.zeros(n, np.uint8)}
+    L = lib()
+
+    def enc():
+        rc = L.so_encode_nested_batch_mt(*[_ptr(a) for a in args], n, _ptr(out), cap, _ptr(ends), nthreads)
+        if rc != 0:
+            raise RuntimeError(f"so_encode_nested_batch_mt rc={rc}")
+
+    def dec():
+        L.so_decode_nested_batch_mt(_ptr(stream), _ptr(ends_in), n, _ptr(args[4]), _ptr(d["id"]), _ptr(d["seq"]),
+                                    _ptr(d["name"]), _ptr(d["key"]), _ptr(d["value"]), _ptr(d["label"]),
+                                    _ptr(d["item_status"]), _ptr(d["status"]), nthreads)
+
+    return enc, dec, out, ends, d
 
 
 def decode_nested_batch(stream: np.ndarray, ends: np.ndarray):

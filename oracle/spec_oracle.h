@@ -340,6 +340,18 @@ int so_decode_nested_batch(const uint8_t *stream, const uint64_t *ends, uint64_t
                            const uint32_t *item_begin, uint8_t *id, int64_t *seq,
                            uint32_t *name, int32_t *key, double *value, uint32_t *label,
                            uint8_t *item_status, uint8_t *status);
+/* The CPU baseline loops on nthreads host threads (contiguous record shards; an encode shard t
+ * writes its records into out + t * (out_cap / nthreads), ends relative to that region). */
+int so_encode_flat_batch_mt(int nfields, const uint16_t *tags, const uint8_t *kinds, const void *const *columns,
+                            const uint8_t *const *heaps, uint64_t n, uint8_t *out, uint64_t out_cap, uint64_t *ends,
+                            int nthreads);
+int so_encode_nested_batch_mt(const uint8_t *id, const int64_t *seq, const uint32_t *name, const uint8_t *name_heap,
+                              const uint32_t *item_begin, const int32_t *key, const double *value,
+                              const uint32_t *label, const uint8_t *label_heap, uint64_t n, uint8_t *out,
+                              uint64_t out_cap, uint64_t *ends, int nthreads);
+int so_decode_nested_batch_mt(const uint8_t *stream, const uint64_t *ends, uint64_t n, const uint32_t *item_begin,
+                              uint8_t *id, int64_t *seq, uint32_t *name, int32_t *key, double *value, uint32_t *label,
+                              uint8_t *item_status, uint8_t *status, int nthreads);
 
 /* ParseMessage per record (spec_parse_messages semantics): status 0 ok, 1-5 trailer class,
  * 6 panic (list element start > end), 7 nested value error; sizes = message bytes or 0.
