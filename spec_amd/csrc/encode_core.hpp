@@ -652,6 +652,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t heap_rsrc(const EncFields &f, 
 template <class Spec>
 struct SpecEnc {
     static constexpr int N = Spec::N;
+    static constexpr bool kBigForced = Spec::big_forced;
     static constexpr bool has_list() {
         for (int f = 0; f < N; f++)
             if (Spec::kind[f] == K_LIST) return true;
@@ -666,9 +667,9 @@ struct SpecEnc {
         uint32_t end[N];  // emit: end offset of each field
     };
 
-    template <int F>
+    template <int F, int E = N>
     static __device__ __forceinline__ void load_col(const EncFields &f, uint64_t r, Rec &x) {
-        if constexpr (F < N) {
+        if constexpr (F < E) {
             const void *col = f.cols[F];
             constexpr uint32_t k = Spec::kind[F];
             if constexpr (k == K_LIST) {
@@ -693,13 +694,13 @@ struct SpecEnc {
             } else { // 64-bit kinds, string/bytes spans
                 x.v[F][0] = ((const uint64_t *)col)[r];
             }
-            load_col<F + 1>(f, r, x);
+            load_col<F + 1, E>(f, r, x);
         }
     }
 
-    template <int F>
+    template <int F, int E = N>
     static __device__ __forceinline__ void load_heap(const EncFields &f, Rec &x) {
-        if constexpr (F < N) {
+        if constexpr (F < E) {
             if constexpr (heap_kind<F>()) {
                 const __amdgpu_buffer_rsrc_t hr = heap_rsrc(f, F);
                 const uint32_t off = (uint32_t)x.v[F][0] & ~3u;
@@ -726,7 +727,7 @@ struct SpecEnc {
                     }
                 }
             }
-            load_heap<F + 1>(f, x);
+            load_heap<F + 1, E>(f, x);
         }
     }
 
@@ -741,10 +742,10 @@ struct SpecEnc {
     static __device__ __forceinline__ void load_cols(const EncFields &f, uint64_t r, Rec &x) { load_col<0>(f, r, x); }
     static __device__ __forceinline__ void load_heaps(const EncFields &f, Rec &x) { load_heap<0>(f, x); }
 
-    template <int F, class Lists>
+    template <int F, class Lists, int E = N>
     static __device__ __forceinline__ uint64_t data_size(const EncFields &f, const Rec &x, uint64_t r, bool check,
                                                          bool &err, const Lists &lists) {
-        if constexpr (F >= N) {
+        if constexpr (F >= E) {
             return 0;
         } else {
             const uint64_t v = x.v[F][0];
@@ -766,7 +767,7 @@ struct SpecEnc {
                 err |= ((uint64_t)len > MAX_SIZE) | (check & ((uint64_t)off + len > f.heap_lens[F]));
                 s = (uint64_t)len + vlen32(len) + 1 + (k == K_STRING ? 1 : 0);
             }
-            return s + data_size<F + 1>(f, x, r, check, err, lists);
+            return s + data_size<F + 1, Lists, E>(f, x, r, check, err, lists);
         }
     }
 
@@ -784,10 +785,10 @@ struct SpecEnc {
         return s;
     }
 
-    template <int F, class E, class Lists>
+    template <int F, class E, class Lists, int FE = N>
     static __device__ __forceinline__ void emit_values(const EncFields &f, E &em, Rec &x, decltype(em.pos) start,
                                                        uint64_t r, const Lists &lists) {
-        if constexpr (F < N) {
+        if constexpr (F < FE) {
             const uint64_t v = x.v[F][0];
             constexpr uint32_t k = Spec::kind[F];
             if constexpr (k == K_LIST) {
@@ -874,7 +875,7 @@ struct SpecEnc {
                 else em.varint32_type(len, T_BYTES);
             }
             x.end[F] = (uint32_t)(em.pos - start);
-            emit_values<F + 1>(f, em, x, start, r, lists);
+            emit_values<F + 1, E, Lists, FE>(f, em, x, start, r, lists);
         }
     }
 
@@ -927,6 +928,42 @@ struct SpecEnc {
             w[d + 1] |= (uint32_t)((T << s) >> 32);
         }
         em.template put_heap_short<RUN_M>(w, 0u, (uint32_t)TB + L + 2);
+    }
+
+    // ---- the write pass on a wave pair (encode_write_pair_body): wave 0 emits fields [0, H),
+    // wave 1 fields [H, N), the table and the trailer ----
+    // x.end[F..E) = base + the field sizes through each field: the ends the emitter records,
+    // known from the sizes before any byte is written
+    template <int F, int E>
+    static __device__ __forceinline__ uint32_t range_ends(const EncFields &f, Rec &x, uint64_t r, uint32_t base) {
+        if constexpr (F < E) {
+            bool err = false;
+            const uint32_t s = (uint32_t)data_size<F, NoLists, F + 1>(f, x, r, false, err, NoLists());
+            x.end[F] = base + s;
+            return range_ends<F + 1, E>(f, x, r, base + s);
+        } else {
+            return base;
+        }
+    }
+    // the values of fields [F0, F1) from em.pos (no finish: the pending dword stays in em.acc)
+    template <int F0, int F1, class E>
+    static __device__ __forceinline__ void emit_range(const EncFields &f, E &em, Rec &x, decltype(em.pos) start,
+                                                      uint64_t r) {
+        emit_values<F0, E, NoListEmit, F1>(f, em, x, start, r, NoListEmit());
+    }
+    // the table and trailer after the values (x.end[] of every field set; no finish)
+    template <class E>
+    static __device__ __forceinline__ void emit_table_trailer(E &em, const Rec &x, const RecSize &rs) {
+        if constexpr (E::kHeadSt4 && !Spec::big_forced && RUN_M <= 18) {
+            if (__ballot(rs.big) == 0) {
+                emit_small_table_trailer(em, x, (uint32_t)rs.data);
+                return;
+            }
+        }
+        emit_table<0>(em, x, rs.big);
+        em.rvarint((uint32_t)rs.data);
+        em.rvarint((uint32_t)(N * (rs.big ? 6 : 3)));
+        em.put1(rs.big ? T_BIG_MESSAGE : T_MESSAGE);
     }
 
     // With a list field the emitter jumps over the list's items (written later by other lanes:
@@ -1073,5 +1110,155 @@ __device__ __forceinline__ void encode_write_body(const A &a, uint8_t *smem) {
 }
 
 constexpr size_t enc_write_lds_bytes() { return ENC_LDS_HEAD + (size_t)(ENC_BLOCK / 64) * ENC_SLAB; }
+
+// ---- the write pass on wave PAIRS (schema-specialised encoders) ---------------------------
+// A 512-thread block takes the size pass's 256-record block as four groups of 64 records; each
+// group is written by a wave PAIR sharing one LDS slab: wave 0 emits fields [0, H) of the 64
+// records, wave 1 fields [H, N) from each record's position of field H, then the table and the
+// trailer (the ends of fields [0, H) come from wave 0 through LDS, known from the sizes before
+// any byte is written).  Twice the waves per slab: one wave's LDS stores and heap loads overlap
+// the other's emission (the decoder's wave pairs, decode_flat_pair, are the same lever).
+// Ordering: a HEAD_ST4 emitter's first dword store covers <= 3 bytes below its start (the bytes
+// of the previous lane's record, or of wave 0's half of the same record), and every emitter
+// keeps its last partial dword pending; all whole-dword stores of both waves happen before a
+// block barrier and every pending tail is stored bytewise after it, so each byte's last writer
+// is its owner.
+// LDS: wsum[4] | per group: d0 (u32 x 64) | wave 0's field ends (u16 x H x 64) | slab.
+constexpr int ENC_PAIR_BLOCK = 512;
+constexpr int ENC_PAIR_HEAD = 64;
+__host__ __device__ constexpr uint32_t enc_pair_xch_bytes(int h) { return (uint32_t)(256 + 128 * h + 15) & ~15u; }
+// the slab of one group: four groups' slabs and exchanges in <= 80 KiB (two blocks per CU)
+__host__ __device__ constexpr uint32_t enc_pair_slab_bytes(int h) {
+    return ((81920u - ENC_PAIR_HEAD) / 4 - enc_pair_xch_bytes(h)) & ~15u;
+}
+__host__ __device__ constexpr uint32_t enc_pair_lds_bytes(int h) {
+    return ENC_PAIR_HEAD + 4 * (enc_pair_xch_bytes(h) + enc_pair_slab_bytes(h));
+}
+
+// copy_slab_out by T threads (one 16-byte store per thread and chunk)
+template <int T>
+__device__ __forceinline__ void copy_slab_out_t(const uint8_t *slab, uint8_t *gbase, uint64_t head, uint64_t lim,
+                                                int tid) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) const v4u lds_v4;
+    typedef __attribute__((address_space(3))) const uint8_t lds_b;
+    lds_v4 *s4 = (lds_v4 *)(lds_b *)slab;
+    lds_b *sb = (lds_b *)slab;
+    v4u *g4 = (v4u *)gbase;
+    const uint64_t h16 = (head + 15) >> 4, l16 = lim >> 4;
+    for (uint64_t q = h16 + tid; q < l16; q += 4 * T) {
+        v4u v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint64_t qq = q + T * u;
+            v[u] = s4[qq < l16 ? qq : q];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (q + T * u < l16) g4[q + T * u] = v[u];
+    }
+    const uint64_t hend = (h16 << 4) < lim ? (h16 << 4) : lim;
+    const uint64_t tb = (l16 << 4) > hend ? (l16 << 4) : hend;
+    if (tid < 16 && head + tid < hend) gbase[head + tid] = sb[head + tid];
+    if (tid >= 16 && tid < 32 && tb + (tid - 16) < lim) gbase[tb + (tid - 16)] = sb[tb + (tid - 16)];
+}
+
+template <class P, int H>
+__device__ __forceinline__ void encode_write_pair_body(const EncodeArgs &a, uint8_t *smem) {
+    static_assert(H >= 1 && H < P::N, "the split leaves fields on both waves");
+    constexpr uint32_t XB = enc_pair_xch_bytes(H), SB = enc_pair_slab_bytes(H);
+    uint64_t *wsum = (uint64_t *)smem;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, grp = wave >> 1, half = wave & 1;
+    uint8_t *gx = smem + ENC_PAIR_HEAD + grp * (XB + SB);
+    uint32_t *xd0 = (uint32_t *)gx;                   // wave 0's data bytes per record
+    uint16_t *xend = (uint16_t *)(gx + 256);          // wave 0's field ends [field][lane]
+    uint8_t *slab = gx + XB;
+    const uint64_t r = (uint64_t)blockIdx.x * ENC_BLOCK + grp * 64 + lane;
+    const bool valid = r < a.n;
+    const uint64_t rr = valid ? r : a.n - 1;
+    typename P::Rec x;
+    if (half == 0) {
+        P::template load_col<0, H>(a.f, rr, x);
+        P::template load_heap<0, H>(a.f, x);
+    } else {
+        P::template load_col<H, P::N>(a.f, rr, x);
+        P::template load_heap<H, P::N>(a.f, x);
+    }
+    const uint64_t total = a.block_sums[a.nblocks], blk_pre = a.block_sums[blockIdx.x];
+    if (total > a.out_cap) return; // capacity error or encoder error (total == ~0): block-uniform
+    bool err = false;
+    uint32_t dmine;
+    if (half == 0) {
+        dmine = P::template range_ends<0, H>(a.f, x, rr, 0u);
+        xd0[lane] = dmine;
+#pragma unroll
+        for (int f = 0; f < H; f++) xend[f * 64 + lane] = (uint16_t)x.end[f];
+    } else {
+        dmine = (uint32_t)P::template data_size<H, NoLists, P::N>(a.f, x, rr, false, err, NoLists());
+    }
+    __syncthreads(); // (1) wave 0's sizes and ends are in LDS
+    const uint32_t d0 = half == 0 ? dmine : xd0[lane];
+    const uint64_t data = (uint64_t)d0 + (half == 0 ? 0u : dmine);
+    uint64_t tot = 0, data_all = data;
+    RecSize rs;
+    if (half == 1) {
+        rs.data = data_all;
+        rs.big = P::kBigForced | (data_all > 65535);
+        const uint64_t tsize = (uint64_t)P::N * (rs.big ? 6 : 3);
+        rs.total = data_all + tsize + vlen32((uint32_t)data_all) + vlen32((uint32_t)tsize) + 1;
+        tot = valid ? rs.total : 0;
+    }
+    // wave 1 owns the record sizes: its scan gives the group's offsets; wave 0 reads its starts
+    uint64_t xs = tot;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(xs, o);
+        if (lane >= o) xs += y;
+    }
+    uint64_t *xstart = (uint64_t *)slab; // (the slab is free until the emission starts)
+    if (half == 1) {
+        if (lane == 63) wsum[grp] = xs;
+        xstart[lane] = xs - tot; // group-relative start of the record
+    }
+    __syncthreads(); // (2) group sums and starts
+    uint64_t pre = blk_pre;
+    for (int g = 0; g < grp; g++) pre += wsum[g];
+    const uint64_t start = pre + xstart[lane];
+    const uint64_t gtot = wsum[grp];
+    if (half == 1 && valid) a.ends[r] = a.ends_base + start + rs.total;
+    const uint64_t gbase_r = (uint64_t)blockIdx.x * ENC_BLOCK + grp * 64;
+    const bool live = gbase_r < a.n; // group-uniform
+    const uint64_t S = pre, E = pre + gtot;
+    const uint64_t head = ((uint64_t)(a.out + S)) & 15;
+    const bool fits = live && head + (E - S) + 16 <= (uint64_t)SB;
+    __syncthreads(); // (3) xstart read: the slab may be written
+    if (!live) return;
+    if (!fits) {
+        // a group larger than its slab: wave 0 writes each record straight to HBM (every field)
+        if (half == 0 && valid) {
+            const typename P::Rec all = P::load(a.f, r);
+            RecSize rs0 = P::size(a.f, all, r, false, err);
+            GlobalSink k{a.out};
+            P::emit(a.f, k, (long long)start, r, all, rs0, (const uint8_t *)nullptr);
+        }
+        return;
+    }
+    LdsSink k{slab, (int)(smem + ENC_PAIR_HEAD - 4 - slab)}; // dummy: the last header dword
+    const int p0 = (int)(head + (start - S));
+    Emit<LdsSink, int, true> em(k, half == 0 ? p0 : p0 + (int)d0);
+    if (valid) {
+        if (half == 0) {
+            P::template emit_range<0, H>(a.f, em, x, p0, r);
+        } else {
+#pragma unroll
+            for (int f = 0; f < H; f++) x.end[f] = xend[f * 64 + lane];
+            P::template emit_range<H, P::N>(a.f, em, x, p0, r);
+            P::emit_table_trailer(em, x, rs);
+        }
+    }
+    __syncthreads(); // (4) every whole-dword store of the group is done
+    if (valid) em.finish(); // the pending tails, bytewise: the owners write last
+    __syncthreads(); // (5) the slab is complete
+    copy_slab_out_t<128>(slab, a.out + S - head, head, head + (E - S), threadIdx.x & 127);
+}
 
 } // namespace spec

@@ -257,6 +257,47 @@ std::string generate_nested_encode(const spec_nested_schema *s) {
     return o.str();
 }
 
+// The write pass on wave pairs (encode_core.hpp encode_write_pair_body): wave 0 takes fields
+// [0, H), wave 1 fields [H, N) plus the table and trailer.  H balances a per-kind emission cost
+// (instructions of the HEAD_ST4 emitter: a string's heap copy and funnel shifts dominate, the
+// table + trailer costs about two strings' worth for 16 fields); 0 = no pair kernel (one field).
+// Build-time A/B (round 6): bit-exact (204 flat/wide/golden/C-ABI GPU tests), but Flat16 encode
+// 0.1255-0.1293 ms with pairs vs 0.1249-0.1287 without (gpurun_out/encab1, three alternating runs
+// on one box): a one-wave group already has all 64 records' loads in flight, so a second wave per
+// slab adds issue slots, not memory parallelism.  Off by default.
+#ifndef SPEC_AB_ENC_PAIR
+#define SPEC_AB_ENC_PAIR 0
+#endif
+int enc_pair_split(const spec_schema *s) {
+    const int n = (int)s->nfields;
+    if (!SPEC_AB_ENC_PAIR || n < 2) return 0;
+    auto cost = [](int k) {
+        switch (k) {
+        case SPEC_KIND_BOOL: case SPEC_KIND_BYTE: return 8;
+        case SPEC_KIND_FLOAT32: return 10;
+        case SPEC_KIND_INT64: case SPEC_KIND_UINT64: return 14;
+        case SPEC_KIND_BIN128: return 16;
+        case SPEC_KIND_BIN256: return 28;
+        case SPEC_KIND_STRING: case SPEC_KIND_BYTES: return 100;
+        }
+        return 12; // 16/32-bit ints, float64, bin64
+    };
+    int total = 40 + 5 * n, pre[SPEC_KFIELDS + 1] = {0};
+    for (int f = 0; f < n; f++) {
+        pre[f + 1] = pre[f] + cost(s->fields[f].kind);
+        total += cost(s->fields[f].kind);
+    }
+    int best = 1, best_max = 1 << 30;
+    for (int h = 1; h < n; h++) {
+        const int m = std::max(pre[h], total - pre[h]);
+        if (m < best_max) {
+            best_max = m;
+            best = h;
+        }
+    }
+    return best;
+}
+
 std::string generate_encode(const spec_schema *s) {
     std::ostringstream o;
     o << "#include \"encode_core.hpp\"\n";
@@ -267,6 +308,10 @@ std::string generate_encode(const spec_schema *s) {
       << "extern \"C\" __global__ __launch_bounds__(256) void spec_encode_write_jit(spec::EncodeArgs a) {\n"
       << "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
       << "  spec::encode_write_body<P>(a, smem);\n}\n";
+    if (const int h = enc_pair_split(s))
+        o << "extern \"C\" __global__ __launch_bounds__(512) void spec_encode_write_pair_jit(spec::EncodeArgs a) {\n"
+          << "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+          << "  spec::encode_write_pair_body<P, " << h << ">(a, smem);\n}\n";
     return o.str();
 }
 
@@ -423,7 +468,7 @@ Entry load(const std::vector<char> &code, Prog p) {
     }
     const char *names[4][4] = {{"spec_decode_flat_jit", "spec_decode_flat_err_jit", "spec_decode_flat_pair_jit",
                                 "spec_decode_flat_err_pair_jit"},
-                               {"spec_encode_size_jit", "spec_encode_write_jit", nullptr, nullptr},
+                               {"spec_encode_size_jit", "spec_encode_write_jit", nullptr, nullptr}, // (+ the pair kernel, optional)
                                {"spec_decode_nested_jit", "spec_decode_nested2_jit", "spec_decode_nested3_jit",
                                 "spec_decode_nested_pair_jit"},
                                {"spec_encode_nested_size_jit", "spec_encode_nested_write_jit", nullptr, nullptr}};
@@ -437,6 +482,10 @@ Entry load(const std::vector<char> &code, Prog p) {
     }
     for (int i = 0; ok && i < 4; i++)
         if (names[p][i]) ok = hipModuleGetFunction(&e.fn[i], e.mod, names[p][i]) == hipSuccess;
+    if (ok && p == ENCODE && hipModuleGetFunction(&e.fn[2], e.mod, "spec_encode_write_pair_jit") != hipSuccess) {
+        (void)hipGetLastError(); // a one-field schema has no pair kernel
+        e.fn[2] = nullptr;
+    }
     if (!ok) {
         (void)hipGetLastError();
         e.failed = true;
@@ -1342,8 +1391,15 @@ int jit_launch_encode(const spec_schema *schema, const EncodeArgs &a, bool write
     size_t size = sizeof(args);
     void *extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size,
                      HIP_LAUNCH_PARAM_END};
-    hipError_t rc = hipModuleLaunchKernel(e->fn[write ? 1 : 0], (unsigned)a.nblocks, 1, 1, ENC_BLOCK, 1, 1,
-                                          write ? (unsigned)enc_write_lds_bytes() : 0, stream, nullptr, extra);
+    hipError_t rc;
+    if (write && e->fn[2]) { // the write pass on wave pairs (encode_write_pair_body)
+        const int h = enc_pair_split(schema);
+        rc = hipModuleLaunchKernel(e->fn[2], (unsigned)a.nblocks, 1, 1, ENC_PAIR_BLOCK, 1, 1,
+                                   (unsigned)enc_pair_lds_bytes(h), stream, nullptr, extra);
+    } else {
+        rc = hipModuleLaunchKernel(e->fn[write ? 1 : 0], (unsigned)a.nblocks, 1, 1, ENC_BLOCK, 1, 1,
+                                   write ? (unsigned)enc_write_lds_bytes() : 0, stream, nullptr, extra);
+    }
     return rc == hipSuccess ? 1 : -1;
 }
 

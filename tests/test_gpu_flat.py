@@ -356,6 +356,28 @@ def test_encode_schemas(dev, kernel, case):
     check_decode(dev, schema, stream, ends, case + "/decode")
 
 
+@pytest.mark.parametrize("n", [1000, 4096 + 33])
+def test_encode_pair_groups_over_slab(dev, kernel, n):
+    """64-record groups whose bytes exceed the write pass's slab (long strings: written straight
+    to HBM) among groups staged in LDS, single long records inside staged groups, a partial last
+    block and group — the bytes stay the oracle Writer's.  (It was written for the wave-pair write
+    pass, encode_write_pair_body, built with -DSPEC_AB_ENC_PAIR=1, and passed there too.)"""
+    a_cols, a_heaps = workload.flat16(n, seed=21)
+    b_cols, b_heaps = workload.gen_columns(FLAT16, n, 22, str_len=(300, 700))
+    big = np.zeros(n, bool)
+    for g in (2, 9, (n - 1) // 64):
+        big[64 * g: 64 * g + 64] = True
+    big[5::97] = True  # single long records inside staged groups
+    cols = [np.where(big[:, None], b, a) for a, b in zip(a_cols, b_cols)]
+    heaps = {}
+    for f, h in a_heaps.items():
+        heaps[f] = np.concatenate([h, b_heaps[f]])
+        sp = cols[f].view(np.uint32).reshape(n, 2).copy()
+        sp[big, 0] += h.size  # b's spans index the second part of the joined heap
+        cols[f] = sp.view(np.uint8).reshape(n, 8)
+    check_encode(dev, FLAT16, cols, heaps, n, f"flat16 pair groups n={n}")
+
+
 def test_encode_capacity_and_errors(dev, kernel):
     import torch
 
