@@ -88,7 +88,9 @@ typedef enum spec_status {
     SPEC_STATUS_INVALID_DATA = 5,       /* "decode message: invalid data"       */
     SPEC_STATUS_PANIC = 6,              /* the reference would panic (malformed list table) */
     SPEC_STATUS_INVALID_VALUE = 7,      /* spec_parse_messages: a nested value failed to parse */
-    SPEC_STATUS_TOO_DEEP = 8,           /* spec_parse_messages: nesting deeper than 32 levels */
+    SPEC_STATUS_TOO_DEEP = 8,           /* spec_parse_messages: nesting deeper than 2,097,152 levels
+                                           (the reference's recursion exhausts Go's 1 GB stack
+                                           at a depth of that order) */
 } spec_status;
 
 typedef enum spec_rc {
@@ -535,7 +537,8 @@ int spec_shard_host_decode(spec_shard *c, const uint8_t *stream_host, uint64_t s
  * mpx runs on each received frame (mpx/conn_reader.go:119).  status[i]: SPEC_STATUS_OK, the
  * top-level trailer class (1-5), SPEC_STATUS_PANIC (a list element whose start > end: Go
  * panics), SPEC_STATUS_INVALID_VALUE (any nested error), or SPEC_STATUS_TOO_DEEP (more than
- * 32 nested containers; the reference recurses without a bound).  sizes[i] (optional) =
+ * 2,097,152 nested containers: records deeper than 32 are parsed again with their stacks in a
+ * stream-ordered HBM scratch of the call, 64 MiB).  sizes[i] (optional) =
  * ParseMessage's size (bytes of the message), 0 on error.  head = bytes before each record
  * (4 for mpx frames, see spec_frames_index). */
 int spec_parse_messages(const uint8_t *stream_bytes, uint64_t stream_len, const uint64_t *ends, uint64_t n,

@@ -156,6 +156,14 @@ int launch_nested_decode(const spec_nested_schema *schema, NestedArgs a, double 
 #define SPEC_AB_LOOKBACK 0
 #endif
 bool nested_lookback() { return SPEC_AB_LOOKBACK != 0; }
+// -DSPEC_AB_NESTED_PAIR_LB=1: spec_decode_nested_onepass on the wave-pair kernel with one
+// look-back per group (round 6, nested_decode_pair ONEPASS: the stream read once).  Config 4:
+// 0.1754-0.1764 ms against 0.1109-0.1131 ms for the count + scan + two-pass pair decode
+// (gpurun_out/nencp2, two runs each on one box): 16 K groups each waiting on the agent-scope
+// look-back words of the groups before it hold their slabs idle; off by default.
+#ifndef SPEC_AB_NESTED_PAIR_LB
+#define SPEC_AB_NESTED_PAIR_LB 0
+#endif
 
 // The two-pass decode on a wave pair per group (decode_nested_core.hpp nested_decode_pair; the
 // JIT kernels only): -DSPEC_AB_NESTED_PAIR=0 runs a wave per group instead.
@@ -174,6 +182,15 @@ int launch_nested_onepass(const spec_nested_schema *schema, NestedArgs a, double
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     if (!nested_lookback()) {
+        if (SPEC_AB_NESTED_PAIR_LB && nested_pair()) {
+            // the wave-pair decode with one look-back per group: the stream read once
+            a.slab = nested_slab_bytes(avg_record);
+            const uint64_t groups = (a.n + 63) / 64;
+            if (hipMemsetAsync(a.group_base, 0, (groups + 1) * sizeof(uint64_t), stream) != hipSuccess) return -1;
+            const int j = jit_launch_nested(schema, a, NESTED_PAIR_ONEPASS, stream);
+            if (j < 0) return -1;
+            if (j > 0) return 0;
+        }
         if (launch_nested_index(a, avg_record, stream)) return -1;
         return launch_nested_decode(schema, a, avg_record, stream);
     }

@@ -559,12 +559,17 @@ __device__ __forceinline__ void nested_decode_body(const NestedArgs &a) {
 // than the slab: wave 0 alone, in two halves of 32 records (nested_decode_part).
 // SELF: the other waves open each record's list themselves (rec_open + list_open, the generic
 // path's lookup) instead of waiting for wave 0's posted lists.
-template <class OSpec, class ISpec, int U = NESTED_ITEM_U, int P = 2, bool SELF = false>
+// ONEPASS (round 6): no index kernels.  The group's item total is known once wave 0 has posted
+// the lists; wave 0 then publishes it and finds the group's first item by the decoupled
+// look-back over the earlier groups (lookback: groups in block order, a.group_base = one state
+// word per group, zeroed by the launcher), both waves wait for it at a barrier and decode the
+// items.  The stream is read once (the count pass re-read each record's tail).
+template <class OSpec, class ISpec, int U = NESTED_ITEM_U, int P = 2, bool SELF = false, bool ONEPASS = false>
 __device__ __forceinline__ void nested_decode_pair(const NestedArgs &a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint64_t g = blockIdx.x;
-    if (a.xcd) {
+    if (a.xcd && !ONEPASS) {
         const uint64_t per = (gridDim.x + 7) / 8;
         g = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
     }
@@ -573,7 +578,7 @@ __device__ __forceinline__ void nested_decode_pair(const NestedArgs &a) {
     uint8_t *slab = smem;
     uint32_t *xl = (uint32_t *)(smem + a.slab); // [4][64]: count, dsize | big << 31, dstart, tstart
     __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(a.stream, a.stream_len);
-    const uint64_t item_base = uniform64(a.group_base[g]);
+    uint64_t item_base = ONEPASS ? 0 : uniform64(a.group_base[g]);
     DecodeArgs d;
     d.stream = a.stream;
     d.stream_len = a.stream_len;
@@ -586,6 +591,13 @@ __device__ __forceinline__ void nested_decode_pair(const NestedArgs &a) {
     const Group gr = make_group(d, base, lane, lo, hi, a.slab);
     if (!gr.in_lds) {
         if (wave == 0) {
+            if constexpr (ONEPASS) { // the group's item total from HBM first, then its base
+                GlobalSrc gs{a.stream, a.stream_len};
+                const uint32_t cnt = base + lane < a.n ? record_count(gs, (long long)gr.rec_lo, (long long)gr.rec_hi, a) : 0u;
+                const uint32_t tot = wave_sum(cnt);
+                item_base = uniform64(lookback(a.group_base, g, tot, lane));
+                if (g == (a.n - 1) / 64 && lane == 0) *a.total = item_base + tot;
+            }
             const uint32_t first = nested_decode_part<OSpec, ISpec, false, U>(a, rsrc, slab, g, item_base, lane, 0, 32);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the first half's LDS reads done
             __builtin_amdgcn_wave_barrier();
@@ -632,6 +644,18 @@ __device__ __forceinline__ void nested_decode_pair(const NestedArgs &a) {
     const uint32_t incl = wave_incl_scan(li.count, lane);
     const uint32_t excl = incl - li.count;
     const uint32_t total = __shfl(incl, 63);
+    if constexpr (ONEPASS) {
+        uint64_t *xb = (uint64_t *)(xl + 256); // the group's base, from wave 0 to the others
+        if (wave == 0) {
+            const uint64_t b = uniform64(lookback(a.group_base, g, total, lane));
+            if (lane == 0) {
+                *xb = b;
+                if (g == (a.n - 1) / 64) *a.total = b + total;
+            }
+        }
+        __syncthreads(); // the base is posted
+        item_base = uniform64(*xb);
+    }
     if (wave == 0 && valid) {
         a.item_begin[r] = (uint32_t)(item_base + excl);
         if (r == a.n - 1) a.item_begin[a.n] = (uint32_t)(item_base + incl);

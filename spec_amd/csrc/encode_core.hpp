@@ -946,10 +946,16 @@ struct SpecEnc {
         }
     }
     // the values of fields [F0, F1) from em.pos (no finish: the pending dword stays in em.acc)
-    template <int F0, int F1, class E>
+    template <int F0, int F1, class E, class Lists = NoListEmit>
     static __device__ __forceinline__ void emit_range(const EncFields &f, E &em, Rec &x, decltype(em.pos) start,
-                                                      uint64_t r) {
-        emit_values<F0, E, NoListEmit, F1>(f, em, x, start, r, NoListEmit());
+                                                      uint64_t r, const Lists &lists = Lists()) {
+        emit_values<F0, E, Lists, F1>(f, em, x, start, r, lists);
+    }
+    // the K_LIST field's index (-1: none)
+    static constexpr int list_field() {
+        for (int f = 0; f < N; f++)
+            if (Spec::kind[f] == K_LIST) return f;
+        return -1;
     }
     // the table and trailer after the values (x.end[] of every field set; no finish)
     template <class E>

@@ -155,11 +155,15 @@ struct KnownListSize {
 // the items start.  An empty list is no jump: the emitter keeps its pending bytes (a HEAD_ST4
 // emitter restarting at the same position would zero the bytes below it, and no item would
 // rewrite them).
+// merge_slab (the pair write pass's A2, run once the items are final): after the jump the
+// HEAD_ST4 emitter resumes with the bytes already in the slab below the list's end (the last
+// item's tail) as its pending bytes, so its first whole-dword store writes them back unchanged.
 struct WaveListEmit {
     const uint32_t *pre; // wave item prefix at this record's first item
     uint32_t count, data;
     bool big;
     mutable int lstart;
+    const uint8_t *merge_slab = nullptr;
     template <class E>
     __device__ __forceinline__ void operator()(E &em, uint32_t, uint64_t) const {
         lstart = (int)em.pos;
@@ -168,6 +172,10 @@ struct WaveListEmit {
             em.pos += data;
             em.lo = em.pos;
             em.acc = 0;
+            if (merge_slab && (em.pos & 3)) {
+                const uint32_t w = *(const uint32_t *)(merge_slab + (em.pos & ~3));
+                em.acc = w & (0xffffffffu >> (32 - 8 * (uint32_t)(em.pos & 3)));
+            }
         }
         const uint32_t p0 = pre[0];
         if constexpr (E::kHeadSt4) {
@@ -179,7 +187,10 @@ struct WaveListEmit {
 #pragma unroll
                 for (int j = 0; j < 8; j++) {
                     const bool in = j < (int)count;
-                    const uint32_t end = pre[in ? j + 1 : 0] - p0; // element offset = item end - list start
+                    // element offset = item end - list start; the last item ends at the list's data
+                    // size (pre[count] belongs to the next record, whose entries the pair write
+                    // pass may already have turned into slab positions)
+                    const uint32_t end = in ? (j + 1 < (int)count ? pre[j + 1] - p0 : data) : 0u;
                     w[j >> 1] |= (in ? (uint32_t)__builtin_bswap16((uint16_t)end) : 0u) << (16 * (j & 1));
                 }
                 const uint32_t L = vlen32(data);
@@ -200,7 +211,7 @@ struct WaveListEmit {
             }
         }
         for (uint32_t j = 0; j < count; j++) {
-            const uint32_t end = pre[j + 1] - p0; // element offset = item end - list start
+            const uint32_t end = j + 1 < count ? pre[j + 1] - p0 : data; // item end - list start
             em.put_n(big ? bswap32(end) : (uint32_t)__builtin_bswap16((uint16_t)end), big ? 4 : 2);
         }
         em.rvarint(data);
@@ -438,6 +449,168 @@ __device__ __forceinline__ void nested_enc_write_body(const NestedEncodeArgs &a,
     }
     wave_sync();
     copy_slab_out(slab, a.out + S - head, head, head + (E - S), lane);
+}
+
+
+// ---- the write pass on wave PAIRS (schema-specialised outer encoder, size-pass prefix cache) ----
+// Items [klo, khi) of the wave's item range (prefix entries already turned into slab positions),
+// chunks of 64 from the LAST to the first, three chunks in flight (as nested_enc_write_body B).
+template <class IP, class Sink>
+__device__ __forceinline__ void emit_item_range(const NestedEncodeArgs &a, const Sink &k, const uint32_t *pre,
+                                                uint32_t I0, uint32_t klo, uint32_t khi, const uint8_t *inv_item,
+                                                int lane) {
+    if (khi <= klo) return;
+    auto idx = [&](int cc) {
+        const uint32_t kk = (uint32_t)cc + (uint32_t)lane;
+        return I0 + (kk < khi ? kk : khi - 1);
+    };
+    int c = (int)(klo + ((khi - klo - 1) & ~63u));
+    typename IP::Rec cur, nxt, nn;
+    cur = IP::load(a.item, idx(c));
+    if (c - 64 >= (int)klo) IP::load_cols(a.item, idx(c - 64), nxt);
+    for (; c >= (int)klo; c -= 64) {
+        if (c - 128 >= (int)klo) IP::load_cols(a.item, idx(c - 128), nn);
+        if (c - 64 >= (int)klo) IP::load_heaps(a.item, nxt);
+        const uint32_t kk = (uint32_t)c + (uint32_t)lane;
+        if (kk < khi) {
+            const uint32_t i = I0 + kk;
+            bool e2 = false;
+            const RecSize irs = IP::size(a.item, cur, i, false, e2);
+            IP::emit(a.item, k, (int)pre[kk], i, cur, irs, inv_item);
+        }
+        wave_sync();
+        cur = nxt;
+        nxt = nn;
+    }
+}
+
+// A 512-thread block takes the size pass's 256-record block as four 64-record groups, each
+// written by a wave PAIR sharing the group's prefix and slab (the same LDS per group as the
+// one-wave pass, twice the waves per CU).  Wave 0 emits the records' outer fields before the
+// list field (A1) and the items of records [0, R0); wave 1 the items of records [R0, 64)
+// concurrently (R0: the record boundary near SPEC_AB_NENC_SPLIT % of the group's items); after a
+// barrier wave 0 emits the rest of each record (A2: list table and trailer, later fields, outer
+// table and trailer) with an emitter that never stores below its start, and both copy the slab
+// out.  Ordering: the HEAD_ST4 emitters of A1 and of the items store whole dwords, the first
+// covering <= 3 bytes below its start; those bytes are a previous item's (same wave: written
+// later in chunk order, as in the one-wave pass), the record's A1 tail (kept pending across the
+// barrier, then stored bytewise) or the previous record's A2 bytes (emitted after the barrier).
+// The split is at a record boundary, so no item byte is covered by the other wave's stores.
+#ifndef SPEC_AB_NENC_SPLIT
+#define SPEC_AB_NENC_SPLIT 45
+#endif
+// measurement builds only (wrong bytes): skip the items (1), the copy-out (2), the outer records (4)
+#ifndef SPEC_AB_NENC_SKIP
+#define SPEC_AB_NENC_SKIP 0
+#endif
+template <class OP, class IP>
+__device__ __forceinline__ void nested_enc_write_pair_body(const NestedEncodeArgs &a, uint8_t *smem) {
+    constexpr int LF = OP::list_field();
+    static_assert(LF >= 0, "the outer schema holds the list field");
+    uint64_t *wsum = (uint64_t *)smem;
+    uint8_t *inv_outer = smem + 32, *inv_item = smem + 96;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, grp = wave >> 1, half = wave & 1;
+    uint64_t blk = blockIdx.x;
+    if (a.xcd) blk = (blockIdx.x & 7) * ((gridDim.x + 7) / 8) + (blockIdx.x >> 3);
+    if (blk >= a.nblocks) return; // block-uniform
+    const uint64_t total = a.block_sums[a.nblocks], blk_pre = a.block_sums[blk];
+    if (threadIdx.x < a.outer.nfields) inv_outer[a.outer.order[threadIdx.x]] = (uint8_t)threadIdx.x;
+    if (threadIdx.x < a.item.nfields) inv_item[a.item.order[threadIdx.x]] = (uint8_t)threadIdx.x;
+    uint32_t *pre = (uint32_t *)(smem + NENC_HEAD + grp * NENC_WAVE_LDS);
+    uint8_t *slab = (uint8_t *)pre + NENC_PRE;
+    const uint64_t r = blk * NENC_BLOCK + grp * 64 + lane, gbase = blk * NENC_BLOCK + grp * 64;
+    const bool valid = r < a.n, live = gbase < a.n; // live: group-uniform
+    typename OP::Rec orec;
+    if (half == 0) orec = OP::load(a.outer, valid ? r : a.n - 1); // in flight across the prefix
+    // the group's items and the size pass's verdict and prefix (both waves load half the prefix)
+    const uint32_t b = live ? a.item_begin[valid ? r : a.n] : 0u;
+    const uint32_t e = valid ? a.item_begin[r + 1] : b;
+    const uint32_t I0 = __builtin_amdgcn_readfirstlane(b);
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(__shfl(e, 63)) - I0;
+    const bool fast = live && a.wave_ok[gbase >> 6] != 0;
+    if (fast) {
+        if (half == 0 && lane == 0) pre[0] = 0;
+        for (uint32_t q = (uint32_t)(half * 64 + lane); q < cnt; q += 128) pre[q + 1] = a.item_pre[I0 + q];
+    }
+    if (total > a.out_cap) return; // capacity or encoder error: block-uniform, before any barrier
+    __syncthreads(); // (1) prefix and inverse orders in LDS
+    ListSize ls = {0, 0, 0, false};
+    RecSize rs = {0, 0, false};
+    bool err = false;
+    if (half == 0 && live) {
+        LaneRecord L;
+        L.r = r;
+        L.valid = valid;
+        L.b = b;
+        L.e = e;
+        L.I0 = I0;
+        L.cnt = cnt;
+        L.fast = fast;
+        rs = lane_record_size<OP>(a, L, orec, pre, false, err, ls);
+        if (!valid) rs.total = 0;
+    }
+    uint64_t x = rs.total; // group exclusive scan of sizes (wave 0)
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (half == 0 && lane == 63) wsum[grp] = live ? x : 0;
+    __syncthreads(); // (2) group sums
+    uint64_t S = blk_pre;
+    for (int g = 0; g < grp; g++) S += wsum[g];
+    const uint64_t E = S + wsum[grp];
+    const uint64_t start = S + x - rs.total; // (wave 0)
+    const uint64_t head = ((uint64_t)(a.out + S)) & 15;
+    const bool staged = live && fast && head + (E - S) + 16 <= (uint64_t)NENC_SLAB; // group-uniform
+    if (half == 0 && valid) a.ends[r] = start + rs.total;
+    const int p0 = (int)(head + (start - S));
+    int lst = 0;
+    if (half == 0 && staged && valid) {
+        // the list's slab position from the sizes of the fields before it; the record's prefix
+        // entries become its items' slab positions
+        bool e1 = false;
+        lst = p0 + (int)OP::template data_size<0, KnownListSize, LF>(a.outer, orec, r, false, e1, KnownListSize{0});
+        if (ls.count > 0) {
+            const uint32_t k0 = b - I0, k1 = e - I0;
+            const int delta = lst - (int)pre[k0];
+            for (uint32_t q = k0; q < k1; q++) pre[q] = (uint32_t)((int)pre[q] + delta);
+        }
+    }
+    // the split: the first record whose items start at or past SPEC_AB_NENC_SPLIT % of the group's
+    uint32_t K0 = cnt;
+    if (staged) {
+        const uint64_t m = __ballot(valid && (uint64_t)(b - I0) * 100 >= (uint64_t)cnt * SPEC_AB_NENC_SPLIT);
+        if (m) K0 = __builtin_amdgcn_readlane(b, __builtin_ctzll(m)) - I0;
+    }
+    __syncthreads(); // (3) item positions
+    LdsSink k{slab, (int)(smem + 160 - slab)}; // dummy dword in the header
+    typename OP::Rec xo = orec;
+    Emit<LdsSink, int, true> em(k, p0);
+    if (staged) {
+        if (half == 0) {
+            if (valid && !(SPEC_AB_NENC_SKIP & 4)) OP::template emit_range<0, LF>(a.outer, em, xo, p0, r); // A1, its tail left pending
+            if (!(SPEC_AB_NENC_SKIP & 1)) emit_item_range<IP>(a, k, pre, I0, 0u, K0, inv_item, lane);
+        } else if (!(SPEC_AB_NENC_SKIP & 1)) {
+            emit_item_range<IP>(a, k, pre, I0, K0, cnt, inv_item, lane);
+        }
+    } else if (half == 0 && valid) {
+        // a group that does not fit the slab (or without the item-parallel verdict): each record
+        // straight to HBM on its lane
+        GlobalSink g{a.out};
+        ListEmitter<GlobalSink, long long> le{&a, &g, inv_item};
+        emit_message(a.outer, g, (long long)start, r, rs, inv_outer, le);
+    }
+    __syncthreads(); // (4) every whole-dword store of A1 and of the items is done
+    if (staged && half == 0 && valid && !(SPEC_AB_NENC_SKIP & 4)) {
+        // A2: the same emitter from the list field on; the hook stores A1's pending tail bytewise
+        // and resumes past the items with their last bytes read back (WaveListEmit merge_slab)
+        WaveListEmit le{pre + (b - I0), ls.count, (uint32_t)ls.data, ls.big, 0, slab};
+        OP::template emit_range<LF, OP::N>(a.outer, em, xo, p0, r, le);
+        OP::emit_table_trailer(em, xo, rs);
+        em.finish();
+    }
+    __syncthreads(); // (5) the group's slab is complete
+    if (staged && !(SPEC_AB_NENC_SKIP & 2)) copy_slab_out_t<128>(slab, a.out + S - head, head, head + (E - S), threadIdx.x & 127);
 }
 
 } // namespace spec

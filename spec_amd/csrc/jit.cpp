@@ -45,7 +45,7 @@ namespace {
 
 struct Entry {
     hipModule_t mod = nullptr;
-    hipFunction_t fn[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipFunction_t fn[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     bool failed = false;
 };
 
@@ -208,7 +208,11 @@ std::string generate_nested(const spec_nested_schema *s) {
       << "extern \"C\" __global__ __launch_bounds__(" << 64 * SPEC_AB_NESTED_WAVES
       << ") void spec_decode_nested_pair_jit(spec::NestedArgs a) {\n"
       << "  spec::nested_decode_pair<" << specs << ", " << SPEC_AB_NESTED_U << ", " << SPEC_AB_NESTED_WAVES
-      << ", " << (SPEC_AB_NESTED_SELF ? "true" : "false") << ">(a);\n}\n";
+      << ", " << (SPEC_AB_NESTED_SELF ? "true" : "false") << ">(a);\n}\n"
+      << "extern \"C\" __global__ __launch_bounds__(" << 64 * SPEC_AB_NESTED_WAVES
+      << ") void spec_decode_nested_pairlb_jit(spec::NestedArgs a) {\n"
+      << "  spec::nested_decode_pair<" << specs << ", " << SPEC_AB_NESTED_U << ", " << SPEC_AB_NESTED_WAVES
+      << ", false, true>(a);\n}\n";
     return o.str();
 }
 
@@ -240,8 +244,18 @@ bool has_nested_encoder(const spec_nested_schema *s) {
     return !nested_wide(s) && (has_outer_encoder(&s->outer) || has_encoder(&s->item));
 }
 
+// build-time A/B of the nested pair write pass (encode_nested_core.hpp), passed into the
+// generated source: the JIT compile sees only what the source defines
+#ifndef SPEC_AB_NENC_SPLIT
+#define SPEC_AB_NENC_SPLIT 45
+#endif
+#ifndef SPEC_AB_NENC_SKIP
+#define SPEC_AB_NENC_SKIP 0
+#endif
 std::string generate_nested_encode(const spec_nested_schema *s) {
     std::ostringstream o;
+    if (SPEC_AB_NENC_SPLIT != 45) o << "#define SPEC_AB_NENC_SPLIT " << SPEC_AB_NENC_SPLIT << "\n";
+    if (SPEC_AB_NENC_SKIP) o << "#define SPEC_AB_NENC_SKIP " << SPEC_AB_NENC_SKIP << "\n";
     o << "#include \"encode_nested_core.hpp\"\n";
     const bool fo = has_outer_encoder(&s->outer), fi = has_encoder(&s->item);
     if (fo) emit_enc_spec(o, "GenOuter", &s->outer);
@@ -254,6 +268,10 @@ std::string generate_nested_encode(const spec_nested_schema *s) {
       << "extern \"C\" __global__ __launch_bounds__(256) void spec_encode_nested_write_jit(spec::NestedEncodeArgs a) {\n"
       << "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
       << "  spec::nested_enc_write_body<OP, IP>(a, smem);\n}\n";
+    if (fo) // the write pass on wave pairs (needs the outer list field at a constant index)
+        o << "extern \"C\" __global__ __launch_bounds__(512) void spec_encode_nested_write_pair_jit(spec::NestedEncodeArgs a) {\n"
+          << "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+          << "  spec::nested_enc_write_pair_body<OP, IP>(a, smem);\n}\n";
     return o.str();
 }
 
@@ -484,6 +502,15 @@ Entry load(const std::vector<char> &code, Prog p) {
         if (names[p][i]) ok = hipModuleGetFunction(&e.fn[i], e.mod, names[p][i]) == hipSuccess;
     if (ok && p == ENCODE && hipModuleGetFunction(&e.fn[2], e.mod, "spec_encode_write_pair_jit") != hipSuccess) {
         (void)hipGetLastError(); // a one-field schema has no pair kernel
+        e.fn[2] = nullptr;
+    }
+    if (ok && p == NESTED && hipModuleGetFunction(&e.fn[4], e.mod, "spec_decode_nested_pairlb_jit") != hipSuccess) {
+        (void)hipGetLastError();
+        e.fn[4] = nullptr;
+    }
+    if (ok && p == NESTED_ENC &&
+        hipModuleGetFunction(&e.fn[2], e.mod, "spec_encode_nested_write_pair_jit") != hipSuccess) {
+        (void)hipGetLastError(); // no specialised outer encoder: no pair kernel
         e.fn[2] = nullptr;
     }
     if (!ok) {
@@ -1426,6 +1453,13 @@ int jit_launch_nested(const spec_nested_schema *schema, const NestedArgs &a, int
         threads = 64 * SPEC_AB_NESTED_WAVES;
         lds = a.slab + 1024; // the posted lists: 4 words per record
     }
+    if (mode == NESTED_PAIR_ONEPASS) { // a wave pair per group, one look-back per group, block order
+        if (!e->fn[4]) return 0;
+        args.xcd = 0;
+        hipError_t rc = hipModuleLaunchKernel(e->fn[4], (unsigned)((a.n + 63) / 64), 1, 1, 64 * SPEC_AB_NESTED_WAVES, 1,
+                                              1, a.slab + 1024 + 16, stream, nullptr, extra);
+        return rc == hipSuccess ? 1 : -1;
+    }
     if (mode == NESTED_ONEPASS) { // DEC_WAVES groups per block: one look-back per block
         grid = (grid + DEC_WAVES - 1) / DEC_WAVES;
         threads = 64 * DEC_WAVES;
@@ -1440,6 +1474,9 @@ long long jit_compile_only_nested_encode(const spec_nested_schema *schema) {
     return (long long)compile_source(generate_nested_encode(schema), NESTED_ENC).size();
 }
 
+#ifndef SPEC_AB_NENC_PAIR
+#define SPEC_AB_NENC_PAIR 1
+#endif
 int jit_launch_nested_encode(const spec_nested_schema *schema, const NestedEncodeArgs &a, bool write,
                              hipStream_t stream) {
     const Entry *e = lookup_nested_encode(schema);
@@ -1451,8 +1488,10 @@ int jit_launch_nested_encode(const spec_nested_schema *schema, const NestedEncod
                      HIP_LAUNCH_PARAM_END};
     const unsigned lds = (unsigned)(write ? nenc_write_lds_bytes() : nenc_size_lds_bytes());
     const unsigned grid = (unsigned)(args.xcd ? (a.nblocks + 7) / 8 * 8 : a.nblocks);
-    hipError_t rc = hipModuleLaunchKernel(e->fn[write ? 1 : 0], grid, 1, 1, NENC_BLOCK, 1, 1, lds,
-                                          stream, nullptr, extra);
+    // the write pass on wave pairs when the size pass left its item prefixes (nested_enc_write_pair_body)
+    const bool pair = write && SPEC_AB_NENC_PAIR && e->fn[2] && a.item_pre && a.wave_ok;
+    hipError_t rc = hipModuleLaunchKernel(e->fn[pair ? 2 : write ? 1 : 0], grid, 1, 1, pair ? 2 * NENC_BLOCK : NENC_BLOCK,
+                                          1, 1, lds, stream, nullptr, extra);
     return rc == hipSuccess ? 1 : -1;
 }
 

@@ -52,7 +52,10 @@ int launch_nested_onepass(const spec_nested_schema *schema, NestedArgs a, double
 // into LDS by their records' lanes), NESTED_HALVES (as GROUPS, slabs for half a group),
 // NESTED_TAILCOUNT (as GROUPS, the count pass from each record's last 64 bytes), NESTED_XCD (as
 // TAILCOUNT with an XCD-aware block order for the decode pass: the default)
-enum { NESTED_ONEPASS = 0, NESTED_GROUPS = 1, NESTED_RANGES = 2, NESTED_HALVES = 3, NESTED_TAILCOUNT = 4, NESTED_XCD = 5 };
+// NESTED_PAIR_ONEPASS (round 6): the decode on wave pairs with one look-back per group, no
+// index kernels (spec_decode_nested_onepass)
+enum { NESTED_ONEPASS = 0, NESTED_GROUPS = 1, NESTED_RANGES = 2, NESTED_HALVES = 3, NESTED_TAILCOUNT = 4, NESTED_XCD = 5,
+       NESTED_PAIR_ONEPASS = 6 };
 int jit_launch_nested(const spec_nested_schema *schema, const NestedArgs &a, int mode, hipStream_t stream);
 bool nested_lookback(); // build-time SPEC_AB_LOOKBACK: spec_decode_nested_onepass runs the look-back kernel
 long long jit_compile_only_nested(const spec_nested_schema *schema);

@@ -9,9 +9,14 @@
 //                    non-empty element (GetBytes: end > dataSize => nil; start > end panics)
 //   ParseValue(b)    internal/types/value.go:49-113 — per type: the decoder's error checks,
 //                    recursion into lists/messages, "unsupported type" otherwise.
-// One lane per record, depth-first with an explicit stack (the reference recurses; nesting
-// deeper than VAL_MAX_DEPTH reports SPEC_STATUS_TOO_DEEP).  Records are staged in LDS like
-// the decoders'; larger spans parse from HBM.
+// One lane per record, depth-first with an explicit stack of VAL_MAX_DEPTH frames (the reference
+// recurses).  Records are staged in LDS like the decoders'; larger spans parse from HBM.  A record
+// nested deeper than VAL_MAX_DEPTH is listed and parsed again by deep_kernel (round 6; the call
+// returned SPEC_STATUS_TOO_DEEP for it before) with its stack in an HBM arena: 8,192 frames per
+// thread, then, for a record deeper still, DEEP_ARENA / sizeof(Frame) = 2,097,152 frames on one
+// thread.  Only deeper nesting reports SPEC_STATUS_TOO_DEEP: the reference's recursion (ParseValue
+// -> ParseMessage / ParseList -> ParseValue per level) would exhaust Go's 1 GB goroutine stack at a
+// depth of that order and crash.
 #include <hip/hip_runtime.h>
 
 #include "decode_core.hpp"
@@ -28,6 +33,29 @@ struct Frame {
     uint32_t nent, i, dsize;
     uint8_t list, big;
 };
+
+// the main pass's stack (registers / scratch) and the deep pass's (a slice of the HBM arena)
+struct LocalStack {
+    Frame f[VAL_MAX_DEPTH];
+    static constexpr int cap = VAL_MAX_DEPTH;
+    __device__ __forceinline__ Frame &operator[](int i) { return f[i]; }
+};
+struct ArenaStack {
+    Frame *f;
+    int cap;
+    __device__ __forceinline__ Frame &operator[](int i) const { return f[i]; }
+};
+
+// the deep pass's workspace (stream-ordered scratch of the call): the records the main pass found
+// too deep, then the frame arena
+constexpr uint32_t DEEP_LIST_CAP = 1u << 16;
+constexpr size_t DEEP_ARENA = 64ull << 20;
+constexpr int DEEP_THREADS = 256;
+struct DeepWs {
+    uint32_t count, pad;
+    uint32_t list[DEEP_LIST_CAP];
+};
+constexpr size_t DEEP_WS_BYTES = ((sizeof(DeepWs) + 255) & ~(size_t)255) + DEEP_ARENA;
 
 // The decoder error checks ParseValue runs for a scalar of type `type` ending at e, and the size
 // it reports (value.go:49-113: n = bytes the decoder consumed from the end): 0 ok, 1 an error,
@@ -100,9 +128,9 @@ __device__ __forceinline__ uint32_t be_at(const Src &s, long long p, int bytes) 
 
 // ParseMessage (root PARSE_MESSAGE), ParseList (PARSE_LIST) or ParseValue (PARSE_VALUE) of record
 // [rs, re): status and size (the parsed size; 0 on error).
-template <class Src>
+template <class Src, class Stack>
 __device__ __forceinline__ uint32_t parse_record(const Src &s, long long rs, long long re, uint32_t root,
-                                                 uint32_t &size) {
+                                                 uint32_t &size, Stack &stk) {
     using pos_t = typename Src::pos_t;
     size = 0;
     bool list = root == SPEC_PARSE_LIST;
@@ -121,7 +149,6 @@ __device__ __forceinline__ uint32_t parse_record(const Src &s, long long rs, lon
     if (re <= rs) return ST_OK; // empty input: zero message / list, no error
     const Trailer top = list ? parse_trailer<true>(s, (pos_t)rs, (pos_t)re) : parse_trailer<false>(s, (pos_t)rs, (pos_t)re);
     if (top.st != ST_OK) return root == SPEC_PARSE_VALUE ? (uint32_t)ST_INVALID_VALUE : top.st;
-    Frame stk[VAL_MAX_DEPTH];
     int sp = 0;
     const uint32_t es0 = list ? (top.big ? 4u : 2u) : (top.big ? 6u : 3u);
     stk[sp++] = Frame{top.dstart, top.tstart, top.tsize / es0, 0, top.dsize, (uint8_t)list, (uint8_t)top.big};
@@ -152,7 +179,7 @@ __device__ __forceinline__ uint32_t parse_record(const Src &s, long long rs, lon
             const bool sub = type == T_LIST || type == T_BIG_LIST;
             const Trailer tr = sub ? parse_trailer<true>(s, (pos_t)lo, (pos_t)e) : parse_trailer<false>(s, (pos_t)lo, (pos_t)e);
             if (tr.st != ST_OK) return ST_INVALID_VALUE;
-            if (sp == VAL_MAX_DEPTH) return ST_TOO_DEEP;
+            if (sp == stk.cap) return ST_TOO_DEEP;
             const uint32_t es = sub ? (tr.big ? 4u : 2u) : (tr.big ? 6u : 3u);
             stk[sp++] = Frame{tr.dstart, tr.tstart, tr.tsize / es, 0, tr.dsize, (uint8_t)sub, (uint8_t)tr.big};
         } else {
@@ -165,7 +192,7 @@ __device__ __forceinline__ uint32_t parse_record(const Src &s, long long rs, lon
     return ST_OK;
 }
 
-__global__ __launch_bounds__(256) void parse_kernel(DecodeArgs a, uint32_t *sizes, uint32_t root) {
+__global__ __launch_bounds__(256) void parse_kernel(DecodeArgs a, uint32_t *sizes, uint32_t root, DeepWs *deep) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t base = a.r0 + ((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave) * 64;
@@ -185,15 +212,57 @@ __global__ __launch_bounds__(256) void parse_kernel(DecodeArgs a, uint32_t *size
         fix_stream_tail(a, rsrc, slab, gr, lane);
         if (!valid) return;
         LdsSrc s{(lds_u8 *)slab};
+        LocalStack stk;
         st = parse_record(s, SLAB_GUARD + (long long)(gr.rec_lo - gr.aligned_lo),
-                          SLAB_GUARD + (long long)(gr.rec_hi - gr.aligned_lo), root, size);
+                          SLAB_GUARD + (long long)(gr.rec_hi - gr.aligned_lo), root, size, stk);
     } else {
         if (!valid) return;
         GlobalSrc s{a.stream, a.stream_len};
-        st = parse_record(s, (long long)gr.rec_lo, (long long)gr.rec_hi, root, size);
+        LocalStack stk;
+        st = parse_record(s, (long long)gr.rec_lo, (long long)gr.rec_hi, root, size, stk);
     }
     a.f.status[r] = (uint8_t)st;
     if (sizes) sizes[r] = size;
+    if (st == ST_TOO_DEEP) { // for the deep pass
+        const uint32_t j = atomicAdd(&deep->count, 1u);
+        if (j < DEEP_LIST_CAP) deep->list[j] = (uint32_t)(r - a.r0);
+    }
+}
+
+// The records the main pass found nested deeper than VAL_MAX_DEPTH, parsed from HBM with their
+// stacks in the arena: DEEP_THREADS threads with 8,192 frames each, then one thread with the whole
+// arena for any still too deep.  More than DEEP_LIST_CAP such records: every record's status is
+// scanned instead.  Exits at once when the main pass listed none.
+__device__ __forceinline__ void deep_one(const DecodeArgs &a, uint32_t *sizes, uint32_t root, uint64_t r,
+                                         ArenaStack stk) {
+    const uint64_t lo = (r == 0 ? 0 : a.ends[r - 1]) + a.head, hi0 = a.ends[r];
+    const uint64_t hi = hi0 < lo ? lo : hi0;
+    GlobalSrc s{a.stream, a.stream_len};
+    uint32_t size = 0;
+    const uint32_t st = parse_record(s, (long long)lo, (long long)hi, root, size, stk);
+    a.f.status[r] = (uint8_t)st;
+    if (sizes) sizes[r] = size;
+}
+
+__global__ __launch_bounds__(DEEP_THREADS) void deep_kernel(DecodeArgs a, uint32_t *sizes, uint32_t root, DeepWs *deep) {
+    const uint32_t count = deep->count;
+    if (count == 0) return;
+    Frame *arena = (Frame *)((uint8_t *)deep + ((sizeof(DeepWs) + 255) & ~(size_t)255));
+    const int slice = (int)(DEEP_ARENA / sizeof(Frame) / DEEP_THREADS);
+    const bool listed = count <= DEEP_LIST_CAP;
+    const uint64_t m = listed ? count : a.n - a.r0;
+    for (uint64_t j = threadIdx.x; j < m; j += DEEP_THREADS) {
+        const uint64_t r = a.r0 + (listed ? deep->list[j] : j);
+        if (a.f.status[r] == ST_TOO_DEEP) deep_one(a, sizes, root, r, ArenaStack{arena + threadIdx.x * slice, slice});
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint64_t j = 0; j < m; j++) {
+            const uint64_t r = a.r0 + (listed ? deep->list[j] : j);
+            if (a.f.status[r] == ST_TOO_DEEP)
+                deep_one(a, sizes, root, r, ArenaStack{arena, (int)(DEEP_ARENA / sizeof(Frame))});
+        }
+    }
 }
 
 } // namespace
@@ -202,7 +271,13 @@ int launch_parse(DecodeArgs a, uint32_t *sizes, uint32_t root, double avg_record
     if (a.n <= a.r0) return 0;
     const DecodeLaunch L = decode_launch(a.n - a.r0, avg_record, device_cus(), false, 1);
     a.slab = L.slab;
-    hipLaunchKernelGGL(parse_kernel, dim3(L.blocks), dim3(64 * L.wpb), L.lds, stream, a, sizes, root);
+    // the deep pass's list and arena: stream-ordered scratch of this call
+    DeepWs *deep = nullptr;
+    if (hipMallocAsync((void **)&deep, DEEP_WS_BYTES, stream) != hipSuccess) return -1;
+    if (hipMemsetAsync(deep, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
+    hipLaunchKernelGGL(parse_kernel, dim3(L.blocks), dim3(64 * L.wpb), L.lds, stream, a, sizes, root, deep);
+    hipLaunchKernelGGL(deep_kernel, dim3(1), dim3(DEEP_THREADS), 0, stream, a, sizes, root, deep);
+    if (hipFreeAsync(deep, stream) != hipSuccess) return -1;
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
