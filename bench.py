@@ -503,12 +503,22 @@ def lz4_leg(stream, ends, dev):
                         p(tot.data_ptr()), p(ws.data_ptr()), wsb, s_)
 
     ms, _ = kernel_time_events(call, 5, lead=1)
+    # the frame's content checksum (xxh32 of the decompressed bytes, what lz4.Reader checks at the
+    # end mark) on the device: serial over 16-byte stripes, timed once over the whole content
+    from spec_amd.lz4 import ContentChecksum
+
+    cc = ContentChecksum(dev)
+    cs_ms, _ = kernel_time_events(lambda: cc.update(out), 1, lead=0)
+    cc2 = ContentChecksum(dev)
+    cc2.update(out)
+    cs_ok = cc2.digest() == O.xxh32(frames)
     t0 = time.perf_counter()
     rc_h, host_out, _ = O.lz4_frame_read(comp, frames.size + 16)
     host_ms = (time.perf_counter() - t0) * 1e3
     return {"plain_bytes": int(frames.size), "compressed_bytes": int(comp.size), "blocks": nb,
             "device_ms": round(ms, 3), "device_gb_s": round(frames.size / (ms * 1e-3) / 1e9, 1),
-            "host_oracle_1core_ms": round(host_ms, 1), "ok": bool(ok and rc_h == 0),
+            "content_checksum_ms": round(cs_ms, 3), "content_checksum_ok": bool(cs_ok),
+            "host_oracle_1core_ms": round(host_ms, 1), "ok": bool(ok and rc_h == 0 and cs_ok),
             "note": "a parser wave and a copier wave per 256 KiB block: speculative next-token windows feed the serial chain, batches of 64 sequences copied while the next is parsed"}
 
 

@@ -37,7 +37,8 @@ extern "C" {
  * and spec_struct_size / spec_struct_offset with its own struct mirrors):
  *   1  rounds 1-4: SPEC_MAX_FIELDS 64, SPEC_TREE_MAX_FIELDS 256 (spec_schema 260 B, spec_tree 2052 B);
  *   2  SPEC_MAX_FIELDS / SPEC_NESTED_MAX_FIELDS / SPEC_TREE_MAX_FIELDS 1024: spec_schema 4100 B,
- *      spec_nested_schema.item at offset 4100, spec_tree 8196 B; spec_struct_size / _offset added. */
+ *      spec_nested_schema.item at offset 4100, spec_tree 8196 B; spec_struct_size / _offset added;
+ *      spec_lz4_state.reserved became content_checksum (same layout); spec_lz4_content added. */
 #define SPEC_AMD_ABI_VERSION 2
 /* Fields of a flat schema.  Schemas of up to 64 fields run the schema-specialised kernels; wider
  * ones decode in chunks of 64 fields (the generic kernel once per chunk, each getter against the
@@ -383,8 +384,9 @@ typedef enum spec_abi_struct {
     SPEC_ABI_TREE_TABLE = 6,    /* spec_tree_table {parent, field, rel, shape, first_column, ncolumns} */
     SPEC_ABI_TREE_COLUMN = 7,   /* spec_tree_column {table, field, role, kind, width} */
     SPEC_ABI_LZ4_BLOCK = 8,     /* spec_lz4_block {src_off, src_len, stored} */
-    SPEC_ABI_LZ4_STATE = 9,     /* spec_lz4_state {in_frame, block_max, flags, reserved} */
-    SPEC_ABI_NSTRUCTS = 10
+    SPEC_ABI_LZ4_STATE = 9,     /* spec_lz4_state {in_frame, block_max, flags, content_checksum} */
+    SPEC_ABI_LZ4_CONTENT = 10,  /* spec_lz4_content {v, total, buf, buffered, started} */
+    SPEC_ABI_NSTRUCTS = 11
 } spec_abi_struct;
 int spec_abi_version(void);
 size_t spec_struct_size(int which);
@@ -472,8 +474,11 @@ int spec_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends, u
  * and lists every COMPLETE block; `state` carries an open frame across calls (zero it for a
  * new connection): a later call continues with the frame's blocks.  *consumed = bytes the listed
  * blocks (and finished frames) span.  SPEC_E_CORRUPT on a bad header, SPEC_E_CAPACITY when more
- * than cap blocks are complete.  The content checksum (only written when a connection closes)
- * is not verified.
+ * than cap blocks are complete.  When a frame that carries a content checksum ends in the call
+ * (its end mark), state->flags bit 2 is set and state->content_checksum holds the stored
+ * checksum: compare it with spec_lz4_content_digest over the frame's decompressed bytes (what
+ * lz4.Reader checks at the frame's end, pierrec/lz4/v4 frame.go; mpx writes it when a connection
+ * closes).
  * spec_lz4_decompress (DEVICE): block k (src[blocks[k].src_off, +src_len)) decompressed into
  * slots + k * slot_bytes (slot_bytes >= the block max size, a multiple of 16; slots 16-byte aligned); sizes[k] = its size, or
  * all-ones and status[k] = 1 for a corrupt block (pierrec decodeBlock's errors).
@@ -487,8 +492,9 @@ typedef struct spec_lz4_block {
 typedef struct spec_lz4_state {
     uint32_t in_frame;  /* 1: the next bytes continue an open frame's blocks */
     uint32_t block_max; /* that frame's block max size */
-    uint32_t flags;     /* bit 0 block checksums, bit 1 content checksum */
-    uint32_t reserved;
+    uint32_t flags;     /* bit 0 block checksums, bit 1 content checksum; bit 2 (output): a frame
+                           with a content checksum ended in this call */
+    uint32_t content_checksum; /* with flags bit 2: that frame's stored content checksum */
 } spec_lz4_state;
 int spec_lz4_frame_blocks(const uint8_t *buf, uint64_t len, spec_lz4_state *state, spec_lz4_block *blocks,
                           uint64_t cap, uint64_t *nblocks, uint64_t *consumed, uint32_t *block_max);
@@ -497,6 +503,22 @@ int spec_lz4_decompress(const uint8_t *src, uint64_t src_len, const spec_lz4_blo
 size_t spec_lz4_pack_workspace_size(uint64_t nblocks);
 int spec_lz4_pack(const uint8_t *slots, uint64_t slot_bytes, const uint32_t *sizes, uint64_t nblocks, uint8_t *out,
                   uint64_t out_cap, uint64_t *total, void *workspace, size_t workspace_size, void *stream);
+/* The frame's content checksum on the DEVICE: xxHash32 (seed 0) of every byte the frame
+ * decompresses to, streamed over any number of calls.  `content` is a DEVICE spec_lz4_content,
+ * all zero for a new frame (hipMemset); spec_lz4_content_update appends data[0, len) (device, any
+ * alignment), spec_lz4_content_digest writes the checksum of everything appended so far to
+ * *digest (device uint32).  Asynchronous.  xxHash32 is serial over 16-byte stripes (four
+ * accumulators): one wave's four lanes run it, a few GB/s — a check at the frame's end, not a
+ * stage of the block pipeline. */
+typedef struct spec_lz4_content {
+    uint32_t v[4];      /* the four accumulators */
+    uint64_t total;     /* bytes appended */
+    uint8_t buf[16];    /* a partial stripe */
+    uint32_t buffered;  /* bytes in buf */
+    uint32_t started;   /* 0: fresh (zeroed) state */
+} spec_lz4_content;
+int spec_lz4_content_update(spec_lz4_content *content, const uint8_t *data, uint64_t len, void *stream);
+int spec_lz4_content_digest(const spec_lz4_content *content, uint32_t *digest, void *stream);
 
 /* ---- host pipeline (the path starts and ends in HOST memory: mpx connection buffers) ----
  * spec_host_decoder decodes a batch held in pinned host memory (spec_host_alloc) into a pinned

@@ -90,10 +90,10 @@ ABI_VERSION = 2
 
 def struct_mirrors():
     """{spec_abi_struct id: ctypes mirror} — every public struct this binding mirrors."""
-    from .lz4 import Lz4Block, Lz4State
+    from .lz4 import Lz4Block, Lz4Content, Lz4State
 
     return {0: SpecSpan, 1: SpecField, 2: SpecSchema, 3: SpecNestedSchema, 4: SpecTreeField, 5: SpecTree,
-            6: SpecTreeTable, 7: SpecTreeColumn, 8: Lz4Block, 9: Lz4State}
+            6: SpecTreeTable, 7: SpecTreeColumn, 8: Lz4Block, 9: Lz4State, 10: Lz4Content}
 
 
 def struct_mismatches(L) -> list:
@@ -191,6 +191,8 @@ def _declare(L):
     L.spec_lz4_pack_workspace_size.argtypes = [C.c_uint64]
     L.spec_lz4_pack_workspace_size.restype = C.c_size_t
     L.spec_lz4_pack.argtypes = [vp, C.c_uint64, vp, C.c_uint64, vp, C.c_uint64, vp, vp, C.c_size_t, vp]
+    L.spec_lz4_content_update.argtypes = [vp, vp, C.c_uint64, vp]
+    L.spec_lz4_content_digest.argtypes = [vp, vp, vp]
     L.spec_tree_layout.argtypes = [C.POINTER(SpecTree), C.POINTER(SpecTreeTable), C.POINTER(C.c_uint32),
                                    C.POINTER(SpecTreeColumn), C.POINTER(C.c_uint32)]
     L.spec_tree_decoder_create.argtypes = [C.POINTER(SpecTree), C.POINTER(vp)]

@@ -310,6 +310,7 @@ size_t spec_struct_size(int which) {
     case SPEC_ABI_TREE_COLUMN: return sizeof(spec_tree_column);
     case SPEC_ABI_LZ4_BLOCK: return sizeof(spec_lz4_block);
     case SPEC_ABI_LZ4_STATE: return sizeof(spec_lz4_state);
+    case SPEC_ABI_LZ4_CONTENT: return sizeof(spec_lz4_content);
     }
     return 0;
 }
@@ -345,7 +346,11 @@ size_t spec_struct_offset(int which, int member) {
                   offsetof(spec_lz4_block, stored));
     case SPEC_ABI_LZ4_STATE:
         SPEC_OFFS(spec_lz4_state, offsetof(spec_lz4_state, in_frame), offsetof(spec_lz4_state, block_max),
-                  offsetof(spec_lz4_state, flags), offsetof(spec_lz4_state, reserved));
+                  offsetof(spec_lz4_state, flags), offsetof(spec_lz4_state, content_checksum));
+    case SPEC_ABI_LZ4_CONTENT:
+        SPEC_OFFS(spec_lz4_content, offsetof(spec_lz4_content, v), offsetof(spec_lz4_content, total),
+                  offsetof(spec_lz4_content, buf), offsetof(spec_lz4_content, buffered),
+                  offsetof(spec_lz4_content, started));
     }
 #undef SPEC_OFFS
     return (size_t)-1;

@@ -53,6 +53,7 @@ int spec_lz4_frame_blocks(const uint8_t *buf, uint64_t len, spec_lz4_state *stat
         return SPEC_E_INVALID_ARGUMENT;
     uint64_t p = 0, k = 0;
     uint32_t bmax_all = state->in_frame ? state->block_max : 0;
+    state->flags &= 3u; // bit 2 reports this call only
     *nblocks = 0;
     *consumed = 0;
     int rc = SPEC_OK;
@@ -86,7 +87,7 @@ int spec_lz4_frame_blocks(const uint8_t *buf, uint64_t len, spec_lz4_state *stat
             }
             state->in_frame = 1;
             state->block_max = 1u << (8 + 2 * ((bd >> 4) & 7));
-            state->flags = ((flg & 0x10) ? 1u : 0u) | ((flg & 0x04) ? 2u : 0u);
+            state->flags = ((flg & 0x10) ? 1u : 0u) | ((flg & 0x04) ? 2u : 0u) | (state->flags & 4u);
             if (state->block_max > bmax_all) bmax_all = state->block_max;
             p += 4 + hlen + 1;
             *consumed = p;
@@ -96,9 +97,13 @@ int spec_lz4_frame_blocks(const uint8_t *buf, uint64_t len, spec_lz4_state *stat
         bool more = false;
         while (p + 4 <= len) {
             const uint32_t w = rd32(buf + p);
-            if (w == 0) { // end mark (+ content checksum, not verified: see include/spec_amd.h)
+            if (w == 0) { // end mark (+ content checksum: reported, see include/spec_amd.h)
                 const uint64_t tail = 4 + (ccs ? 4 : 0);
                 if (p + tail > len) break;
+                if (ccs) {
+                    state->flags |= 4u;
+                    state->content_checksum = rd32(buf + p + 4);
+                }
                 p += tail;
                 *consumed = p;
                 state->in_frame = 0;
@@ -147,6 +152,17 @@ int spec_lz4_decompress(const uint8_t *src, uint64_t src_len, const spec_lz4_blo
 }
 
 size_t spec_lz4_pack_workspace_size(uint64_t nblocks) { return (size_t)(nblocks + 1) * 8; }
+
+int spec_lz4_content_update(spec_lz4_content *content, const uint8_t *data, uint64_t len, void *stream) {
+    if (!content || (len && !data)) return SPEC_E_INVALID_ARGUMENT;
+    return spec::launch_lz4_content(content, data, len, nullptr, (hipStream_t)stream) ? SPEC_E_HIP : SPEC_OK;
+}
+
+int spec_lz4_content_digest(const spec_lz4_content *content, uint32_t *digest, void *stream) {
+    if (!content || !digest) return SPEC_E_INVALID_ARGUMENT;
+    return spec::launch_lz4_content((spec_lz4_content *)content, nullptr, 0, digest, (hipStream_t)stream) ? SPEC_E_HIP
+                                                                                                          : SPEC_OK;
+}
 
 int spec_lz4_pack(const uint8_t *slots, uint64_t slot_bytes, const uint32_t *sizes, uint64_t nblocks, uint8_t *out,
                   uint64_t out_cap, uint64_t *total, void *workspace, size_t workspace_size, void *stream) {

@@ -27,6 +27,8 @@ int launch_lz4_decompress(const uint8_t *src, uint64_t src_len, const spec_lz4_b
                           uint8_t *slots, uint64_t slot, uint32_t *sizes, uint8_t *status, hipStream_t stream);
 int launch_lz4_pack(const uint8_t *slots, uint64_t slot, const uint32_t *sizes, uint64_t nblocks, uint8_t *out,
                     uint64_t out_cap, uint64_t *offsets, uint64_t *total, hipStream_t stream);
+// xxHash32 of the frame content: data != null appends data[0, len); digest != null writes the digest
+int launch_lz4_content(spec_lz4_content *c, const uint8_t *data, uint64_t len, uint32_t *digest, hipStream_t stream);
 // frames_device.hip
 size_t frames_index_device_workspace(uint64_t len);
 int launch_frames_index_device(const uint8_t *buf, uint64_t len, uint64_t *ends, uint64_t cap, uint64_t *count,

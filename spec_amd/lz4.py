@@ -25,8 +25,37 @@ class Lz4Block(C.Structure):
 
 
 class Lz4State(C.Structure):
-    """An open frame carried across calls (zero for a new connection)."""
-    _fields_ = [("in_frame", C.c_uint32), ("block_max", C.c_uint32), ("flags", C.c_uint32), ("reserved", C.c_uint32)]
+    """An open frame carried across calls (zero for a new connection).  After a call, flags bit 2
+    says a frame with a content checksum ended in it; content_checksum is that checksum."""
+    _fields_ = [("in_frame", C.c_uint32), ("block_max", C.c_uint32), ("flags", C.c_uint32),
+                ("content_checksum", C.c_uint32)]
+
+
+class Lz4Content(C.Structure):
+    """spec_lz4_content (lives in device memory; zero = a fresh frame)."""
+    _fields_ = [("v", C.c_uint32 * 4), ("total", C.c_uint64), ("buf", C.c_uint8 * 16), ("buffered", C.c_uint32),
+                ("started", C.c_uint32)]
+
+
+class ContentChecksum:
+    """The frame's content checksum on the device (spec_lz4_content_update / _digest): xxHash32 of
+    every decompressed byte appended, over any number of calls — what lz4.Reader verifies at the
+    frame's end (compare with Lz4State.content_checksum once flags bit 2 is set)."""
+
+    def __init__(self, device="cuda"):
+        self.state = torch.zeros(C.sizeof(Lz4Content), dtype=torch.uint8, device=device)
+        self.out = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def update(self, data: torch.Tensor, cuda_stream=None):
+        _check_dev(data, "data", torch.uint8)
+        _lib.check(_lib.lib().spec_lz4_content_update(_ptr(self.state), _ptr(data) if data.numel() else None,
+                                                      data.numel(), _stream_handle(cuda_stream)),
+                   "spec_lz4_content_update")
+
+    def digest(self, cuda_stream=None) -> int:
+        _lib.check(_lib.lib().spec_lz4_content_digest(_ptr(self.state), _ptr(self.out), _stream_handle(cuda_stream)),
+                   "spec_lz4_content_digest")
+        return int(self.out.item()) & 0xFFFFFFFF
 
 
 def frame_blocks(buf: np.ndarray, state: Lz4State | None = None, cap: int | None = None):

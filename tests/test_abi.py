@@ -59,7 +59,8 @@ def test_struct_layouts_match_header():
                6: ("spec_tree_table", ["parent", "field", "rel", "shape", "first_column", "ncolumns"]),
                7: ("spec_tree_column", ["table", "field", "role", "kind", "width"]),
                8: ("spec_lz4_block", ["src_off", "src_len", "stored"]),
-               9: ("spec_lz4_state", ["in_frame", "block_max", "flags", "reserved"])}
+               9: ("spec_lz4_state", ["in_frame", "block_max", "flags", "content_checksum"]),
+               10: ("spec_lz4_content", ["v", "total", "buf", "buffered", "started"])}
     assert len(structs) == len(_lib.struct_mirrors())
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "spec_amd.h"', "int main(void) {"]
     for which, (s, members) in structs.items():

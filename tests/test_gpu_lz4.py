@@ -128,3 +128,49 @@ def test_compressed_receive_path(dev):
         if FLAT16.kinds[f] in (spec_amd.Kind.STRING, spec_amd.Kind.BYTES):
             continue  # spans point into the framed buffer, not the compact stream
         assert np.array_equal(got.cols[f].cpu().numpy(), want_cols[f]), f
+
+
+@pytest.mark.parametrize("chunks", [[0], [5], [16], [17, 3, 40], [1000, 1, 15, 16, 4096, 77777], [300_000]])
+def test_content_checksum_device(dev, chunks):
+    """spec_lz4_content_update / _digest: xxHash32 streamed over any split of the data (empty,
+    partial stripes carried between calls, long runs), equal to the oracle's xxh32."""
+    import torch
+
+    from spec_amd.lz4 import ContentChecksum
+
+    rng = np.random.default_rng(sum(chunks))
+    data = rng.integers(0, 256, sum(chunks), dtype=np.uint8)
+    d = torch.from_numpy(data).to(dev) if data.size else torch.zeros(0, dtype=torch.uint8, device=dev)
+    cc = ContentChecksum(dev)
+    p = 0
+    for c in chunks:
+        cc.update(d[p: p + c])
+        p += c
+    assert cc.digest() == O.xxh32(data)
+
+
+def test_content_checksum_receive_path(dev):
+    """A compressed connection's frame end: the blocks decompressed on the device, the content
+    checksum computed on the device over the decompressed bytes equals the one the frame stores
+    (frame_blocks reports it), and a corrupted stored checksum is detected."""
+    import torch
+
+    from spec_amd.lz4 import ContentChecksum, Lz4State
+
+    n = 20_000
+    cols, heaps = workload.flat16(n, seed=8)
+    stream, ends = O.encode_flat_batch(FLAT16.tags, FLAT16.kinds, cols, [heaps.get(f) for f in range(16)], n)
+    fr = spec_amd.make_frames(stream, ends)
+    comp = O.lz4_frame_write(fr, None, 256 << 10)
+    st = Lz4State()
+    blocks, used, bmax, rc = frame_blocks(comp, st)
+    assert rc == 0 and (st.flags & 4)
+    out, _, _ = decompress(torch.from_numpy(comp).to(dev), blocks, bmax)
+    cc = ContentChecksum(dev)
+    cc.update(out)
+    assert cc.digest() == st.content_checksum == O.xxh32(fr)
+    bad = comp.copy()
+    bad[-1] ^= 0x40  # the stored checksum's last byte
+    st2 = Lz4State()
+    frame_blocks(bad, st2)
+    assert (st2.flags & 4) and st2.content_checksum != cc.digest()

@@ -62,3 +62,22 @@ def test_corrupt_and_capacity():
     blocks, used, _, rc = frame_blocks(f, cap=2)
     assert rc == -4 and len(blocks) == 2 and used == int(blocks[1]["src_off"] + blocks[1]["src_len"])
     assert frame_blocks(f[:3])[1:] == (0, 0, 0)
+
+
+def test_content_checksum_reported():
+    """The frame's stored content checksum (xxh32 of its content, what lz4.Reader verifies at the
+    end mark) is reported in the state of the call that reaches the end mark, and only there."""
+    rng = np.random.default_rng(4)
+    data = rng.integers(0, 8, 300_000, dtype=np.uint8)
+    f = O.lz4_frame_write(data, [100_000, data.size], 64 << 10)
+    st = Lz4State()
+    blocks, used, _, rc = frame_blocks(f[: f.size // 2], st)
+    assert rc == 0 and not (st.flags & 4) and st.in_frame
+    blocks, used2, _, rc = frame_blocks(f[used:], st)
+    assert rc == 0 and (st.flags & 4) and not st.in_frame
+    assert st.content_checksum == O.xxh32(data)
+    # no content checksum in the frame: bit 2 stays clear
+    g = O.lz4_frame_write(data, None, 64 << 10, content_checksum=False)
+    st2 = Lz4State()
+    frame_blocks(g, st2)
+    assert not (st2.flags & 4) and st2.content_checksum == 0
