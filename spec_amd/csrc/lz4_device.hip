@@ -573,9 +573,11 @@ int launch_lz4_decompress(const uint8_t *src, uint64_t src_len, const spec_lz4_b
 
 // ---- the frame's content checksum: xxHash32 (seed 0) streamed over the decompressed bytes ----
 // (the published algorithm; oracle/lz4.c so_xxh32 and lz4_host.cpp xxh32 are the host versions).
-// One lane: it merges a partial stripe carried in the state, runs the four accumulators over the
-// 16-byte stripes (interleaved, loads 16 stripes ahead of the chains) and keeps the tail.  A
-// chain per lane (four lanes) ran at 0.58 GB/s: each step waited on the previous multiply.
+// One wave: lane 0 merges a partial stripe carried in the state, lanes 0..3 run the four
+// accumulators over the 16-byte stripes (each lane dword i of every stripe, from aligned dword
+// loads funnel-shifted to the data's byte phase, 32 stripes ahead of the chain), lane 0 keeps the
+// tail.  (Byte-wise loads of unaligned words: 0.58 GB/s with a lane per accumulator, 0.31 GB/s
+// with the four chains interleaved in one lane.)
 namespace {
 constexpr uint32_t XP1 = 2654435761u, XP2 = 2246822519u, XP3 = 3266489917u, XP4 = 668265263u, XP5 = 374761393u;
 
@@ -617,53 +619,43 @@ __global__ __launch_bounds__(64) void lz4_content_kernel(spec_lz4_content *c, co
     if (data) {
         const uint64_t p0 = head_bytes;
         const uint64_t ns = len > p0 ? (len - p0) / 16 : 0;
-        if (lane == 0) {
-            // the four accumulators' chains interleaved in one lane (their latencies overlap: with
-            // a chain per lane every step waited on the previous multiply), the next 16 stripes'
-            // loads in flight while this batch is hashed
-            uint32_t v0 = vv[0], v1 = vv[1], v2 = vv[2], v3 = vv[3];
-            const uint8_t *q = data + p0;
-            constexpr int U = 16;
+        if (lane < 4) {
+            // lane i: accumulator i over dword i of every stripe, read as aligned dwords and
+            // funnel-shifted (the data may start at any byte; an aligned dword that holds a byte
+            // of the data lies in a mapped page), 32 stripes' loads ahead of the chain
+            const uintptr_t qa = (uintptr_t)(data + p0);
+            const uint32_t *w = (const uint32_t *)(qa & ~(uintptr_t)3) + lane;
+            const uint32_t sh = (uint32_t)(qa & 3);
+            uint32_t v = vv[lane];
+            constexpr int U = 32;
             uint64_t s = 0;
+            auto word = [&](uint64_t st) __attribute__((always_inline)) {
+                const uint32_t lo = w[4 * st], hi = sh ? w[4 * st + 1] : 0u;
+                return __builtin_amdgcn_alignbyte(hi, lo, sh);
+            };
             if (ns >= U) {
-                uint4 x[U];
+                uint32_t x[U];
 #pragma unroll
-                for (int k = 0; k < U; k++) __builtin_memcpy(&x[k], q + 16 * k, 16);
+                for (int k = 0; k < U; k++) x[k] = word(k);
                 for (; s + 2 * U <= ns; s += U) {
-                    uint4 y[U];
+                    uint32_t y[U];
 #pragma unroll
-                    for (int k = 0; k < U; k++) __builtin_memcpy(&y[k], q + 16 * (s + U + k), 16);
+                    for (int k = 0; k < U; k++) y[k] = word(s + U + k); // the next batch in flight
 #pragma unroll
-                    for (int k = 0; k < U; k++) {
-                        v0 = xround(v0, x[k].x);
-                        v1 = xround(v1, x[k].y);
-                        v2 = xround(v2, x[k].z);
-                        v3 = xround(v3, x[k].w);
-                    }
+                    for (int k = 0; k < U; k++) v = xround(v, x[k]);
 #pragma unroll
                     for (int k = 0; k < U; k++) x[k] = y[k];
                 }
 #pragma unroll
-                for (int k = 0; k < U; k++) {
-                    v0 = xround(v0, x[k].x);
-                    v1 = xround(v1, x[k].y);
-                    v2 = xround(v2, x[k].z);
-                    v3 = xround(v3, x[k].w);
-                }
+                for (int k = 0; k < U; k++) v = xround(v, x[k]);
                 s += U;
             }
-            for (; s < ns; s++) {
-                uint4 x1;
-                __builtin_memcpy(&x1, q + 16 * s, 16);
-                v0 = xround(v0, x1.x);
-                v1 = xround(v1, x1.y);
-                v2 = xround(v2, x1.z);
-                v3 = xround(v3, x1.w);
-            }
-            c->v[0] = v0;
-            c->v[1] = v1;
-            c->v[2] = v2;
-            c->v[3] = v3;
+            for (; s < ns; s++) v = xround(v, word(s));
+            vv[lane] = v;
+        }
+        __syncthreads();
+        if (lane == 0) {
+            for (int i = 0; i < 4; i++) c->v[i] = vv[i];
             const uint64_t done = p0 + 16 * ns;
             for (uint64_t i = done; i < len; i++) c->buf[c->buffered++] = data[i];
             c->total += len;
