@@ -1125,7 +1125,7 @@ def run(args, env):
                 extras["config5_sharded"] = shard_leg(args, dist, rank, world, dev)
             except Exception as e:
                 extras["config5_sharded"] = {"error": repr(e)[:300]}
-        if rank == 0 and world == 1:
+        if rank == 0:  # one-GPU legs: at N>1 rank 0 runs them on its own device after the timed region
             try:
                 extras["decode_wide"] = wide_leg(dev)
                 checks["wide_parity"] = all(v["jit_vs_generic_same"] and v["oracle_sample_ok"]
@@ -1133,7 +1133,8 @@ def run(args, env):
             except Exception as e:
                 extras["decode_wide"] = {"error": repr(e)[:300]}
             try:
-                extras["nested"] = nested_leg(n, args.seed, dev, 0.0 if args.no_cpu else args.cpu_seconds)
+                extras["nested"] = nested_leg(n, args.seed, dev,
+                                              0.0 if (args.no_cpu or world > 1) else args.cpu_seconds)
             except Exception as e:
                 extras["nested"] = {"error": repr(e)[:300]}
             try:

@@ -830,6 +830,179 @@ void gen_message_table(std::ostringstream &o, const TreeDesc &D, uint32_t t, con
       << "  }\n";
 }
 
+// an eager writer's table in the Writer's tie-sorted order over the present fields (e<k> marks),
+// then its trailer; `data`, `nf`, `big` in scope
+void gen_table_trailer(std::ostringstream &o, const TreeDesc &D, const TTable &T) {
+    o << "  if (!big) {\n";
+    for (uint32_t j = 0; j < T.nd; j++) {
+        const uint32_t fi = D.sorted[T.d0 + j], slot = D.sslot[T.d0 + j];
+        if (D.f[fi].tag > 255) continue; // a present one makes the table big
+        o << "    if (e" << slot << " != 0xffffffffu) em.put_n(" << D.f[fi].tag << "u | ((uint64_t)__builtin_bswap16((uint16_t)e"
+          << slot << ") << 8), 3);\n";
+    }
+    o << "  } else {\n";
+    for (uint32_t j = 0; j < T.nd; j++) {
+        const uint32_t fi = D.sorted[T.d0 + j], slot = D.sslot[T.d0 + j];
+        o << "    if (e" << slot << " != 0xffffffffu) { em.be(" << D.f[fi].tag << "u, 2); em.be(e" << slot << ", 4); }\n";
+    }
+    o << "  }\n"
+      << "  em.rvarint(data);\n  em.rvarint((uint64_t)nf * (big ? 6 : 3));\n"
+      << "  em.put1(big ? T_BIG_MESSAGE : T_MESSAGE);\n  em.finish();\n";
+}
+
+// The generated Write() of a message table (internal/lang/generator/message.go:319-439,
+// internal/writer/writer.go:376-553) for one row at start: every column read issued before the
+// first byte is written, then the fields in write order (constant kinds, heaps and tags), the
+// table in the Writer's tie-sorted order over the present fields, the trailer.  Sub-messages and
+// list elements are children written by their tables' later launches into the gaps skipped here.
+// the column reads of direct field k of table T issued before the first byte (values; a
+// sub-message's or list's presence; a sub-message's size)
+// (sfx / rv: the variables' suffix and the row expression, for a writer over two rows at once)
+void gen_field_loads(std::ostringstream &o, const TreeDesc &D, const TTable &T, uint32_t k, bool eager, const char *ind,
+                     const std::string &sfx = "", const std::string &rv = "row") {
+    const TField &F = D.f[D.direct[T.d0 + k]];
+    if ((F.kind >= spec::K_BOOL && F.kind <= spec::K_BYTES) || F.kind == spec::K_ANY) {
+        if (eager)
+            o << ind << "uint64_t a" << k << sfx << "[4];\n" << ind << "load_value_k<" << (int)F.kind << ">(" << col_expr(F.col)
+              << ", " << rv << ", a" << k << sfx << ");\n";
+    } else if (F.kind == spec::K_MESSAGE || F.kind == spec::K_LIST)
+        o << ind << "const uint32_t pr" << k << sfx << " = ((const uint8_t *)" << col_expr(F.present) << ")[" << rv << "];\n";
+    if (F.kind == spec::K_MESSAGE) o << ind << "const uint32_t sz" << k << sfx << " = B.size[" << F.table << "][" << rv << "];\n";
+    // a struct's member values (every scalar member of its subtree: gen_struct_emit)
+    if (F.kind == spec::K_STRUCT && eager) {
+        const uint32_t fi = D.direct[T.d0 + k];
+        for (uint32_t i = fi + 1; i < F.send; i++)
+            if (D.f[i].kind != spec::K_STRUCT)
+                o << ind << "uint64_t m" << i << sfx << "[4];\n" << ind << "load_value_k<" << (int)D.f[i].kind << ">("
+                  << col_expr(D.f[i].col) << ", " << rv << ", m" << i << sfx << ");\n";
+    }
+    // a list's element range [begin[row], begin[row + 1]) (the size pass checked BEGIN)
+    if (F.kind == spec::K_LIST)
+        o << ind << "const uint32_t j0_" << k << sfx << " = ((const uint32_t *)" << col_expr(D.t[F.table].begin_col) << ")[" << rv
+          << "], j1_" << k << sfx << " = ((const uint32_t *)" << col_expr(D.t[F.table].begin_col) << ")[" << rv << " + 1];\n";
+}
+
+// binds gen_field_loads' suffixed variables of field k to the names gen_field_write reads
+void gen_field_bind(std::ostringstream &o, const TreeDesc &D, const TTable &T, uint32_t k, const std::string &sfx,
+                    const char *ind) {
+    const TField &F = D.f[D.direct[T.d0 + k]];
+    if ((F.kind >= spec::K_BOOL && F.kind <= spec::K_BYTES) || F.kind == spec::K_ANY)
+        o << ind << "uint64_t (&a" << k << ")[4] = a" << k << sfx << ";\n";
+    else if (F.kind == spec::K_MESSAGE || F.kind == spec::K_LIST)
+        o << ind << "const uint32_t pr" << k << " = pr" << k << sfx << ";\n";
+    if (F.kind == spec::K_MESSAGE) o << ind << "const uint32_t sz" << k << " = sz" << k << sfx << ";\n";
+    if (F.kind == spec::K_LIST)
+        o << ind << "const uint32_t j0_" << k << " = j0_" << k << sfx << ", j1_" << k << " = j1_" << k << sfx << ";\n";
+    if (F.kind == spec::K_STRUCT) {
+        const uint32_t fi = D.direct[T.d0 + k];
+        for (uint32_t i = fi + 1; i < F.send; i++)
+            if (D.f[i].kind != spec::K_STRUCT) o << ind << "uint64_t (&m" << i << ")[4] = m" << i << sfx << ";\n";
+    }
+}
+
+// struct field sf's EncodeXxxTo (internal/lang/generator/struct.go:115-142) from its loaded
+// members m<i>: the members in declaration order (an inner struct is its own EncodeXxxTo in
+// place), then EncodeStruct's rvarint(data size) | TypeStruct (tree_core.hpp emit_struct)
+void gen_struct_emit(std::ostringstream &o, const TreeDesc &D, uint32_t sf, int d, const std::string &ind) {
+    const TField &F = D.f[sf];
+    o << ind << "{ const uint64_t ss" << d << " = em.pos;\n";
+    for (uint32_t k = 0; k < F.nmem; k++) {
+        const uint32_t mi = D.members[F.mem0 + k];
+        const TField &M = D.f[mi];
+        if (M.kind == spec::K_STRUCT) {
+            gen_struct_emit(o, D, mi, d + 1, ind + "  ");
+        } else {
+            const bool heap = M.kind == spec::K_STRING || M.kind == spec::K_BYTES;
+            o << ind << "  emit_value_k<" << (int)M.kind << ">(em, m" << mi << ", "
+              << (heap ? "B.heaps[" + std::to_string(M.col) + "], B.heap_lens[" + std::to_string(M.col) + "]" : "nullptr, 0")
+              << ");\n";
+        }
+    }
+    o << ind << "  em.rvarint(em.pos - ss" << d << ");\n" << ind << "  em.put1(T_STRUCT);\n" << ind << "}\n";
+}
+
+// the size expression of a scalar value v (a loaded column element) of kind K (encode_core.hpp
+// field_size rules)
+std::string value_size_expr(int K, const std::string &v) {
+    if (K == spec::K_BOOL) return "1";
+    if (K == spec::K_BYTE) return "2";
+    if (K == spec::K_INT16) return "(vlen32(zigzag32((int16_t)" + v + "[0])) + 1)";
+    if (K == spec::K_INT32) return "(vlen32(zigzag32((int32_t)" + v + "[0])) + 1)";
+    if (K == spec::K_INT64) return "(vlen64(zigzag64((int64_t)" + v + "[0])) + 1)";
+    if (K == spec::K_UINT16 || K == spec::K_UINT32 || K == spec::K_UINT64) return "(vlen64(" + v + "[0]) + 1)";
+    if (K == spec::K_FLOAT32) return "5";
+    if (K == spec::K_FLOAT64 || K == spec::K_BIN64) return "9";
+    if (K == spec::K_BIN128) return "17";
+    if (K == spec::K_BIN256) return "33";
+    const std::string len = "(uint64_t)(uint32_t)(" + v + "[0] >> 32)";
+    if (K == spec::K_STRING) return "(" + len + " + vlen32((uint32_t)(" + v + "[0] >> 32)) + 2)";
+    return "(" + len + " + vlen32((uint32_t)(" + v + "[0] >> 32)) + 1)"; // BYTES
+}
+
+// struct field sf's encoded size (tree_core.hpp struct_size) from its loaded members m<i>, into
+// the variable `var` (declared here); a data size past MAX_SIZE sets err
+void gen_struct_size(std::ostringstream &o, const TreeDesc &D, uint32_t sf, const std::string &var, const std::string &ind) {
+    const TField &F = D.f[sf];
+    o << ind << "uint64_t " << var << " = 0;\n" << ind << "{\n";
+    for (uint32_t k = 0; k < F.nmem; k++) {
+        const uint32_t mi = D.members[F.mem0 + k];
+        const TField &M = D.f[mi];
+        if (M.kind == spec::K_STRUCT) {
+            gen_struct_size(o, D, mi, var + "_" + std::to_string(k), ind + "  ");
+            o << ind << "  " << var << " += " << var << "_" << k << ";\n";
+        } else {
+            o << ind << "  " << var << " += " << value_size_expr(M.kind, "m" + std::to_string(mi)) << ";\n";
+            if (M.kind == spec::K_STRING || M.kind == spec::K_BYTES)
+                o << ind << "  { const uint32_t off = (uint32_t)m" << mi << "[0], len = (uint32_t)(m" << mi << "[0] >> 32);\n"
+                  << ind << "    if ((uint64_t)len > MAX_SIZE || (uint64_t)off + len > B.heap_lens[" << M.col << "]) err = true; }\n";
+        }
+    }
+    o << ind << "  if (" << var << " > MAX_SIZE) err = true;\n"
+      << ind << "  " << var << " += vlen64(" << var << ") + 1;\n" << ind << "}\n";
+}
+
+// direct field k of table T in write order: its bytes through em (children: the gaps they fill,
+// their rows' positions), then its end mark (e<k> or ends_[k] = em.pos - start), nf, bigtag
+void gen_field_write(std::ostringstream &o, const TreeDesc &D, const TTable &T, uint32_t k, bool eager) {
+    const uint32_t fi = D.direct[T.d0 + k];
+    const TField &F = D.f[fi];
+    auto load = [&](const char *ind) {
+        o << ind << "uint64_t a" << k << "[4];\n" << ind << "load_value_k<" << (int)F.kind << ">(" << col_expr(F.col)
+          << ", row, a" << k << ");\n";
+    };
+    const std::string ev = eager ? "e" + std::to_string(k) : "ends_[" + std::to_string(k) + "]";
+    const std::string mark = "    " + ev + " = (uint32_t)(em.pos - start);\n    nf++;\n" +
+                             (F.tag > 255 ? "    bigtag = true;\n" : "");
+    if (eager) o << "  uint32_t e" << k << " = 0xffffffffu; // field " << fi << " tag " << F.tag << "\n";
+    else o << "  ends_[" << k << "] = 0xffffffffu; // field " << fi << " tag " << F.tag << "\n";
+    if (F.kind >= spec::K_BOOL && F.kind <= spec::K_BYTES) {
+        const bool heap = F.kind == spec::K_STRING || F.kind == spec::K_BYTES;
+        o << "  {\n";
+        if (!eager) load("    ");
+        o << "    emit_value_k<" << (int)F.kind << ">(em, a" << k << ", "
+          << (heap ? "B.heaps[" + std::to_string(F.col) + "], B.heap_lens[" + std::to_string(F.col) + "]" : "nullptr, 0")
+          << ");\n" << mark << "  }\n";
+    } else if (F.kind == spec::K_ANY) {
+        if (!eager) load("  ");
+        o << "  if ((uint32_t)(a" << k << "[0] >> 32)) {\n    emit_value_k<" << (int)F.kind << ">(em, a" << k
+          << ", B.heaps[" << F.col << "], B.heap_lens[" << F.col << "]);\n" << mark << "  }\n";
+    } else if (F.kind == spec::K_STRUCT) {
+        if (eager) gen_struct_emit(o, D, fi, 0, "  ");
+        else o << "  emit_struct(em, B, D, " << fi << "u, row);\n";
+        o << "  {\n" << mark << "  }\n";
+    } else if (F.kind == spec::K_MESSAGE) {
+        o << "  if (pr" << k << ") {\n    B.pos[" << F.table << "][row] = em.pos;\n    em.skip(sz" << k << ");\n" << mark
+          << "  } else {\n    B.pos[" << F.table << "][row] = ~0ull; // absent: its row is not written\n  }\n";
+    } else if (F.kind == spec::K_LIST) {
+        const int y = F.table;
+        o << "  if (!pr" << k << ") { // absent: rows in its range (if any) are not written\n"
+          << "    for (uint32_t j = j0_" << k << "; j < j1_" << k << "; j++) B.pos[" << y << "][j] = ~0ull;\n  }\n";
+        o << "  if (pr" << k << ") {\n"
+          << "    emit_list(em, B, " << y << "u, j0_" << k << ", j1_" << k << ");\n"
+          << mark << "  }\n";
+    }
+}
+
 // The generated Write() of a message table (internal/lang/generator/message.go:319-439,
 // internal/writer/writer.go:376-553) for one row at start: every column read issued before the
 // first byte is written, then the fields in write order (constant kinds, heaps and tags), the
@@ -846,64 +1019,11 @@ void gen_write_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
     const bool inl = eager && D.ntables <= 32;
     o << "template <class E>\n__device__ " << (inl ? "__forceinline__" : "__noinline__") << " void gen_wrow_" << t
       << "(E &em, const TreeDesc &D, const TreeBufs &B, uint64_t row, uint64_t start) {\n";
-    auto load = [&](uint32_t k, const TField &F, const char *ind) {
-        o << ind << "uint64_t a" << k << "[4];\n" << ind << "load_value_k<" << (int)F.kind << ">(" << col_expr(F.col)
-          << ", row, a" << k << ");\n";
-    };
-    for (uint32_t k = 0; k < T.nd; k++) {
-        const TField &F = D.f[D.direct[T.d0 + k]];
-        if ((F.kind >= spec::K_BOOL && F.kind <= spec::K_BYTES) || F.kind == spec::K_ANY) {
-            if (eager) load(k, F, "  ");
-        } else if (F.kind == spec::K_MESSAGE || F.kind == spec::K_LIST)
-            o << "  const uint32_t pr" << k << " = ((const uint8_t *)" << col_expr(F.present) << ")[row];\n";
-        if (F.kind == spec::K_MESSAGE) o << "  const uint32_t sz" << k << " = B.size[" << F.table << "][row];\n";
-    }
+    for (uint32_t k = 0; k < T.nd; k++) gen_field_loads(o, D, T, k, eager, "  ");
     o << "  uint32_t nf = 0;\n  bool bigtag = false;\n";
     // field ends: registers (e<k>), or for a wide table an array the table loop reads at run time
     if (!eager) o << "  uint32_t ends_[" << T.nd << "];\n";
-    auto ev = [&](uint32_t k) { return eager ? "e" + std::to_string(k) : "ends_[" + std::to_string(k) + "]"; };
-    for (uint32_t k = 0; k < T.nd; k++) {
-        const uint32_t fi = D.direct[T.d0 + k];
-        const TField &F = D.f[fi];
-        const std::string mark = "    " + ev(k) + " = (uint32_t)(em.pos - start);\n    nf++;\n" +
-                                 (F.tag > 255 ? "    bigtag = true;\n" : "");
-        if (eager) o << "  uint32_t e" << k << " = 0xffffffffu; // field " << fi << " tag " << F.tag << "\n";
-        else o << "  ends_[" << k << "] = 0xffffffffu; // field " << fi << " tag " << F.tag << "\n";
-        if (F.kind >= spec::K_BOOL && F.kind <= spec::K_BYTES) {
-            const bool heap = F.kind == spec::K_STRING || F.kind == spec::K_BYTES;
-            o << "  {\n";
-            if (!eager) load(k, F, "    ");
-            o << "    emit_value_k<" << (int)F.kind << ">(em, a" << k << ", "
-              << (heap ? "B.heaps[" + std::to_string(F.col) + "], B.heap_lens[" + std::to_string(F.col) + "]" : "nullptr, 0")
-              << ");\n" << mark << "  }\n";
-        } else if (F.kind == spec::K_ANY) {
-            if (!eager) load(k, F, "  ");
-            o << "  if ((uint32_t)(a" << k << "[0] >> 32)) {\n    emit_value_k<" << (int)F.kind << ">(em, a" << k
-              << ", B.heaps[" << F.col << "], B.heap_lens[" << F.col << "]);\n" << mark << "  }\n";
-        } else if (F.kind == spec::K_STRUCT) {
-            o << "  {\n    emit_struct(em, B, D, " << fi << "u, row);\n" << mark << "  }\n";
-        } else if (F.kind == spec::K_MESSAGE) {
-            o << "  if (pr" << k << ") {\n    B.pos[" << F.table << "][row] = em.pos;\n    em.skip(sz" << k << ");\n" << mark
-              << "  } else {\n    B.pos[" << F.table << "][row] = ~0ull; // absent: its row is not written\n  }\n";
-        } else if (F.kind == spec::K_LIST) {
-            const int y = F.table;
-            o << "  if (!pr" << k << ") { // absent: rows in its range (if any) are not written\n"
-              << "    bool lerr = false;\n    uint32_t j0, j1;\n"
-              << "    list_span(B, D, " << y << "u, row, j0, j1, lerr);\n"
-              << "    for (uint32_t j = j0; j < j1; j++) B.pos[" << y << "][j] = ~0ull;\n  }\n";
-            o << "  if (pr" << k << ") {\n"
-              << "    bool lerr = false;\n    uint32_t j0, j1;\n"
-              << "    list_span(B, D, " << y << "u, row, j0, j1, lerr);\n"
-              << "    const TreeListSize L = list_size(B, D, " << y << "u, row, lerr);\n"
-              << "    for (uint32_t j = j0; j < j1; j++) {\n      B.pos[" << y << "][j] = em.pos;\n      em.skip(B.size[" << y
-              << "][j]);\n    }\n"
-              << "    uint64_t off = 0;\n"
-              << "    for (uint32_t j = j0; j < j1; j++) {\n      off += B.size[" << y << "][j];\n      em.be(off, L.big ? 4 : 2);\n    }\n"
-              << "    em.rvarint(L.data);\n    em.rvarint((uint64_t)L.count * (L.big ? 4 : 2));\n"
-              << "    em.put1(L.big ? T_BIG_LIST : T_LIST);\n"
-              << mark << "  }\n";
-        }
-    }
+    for (uint32_t k = 0; k < T.nd; k++) gen_field_write(o, D, T, k, eager);
     // IsBigMessage (internal/format/msg.go:43-61), the table (encode/msg.go:58-72), the trailer
     o << "  const uint64_t data = em.pos - start;\n"
       << "  const bool big = bigtag || (nf > 0 && data > 65535);\n";
@@ -919,21 +1039,8 @@ void gen_write_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
           << "  em.rvarint(data);\n  em.rvarint((uint64_t)nf * (big ? 6 : 3));\n"
           << "  em.put1(big ? T_BIG_MESSAGE : T_MESSAGE);\n  em.finish();\n}\n";
     } else {
-    o << "  if (!big) {\n";
-    for (uint32_t j = 0; j < T.nd; j++) {
-        const uint32_t fi = D.sorted[T.d0 + j], slot = D.sslot[T.d0 + j];
-        if (D.f[fi].tag > 255) continue; // a present one makes the table big
-        o << "    if (e" << slot << " != 0xffffffffu) em.put_n(" << D.f[fi].tag << "u | ((uint64_t)__builtin_bswap16((uint16_t)e"
-          << slot << ") << 8), 3);\n";
-    }
-    o << "  } else {\n";
-    for (uint32_t j = 0; j < T.nd; j++) {
-        const uint32_t fi = D.sorted[T.d0 + j], slot = D.sslot[T.d0 + j];
-        o << "    if (e" << slot << " != 0xffffffffu) { em.be(" << D.f[fi].tag << "u, 2); em.be(e" << slot << ", 4); }\n";
-    }
-    o << "  }\n"
-      << "  em.rvarint(data);\n  em.rvarint((uint64_t)nf * (big ? 6 : 3));\n"
-      << "  em.put1(big ? T_BIG_MESSAGE : T_MESSAGE);\n  em.finish();\n}\n";
+        gen_table_trailer(o, D, T);
+        o << "}\n";
     }
     // a row no owner placed (its own owner absent or unplaced): its children are not written either
     o << "__device__ __forceinline__ void gen_unplace_" << t << "(const TreeDesc &D, const TreeBufs &B, uint64_t row) {\n";
@@ -949,6 +1056,9 @@ void gen_write_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
     o << "}\n";
 }
 
+bool tree_tile(const TreeDesc &D);
+void tile_cuts(const TreeDesc &D, uint32_t *cut);
+
 // The generated writer's size pass for a message table (tree.hip tree_size_kernel with constant
 // kinds, columns and tags): every column read first, then the encoded sizes, IsBigMessage.
 void gen_size_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
@@ -963,21 +1073,36 @@ void gen_size_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
               << ");\n";
         else if (F.kind == spec::K_MESSAGE || F.kind == spec::K_LIST)
             o << "    const uint32_t pr" << k << " = ((const uint8_t *)" << col_expr(F.present) << ")[row];\n";
+        if (F.kind == spec::K_STRUCT) gen_field_loads(o, D, T, k, true, "    ");
+        if (F.kind == spec::K_LIST)
+            o << "    const uint32_t j0_" << k << " = ((const uint32_t *)" << col_expr(D.t[F.table].begin_col) << ")[row], j1_" << k
+              << " = ((const uint32_t *)" << col_expr(D.t[F.table].begin_col) << ")[row + 1];\n";
     }
-    o << "    uint64_t data = 0;\n    uint32_t nf = 0;\n    bool bigtag = false;\n";
+    // the records' table under the record-tile writer (gen_tile): also each field block's end
+    // offset (B.tblk, inclusive prefix over the blocks) and the present direct fields (B.tmask)
+    const bool tile = t == 0 && tree_tile(D);
+    uint32_t cut[spec::TREE_TILE_W + 1];
+    if (tile) tile_cuts(D, cut);
+    o << "    uint64_t data = 0;\n    uint32_t nf = 0;\n    bool bigtag = false;\n"
+      << (tile ? "    uint64_t bm = 0;\n" : "");
     for (uint32_t k = 0; k < T.nd; k++) {
         const uint32_t fi = D.direct[T.d0 + k];
         const TField &F = D.f[fi];
-        const std::string tg = F.tag > 255 ? " bigtag = true;" : "";
+        const std::string tg = (F.tag > 255 ? " bigtag = true;" : "") +
+                               (tile ? " bm |= 1ull << " + std::to_string(k) + ";" : std::string());
+        for (int bl = 0; tile && bl < spec::TREE_TILE_W; bl++) // blocks ending before field k
+            if (cut[bl + 1] == k) o << "    const uint64_t tb" << bl << " = data;\n";
         switch (F.kind) {
         case spec::K_MESSAGE:
             o << "    if (pr" << k << ") { data += B.size[" << F.table << "][row]; nf++;" << tg << " }\n";
             break;
         case spec::K_LIST:
-            o << "    if (pr" << k << ") { data += list_size(B, D, " << F.table << "u, row, err).total; nf++;" << tg << " }\n";
+            o << "    if (pr" << k << ") { data += list_total(B, " << F.table << "u, j0_" << k << ", j1_" << k << ", err); nf++;" << tg
+              << " }\n";
             break;
         case spec::K_STRUCT:
-            o << "    data += struct_size(B, D, " << fi << "u, row, err); nf++;" << tg << "\n";
+            gen_struct_size(o, D, fi, "st" + std::to_string(k), "    ");
+            o << "    data += st" << k << "; nf++;" << tg << "\n";
             break;
         case spec::K_ANY:
             o << "    { const uint32_t off = (uint32_t)a" << k << "[0], len = (uint32_t)(a" << k << "[0] >> 32);\n"
@@ -1007,6 +1132,12 @@ void gen_size_table(std::ostringstream &o, const TreeDesc &D, uint32_t t) {
             o << "    data += " << sz << "; nf++;" << tg << "\n";
         }
         }
+    }
+    if (tile) {
+        for (int bl = 0; bl < spec::TREE_TILE_W; bl++)
+            if (cut[bl + 1] == T.nd) o << "    const uint64_t tb" << bl << " = data;\n";
+        for (int bl = 0; bl < spec::TREE_TILE_W; bl++) o << "    B.tblk[row * " << spec::TREE_TILE_W << " + " << bl << "] = (uint32_t)tb" << bl << ";\n";
+        o << "    B.tmask[row] = bm;\n";
     }
     // IsBigMessage (internal/format/msg.go:43-61), encodeMessageTable sizes
     o << "    const bool big = bigtag || (nf > 0 && data > 65535);\n"
@@ -1145,6 +1276,247 @@ void gen_pair_rows(std::ostringstream &o, const TreeDesc &D, uint32_t x, int P) 
       << "}\n";
 }
 
+// ---- the record-tile writer (tree_core.hpp MkL, tile_copy_out) ----
+// spec_tree_write_tile: one workgroup of TILE_W waves per 64 consecutive records.  Depth 0: the
+// records' direct fields are split into TILE_W contiguous blocks, wave w writing block w of all
+// 64 records (so a wave runs one block's code, no divergence) at the block's offset, which the
+// size pass left per record with the record's present fields (B.tblk, B.tmask), and their table
+// entries at (popcount of the present fields before them in the Writer's order); the last wave
+// writes the trailer.  Depth d > 0: the tile's rows of every table at depth d (a
+// contiguous row range per table, from the records' range through BEGIN columns) over all lanes,
+// through the tables' generated writers.  A barrier between depths (children placed by their
+// owners).  Everything goes to an LDS image of the tile's output range, stored once with 16-byte
+// stores; the bytes of a range longer than the image past its first cap bytes are stored straight
+// to HBM (a loop of passes over windows of the range tripled the kernel's compile time).
+constexpr int TILE_W = spec::TREE_TILE_W;
+
+bool tree_tile(const TreeDesc &D) {
+    if (!SPEC_AB_TREE_TILE || D.ntables > 32 || D.t[0].shape != spec::SHAPE_MESSAGE) return false;
+    for (uint32_t t = 0; t < D.ntables; t++)
+        if (D.t[t].shape == spec::SHAPE_MESSAGE && D.t[t].nd > 64) return false;
+    return true;
+}
+
+uint32_t tile_field_cost(const TreeDesc &D, const TField &F) {
+    switch (F.kind) {
+    case spec::K_STRING: case spec::K_BYTES: case spec::K_ANY: return 4;
+    case spec::K_BIN128: return 2;
+    case spec::K_BIN256: return 3;
+    case spec::K_STRUCT: return 1 + (F.send - 1u - (uint32_t)(&F - D.f));
+    case spec::K_LIST: return 4;
+    case spec::K_MESSAGE: return 2;
+    default: return 1;
+    }
+}
+
+// the records' direct fields in TILE_W contiguous blocks of about equal cost: block b is
+// [cut[b], cut[b + 1])
+void tile_cuts(const TreeDesc &D, uint32_t *cut) {
+    const TTable &T = D.t[0];
+    std::vector<uint32_t> cost(T.nd);
+    uint32_t total = 0;
+    for (uint32_t k = 0; k < T.nd; k++) total += cost[k] = tile_field_cost(D, D.f[D.direct[T.d0 + k]]);
+    uint32_t k = 0, acc = 0;
+    cut[0] = 0;
+    for (int b = 0; b < TILE_W; b++) {
+        const uint64_t target = (uint64_t)total * (b + 1) / TILE_W;
+        while (k < T.nd && (acc < target || b == TILE_W - 1)) acc += cost[k++];
+        cut[b + 1] = k;
+    }
+    cut[TILE_W] = T.nd;
+}
+
+// a table whose tile rows run two per lane at a time (both rows' reads in flight together):
+// message tables and lists of scalars, strings, bytes (build-time A/B SPEC_AB_TILE_PAIR)
+bool tile_pair_ok(const TreeDesc &D, uint32_t x) {
+    const TTable &X = D.t[x];
+    if (!SPEC_AB_TILE_PAIR) return false;
+    if (X.shape == spec::SHAPE_MESSAGE) return true;
+    return X.shape == spec::SHAPE_VALUE && D.f[X.field].elem >= spec::K_BOOL && D.f[X.field].elem <= spec::K_BYTES;
+}
+
+void gen_tile(std::ostringstream &o, const TreeDesc &D) {
+    const TTable &T = D.t[0];
+    uint32_t cut[TILE_W + 1];
+    tile_cuts(D, cut);
+    // PRE[k]: the direct fields before k in the Writer's table order; BIGM: tags past 255
+    std::vector<uint64_t> pre(T.nd, 0);
+    uint64_t bigm = 0, seen = 0;
+    for (uint32_t j = 0; j < T.nd; j++) {
+        const uint32_t slot = D.sslot[T.d0 + j];
+        pre[slot] = seen;
+        seen |= 1ull << slot;
+    }
+    for (uint32_t k = 0; k < T.nd; k++)
+        if (D.f[D.direct[T.d0 + k]].tag > 255) bigm |= 1ull << k;
+    // block b of a record: its offset and the record's data size and present fields from the size
+    // pass (gen_size_table: B.tblk, B.tmask), so the waves need not meet before writing
+    for (int b = 0; b < TILE_W; b++) {
+        o << "template <class Mk>\n__device__ __forceinline__ void gen_troot_" << b
+          << "(const Mk &mk, const TreeDesc &D, const TreeBufs &B, uint64_t row) {\n"
+          << "  const uint64_t start = B.offsets[row];\n"
+          << "  const uint64_t off = " << (b ? "B.tblk[row * " + std::to_string(TILE_W) + " + " + std::to_string(b - 1) + "]" : "0")
+          << ", data = B.tblk[row * " << TILE_W << " + " << TILE_W - 1 << "];\n"
+          << "  const uint64_t m = B.tmask[row];\n";
+        for (uint32_t k = cut[b]; k < cut[b + 1]; k++) gen_field_loads(o, D, T, k, true, "  ");
+        if (b == 0) o << "  if (B.ends_out) B.ends_out[row] = start + B.size[0][row];\n";
+        o << "  const bool big = (m & 0x" << std::hex << bigm << std::dec << "ull) != 0 || (m != 0 && data > 65535);\n"
+          << "  auto em = mk(start + off);\n  uint32_t nf = 0;\n  bool bigtag = false;\n";
+        for (uint32_t k = cut[b]; k < cut[b + 1]; k++) gen_field_write(o, D, T, k, true);
+        o << "  em.finish();\n  const uint64_t tb = start + data;\n";
+        for (uint32_t k = cut[b]; k < cut[b + 1]; k++) {
+            const uint32_t tag = D.f[D.direct[T.d0 + k]].tag;
+            o << "  if (e" << k << " != 0xffffffffu) {\n"
+              << "    const uint64_t p = tb + (big ? 6u : 3u) * (uint32_t)__popcll(m & 0x" << std::hex << pre[k] << std::dec
+              << "ull);\n"
+              << "    if (!big) em.put_at(p, " << (tag & 0xff) << "u | ((uint64_t)__builtin_bswap16((uint16_t)e" << k
+              << ") << 8), 3);\n"
+              << "    else em.put_at(p, " << (((tag & 0xff) << 8) | (tag >> 8)) << "u | ((uint64_t)__builtin_bswap32(e" << k
+              << ") << 16), 6);\n  }\n";
+        }
+        if (b == TILE_W - 1)
+            o << "  { const uint32_t nt = (uint32_t)__popcll(m) * (big ? 6u : 3u);\n"
+              << "    auto tr = mk(tb + nt);\n    tr.rvarint(data);\n    tr.rvarint(nt);\n"
+              << "    tr.put1(big ? T_BIG_MESSAGE : T_MESSAGE);\n    tr.finish(); }\n";
+        o << "  (void)nf; (void)bigtag;\n}\n";
+    }
+    // the rows of tables 1.. at their placed positions: a message row's column reads and its
+    // position issued together (one round trip), the position checked after them
+    for (uint32_t x = 1; x < D.ntables; x++) {
+        const TTable &X = D.t[x];
+        o << "template <class Mk>\n__device__ __forceinline__ void gen_trow_" << x
+          << "(const Mk &mk, const TreeDesc &D, const TreeBufs &B, uint64_t row) {\n";
+        if (X.shape == spec::SHAPE_MESSAGE) {
+            for (uint32_t k = 0; k < X.nd; k++) gen_field_loads(o, D, X, k, true, "  ");
+            o << "  const uint64_t start = B.pos[" << x << "][row];\n"
+              << "  if (start == ~0ull) { gen_unplace_" << x << "(D, B, row); return; }\n"
+              << "  auto em = mk(start);\n  uint32_t nf = 0;\n  bool bigtag = false;\n";
+            for (uint32_t k = 0; k < X.nd; k++) gen_field_write(o, D, X, k, true);
+            o << "  const uint64_t data = em.pos - start;\n"
+              << "  const bool big = bigtag || (nf > 0 && data > 65535);\n";
+            gen_table_trailer(o, D, X);
+        } else if (X.shape == spec::SHAPE_VALUE && D.f[X.field].elem >= spec::K_BOOL && D.f[X.field].elem <= spec::K_BYTES) {
+            const TField &F = D.f[X.field];
+            const bool heap = F.elem == spec::K_STRING || F.elem == spec::K_BYTES;
+            o << "  uint64_t a[4];\n  load_value_k<" << (int)F.elem << ">(" << col_expr(F.col) << ", row, a);\n"
+              << "  const uint64_t start = B.pos[" << x << "][row];\n  if (start == ~0ull) return;\n"
+              << "  auto em = mk(start);\n  emit_value_k<" << (int)F.elem << ">(em, a, "
+              << (heap ? "B.heaps[" + std::to_string(F.col) + "], B.heap_lens[" + std::to_string(F.col) + "]" : "nullptr, 0")
+              << ");\n  em.finish();\n";
+        } else if (X.shape == spec::SHAPE_STRUCT) { // a list of structs: the element's EncodeXxxTo
+            const TField &F = D.f[X.field];
+            for (uint32_t i = X.field + 1u; i < F.send; i++)
+                if (D.f[i].kind != spec::K_STRUCT)
+                    o << "  uint64_t m" << i << "[4];\n  load_value_k<" << (int)D.f[i].kind << ">(" << col_expr(D.f[i].col)
+                      << ", row, m" << i << ");\n";
+            o << "  const uint64_t start = B.pos[" << x << "][row];\n  if (start == ~0ull) return;\n"
+              << "  auto em = mk(start);\n";
+            gen_struct_emit(o, D, X.field, 0, "  ");
+            o << "  em.finish();\n";
+        } else {
+            o << "  const uint64_t start = B.pos[" << x << "][row];\n  if (start == ~0ull) return;\n"
+              << "  auto em = mk(start);\n  emit_row_shaped(em, D, B, " << x << "u, row);\n";
+        }
+        o << "}\n";
+        if (!tile_pair_ok(D, x)) continue;
+        // two rows (rowA, and rowB if hasB) with both rows' reads issued before either is written
+        o << "template <class Mk>\n__device__ __forceinline__ void gen_trow2_" << x
+          << "(const Mk &mk, const TreeDesc &D, const TreeBufs &B, uint64_t rowA, uint64_t rowB, bool hasB) {\n";
+        if (X.shape == spec::SHAPE_MESSAGE) {
+            for (const char *sf : {"_A", "_B"})
+                for (uint32_t k = 0; k < X.nd; k++) gen_field_loads(o, D, X, k, true, "  ", sf, std::string("row") + sf[1]);
+            o << "  const uint64_t startA = B.pos[" << x << "][rowA], startB = B.pos[" << x << "][rowB];\n";
+            for (const char *sf : {"_A", "_B"}) {
+                o << (sf[1] == 'A' ? "  {\n" : "  if (hasB) {\n") << "  const uint64_t row = row" << sf[1]
+                  << ", start = start" << sf[1] << ";\n";
+                for (uint32_t k = 0; k < X.nd; k++) gen_field_bind(o, D, X, k, sf, "  ");
+                o << "  if (start == ~0ull) {\n    gen_unplace_" << x << "(D, B, row);\n  } else {\n"
+                  << "  auto em = mk(start);\n  uint32_t nf = 0;\n  bool bigtag = false;\n";
+                for (uint32_t k = 0; k < X.nd; k++) gen_field_write(o, D, X, k, true);
+                o << "  const uint64_t data = em.pos - start;\n"
+                  << "  const bool big = bigtag || (nf > 0 && data > 65535);\n";
+                gen_table_trailer(o, D, X);
+                o << "  }\n  }\n";
+            }
+        } else {
+            const TField &F = D.f[X.field];
+            const bool heap = F.elem == spec::K_STRING || F.elem == spec::K_BYTES;
+            o << "  uint64_t aA[4], aB[4];\n  load_value_k<" << (int)F.elem << ">(" << col_expr(F.col) << ", rowA, aA);\n"
+              << "  load_value_k<" << (int)F.elem << ">(" << col_expr(F.col) << ", rowB, aB);\n"
+              << "  const uint64_t startA = B.pos[" << x << "][rowA], startB = B.pos[" << x << "][rowB];\n";
+            for (const char *sf : {"A", "B"})
+                o << "  if (" << (sf[0] == 'A' ? "true" : "hasB") << " && start" << sf << " != ~0ull) {\n"
+                  << "    auto em = mk(start" << sf << ");\n    emit_value_k<" << (int)F.elem << ">(em, a" << sf << ", "
+                  << (heap ? "B.heaps[" + std::to_string(F.col) + "], B.heap_lens[" + std::to_string(F.col) + "]" : "nullptr, 0")
+                  << ");\n    em.finish();\n  }\n";
+        }
+        o << "}\n";
+    }
+    int depth[spec::TREE_MAX_T] = {0}, maxd = 0;
+    for (uint32_t x = 1; x < D.ntables; x++) {
+        depth[x] = depth[D.t[x].parent] + 1;
+        maxd = std::max(maxd, depth[x]);
+    }
+    o << "template <class Mk>\n__device__ __forceinline__ void gen_tile_body(const Mk &mk, const TreeDesc &D, const TreeBufs &B, "
+         "uint64_t r0, uint64_t r1) {\n"
+      << "  const uint64_t row = r0 + (threadIdx.x & 63);\n"
+      << (SPEC_AB_TILE_CLOCK ? "  const uint64_t c0 = wall_clock64();\n" : "")
+      << "  if (row < r1) switch (threadIdx.x >> 6) {\n";
+    for (int b = 0; b < TILE_W; b++) o << "  case " << b << ": gen_troot_" << b << "(mk, D, B, row); break;\n";
+    o << "  }\n  __syncthreads();\n  const uint64_t lo0 = r0, hi0 = r1;\n";
+    if (SPEC_AB_TILE_CLOCK) o << "  if (threadIdx.x == 0) { B.tmask[r0] = c0; B.tmask[r0 + 1] = wall_clock64(); }\n";
+    for (uint32_t x = 1; x < D.ntables; x++) {
+        const TTable &X = D.t[x];
+        // (an owner range that is empty reads no BEGIN: the column may be absent then)
+        if (X.rel == spec::REL_MANY)
+            o << "  const bool ne" << x << " = hi" << X.parent << " > lo" << X.parent << ";\n"
+              << "  const uint64_t lo" << x << " = ne" << x << " ? ((const uint32_t *)" << col_expr(X.begin_col) << ")[lo"
+              << X.parent << "] : 0, hi" << x << " = ne" << x << " ? ((const uint32_t *)" << col_expr(X.begin_col) << ")[hi"
+              << X.parent << "] : 0;\n";
+        else
+            o << "  const uint64_t lo" << x << " = lo" << X.parent << ", hi" << x << " = hi" << X.parent << ";\n";
+    }
+    // depth d: the tables' row ranges laid end to end, index i to thread i mod blockDim (one loop
+    // per table over this thread's indices in its segment: an if-chain over the tables inside one
+    // loop took the register coalescer minutes)
+    for (int d = 1; d <= maxd; d++) {
+        o << "  { // depth " << d << "\n    uint64_t base = 0;\n";
+        for (uint32_t x = 1; x < D.ntables; x++)
+            if (depth[x] == d) {
+                if (tile_pair_ok(D, x))
+                    o << "    for (uint64_t i = base + (uint32_t)(threadIdx.x - base) % blockDim.x; i < base + (hi" << x << " - lo"
+                      << x << "); i += 2 * blockDim.x) {\n"
+                      << "      const bool hb = i + blockDim.x < base + (hi" << x << " - lo" << x << ");\n"
+                      << "      const uint64_t ra = lo" << x << " + (i - base);\n"
+                      << "      gen_trow2_" << x << "(mk, D, B, ra, hb ? ra + blockDim.x : ra, hb);\n    }\n";
+                else
+                    o << "    for (uint64_t i = base + (uint32_t)(threadIdx.x - base) % blockDim.x; i < base + (hi" << x << " - lo"
+                      << x << "); i += blockDim.x)\n      gen_trow_" << x << "(mk, D, B, lo" << x << " + (i - base));\n";
+                o << "    base += hi" << x << " - lo" << x << ";\n";
+            }
+        o << "    (void)base;\n  }\n  __syncthreads();\n";
+        if (SPEC_AB_TILE_CLOCK) o << "  if (threadIdx.x == 0) B.tmask[r0 + " << d + 1 << "] = wall_clock64();\n";
+    }
+    o << "}\n"
+      << "extern \"C\" __global__ __launch_bounds__(" << TILE_W * 64
+      << ") __attribute__((amdgpu_waves_per_eu(" << spec::TREE_TILE_WPE
+      << "))) void spec_tree_write_tile(const TreeDesc *Dp, const TreeBufs *Bp, "
+         "uint32_t cap) {\n"
+      << "  const TreeDesc &D = *Dp;\n  const TreeBufs &B = *Bp;\n"
+      << "  if (!B.out || *B.err || *B.total > B.out_cap) return;\n"
+      << "  const uint64_t n = B.rows[0], r0 = (uint64_t)blockIdx.x * 64;\n  if (r0 >= n) return;\n"
+      << "  const uint64_t r1 = r0 + 64 < n ? r0 + 64 : n;\n"
+      << "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+      << "  TileU8 *img = (TileU8 *)smem;\n"
+      << "  const uint64_t org = B.offsets[r0], fin = B.offsets[r1 - 1] + B.size[0][r1 - 1];\n"
+      // (out + sh 16-byte aligned: the image's chunks are the output's)
+      << "  const uint64_t sh = org - (((unsigned long long)B.out + org) & 15);\n"
+      << "  gen_tile_body(MkL{img, B.out, sh, cap}, D, B, r0, r1);\n"
+      << "  tile_copy_out(B.out, img, sh, org, fin < sh + cap ? fin : sh + cap);\n"
+      << (SPEC_AB_TILE_CLOCK ? "  __syncthreads();\n  if (threadIdx.x == 0) B.tmask[r0 + 63] = wall_clock64();\n" : "")
+      << "}\n";
+}
+
 std::string generate_tree(const TreeDesc &D, bool *has) {
     std::ostringstream o;
     o << "#include \"tree_decode_core.hpp\"\nusing namespace spec;\n";
@@ -1169,35 +1541,38 @@ std::string generate_tree(const TreeDesc &D, bool *has) {
       << "      if (total > 0xffffffffull) err = true;\n"
       << "      B.size[x][row] = (uint32_t)total;\n"
       << "    }\n  }\n  if (err) *B.err = 1;\n}\n";
-    o << "extern \"C\" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void spec_tree_write_set("
-         "const TreeDesc *Dp, const TreeBufs *Bp, TableSet s) {\n"
-      << "  const TreeDesc &D = *Dp;\n  const TreeBufs &B = *Bp;\n"
-      << "  if (!B.out || *B.err || *B.total > B.out_cap) return;\n"
-      << "  const uint32_t x = s.t[blockIdx.y];\n  const uint64_t rows = B.rows[x];\n"
-      << "  switch (x) {\n";
-    for (uint32_t t = 0; t < D.ntables; t++)
-        if (D.t[t].shape == spec::SHAPE_MESSAGE)
-            o << "  case " << t << ":\n"
-              << "    for (uint64_t row = grid_first(); row < rows; row += grid_stride()) {\n"
-              // a row outside its owners' BEGIN ranges is not written, and neither is anything
-              // under it: its children's positions are marked unplaced (they may hold stale
-              // workspace bytes otherwise, and the next depth's writer would emit at them)
-              << (D.t[t].rel == spec::REL_MANY
-                      ? "      if (!list_row_covered(D, B, x, row)) { gen_unplace_" + std::to_string(t) +
-                            "(D, B, row); continue; }\n"
-                      : std::string())
-              << "      const uint64_t start = x == 0 ? B.offsets[row] : B.pos[x][row];\n"
-              << "      if (start == ~0ull) { gen_unplace_" << t << "(D, B, row); continue; }\n"
-              << "      if (x == 0 && B.ends_out) B.ends_out[row] = start + B.size[0][row];\n"
-              // the records' rows are long: 16-byte chunk stores (BEmit16); the shorter rows of
-              // the tables below them keep the dword emitter (measured on pkg1: records 170 ->
-              // 134 us with BEmit16, the depth-1 tables 159 -> 180 us)
-              << (t == 0 ? "      BEmit16 em{B.out, start, start};\n" : "      BEmit em{B.out, start, start};\n")
-              << "      gen_wrow_" << t << "(em, D, B, row, start);\n"
-              << "    }\n    break;\n";
-    o << "  default:\n"
-      << "    for (uint64_t row = grid_first(); row < rows; row += grid_stride()) write_row_shaped(D, B, x, row);\n"
-      << "  }\n}\n";
+    // the level-fused writer: where the record-tile writer does not apply (or is switched off)
+    if (!tree_tile(D)) {
+        o << "extern \"C\" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void spec_tree_write_set("
+             "const TreeDesc *Dp, const TreeBufs *Bp, TableSet s) {\n"
+          << "  const TreeDesc &D = *Dp;\n  const TreeBufs &B = *Bp;\n"
+          << "  if (!B.out || *B.err || *B.total > B.out_cap) return;\n"
+          << "  const uint32_t x = s.t[blockIdx.y];\n  const uint64_t rows = B.rows[x];\n"
+          << "  switch (x) {\n";
+        for (uint32_t t = 0; t < D.ntables; t++)
+            if (D.t[t].shape == spec::SHAPE_MESSAGE)
+                o << "  case " << t << ":\n"
+                  << "    for (uint64_t row = grid_first(); row < rows; row += grid_stride()) {\n"
+                  // a row outside its owners' BEGIN ranges is not written, and neither is anything
+                  // under it: its children's positions are marked unplaced (they may hold stale
+                  // workspace bytes otherwise, and the next depth's writer would emit at them)
+                  << (D.t[t].rel == spec::REL_MANY
+                          ? "      if (!list_row_covered(D, B, x, row)) { gen_unplace_" + std::to_string(t) +
+                                "(D, B, row); continue; }\n"
+                          : std::string())
+                  << "      const uint64_t start = x == 0 ? B.offsets[row] : B.pos[x][row];\n"
+                  << "      if (start == ~0ull) { gen_unplace_" << t << "(D, B, row); continue; }\n"
+                  << "      if (x == 0 && B.ends_out) B.ends_out[row] = start + B.size[0][row];\n"
+                  // the records' rows are long: 16-byte chunk stores (BEmit16); the shorter rows of
+                  // the tables below them keep the dword emitter (measured on pkg1: records 170 ->
+                  // 134 us with BEmit16, the depth-1 tables 159 -> 180 us)
+                  << (t == 0 ? "      BEmit16 em{B.out, start, start};\n" : "      BEmit em{{B.out}, start, start};\n")
+                  << "      gen_wrow_" << t << "(em, D, B, row, start);\n"
+                  << "    }\n    break;\n";
+        o << "  default:\n"
+          << "    for (uint64_t row = grid_first(); row < rows; row += grid_stride()) write_row_shaped(D, B, x, row);\n"
+          << "  }\n}\n";
+    }
     for (uint32_t x = 0; x < D.ntables; x++) {
         const TTable &T = D.t[x];
         has[x] = false;
@@ -1274,6 +1649,7 @@ std::string generate_tree(const TreeDesc &D, bool *has) {
                   << "    });\n    break;\n";
         o << "  default: break;\n  }\n}\n";
     }
+    if (tree_tile(D)) gen_tile(o, D);
     return o.str();
 }
 
@@ -1282,8 +1658,9 @@ struct TreeEntry {
     // [x]: decode, staged rows; [TREE_MAX_T + x]: decode, rows from HBM; [2 TREE_MAX_T + x]:
     // decode on 2 waves per 64 rows (the root group, gen_pair_rows; nullptr if not split);
     // [4 TREE_MAX_T], [+1]: the
-    // level-fused encode size / write kernels; [+2]: the level-fused list-group decode kernel
-    hipFunction_t fn[4 * spec::TREE_MAX_T + 3] = {};
+    // level-fused encode size / write kernels; [+2]: the level-fused list-group decode kernel;
+    // [+3]: the record-tile writer (nullptr where gen_tile does not apply)
+    hipFunction_t fn[4 * spec::TREE_MAX_T + 4] = {};
     bool failed = false;
 };
 std::unordered_map<std::string, TreeEntry> g_tree_cache;
@@ -1304,7 +1681,9 @@ long long jit_compile_only_tree(const TreeDesc &D) {
 // (nullptr where the run-time kernel runs), fn[TREE_MAX_T + x] its variant without staging,
 // fn[2 TREE_MAX_T + x] its 2-wave variant (root group only; nullptr when not split),
 // fn[4 TREE_MAX_T] / fn[4 TREE_MAX_T + 1] the level-fused size / write kernels of the encoder,
-// fn[4 TREE_MAX_T + 2] the level-fused list-group decode kernel; nullptr when the JIT is off or failed.
+// fn[4 TREE_MAX_T + 2] the level-fused list-group decode kernel, fn[4 TREE_MAX_T + 3] the
+// record-tile writer (one of the two writers is generated: nullptr for the other); nullptr
+// when the JIT is off or failed.
 const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
     if (!enabled()) return nullptr;
     int dev = 0;
@@ -1333,8 +1712,9 @@ const hipFunction_t *jit_tree_kernels(const TreeDesc &D) {
         bool ok = !code.empty() && hipModuleLoadData(&e.mod, code.data()) == hipSuccess;
         if (ok)
             ok = hipModuleGetFunction(&e.fn[4 * TREE_MAX_T], e.mod, "spec_tree_size_set") == hipSuccess &&
-                 hipModuleGetFunction(&e.fn[4 * TREE_MAX_T + 1], e.mod, "spec_tree_write_set") == hipSuccess &&
-                 hipModuleGetFunction(&e.fn[4 * TREE_MAX_T + 2], e.mod, "spec_tree_group_set") == hipSuccess;
+                 hipModuleGetFunction(&e.fn[4 * TREE_MAX_T + 2], e.mod, "spec_tree_group_set") == hipSuccess &&
+                 hipModuleGetFunction(&e.fn[4 * TREE_MAX_T + (tree_tile(D) ? 3 : 1)], e.mod,
+                                      tree_tile(D) ? "spec_tree_write_tile" : "spec_tree_write_set") == hipSuccess;
         for (uint32_t x = 0; ok && x < D.ntables; x++) {
             if (!has[x]) continue;
             const std::string name = "spec_tree_group_" + std::to_string(x);

@@ -13,6 +13,32 @@
 
 namespace spec {
 
+// Build-time A/B (make HIPFLAGS+="-DSPEC_AB_TREE_TILE=0"): 1 generates the tree encoder's
+// record-tile writer (jit.cpp gen_tile) where it applies, 0 the level-fused write sets always.
+#ifndef SPEC_AB_TREE_TILE
+#define SPEC_AB_TREE_TILE 1
+#endif
+// the tile writer's waves per workgroup (= field blocks of the records' table) and waves per SIMD
+// (its register budget): 4 WPE / W workgroups per CU share the LDS, per workgroup the image of
+// the tile's output range and a dummy dword
+#ifndef SPEC_AB_TREE_TILE_W
+#define SPEC_AB_TREE_TILE_W 4
+#endif
+#ifndef SPEC_AB_TREE_TILE_WPE
+#define SPEC_AB_TREE_TILE_WPE 4 // waves per SIMD the kernel is compiled for (amdgpu_waves_per_eu)
+#endif
+constexpr int TREE_TILE_W = SPEC_AB_TREE_TILE_W, TREE_TILE_WPE = SPEC_AB_TREE_TILE_WPE;
+// measurement build (-DSPEC_AB_TILE_CLOCK=1, tools/tile_clock.py): each tile's workgroup stores the
+// wall clock at its phase boundaries over its records' B.tmask entries (read back from the workspace)
+#ifndef SPEC_AB_TILE_CLOCK
+#define SPEC_AB_TILE_CLOCK 0
+#endif
+// the tile writer's rows below the records two per lane at a time (jit.cpp tile_pair_ok)
+#ifndef SPEC_AB_TILE_PAIR
+#define SPEC_AB_TILE_PAIR 0
+#endif
+constexpr uint32_t TREE_TILE_IMG = ((163840u / (4u * TREE_TILE_WPE / TREE_TILE_W)) - 32u) & ~15u;
+
 // encode_nested.hip
 int launch_nested_encode(const spec_nested_schema *schema, const NestedEncodeArgs &a, bool write,
                          hipStream_t stream);

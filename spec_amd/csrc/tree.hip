@@ -91,7 +91,7 @@ __global__ __launch_bounds__(TB) void tree_write_kernel(const TreeDesc *Dp, cons
         const uint64_t start = x == 0 ? B.offsets[row] : B.pos[x][row];
         if (start == ~0ull) continue; // a row no written owner placed (absent message / list)
         if (x == 0 && B.ends_out) B.ends_out[row] = start + B.size[0][row];
-        BEmit em{B.out, start, start};
+        BEmit em{{B.out}, start, start};
         if (T.shape == SHAPE_VALUE) {
             const TField &F = D.f[T.field];
             emit_value(em, B, D, F.col, F.elem, row);
@@ -512,7 +512,7 @@ int spec_tree_layout(const spec_tree *tree, spec_tree_table *tables, uint32_t *n
 
 namespace {
 struct EncWs {
-    size_t desc, bufs, size[TREE_MAX_T], pos[TREE_MAX_T], offsets, scan, err, total;
+    size_t desc, bufs, size[TREE_MAX_T], pos[TREE_MAX_T], offsets, scan, err, total, tblk, tmask;
 };
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -542,6 +542,11 @@ size_t enc_plan(const Layout &L, const uint64_t *rows, EncWs &w) {
     o += align256(scan_ws_bytes(rows[0]));
     w.total = o;
     o += 256;
+    // the record-tile writer's per-record field-block offsets and presence masks (size pass)
+    w.tblk = o;
+    o += align256(std::max<uint64_t>(rows[0], 1) * TREE_TILE_W * sizeof(uint32_t));
+    w.tmask = o;
+    o += align256(std::max<uint64_t>(rows[0], 1) * sizeof(uint64_t));
     return o;
 }
 } // namespace
@@ -627,6 +632,8 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
     B->out_cap = out ? out_cap : 0;
     B->ends_out = ends;
     B->offsets = (uint64_t *)(ws + w.offsets);
+    B->tblk = (uint32_t *)(ws + w.tblk);
+    B->tmask = (uint64_t *)(ws + w.tmask);
     B->total = total;
     B->err = (uint32_t *)(ws + w.err);
     const TreeDesc *Dd = (const TreeDesc *)(ws + w.desc);
@@ -636,7 +643,7 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
     // level-fused launches (tree_core.hpp TableSet) when the generated module has them: the
     // tables of one height sized together (children have smaller heights), the tables of one
     // depth written together (owners have smaller depths)
-    const bool sets = jit && jit[4 * TREE_MAX_T] && jit[4 * TREE_MAX_T + 1];
+    const bool sets = jit && jit[4 * TREE_MAX_T] && (jit[4 * TREE_MAX_T + 1] || jit[4 * TREE_MAX_T + 3]);
     // the run-time writer keeps a message's field ends in LDS ([wave][field][lane], 256 B per field
     // per wave, 160 KiB per block at most): a table of more than 640 direct fields needs the
     // generated writer (jit.cpp).  Checked before anything is issued, so a call that cannot run
@@ -718,7 +725,17 @@ int spec_encode_tree(const spec_tree *tree, const void *const *columns, const ui
             hipLaunchKernelGGL(tree_pos_fill_kernel, dim3(gx, L.nt - 1), dim3(256), 0, st, pf);
         }
     }
-    for (int d = 0; sets && ok && out && d <= maxd; d++) ok = launch_set(jit[4 * TREE_MAX_T + 1], depth, d);
+    const bool tile = sets && jit[4 * TREE_MAX_T + 3];
+    if (tile && ok && out && n) {
+        uint32_t cap = TREE_TILE_IMG;
+        void *args[] = {(void *)&Dd, (void *)&Bd, &cap};
+        const hipError_t le = hipModuleLaunchKernel(jit[4 * TREE_MAX_T + 3], (unsigned)((n + 63) / 64), 1, 1,
+                                                    64 * TREE_TILE_W, 1, 1, TREE_TILE_IMG + 16, st, args,
+                                                    nullptr);
+        if (le != hipSuccess) note_hip_error(le);
+        ok = le == hipSuccess;
+    }
+    for (int d = 0; sets && !tile && ok && out && d <= maxd; d++) ok = launch_set(jit[4 * TREE_MAX_T + 1], depth, d);
     bool too_wide = false;
     for (uint32_t x = 0; !sets && ok && out && !too_wide && x < L.nt; x++)
         if (rows[x]) {

@@ -93,6 +93,8 @@ struct TreeBufs {
     uint64_t *offsets; // encode: record starts (exclusive scan of size[0])
     uint64_t *total;
     uint32_t *err;
+    uint32_t *tblk;  // encode, record-tile writer: per record, the offsets of its field blocks (jit.cpp gen_tile)
+    uint64_t *tmask; // encode, record-tile writer: per record, its present direct fields
 };
 
 __device__ __forceinline__ uint64_t grid_stride() { return (uint64_t)gridDim.x * blockDim.x; }
@@ -559,40 +561,66 @@ __device__ __forceinline__ TreeListSize list_size(const TreeBufs &B, const TreeD
 // `lo` (the row start) and up to the end (finish()).  skip(n) jumps over a child's bytes (a
 // sub-message, list elements) written by a LATER launch: a dword stored across such a gap may
 // hold zeros for the child's bytes, which the child's own launch then overwrites.
-struct BEmit {
+// The emitter's memory: GSink the output in HBM (dword phase = the byte offset's), LSink a
+// workgroup's LDS image of an output range (the tile writer, jit.cpp gen_tile): out byte p lives
+// at img[p - sh], sh chosen so that LDS and memory agree on p's position in its 16-byte chunk.
+struct GSink {
     uint8_t *out;
+    __device__ __forceinline__ uint32_t ph(uint64_t p) const { return (uint32_t)(p & 3); }
+    __device__ __forceinline__ void st32(uint64_t p, uint32_t v) const { *(uint32_t *)(out + p) = v; }
+    __device__ __forceinline__ void st8(uint64_t p, uint32_t b) const { out[p] = (uint8_t)b; }
+};
+// (a tile's range may exceed the image: bytes past the image's window [sh, sh + cap) are stored
+// straight to the output — dwords are 4-byte aligned in both, so none straddles the window's end)
+typedef __attribute__((address_space(3))) uint8_t TileU8; // (writable: spec_device.hpp's lds_u8 is const)
+typedef __attribute__((address_space(3))) uint32_t TileU32;
+typedef __attribute__((address_space(3))) uint64_t TileU64;
+struct LSink {
+    TileU8 *img;
+    uint8_t *out;
+    uint64_t sh;
+    uint32_t cap;
+    __device__ __forceinline__ uint32_t ph(uint64_t p) const { return (uint32_t)(p - sh) & 3; }
+    __device__ __forceinline__ void st32(uint64_t p, uint32_t v) const {
+        if (p - sh < cap) *(TileU32 *)(img + (uint32_t)(p - sh)) = v;
+        else *(uint32_t *)(out + p) = v;
+    }
+    __device__ __forceinline__ void st8(uint64_t p, uint32_t b) const {
+        if (p - sh < cap) img[(uint32_t)(p - sh)] = (uint8_t)b;
+        else out[p] = (uint8_t)b;
+    }
+};
+
+template <class S>
+struct DEmit {
+    S k;
     uint64_t pos;
     uint64_t lo;    // first byte of the row (bytes below belong to another row)
     uint32_t w = 0; // pending bytes of the dword holding pos
-    __device__ __forceinline__ void store_pending(uint64_t base, uint64_t end) { // bytes [base, end) of w
-        if (base >= lo && end == base + 4) {
-            *(uint32_t *)(out + base) = w;
-        } else {
-            for (uint64_t q = base > lo ? base : lo; q < end; q++) out[q] = (uint8_t)(w >> (8 * (q - base)));
-        }
-    }
     __device__ __forceinline__ void store_word(uint64_t base, uint64_t end, uint32_t v) { // bytes [base, end) of v
         if (base >= lo && end == base + 4) {
-            *(uint32_t *)(out + base) = v;
+            k.st32(base, v);
         } else {
-            for (uint64_t q = base > lo ? base : lo; q < end; q++) out[q] = (uint8_t)(v >> (8 * (q - base)));
+            for (uint64_t q = base > lo ? base : lo; q < end; q++) k.st8(q, v >> (8 * (q - base)));
         }
     }
+    __device__ __forceinline__ void store_pending(uint64_t base, uint64_t end) { store_word(base, end, w); }
     __device__ __forceinline__ void put1(uint32_t b) {
-        w |= (b & 0xffu) << (8 * (pos & 3));
+        const uint32_t ph = k.ph(pos);
+        w |= (b & 0xffu) << (8 * ph);
         pos++;
-        if ((pos & 3) == 0) {
+        if (ph == 3) {
             store_pending(pos - 4, pos);
             w = 0;
         }
     }
     // nb (<= 8) bytes of v, lowest first, merged with the pending bytes: the full dwords stored
     __device__ __forceinline__ void put_n(uint64_t v, uint32_t nb) {
-        const uint32_t ph = (uint32_t)(pos & 3), sh = 8 * ph;
+        const uint32_t ph = k.ph(pos), sh = 8 * ph;
         const uint64_t lo64 = (uint64_t)w | (v << sh);
         const uint32_t hi32 = sh ? (uint32_t)(v >> (64 - sh)) : 0u;
         const uint32_t total = ph + nb;
-        const uint64_t d = pos & ~3ull;
+        const uint64_t d = pos - ph;
         if (total >= 4) store_word(d, d + 4, (uint32_t)lo64);
         if (total >= 8) store_word(d + 4, d + 8, (uint32_t)(lo64 >> 32));
         const uint32_t full = total >> 2;
@@ -603,16 +631,23 @@ struct BEmit {
     }
     __device__ __forceinline__ void skip(uint64_t n) {
         if (!n) return;
-        const uint64_t np = pos + n;
-        if ((np & ~3ull) != (pos & ~3ull)) {
-            if (pos & 3) store_pending(pos & ~3ull, (pos & ~3ull) + 4); // the gap's bytes: the child's
+        const uint32_t ph = k.ph(pos);
+        const uint64_t d = pos - ph;
+        pos += n;
+        if (pos >= d + 4) {
+            if (ph) store_pending(d, d + 4); // the gap's bytes: the child's
             w = 0;
         }
-        pos = np;
     }
     __device__ __forceinline__ void finish() {
-        if (pos & 3) store_pending(pos & ~3ull, pos);
+        const uint32_t ph = k.ph(pos);
+        if (ph) store_pending(pos - ph, pos);
         w = 0;
+    }
+    // nb (<= 8) bytes of v, lowest first, at p, bytewise (a table entry: its neighbours are
+    // other fields' entries, written by other waves)
+    __device__ __forceinline__ void put_at(uint64_t p, uint64_t v, uint32_t nb) {
+        for (uint32_t i = 0; i < nb; i++) k.st8(p + i, (uint32_t)(v >> (8 * i)));
     }
     // reverse varint (oracle/compactint.c so_put_reverse_*): top group first, MSB clear, the
     // following groups with 0x80; up to 8 bytes (values < 2^56) built in a register at once
@@ -662,6 +697,9 @@ struct BEmit {
         }
     }
 };
+using BEmit = DEmit<GSink>;
+using LEmit = DEmit<LSink>;
+
 
 // BEmit16: the same contract with 16-byte chunks (the generated writer of the records' table,
 // whose rows are long: jit.cpp gen_write_table).  A row's bytes at out[pos..] are merged into the
@@ -927,6 +965,95 @@ __device__ __forceinline__ void emit_struct(E &em, const TreeBufs &B, const Tree
     }
 }
 
+// list_size's total over elements [j0, j1) of list table y (its BEGIN range, already read): the
+// elements' sizes loaded 8 at a time (one round of loads for a short list)
+__device__ __forceinline__ uint64_t list_total(const TreeBufs &B, uint32_t y, uint32_t j0, uint32_t j1, bool &err) {
+    if (j1 < j0 || (uint64_t)j1 > B.rows[y]) { // (list_span's check)
+        err = true;
+        j1 = j0;
+    }
+    const uint32_t *sz = B.size[y];
+    uint64_t data = 0;
+    for (uint32_t j = j0; j < j1; j += 8) {
+        uint32_t s[8];
+#pragma unroll
+        for (uint32_t i = 0; i < 8; i++) s[i] = j + i < j1 ? sz[j + i] : 0u;
+#pragma unroll
+        for (uint32_t i = 0; i < 8; i++) data += s[i];
+    }
+    const uint32_t count = j1 - j0;
+    const bool big = count > 255 || (count > 0 && data > 65535);
+    const uint64_t tsize = (uint64_t)count * (big ? 4 : 2);
+    if (data > MAX_SIZE) err = true;
+    return data + tsize + vlen64(data) + vlen64(tsize) + 1;
+}
+
+// A present list field's bytes (EncodeListTable, internal/encode/list.go:15-75) over elements
+// [j0, j1) of list table y: the elements' gaps (their rows' positions), the offset table
+// (IsBigList: count > 255 or data > 65535), the trailer.  Up to 8 elements take one round of size
+// loads (issued together, kept in registers for the table); longer lists loop 4 at a time.
+template <class E>
+__device__ __forceinline__ void emit_list(E &em, const TreeBufs &B, uint32_t y, uint32_t j0, uint32_t j1) {
+    const uint32_t *sz = B.size[y];
+    uint64_t *pos = B.pos[y];
+    const uint32_t cnt = j1 - j0;
+    if (cnt <= 8) {
+        uint32_t s[8];
+#pragma unroll
+        for (uint32_t i = 0; i < 8; i++) s[i] = i < cnt ? sz[j0 + i] : 0u;
+        uint64_t p = em.pos;
+#pragma unroll
+        for (uint32_t i = 0; i < 8; i++)
+            if (i < cnt) {
+                pos[j0 + i] = p;
+                p += s[i];
+            }
+        const uint64_t data = p - em.pos;
+        em.skip(data);
+        const bool big = data > 65535;
+        uint64_t off = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 8; i++)
+            if (i < cnt) {
+                off += s[i];
+                em.be(off, big ? 4 : 2);
+            }
+        em.rvarint(data);
+        em.rvarint((uint64_t)cnt * (big ? 4 : 2));
+        em.put1(big ? T_BIG_LIST : T_LIST);
+        return;
+    }
+    uint64_t data = 0;
+    for (uint32_t j = j0; j < j1; j += 4) {
+        uint32_t s[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) s[i] = j + i < j1 ? sz[j + i] : 0u;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++)
+            if (j + i < j1) {
+                pos[j + i] = em.pos + data;
+                data += s[i];
+            }
+    }
+    em.skip(data);
+    const bool big = cnt > 255 || data > 65535;
+    uint64_t off = 0;
+    for (uint32_t j = j0; j < j1; j += 4) {
+        uint32_t s[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) s[i] = j + i < j1 ? sz[j + i] : 0u;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++)
+            if (j + i < j1) {
+                off += s[i];
+                em.be(off, big ? 4 : 2);
+            }
+    }
+    em.rvarint(data);
+    em.rvarint((uint64_t)cnt * (big ? 4 : 2));
+    em.put1(big ? T_BIG_LIST : T_LIST);
+}
+
 // ---- level-fused encode launches (jit.cpp spec_tree_size_set / spec_tree_write_set) ---------
 // Tables with no size dependency between them (the same height: every child sized first) are
 // sized in ONE launch, tables at the same depth (every owner written first) written in one:
@@ -957,14 +1084,10 @@ __device__ __forceinline__ bool list_row_covered(const TreeDesc &D, const TreeBu
     return row >= b[0] && row < b[B.rows[D.t[y].parent]];
 }
 
-// the bytes of row `row` of a VALUE or STRUCT table (list elements) at its position
-// (tree_write_kernel's rules)
-__device__ __forceinline__ void write_row_shaped(const TreeDesc &D, const TreeBufs &B, uint32_t x, uint64_t row) {
+// the bytes of row `row` of a VALUE or STRUCT table (a list element) through emitter em
+template <class E>
+__device__ __forceinline__ void emit_row_shaped(E &em, const TreeDesc &D, const TreeBufs &B, uint32_t x, uint64_t row) {
     const TTable &T = D.t[x];
-    if (!list_row_covered(D, B, x, row)) return;
-    const uint64_t start = B.pos[x][row];
-    if (start == ~0ull) return; // a row no written owner placed
-    BEmit em{B.out, start, start};
     if (T.shape == SHAPE_VALUE) {
         const TField &F = D.f[T.field];
         emit_value(em, B, D, F.col, F.elem, row);
@@ -972,6 +1095,45 @@ __device__ __forceinline__ void write_row_shaped(const TreeDesc &D, const TreeBu
         emit_struct(em, B, D, T.field, row);
     }
     em.finish();
+}
+
+// the bytes of row `row` of a VALUE or STRUCT table (list elements) at its position
+// (tree_write_kernel's rules)
+__device__ __forceinline__ void write_row_shaped(const TreeDesc &D, const TreeBufs &B, uint32_t x, uint64_t row) {
+    if (!list_row_covered(D, B, x, row)) return;
+    const uint64_t start = B.pos[x][row];
+    if (start == ~0ull) return; // a row no written owner placed
+    BEmit em{{B.out}, start, start};
+    emit_row_shaped(em, D, B, x, row);
+}
+
+// ---- the record-tile writer (jit.cpp gen_tile: spec_tree_write_tile) ------------------------
+// One workgroup writes 64 consecutive records with every row under them, depth by depth, into an
+// LDS image of their output range, then stores the image once with 16-byte stores.  The bytes of
+// a range longer than the image past its first cap bytes go straight to HBM (LSink).
+struct MkL { // emitters over the LDS image of the window [sh, sh + cap), HBM past it
+    TileU8 *img;
+    uint8_t *out;
+    uint64_t sh;
+    uint32_t cap;
+    __device__ __forceinline__ LEmit operator()(uint64_t p) const { return LEmit{{img, out, sh, cap}, p, p}; }
+};
+
+// out[org, fin) from the image (out byte p at img[p - sh]; out + sh is 16-byte aligned): whole
+// chunks with 16-byte stores, the partial chunks at the ends bytewise (the neighbours' bytes)
+__device__ __forceinline__ void tile_copy_out(uint8_t *out, const TileU8 *img, uint64_t sh, uint64_t org, uint64_t fin) {
+    const uint32_t q0 = (uint32_t)(org - sh), q1 = (uint32_t)(fin - sh);
+    uint8_t *o = out + sh;
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) const v4u lds_v4u;
+    for (uint32_t a = threadIdx.x * 16u; a < q1; a += blockDim.x * 16u) {
+        if (a >= q0 && a + 16 <= q1) {
+            *(v4u *)(o + a) = *(lds_v4u *)(img + a);
+        } else {
+            const uint32_t b1 = a + 16 < q1 ? a + 16 : q1;
+            for (uint32_t b = a > q0 ? a : q0; b < b1; b++) o[b] = img[b];
+        }
+    }
 }
 
 } // namespace spec

@@ -120,6 +120,20 @@ def test_pkg1_root_pair_over_slab_and_stream_end(dev, case):
     assert mismatches(tree, got, want) == []
 
 
+@pytest.mark.parametrize("n,str_len", [(200, (0, 3000)), (3, (80_000, 100_000)), (130, (0, 600))])
+def test_pkg1_tiles_over_the_image(dev, n, str_len):
+    """The record-tile writer (jit.cpp gen_tile) on tiles whose output range exceeds its LDS image
+    (36 KiB at 4 waves per workgroup): the bytes past the image's window go straight to HBM (tree_core.hpp LSink), whether
+    64 records add up past it (25 KB records) or one record alone does (a 100 KB string), and a
+    batch whose last tile is partial (130 records)."""
+    tree = spec_amd.pkg1_tree()
+    cols, heaps, rows = workload.tree_batch(tree, n, 500 + n, str_len=str_len)
+    stream, ends = check_encode_decode(tree, cols, heaps, rows, dev, n)
+    starts = np.concatenate([[0], ends[:-1]]).astype(np.int64)
+    tiles = [int(ends[min(n, t + 64) - 1]) - int(starts[t]) for t in range(0, n, 64)]
+    assert max(tiles) > 72 * 1024 or str_len[1] < 1000  # past the image at any TREE_TILE_W
+
+
 @pytest.mark.parametrize("depth", [1, 3])
 def test_pkg1_depths(dev, depth):
     tree = spec_amd.pkg1_tree(depth)
