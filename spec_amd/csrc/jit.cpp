@@ -1326,13 +1326,94 @@ void tile_cuts(const TreeDesc &D, uint32_t *cut) {
     cut[TILE_W] = T.nd;
 }
 
-// a table whose tile rows run two per lane at a time (both rows' reads in flight together):
-// message tables and lists of scalars, strings, bytes (build-time A/B SPEC_AB_TILE_PAIR)
-bool tile_pair_ok(const TreeDesc &D, uint32_t x) {
+// A table whose tile rows at one depth run in ROUNDS (SPEC_AB_TILE_ROUNDS): each thread issues the
+// reads of its next row of every such table at once, then writes them one after another — a
+// thread holds about one row per table per tile, so per-table loops were one dependent chain of
+// reads per table.  Message tables, lists of scalars / strings / bytes, lists of structs.
+bool tile_round_ok(const TreeDesc &D, uint32_t x) {
     const TTable &X = D.t[x];
-    if (!SPEC_AB_TILE_PAIR) return false;
-    if (X.shape == spec::SHAPE_MESSAGE) return true;
+    if (!SPEC_AB_TILE_ROUNDS) return false;
+    if (X.shape == spec::SHAPE_MESSAGE || X.shape == spec::SHAPE_STRUCT) return true;
     return X.shape == spec::SHAPE_VALUE && D.f[X.field].elem >= spec::K_BOOL && D.f[X.field].elem <= spec::K_BYTES;
+}
+
+// the reads of row `rv` of table x (round mode) into variables suffixed sfx: declarations
+// (zeroed) into decl, the reads, under the row's validity, into rd
+void gen_round_loads(std::ostringstream &decl, std::ostringstream &rd, const TreeDesc &D, uint32_t x,
+                     const std::string &sfx, const std::string &rv) {
+    const TTable &X = D.t[x];
+    auto member_loads = [&](uint32_t sf) {
+        for (uint32_t i = sf + 1u; i < D.f[sf].send; i++)
+            if (D.f[i].kind != spec::K_STRUCT) {
+                decl << "    uint64_t m" << i << sfx << "[4] = {0, 0, 0, 0};\n";
+                rd << "      load_value_k<" << (int)D.f[i].kind << ">(" << col_expr(D.f[i].col) << ", " << rv << ", m" << i << sfx
+                   << ");\n";
+            }
+    };
+    decl << "    uint64_t start" << sfx << " = ~0ull;\n";
+    rd << "      start" << sfx << " = B.pos[" << x << "][" << rv << "];\n";
+    if (X.shape == spec::SHAPE_VALUE) {
+        const TField &F = D.f[X.field];
+        decl << "    uint64_t a" << sfx << "[4] = {0, 0, 0, 0};\n";
+        rd << "      load_value_k<" << (int)F.elem << ">(" << col_expr(F.col) << ", " << rv << ", a" << sfx << ");\n";
+        return;
+    }
+    if (X.shape == spec::SHAPE_STRUCT) {
+        member_loads(X.field);
+        return;
+    }
+    for (uint32_t k = 0; k < X.nd; k++) {
+        const uint32_t fi = D.direct[X.d0 + k];
+        const TField &F = D.f[fi];
+        const std::string ks = std::to_string(k);
+        if ((F.kind >= spec::K_BOOL && F.kind <= spec::K_BYTES) || F.kind == spec::K_ANY) {
+            decl << "    uint64_t a" << k << sfx << "[4] = {0, 0, 0, 0};\n";
+            rd << "      load_value_k<" << (int)F.kind << ">(" << col_expr(F.col) << ", " << rv << ", a" << k << sfx << ");\n";
+        } else if (F.kind == spec::K_MESSAGE || F.kind == spec::K_LIST) {
+            decl << "    uint32_t pr" << k << sfx << " = 0;\n";
+            rd << "      pr" << k << sfx << " = ((const uint8_t *)" << col_expr(F.present) << ")[" << rv << "];\n";
+        }
+        if (F.kind == spec::K_MESSAGE) {
+            decl << "    uint32_t sz" << k << sfx << " = 0;\n";
+            rd << "      sz" << k << sfx << " = B.size[" << F.table << "][" << rv << "];\n";
+        }
+        if (F.kind == spec::K_LIST) {
+            const std::string bc = "((const uint32_t *)" + col_expr(D.t[F.table].begin_col) + ")";
+            decl << "    uint32_t j0_" << k << sfx << " = 0, j1_" << k << sfx << " = 0;\n";
+            rd << "      j0_" << k << sfx << " = " << bc << "[" << rv << "];\n      j1_" << k << sfx << " = " << bc << "[" << rv
+               << " + 1];\n";
+        }
+        if (F.kind == spec::K_STRUCT) member_loads(fi);
+    }
+}
+
+// the write of the row read by gen_round_loads (valid, placed)
+void gen_round_write(std::ostringstream &o, const TreeDesc &D, uint32_t x, const std::string &sfx, const std::string &rv) {
+    const TTable &X = D.t[x];
+    o << "      {\n      const uint64_t row = " << rv << ", start = start" << sfx << ";\n      (void)row;\n";
+    if (X.shape == spec::SHAPE_VALUE) {
+        const TField &F = D.f[X.field];
+        const bool heap = F.elem == spec::K_STRING || F.elem == spec::K_BYTES;
+        o << "      if (start != ~0ull) {\n      auto em = mk(start);\n      emit_value_k<" << (int)F.elem << ">(em, a" << sfx << ", "
+          << (heap ? "B.heaps[" + std::to_string(F.col) + "], B.heap_lens[" + std::to_string(F.col) + "]" : "nullptr, 0")
+          << ");\n      em.finish();\n      }\n      }\n";
+        return;
+    }
+    if (X.shape == spec::SHAPE_STRUCT) {
+        for (uint32_t i = X.field + 1u; i < D.f[X.field].send; i++)
+            if (D.f[i].kind != spec::K_STRUCT) o << "      uint64_t (&m" << i << ")[4] = m" << i << sfx << ";\n";
+        o << "      if (start != ~0ull) {\n      auto em = mk(start);\n";
+        gen_struct_emit(o, D, X.field, 0, "      ");
+        o << "      em.finish();\n      }\n      }\n";
+        return;
+    }
+    for (uint32_t k = 0; k < X.nd; k++) gen_field_bind(o, D, X, k, sfx, "      ");
+    o << "      if (start == ~0ull) {\n        gen_unplace_" << x << "(D, B, row);\n      } else {\n"
+      << "      auto em = mk(start);\n      uint32_t nf = 0;\n      bool bigtag = false;\n";
+    for (uint32_t k = 0; k < X.nd; k++) gen_field_write(o, D, X, k, true);
+    o << "  const uint64_t data = em.pos - start;\n  const bool big = bigtag || (nf > 0 && data > 65535);\n";
+    gen_table_trailer(o, D, X);
+    o << "      }\n      }\n";
 }
 
 void gen_tile(std::ostringstream &o, const TreeDesc &D) {
@@ -1418,39 +1499,6 @@ void gen_tile(std::ostringstream &o, const TreeDesc &D) {
               << "  auto em = mk(start);\n  emit_row_shaped(em, D, B, " << x << "u, row);\n";
         }
         o << "}\n";
-        if (!tile_pair_ok(D, x)) continue;
-        // two rows (rowA, and rowB if hasB) with both rows' reads issued before either is written
-        o << "template <class Mk>\n__device__ __forceinline__ void gen_trow2_" << x
-          << "(const Mk &mk, const TreeDesc &D, const TreeBufs &B, uint64_t rowA, uint64_t rowB, bool hasB) {\n";
-        if (X.shape == spec::SHAPE_MESSAGE) {
-            for (const char *sf : {"_A", "_B"})
-                for (uint32_t k = 0; k < X.nd; k++) gen_field_loads(o, D, X, k, true, "  ", sf, std::string("row") + sf[1]);
-            o << "  const uint64_t startA = B.pos[" << x << "][rowA], startB = B.pos[" << x << "][rowB];\n";
-            for (const char *sf : {"_A", "_B"}) {
-                o << (sf[1] == 'A' ? "  {\n" : "  if (hasB) {\n") << "  const uint64_t row = row" << sf[1]
-                  << ", start = start" << sf[1] << ";\n";
-                for (uint32_t k = 0; k < X.nd; k++) gen_field_bind(o, D, X, k, sf, "  ");
-                o << "  if (start == ~0ull) {\n    gen_unplace_" << x << "(D, B, row);\n  } else {\n"
-                  << "  auto em = mk(start);\n  uint32_t nf = 0;\n  bool bigtag = false;\n";
-                for (uint32_t k = 0; k < X.nd; k++) gen_field_write(o, D, X, k, true);
-                o << "  const uint64_t data = em.pos - start;\n"
-                  << "  const bool big = bigtag || (nf > 0 && data > 65535);\n";
-                gen_table_trailer(o, D, X);
-                o << "  }\n  }\n";
-            }
-        } else {
-            const TField &F = D.f[X.field];
-            const bool heap = F.elem == spec::K_STRING || F.elem == spec::K_BYTES;
-            o << "  uint64_t aA[4], aB[4];\n  load_value_k<" << (int)F.elem << ">(" << col_expr(F.col) << ", rowA, aA);\n"
-              << "  load_value_k<" << (int)F.elem << ">(" << col_expr(F.col) << ", rowB, aB);\n"
-              << "  const uint64_t startA = B.pos[" << x << "][rowA], startB = B.pos[" << x << "][rowB];\n";
-            for (const char *sf : {"A", "B"})
-                o << "  if (" << (sf[0] == 'A' ? "true" : "hasB") << " && start" << sf << " != ~0ull) {\n"
-                  << "    auto em = mk(start" << sf << ");\n    emit_value_k<" << (int)F.elem << ">(em, a" << sf << ", "
-                  << (heap ? "B.heaps[" + std::to_string(F.col) + "], B.heap_lens[" + std::to_string(F.col) + "]" : "nullptr, 0")
-                  << ");\n    em.finish();\n  }\n";
-        }
-        o << "}\n";
     }
     int depth[spec::TREE_MAX_T] = {0}, maxd = 0;
     for (uint32_t x = 1; x < D.ntables; x++) {
@@ -1476,24 +1524,39 @@ void gen_tile(std::ostringstream &o, const TreeDesc &D) {
         else
             o << "  const uint64_t lo" << x << " = lo" << X.parent << ", hi" << x << " = hi" << X.parent << ";\n";
     }
-    // depth d: the tables' row ranges laid end to end, index i to thread i mod blockDim (one loop
-    // per table over this thread's indices in its segment: an if-chain over the tables inside one
-    // loop took the register coalescer minutes)
+    // depth d: the tables' row ranges laid end to end, index i to thread i mod blockDim; the
+    // tables of tile_round_ok in rounds (every such table's next row of this thread read at once),
+    // the others in one loop per table over this thread's indices in its segment (an if-chain
+    // over the tables inside one loop took the register coalescer minutes)
     for (int d = 1; d <= maxd; d++) {
         o << "  { // depth " << d << "\n    uint64_t base = 0;\n";
+        std::vector<uint32_t> rt;
         for (uint32_t x = 1; x < D.ntables; x++)
             if (depth[x] == d) {
-                if (tile_pair_ok(D, x))
-                    o << "    for (uint64_t i = base + (uint32_t)(threadIdx.x - base) % blockDim.x; i < base + (hi" << x << " - lo"
-                      << x << "); i += 2 * blockDim.x) {\n"
-                      << "      const bool hb = i + blockDim.x < base + (hi" << x << " - lo" << x << ");\n"
-                      << "      const uint64_t ra = lo" << x << " + (i - base);\n"
-                      << "      gen_trow2_" << x << "(mk, D, B, ra, hb ? ra + blockDim.x : ra, hb);\n    }\n";
+                o << "    const uint64_t c" << x << " = hi" << x << " - lo" << x << ", b" << x << " = base;\n    base += c" << x << ";\n";
+                if (tile_round_ok(D, x)) rt.push_back(x);
                 else
-                    o << "    for (uint64_t i = base + (uint32_t)(threadIdx.x - base) % blockDim.x; i < base + (hi" << x << " - lo"
-                      << x << "); i += blockDim.x)\n      gen_trow_" << x << "(mk, D, B, lo" << x << " + (i - base));\n";
-                o << "    base += hi" << x << " - lo" << x << ";\n";
+                    o << "    for (uint64_t i = (uint32_t)(threadIdx.x - b" << x << ") % blockDim.x; i < c" << x
+                      << "; i += blockDim.x)\n      gen_trow_" << x << "(mk, D, B, lo" << x << " + i);\n";
             }
+        if (!rt.empty()) {
+            o << "    for (uint64_t r = 0;; r += blockDim.x) {\n";
+            std::ostringstream decl, rd, wr;
+            for (uint32_t x : rt) {
+                const std::string sx = "_t" + std::to_string(x), rv = "rw" + std::to_string(x);
+                o << "    const uint64_t j" << x << " = (uint32_t)(threadIdx.x - b" << x << ") % blockDim.x + r;\n"
+                  << "    const bool v" << x << " = j" << x << " < c" << x << ";\n"
+                  << "    const uint64_t " << rv << " = lo" << x << " + j" << x << ";\n";
+                rd << "      if (v" << x << ") {\n";
+                gen_round_loads(decl, rd, D, x, sx, rv);
+                rd << "      }\n";
+                wr << "      if (v" << x << ") \n";
+                gen_round_write(wr, D, x, sx, rv);
+            }
+            o << "    if (!(false";
+            for (uint32_t x : rt) o << " || v" << x;
+            o << ")) break;\n" << decl.str() << rd.str() << wr.str() << "    }\n";
+        }
         o << "    (void)base;\n  }\n  __syncthreads();\n";
         if (SPEC_AB_TILE_CLOCK) o << "  if (threadIdx.x == 0) B.tmask[r0 + " << d + 1 << "] = wall_clock64();\n";
     }
@@ -1531,10 +1594,34 @@ std::string generate_tree(const TreeDesc &D, bool *has) {
       << "  const TreeDesc &D = *Dp;\n  const TreeBufs &B = *Bp;\n  bool err = false;\n"
       << "  const uint32_t x = s.t[blockIdx.y];\n  const uint64_t rows = B.rows[x];\n"
       << "  switch (x) {\n";
-    for (uint32_t t = 0; t < D.ntables; t++)
-        if (D.t[t].shape == spec::SHAPE_MESSAGE)
+    for (uint32_t t = 0; t < D.ntables; t++) {
+        const TTable &X = D.t[t];
+        if (X.shape == spec::SHAPE_MESSAGE) {
             o << "  case " << t << ": for (uint64_t row = grid_first(); row < rows; row += grid_stride()) gen_srow_" << t
               << "(D, B, x, row, err); break;\n";
+            continue;
+        }
+        // list elements: scalars, strings, bytes and structs with constant kinds (value_size /
+        // struct_size's rules); other elements (any) by the run-time rule below
+        const TField &F = D.f[X.field];
+        const bool val = X.shape == spec::SHAPE_VALUE && F.elem >= spec::K_BOOL && F.elem <= spec::K_BYTES;
+        if (!val && X.shape != spec::SHAPE_STRUCT) continue;
+        o << "  case " << t << ":\n    for (uint64_t row = grid_first(); row < rows; row += grid_stride()) {\n";
+        if (val) {
+            o << "      uint64_t a[4];\n      load_value_k<" << (int)F.elem << ">(" << col_expr(F.col) << ", row, a);\n"
+              << "      const uint64_t total = " << value_size_expr(F.elem, "a") << ";\n";
+            if (F.elem == spec::K_STRING || F.elem == spec::K_BYTES)
+                o << "      { const uint32_t off = (uint32_t)a[0], len = (uint32_t)(a[0] >> 32);\n"
+                  << "        if ((uint64_t)len > MAX_SIZE || (uint64_t)off + len > B.heap_lens[" << F.col << "]) err = true; }\n";
+        } else {
+            for (uint32_t i = X.field + 1u; i < F.send; i++)
+                if (D.f[i].kind != spec::K_STRUCT)
+                    o << "      uint64_t m" << i << "[4];\n      load_value_k<" << (int)D.f[i].kind << ">(" << col_expr(D.f[i].col)
+                      << ", row, m" << i << ");\n";
+            gen_struct_size(o, D, X.field, "total", "      ");
+        }
+        o << "      if (total > 0xffffffffull) err = true;\n      B.size[x][row] = (uint32_t)total;\n    }\n    break;\n";
+    }
     o << "  default:\n"
       << "    for (uint64_t row = grid_first(); row < rows; row += grid_stride()) {\n"
       << "      const uint64_t total = size_row_shaped(D, B, x, row, err);\n"

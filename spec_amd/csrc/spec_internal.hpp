@@ -33,9 +33,11 @@ constexpr int TREE_TILE_W = SPEC_AB_TREE_TILE_W, TREE_TILE_WPE = SPEC_AB_TREE_TI
 #ifndef SPEC_AB_TILE_CLOCK
 #define SPEC_AB_TILE_CLOCK 0
 #endif
-// the tile writer's rows below the records two per lane at a time (jit.cpp tile_pair_ok)
-#ifndef SPEC_AB_TILE_PAIR
-#define SPEC_AB_TILE_PAIR 0
+// the tile writer's rows below the records in rounds over the tables of a depth (jit.cpp
+// tile_round_ok); 0: one loop per table.  Measured on pkg1: depth-1 phase 24.0 vs 23.7 us per
+// tile (tools/tile_clock.py), encode 0.2864 vs 0.2844 ms — no gain, off
+#ifndef SPEC_AB_TILE_ROUNDS
+#define SPEC_AB_TILE_ROUNDS 0
 #endif
 constexpr uint32_t TREE_TILE_IMG = ((163840u / (4u * TREE_TILE_WPE / TREE_TILE_W)) - 32u) & ~15u;
 
