@@ -1574,6 +1574,7 @@ void gen_tile(std::ostringstream &o, const TreeDesc &D) {
       << "  const uint64_t org = B.offsets[r0], fin = B.offsets[r1 - 1] + B.size[0][r1 - 1];\n"
       // (out + sh 16-byte aligned: the image's chunks are the output's)
       << "  const uint64_t sh = org - (((unsigned long long)B.out + org) & 15);\n"
+      << (SPEC_AB_TILE_OR ? "  tile_clear(img, fin - sh < cap ? (uint32_t)(fin - sh) : cap);\n  __syncthreads();\n" : "")
       << "  gen_tile_body(MkL{img, B.out, sh, cap}, D, B, r0, r1);\n"
       << "  tile_copy_out(B.out, img, sh, org, fin < sh + cap ? fin : sh + cap);\n"
       << (SPEC_AB_TILE_CLOCK ? "  __syncthreads();\n  if (threadIdx.x == 0) B.tmask[r0 + 63] = wall_clock64();\n" : "")
@@ -1582,7 +1583,7 @@ void gen_tile(std::ostringstream &o, const TreeDesc &D) {
 
 std::string generate_tree(const TreeDesc &D, bool *has) {
     std::ostringstream o;
-    o << "#include \"tree_decode_core.hpp\"\nusing namespace spec;\n";
+    o << (SPEC_AB_TILE_OR ? "#define SPEC_TILE_OR 1\n" : "") << "#include \"tree_decode_core.hpp\"\nusing namespace spec;\n";
     for (uint32_t t = 0; t < D.ntables; t++)
         if (D.t[t].shape == spec::SHAPE_MESSAGE) {
             gen_write_table(o, D, t);

@@ -39,6 +39,11 @@ constexpr int TREE_TILE_W = SPEC_AB_TREE_TILE_W, TREE_TILE_WPE = SPEC_AB_TREE_TI
 #ifndef SPEC_AB_TILE_ROUNDS
 #define SPEC_AB_TILE_ROUNDS 0
 #endif
+// the tile writer's LDS image starts zeroed and rows OR their dwords into it (tree_core.hpp
+// LSink::word), so the emitter's stores need no edge cases
+#ifndef SPEC_AB_TILE_OR
+#define SPEC_AB_TILE_OR 1
+#endif
 constexpr uint32_t TREE_TILE_IMG = ((163840u / (4u * TREE_TILE_WPE / TREE_TILE_W)) - 32u) & ~15u;
 
 // encode_nested.hip

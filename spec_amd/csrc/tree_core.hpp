@@ -569,9 +569,21 @@ struct GSink {
     __device__ __forceinline__ uint32_t ph(uint64_t p) const { return (uint32_t)(p & 3); }
     __device__ __forceinline__ void st32(uint64_t p, uint32_t v) const { *(uint32_t *)(out + p) = v; }
     __device__ __forceinline__ void st8(uint64_t p, uint32_t b) const { out[p] = (uint8_t)b; }
+    // bytes [from, end) of the dword v at base (from >= base, end <= base + 4): whole, or bytewise
+    // where the dword is shared with a neighbour
+    __device__ __forceinline__ void word(uint64_t base, uint64_t from, uint64_t end, uint32_t v) const {
+        if (from == base && end == base + 4) {
+            st32(base, v);
+        } else {
+            for (uint64_t q = from; q < end; q++) st8(q, v >> (8 * (q - base)));
+        }
+    }
 };
 // (a tile's range may exceed the image: bytes past the image's window [sh, sh + cap) are stored
 // straight to the output — dwords are 4-byte aligned in both, so none straddles the window's end)
+#ifndef SPEC_TILE_OR
+#define SPEC_TILE_OR 0
+#endif
 typedef __attribute__((address_space(3))) uint8_t TileU8; // (writable: spec_device.hpp's lds_u8 is const)
 typedef __attribute__((address_space(3))) uint32_t TileU32;
 typedef __attribute__((address_space(3))) uint64_t TileU64;
@@ -589,6 +601,22 @@ struct LSink {
         if (p - sh < cap) img[(uint32_t)(p - sh)] = (uint8_t)b;
         else out[p] = (uint8_t)b;
     }
+    __device__ __forceinline__ void word(uint64_t base, uint64_t from, uint64_t end, uint32_t v) const {
+#if SPEC_TILE_OR
+        // the image starts zeroed and every byte belongs to one row: v's bytes outside [from, end)
+        // are zero (a row's pending dword holds only its own bytes), so an OR merges the dword
+        // with its neighbours' without the edge cases
+        if (base - sh < cap) {
+            __hip_atomic_fetch_or((TileU32 *)(img + (uint32_t)(base - sh)), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return;
+        }
+#endif
+        if (from == base && end == base + 4) {
+            st32(base, v);
+        } else {
+            for (uint64_t q = from; q < end; q++) st8(q, v >> (8 * (q - base)));
+        }
+    }
 };
 
 template <class S>
@@ -598,11 +626,7 @@ struct DEmit {
     uint64_t lo;    // first byte of the row (bytes below belong to another row)
     uint32_t w = 0; // pending bytes of the dword holding pos
     __device__ __forceinline__ void store_word(uint64_t base, uint64_t end, uint32_t v) { // bytes [base, end) of v
-        if (base >= lo && end == base + 4) {
-            k.st32(base, v);
-        } else {
-            for (uint64_t q = base > lo ? base : lo; q < end; q++) k.st8(q, v >> (8 * (q - base)));
-        }
+        k.word(base, base > lo ? base : lo, end, v);
     }
     __device__ __forceinline__ void store_pending(uint64_t base, uint64_t end) { store_word(base, end, w); }
     __device__ __forceinline__ void put1(uint32_t b) {
@@ -1118,6 +1142,12 @@ struct MkL { // emitters over the LDS image of the window [sh, sh + cap), HBM pa
     uint32_t cap;
     __device__ __forceinline__ LEmit operator()(uint64_t p) const { return LEmit{{img, out, sh, cap}, p, p}; }
 };
+
+// zeroes the image's first `len` bytes (SPEC_TILE_OR: the rows OR their dwords into it)
+__device__ __forceinline__ void tile_clear(TileU8 *img, uint32_t len) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    for (uint32_t a = threadIdx.x * 16u; a < len; a += blockDim.x * 16u) *(__attribute__((address_space(3))) v4u *)(img + a) = v4u{0, 0, 0, 0};
+}
 
 // out[org, fin) from the image (out byte p at img[p - sh]; out + sh is 16-byte aligned): whole
 // chunks with 16-byte stores, the partial chunks at the ends bytewise (the neighbours' bytes)
