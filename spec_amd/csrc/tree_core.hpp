@@ -590,15 +590,17 @@ typedef __attribute__((address_space(3))) uint64_t TileU64;
 struct LSink {
     TileU8 *img;
     uint8_t *out;
-    uint64_t sh;
-    uint32_t cap;
-    __device__ __forceinline__ uint32_t ph(uint64_t p) const { return (uint32_t)(p - sh) & 3; }
+    uint64_t lim;  // sh + cap: bytes at or past it go to HBM
+    uint32_t sh32; // sh's low 32 bits: every byte of the tile is >= sh and an in-window one < sh + cap, so
+                   // its image offset p - sh is (uint32_t)p - sh32 (32-bit arithmetic: fewer VALU per store)
+    __device__ __forceinline__ uint32_t at(uint64_t p) const { return (uint32_t)p - sh32; }
+    __device__ __forceinline__ uint32_t ph(uint64_t p) const { return at(p) & 3; }
     __device__ __forceinline__ void st32(uint64_t p, uint32_t v) const {
-        if (p - sh < cap) *(TileU32 *)(img + (uint32_t)(p - sh)) = v;
+        if (p < lim) *(TileU32 *)(img + at(p)) = v;
         else *(uint32_t *)(out + p) = v;
     }
     __device__ __forceinline__ void st8(uint64_t p, uint32_t b) const {
-        if (p - sh < cap) img[(uint32_t)(p - sh)] = (uint8_t)b;
+        if (p < lim) img[at(p)] = (uint8_t)b;
         else out[p] = (uint8_t)b;
     }
     __device__ __forceinline__ void word(uint64_t base, uint64_t from, uint64_t end, uint32_t v) const {
@@ -606,8 +608,8 @@ struct LSink {
         // the image starts zeroed and every byte belongs to one row: v's bytes outside [from, end)
         // are zero (a row's pending dword holds only its own bytes), so an OR merges the dword
         // with its neighbours' without the edge cases
-        if (base - sh < cap) {
-            __hip_atomic_fetch_or((TileU32 *)(img + (uint32_t)(base - sh)), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (base < lim) {
+            __hip_atomic_fetch_or((TileU32 *)(img + at(base)), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             return;
         }
 #endif
@@ -1140,7 +1142,7 @@ struct MkL { // emitters over the LDS image of the window [sh, sh + cap), HBM pa
     uint8_t *out;
     uint64_t sh;
     uint32_t cap;
-    __device__ __forceinline__ LEmit operator()(uint64_t p) const { return LEmit{{img, out, sh, cap}, p, p}; }
+    __device__ __forceinline__ LEmit operator()(uint64_t p) const { return LEmit{{img, out, sh + cap, (uint32_t)sh}, p, p}; }
 };
 
 // zeroes the image's first `len` bytes (SPEC_TILE_OR: the rows OR their dwords into it)
