@@ -1297,14 +1297,16 @@ bool tree_tile(const TreeDesc &D) {
     return true;
 }
 
+// a records' field's share of its wave's time in the tile writer, in scalar fields (fitted to the
+// per-wave clocks of a -DSPEC_AB_TILE_CLOCK=1 build on pkg1: a list ≈ 5, a string ≈ 2)
 uint32_t tile_field_cost(const TreeDesc &D, const TField &F) {
     switch (F.kind) {
-    case spec::K_STRING: case spec::K_BYTES: case spec::K_ANY: return 4;
+    case spec::K_STRING: case spec::K_BYTES: case spec::K_ANY: return 2;
     case spec::K_BIN128: return 2;
     case spec::K_BIN256: return 3;
     case spec::K_STRUCT: return 1 + (F.send - 1u - (uint32_t)(&F - D.f));
-    case spec::K_LIST: return 4;
-    case spec::K_MESSAGE: return 2;
+    case spec::K_LIST: return 5;
+    case spec::K_MESSAGE: return 1;
     default: return 1;
     }
 }
@@ -1319,8 +1321,11 @@ void tile_cuts(const TreeDesc &D, uint32_t *cut) {
     uint32_t k = 0, acc = 0;
     cut[0] = 0;
     for (int b = 0; b < TILE_W; b++) {
-        const uint64_t target = (uint64_t)total * (b + 1) / TILE_W;
-        while (k < T.nd && (acc < target || b == TILE_W - 1)) acc += cost[k++];
+        // fields while below the block's share of the total, the last one only if that lands closer
+        const int64_t target = (int64_t)total * (b + 1) / TILE_W;
+        while (k < T.nd && (b == TILE_W - 1 || ((int64_t)acc < target &&
+                                                 (int64_t)(acc + cost[k]) - target <= target - (int64_t)acc)))
+            acc += cost[k++];
         cut[b + 1] = k;
     }
     cut[TILE_W] = T.nd;
